@@ -1,0 +1,835 @@
+// api.cpp — the C ABI of libm3d.so (include/m3d.h): contexts, packed objects, batching and
+// the host-side drivers of the device loops.  No numerical work happens here except the
+// MT19937 replay of the reference RNG (m3d_replay_triples) and O(1) bookkeeping.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "linalg.h"
+#include "m3d_internal.h"
+
+namespace m3d {
+hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st);
+hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hipStream_t st);
+hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStream_t st);
+int64_t terms_blocks(int64_t ns);
+}  // namespace m3d
+
+using namespace m3d;
+
+int m3d_fail(m3d_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+KTimer::KTimer(m3d_ctx* c, int kid, hipStream_t s) : ctx(c), id(kid), st(s) {
+  if (!ctx || !ctx->profiling) return;
+  auto& v = ctx->ev[id];
+  size_t k = ctx->ev_used[id];
+  if (k >= 65536) return;  // cap; read regularly
+  if (k == v.size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) return;
+    if (hipEventCreate(&b) != hipSuccess) {
+      hipEventDestroy(a);
+      return;
+    }
+    v.emplace_back(a, b);
+  }
+  if (hipEventRecord(v[k].first, st) != hipSuccess) return;
+  end = v[k].second;
+  ctx->ev_used[id] = k + 1;
+}
+
+KTimer::~KTimer() {
+  if (end) hipEventRecord(end, st);
+}
+
+#define CHECK_ARG(ctx, cond, msg) \
+  do {                            \
+    if (!(cond)) return m3d_fail((ctx), M3D_ERR_INVALID, (msg)); \
+  } while (0)
+
+#define HIPX(ctx, expr) M3D_HIP_CHECK(ctx, expr)
+
+static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+namespace {
+
+constexpr int64_t kCorrPad = 2048;  // score kernel block footprint (ransac.hip kBlockCorr)
+constexpr int64_t kCloudPad = 1024; // NN tile multiple
+constexpr float kFar = 1.0e18f;
+
+template <class T>
+int dev_alloc(m3d_ctx* ctx, T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) return M3D_OK;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (size_t)count);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return m3d_fail(ctx, M3D_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  return M3D_OK;
+}
+
+// Bump allocator over the context scratch arena.  Growing synchronises the device.
+struct Arena {
+  m3d_ctx* ctx;
+  size_t off = 0;
+  explicit Arena(m3d_ctx* c) : ctx(c) {}
+  size_t take(size_t bytes) {
+    size_t o = (off + 255) & ~size_t(255);
+    off = o + bytes;
+    return o;
+  }
+  int commit() {
+    if (off <= ctx->scratch_bytes) return M3D_OK;
+    if (ctx->scratch) {
+      hipDeviceSynchronize();
+      hipFree(ctx->scratch);
+      ctx->scratch = nullptr;
+      ctx->scratch_bytes = 0;
+    }
+    size_t want = std::max(off, ctx->scratch_bytes * 3 / 2);
+    hipError_t e = hipMalloc(&ctx->scratch, want);
+    if (e != hipSuccess) {
+      ctx->scratch = nullptr;
+      return m3d_fail(ctx, M3D_ERR_OOM, "scratch hipMalloc failed");
+    }
+    ctx->scratch_bytes = want;
+    return M3D_OK;
+  }
+  template <class T>
+  T* at(size_t o) const {
+    return reinterpret_cast<T*>(static_cast<char*>(ctx->scratch) + o);
+  }
+};
+
+// deterministic mean of an n×3 device array (block partials summed in fixed order on host)
+int device_mean3(m3d_ctx* ctx, const double* a, int64_t n, double out[3], hipStream_t st) {
+  out[0] = out[1] = out[2] = 0.0;
+  if (n == 0) return M3D_OK;
+  const int blocks = 128;
+  double* part = nullptr;
+  int rc = dev_alloc(ctx, &part, blocks * 3);
+  if (rc) return rc;
+  hipError_t e = launch_sum3(a, n, part, blocks, st);
+  std::vector<double> h(blocks * 3);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), part, sizeof(double) * blocks * 3,
+                                          hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipFree(part);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  for (int b = 0; b < blocks; ++b)
+    for (int k = 0; k < 3; ++k) out[k] += h[3 * b + k];
+  for (int k = 0; k < 3; ++k) out[k] /= (double)n;
+  return M3D_OK;
+}
+
+int center_pack(m3d_ctx* ctx, const double* a, int64_t n, int64_t n_pad, const double c[3],
+                float4* out, float pad, double* maxv, hipStream_t st) {
+  *maxv = 0.0;
+  if (n_pad == 0) return M3D_OK;
+  const int blocks = (int)std::min<int64_t>(1024, (n_pad + 255) / 256);
+  float* part = nullptr;
+  int rc = dev_alloc(ctx, &part, blocks);
+  if (rc) return rc;
+  hipError_t e = launch_center_pack(a, n, n_pad, c, out, pad, part, blocks, 1, st);
+  std::vector<float> h(blocks);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h.data(), part, sizeof(float) * blocks, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipFree(part);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  float m = 0.0f;
+  for (float v : h) m = std::max(m, v);
+  *maxv = (double)m * (1.0 + 1e-6);
+  return M3D_OK;
+}
+
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+}  // namespace
+
+extern "C" {
+
+int m3d_abi_version(void) { return M3D_ABI_VERSION; }
+
+int m3d_device_count(int* count) {
+  if (!count) return M3D_ERR_INVALID;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return M3D_OK;
+}
+
+int m3d_create(int device, m3d_ctx** out) {
+  if (!out) return M3D_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return M3D_ERR_NODEVICE;
+  if (device < 0 || device >= n) return M3D_ERR_INVALID;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return M3D_ERR_HIP;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return M3D_ERR_NODEVICE;
+  if (hipSetDevice(device) != hipSuccess) return M3D_ERR_HIP;
+  m3d_ctx* ctx = new m3d_ctx();
+  ctx->device = device;
+  if (hipMalloc(&ctx->stats, 8 * sizeof(int64_t)) != hipSuccess ||
+      hipMalloc(&ctx->rstate, sizeof(RansacState)) != hipSuccess ||
+      hipMemset(ctx->stats, 0, 8 * sizeof(int64_t)) != hipSuccess) {
+    m3d_destroy(ctx);
+    return M3D_ERR_OOM;
+  }
+  *out = ctx;
+  return M3D_OK;
+}
+
+void m3d_destroy(m3d_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipDeviceSynchronize();
+  if (ctx->scratch) hipFree(ctx->scratch);
+  if (ctx->stats) hipFree(ctx->stats);
+  if (ctx->rstate) hipFree(ctx->rstate);
+  for (auto& v : ctx->ev)
+    for (auto& pr : v) {
+      hipEventDestroy(pr.first);
+      hipEventDestroy(pr.second);
+    }
+  delete ctx;
+}
+
+const char* m3d_last_error(const m3d_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int m3d_get_stats(m3d_ctx* ctx, int64_t* out8) {
+  CHECK_ARG(ctx, out8 != nullptr, "null output");
+  HIPX(ctx, hipMemcpy(out8, ctx->stats, 8 * sizeof(int64_t), hipMemcpyDeviceToHost));
+  return M3D_OK;
+}
+
+int m3d_profile_enable(m3d_ctx* ctx, int enable) {
+  if (!ctx) return M3D_ERR_INVALID;
+  ctx->profiling = enable != 0;
+  return M3D_OK;
+}
+
+int m3d_profile_read(m3d_ctx* ctx, int kernel, double* total_ms, int64_t* launches) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, kernel >= 0 && kernel < 4 && total_ms && launches, "invalid arguments");
+  double tot = 0.0;
+  const size_t n = ctx->ev_used[kernel];
+  for (size_t k = 0; k < n; ++k) {
+    auto& pr = ctx->ev[kernel][k];
+    HIPX(ctx, hipEventSynchronize(pr.second));
+    float ms = 0.0f;
+    HIPX(ctx, hipEventElapsedTime(&ms, pr.first, pr.second));
+    tot += ms;
+  }
+  ctx->ev_used[kernel] = 0;
+  *total_ms = tot;
+  *launches = (int64_t)n;
+  return M3D_OK;
+}
+
+// ------------------------------------------------------------------------------- corrset
+static int corrset_build(m3d_ctx* ctx, const double* src, int64_t ns, const double* tgt, int64_t nt,
+                         const int32_t* corr, const double* p_src, const double* p_tgt, int64_t nc,
+                         void* stream, m3d_corrset** out) {
+  CHECK_ARG(ctx, out != nullptr, "null output");
+  CHECK_ARG(ctx, nc >= 0 && nc < (int64_t)1 << 31, "correspondence count out of range");
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  std::vector<int32_t> fixed;
+  const int32_t* corr_dev = corr;
+  int32_t* corr_tmp = nullptr;
+  if (corr != nullptr && nc > 0) {
+    // validate rows like numpy fancy indexing: negative indices wrap once, others raise
+    fixed.resize(2 * nc);
+    HIPX(ctx, hipMemcpyAsync(fixed.data(), corr, sizeof(int32_t) * 2 * nc, hipMemcpyDeviceToHost, st));
+    HIPX(ctx, hipStreamSynchronize(st));
+    bool changed = false;
+    for (int64_t i = 0; i < nc; ++i) {
+      for (int c = 0; c < 2; ++c) {
+        int64_t lim = c == 0 ? ns : nt;
+        int64_t v = fixed[2 * i + c];
+        if (v < 0) {
+          v += lim;
+          changed = true;
+        }
+        if (v < 0 || v >= lim)
+          return m3d_fail(ctx, M3D_ERR_INVALID, "correspondence index " +
+                                                    std::to_string(fixed[2 * i + c]) +
+                                                    " out of bounds for axis 0 with size " +
+                                                    std::to_string(lim));
+        fixed[2 * i + c] = (int32_t)v;
+      }
+    }
+    if (changed) {
+      int rc = dev_alloc(ctx, &corr_tmp, 2 * nc);
+      if (rc) return rc;
+      HIPX(ctx, hipMemcpyAsync(corr_tmp, fixed.data(), sizeof(int32_t) * 2 * nc,
+                               hipMemcpyHostToDevice, st));
+      corr_dev = corr_tmp;
+    }
+  }
+  m3d_corrset* cs = new m3d_corrset();
+  cs->ctx = ctx;
+  cs->nc = nc;
+  cs->nc_pad = nc > 0 ? round_up(nc, kCorrPad) : 0;
+  int rc = dev_alloc(ctx, &cs->p64, 3 * nc);
+  if (!rc) rc = dev_alloc(ctx, &cs->q64, 3 * nc);
+  if (!rc) rc = dev_alloc(ctx, &cs->p32, cs->nc_pad);
+  if (!rc) rc = dev_alloc(ctx, &cs->q32, cs->nc_pad);
+  if (rc) {
+    if (corr_tmp) hipFree(corr_tmp);
+    m3d_corrset_destroy(cs);
+    return rc;
+  }
+  hipError_t e = launch_pack_corr(src, tgt, corr_dev, nc, p_src, p_tgt, cs->p64, cs->q64, st);
+  if (e != hipSuccess) {
+    if (corr_tmp) hipFree(corr_tmp);
+    m3d_corrset_destroy(cs);
+    return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  }
+  rc = device_mean3(ctx, cs->p64, nc, cs->cs, st);
+  if (!rc) rc = device_mean3(ctx, cs->q64, nc, cs->ct, st);
+  // pad: source 0, target far away → padded pairs are never inliers nor ambiguous
+  if (!rc) rc = center_pack(ctx, cs->p64, nc, cs->nc_pad, cs->cs, cs->p32, 0.0f, &cs->pmax2, st);
+  if (!rc) rc = center_pack(ctx, cs->q64, nc, cs->nc_pad, cs->ct, cs->q32, kFar, &cs->qmaxinf, st);
+  if (corr_tmp) {
+    hipStreamSynchronize(st);
+    hipFree(corr_tmp);
+  }
+  if (rc) {
+    m3d_corrset_destroy(cs);
+    return rc;
+  }
+  *out = cs;
+  return M3D_OK;
+}
+
+int m3d_corrset_create(m3d_ctx* ctx, const double* src_xyz, int64_t ns, const double* tgt_xyz,
+                       int64_t nt, const int32_t* corr, int64_t nc, void* stream,
+                       m3d_corrset** out) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, nc == 0 || (src_xyz && tgt_xyz && corr), "null device pointer");
+  CHECK_ARG(ctx, ns >= 0 && nt >= 0, "negative size");
+  return corrset_build(ctx, src_xyz, ns, tgt_xyz, nt, corr, nullptr, nullptr, nc, stream, out);
+}
+
+int m3d_corrset_create_gathered(m3d_ctx* ctx, const double* p_src, const double* p_tgt,
+                                int64_t nc, void* stream, m3d_corrset** out) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, nc == 0 || (p_src && p_tgt), "null device pointer");
+  return corrset_build(ctx, nullptr, 0, nullptr, 0, nullptr, p_src, p_tgt, nc, stream, out);
+}
+
+void m3d_corrset_destroy(m3d_corrset* cs) {
+  if (!cs) return;
+  hipFree(cs->p64);
+  hipFree(cs->q64);
+  hipFree(cs->p32);
+  hipFree(cs->q32);
+  delete cs;
+}
+
+int64_t m3d_corrset_size(const m3d_corrset* cs) { return cs ? cs->nc : -1; }
+
+// ------------------------------------------------------------------------------- a1
+int m3d_kabsch3_batch(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triples, uint64_t seed,
+                      int64_t hyp0, int64_t H, double* T_out, uint8_t* status, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, cs != nullptr && H >= 0 && (H == 0 || T_out), "invalid arguments");
+  CHECK_ARG(ctx, triples != nullptr || cs->nc >= 3 || cs->nc < 3, "");
+  hipSetDevice(ctx->device);
+  Arena a(ctx);
+  size_t o_h = a.take(sizeof(HypF32) * (size_t)std::max<int64_t>(H, 1));
+  int rc = a.commit();
+  if (rc) return rc;
+  hipError_t e = launch_kabsch3(cs, triples, seed, hyp0, H, 0.0, T_out, status,
+                                a.at<HypF32>(o_h), nullptr, S(stream));
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  return M3D_OK;
+}
+
+// ------------------------------------------------------------------------------- a2/a3
+namespace {
+struct ScoreScratch {
+  HypF32* hypf;
+  AmbRecord* amb;
+  int32_t* ctr;  // [0] amb_count [1] full_count
+  int32_t* full_flag;
+  int32_t* full_list;
+  int32_t amb_cap;
+};
+
+size_t score_layout(Arena& a, int64_t H, size_t* o) {
+  const int64_t Hn = std::max<int64_t>(H, 1);
+  o[0] = a.take(sizeof(HypF32) * Hn);
+  o[1] = a.take(sizeof(AmbRecord) * (size_t)std::min<int64_t>(std::max<int64_t>(4 * Hn, 1 << 16), 1 << 22));
+  o[2] = a.take(sizeof(int32_t) * 64);
+  o[3] = a.take(sizeof(int32_t) * Hn);
+  o[4] = a.take(sizeof(int32_t) * Hn);
+  return 0;
+}
+
+ScoreScratch score_bind(const Arena& a, const size_t* o, int64_t H) {
+  const int64_t Hn = std::max<int64_t>(H, 1);
+  ScoreScratch s;
+  s.hypf = a.at<HypF32>(o[0]);
+  s.amb = a.at<AmbRecord>(o[1]);
+  s.ctr = a.at<int32_t>(o[2]);
+  s.full_flag = a.at<int32_t>(o[3]);
+  s.full_list = a.at<int32_t>(o[4]);
+  s.amb_cap = (int32_t)std::min<int64_t>(std::max<int64_t>(4 * Hn, 1 << 16), 1 << 22);
+  return s;
+}
+
+double thr_sq_of(double thr, int mode) { return mode == M3D_SCORE_SQUARED ? thr : thr * thr; }
+
+// score H transforms T (device) whose fp32 blocks are already in s.hypf
+hipError_t score_enqueue(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64_t H,
+                         double thr, int mode, int32_t* counts, const ScoreScratch& s,
+                         const int32_t* done, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(counts, 0, sizeof(int32_t) * H, st);
+  if (e == hipSuccess) e = hipMemsetAsync(s.ctr, 0, sizeof(int32_t) * 64, st);
+  if (e == hipSuccess) e = hipMemsetAsync(s.full_flag, 0, sizeof(int32_t) * H, st);
+  if (e == hipSuccess) {
+    KTimer kt(ctx, M3D_KERNEL_SCORE, st);
+    e = launch_score(cs, s.hypf, H, counts, s.amb, s.ctr, s.amb_cap, s.full_flag, s.full_list,
+                     s.ctr + 1, done, st);
+  }
+  if (e == hipSuccess)
+    e = launch_recheck(cs, T, H, thr, mode, counts, s.amb, s.ctr, s.amb_cap, s.full_list, s.ctr + 1,
+                       ctx->stats, done, st);
+  return e;
+}
+}  // namespace
+
+int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64_t H, double thr,
+                     int mode, int32_t* counts, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, cs != nullptr && H >= 0, "invalid arguments");
+  CHECK_ARG(ctx, H == 0 || (T && counts), "null device pointer");
+  CHECK_ARG(ctx, mode == M3D_SCORE_SQUARED || mode == M3D_SCORE_NORM, "unknown score mode");
+  if (H == 0) return M3D_OK;
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  if (cs->nc == 0) {  // ransac.py:220-221 — ratio 0.0
+    HIPX(ctx, hipMemsetAsync(counts, 0, sizeof(int32_t) * H, st));
+    return M3D_OK;
+  }
+  Arena a(ctx);
+  size_t o[5];
+  score_layout(a, H, o);
+  int rc = a.commit();
+  if (rc) return rc;
+  ScoreScratch s = score_bind(a, o, H);
+  hipError_t e = launch_hypf_from_T(cs, T, H, thr_sq_of(thr, mode), s.hypf, st);
+  if (e == hipSuccess) e = score_enqueue(ctx, cs, T, H, thr, mode, counts, s, nullptr, st);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  return M3D_OK;
+}
+
+// ------------------------------------------------------------------------------- a4
+int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_params* p,
+                         const int32_t* triples, int32_t* counts_out,
+                         m3d_ransac_result* result_dev, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, cs && p && result_dev, "invalid arguments");
+  CHECK_ARG(ctx, p->max_iter >= 0, "max_iter must be >= 0");
+  CHECK_ARG(ctx, p->mode == M3D_SCORE_SQUARED || p->mode == M3D_SCORE_NORM, "unknown score mode");
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  const int64_t nc = cs->nc;
+  const int64_t max_iter = p->max_iter;
+  int64_t B = p->batch;
+  if (B <= 0) {
+    // ~2e8 pair evaluations per batch keeps the chip busy; early stop wants small first batches
+    B = nc > 0 ? std::max<int64_t>(1024, (int64_t)2e8 / std::max<int64_t>(nc, 1)) : 1024;
+    if (p->early_stop) B = std::min<int64_t>(B, 16384);
+  }
+  B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(max_iter, 1)));
+  Arena a(ctx);
+  size_t o[5];
+  score_layout(a, B, o);
+  size_t o_T = a.take(sizeof(double) * 16 * B);
+  size_t o_c = a.take(sizeof(int32_t) * B);
+  int rc = a.commit();
+  if (rc) return rc;
+  ScoreScratch s = score_bind(a, o, B);
+  double* Tb = a.at<double>(o_T);
+  int32_t* cb = a.at<int32_t>(o_c);
+  RansacState init;
+  memset(&init, 0, sizeof(init));
+  for (int k = 0; k < 16; ++k) init.T_best[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  init.best_count = -1;
+  init.best_index = -1;
+  init.iterations = 0;
+  init.done = (max_iter == 0) ? 1 : 0;
+  HIPX(ctx, hipMemcpyAsync(ctx->rstate, &init, sizeof(init), hipMemcpyHostToDevice, st));
+  const int32_t* done = &ctx->rstate->done;
+  const double thr_sq = thr_sq_of(p->thr, p->mode);
+  for (int64_t b0 = 0; b0 < max_iter; b0 += B) {
+    const int64_t n = std::min(B, max_iter - b0);
+    const int32_t* tri = triples ? triples + 3 * b0 : nullptr;
+    int32_t* cnt = counts_out ? counts_out + b0 : cb;
+    hipError_t e;
+    {
+      KTimer kt(ctx, M3D_KERNEL_KABSCH, st);
+      e = launch_kabsch3(cs, tri, p->seed, p->hyp0 + b0, n, thr_sq, Tb, nullptr, s.hypf, done, st);
+    }
+    if (e == hipSuccess) {
+      if (nc > 0)
+        e = score_enqueue(ctx, cs, Tb, n, p->thr, p->mode, cnt, s, done, st);
+      else
+        e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * n, st);
+    }
+    if (e == hipSuccess)
+      e = launch_select(cnt, b0, n, std::max<int64_t>(nc, 1), max_iter, p->early_stop,
+                        p->es_threshold, p->es_confidence, Tb, ctx->rstate, st);
+    if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  }
+  hipError_t e = launch_copy_result(ctx->rstate, nc, result_dev, st);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  return M3D_OK;
+}
+
+int m3d_ransac_run(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_params* p,
+                   const int32_t* triples, m3d_ransac_result* out, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, out != nullptr, "null output");
+  m3d_ransac_result* dres = nullptr;
+  int rc = dev_alloc(ctx, &dres, 1);
+  if (rc) return rc;
+  hipMemsetAsync(dres, 0, sizeof(*dres), S(stream));
+  rc = m3d_ransac_run_async(ctx, cs, p, triples, nullptr, dres, stream);
+  if (!rc) {
+    hipError_t e = hipMemcpyAsync(out, dres, sizeof(*out), hipMemcpyDeviceToHost, S(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(S(stream));
+    if (e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  }
+  hipFree(dres);
+  return rc;
+}
+
+// ------------------------------------------------------------------------------- MT19937 replay
+namespace {
+struct MT {
+  uint32_t key[624];
+  int pos;
+  void gen() {
+    const uint32_t A = 0x9908b0dfu, UP = 0x80000000u, LO = 0x7fffffffu;
+    int i;
+    uint32_t y;
+    for (i = 0; i < 624 - 397; ++i) {
+      y = (key[i] & UP) | (key[i + 1] & LO);
+      key[i] = key[i + 397] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+    }
+    for (; i < 623; ++i) {
+      y = (key[i] & UP) | (key[i + 1] & LO);
+      key[i] = key[i + (397 - 624)] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+    }
+    y = (key[623] & UP) | (key[0] & LO);
+    key[623] = key[396] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+    pos = 0;
+  }
+  uint32_t next() {
+    if (pos >= 624) gen();
+    uint32_t y = key[pos++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+  // numpy random_interval(max) for max <= 0xffffffff (masked rejection)
+  uint32_t interval(uint32_t max) {
+    if (max == 0) return 0;
+    uint32_t mask = max;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    uint32_t v;
+    while ((v = (next() & mask)) > max) {
+    }
+    return v;
+  }
+};
+}  // namespace
+
+int m3d_replay_triples(uint32_t* mt_key, int32_t* mt_pos, int64_t nc, int64_t H,
+                       int32_t* triples_out) {
+  if (!mt_key || !mt_pos || (H > 0 && !triples_out)) return M3D_ERR_INVALID;
+  if (nc < 3 || nc > 0xffffffffll) return M3D_ERR_INVALID;
+  MT mt;
+  memcpy(mt.key, mt_key, sizeof(mt.key));
+  mt.pos = *mt_pos;
+  // legacy RandomState.choice(nc, 3, replace=False) == permutation(nc)[:3]; permutation shuffles
+  // arange(nc) with i = nc-1 .. 1, j = random_interval(i), swap(x[i], x[j]).  Only positions 0..2
+  // are needed; version stamps avoid re-initialising the O(nc) array per hypothesis.
+  std::vector<int64_t> val((size_t)nc);
+  std::vector<uint32_t> stamp((size_t)nc, 0u);
+  uint32_t cur = 0;
+  for (int64_t h = 0; h < H; ++h) {
+    ++cur;
+    if (cur == 0) {
+      std::fill(stamp.begin(), stamp.end(), 0u);
+      cur = 1;
+    }
+    auto get = [&](int64_t k) { return stamp[k] == cur ? val[k] : k; };
+    for (int64_t i = nc - 1; i >= 1; --i) {
+      const int64_t j = (int64_t)mt.interval((uint32_t)i);
+      const int64_t vi = get(i), vj = get(j);
+      val[i] = vj;
+      stamp[i] = cur;
+      val[j] = vi;
+      stamp[j] = cur;
+    }
+    for (int k = 0; k < 3; ++k) triples_out[3 * h + k] = (int32_t)get(k);
+  }
+  memcpy(mt_key, mt.key, sizeof(mt.key));
+  *mt_pos = mt.pos;
+  return M3D_OK;
+}
+
+// ------------------------------------------------------------------------------- clouds
+int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                     void* stream, m3d_cloud** out) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, out != nullptr, "null output");
+  CHECK_ARG(ctx, n >= 0 && n < (int64_t)1 << 31, "point count out of range");
+  CHECK_ARG(ctx, n == 0 || xyz != nullptr, "null device pointer");
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  m3d_cloud* c = new m3d_cloud();
+  c->ctx = ctx;
+  c->n = n;
+  c->n_pad = round_up(std::max<int64_t>(n, 1), kCloudPad);
+  int rc = dev_alloc(ctx, &c->xyz64, 3 * n);
+  if (!rc && normals) rc = dev_alloc(ctx, &c->nrm64, 3 * n);
+  if (!rc) rc = dev_alloc(ctx, &c->xyz32, c->n_pad);
+  if (rc) {
+    m3d_cloud_destroy(c);
+    return rc;
+  }
+  if (n > 0) {
+    hipError_t e = hipMemcpyAsync(c->xyz64, xyz, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && normals)
+      e = hipMemcpyAsync(c->nrm64, normals, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) {
+      m3d_cloud_destroy(c);
+      return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+    }
+  }
+  rc = device_mean3(ctx, c->xyz64, n, c->center, st);
+  if (!rc) rc = center_pack(ctx, c->xyz64, n, c->n_pad, c->center, c->xyz32, kFar, &c->rmax, st);
+  if (rc) {
+    m3d_cloud_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return M3D_OK;
+}
+
+void m3d_cloud_destroy(m3d_cloud* c) {
+  if (!c) return;
+  hipFree(c->xyz64);
+  hipFree(c->nrm64);
+  hipFree(c->xyz32);
+  delete c;
+}
+
+int64_t m3d_cloud_size(const m3d_cloud* c) { return c ? c->n : -1; }
+
+// ------------------------------------------------------------------------------- ICP
+int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
+                   const m3d_icp_params* params, m3d_icp** out) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, src && tgt && params && out, "invalid arguments");
+  CHECK_ARG(ctx, max_dist > 0.0, "Invalid max_correspondence_distance.");
+  CHECK_ARG(ctx, params->estimation == M3D_EST_POINT_TO_PLANE ||
+                     params->estimation == M3D_EST_POINT_TO_POINT,
+            "unknown estimation");
+  CHECK_ARG(ctx, params->estimation != M3D_EST_POINT_TO_PLANE || tgt->nrm64 != nullptr || tgt->n == 0,
+            "TransformationEstimationPointToPlane requires pre-computed normal vectors for target "
+            "PointCloud.");
+  CHECK_ARG(ctx, params->max_iteration >= 0, "max_iteration must be >= 0");
+  hipSetDevice(ctx->device);
+  m3d_icp* s = new m3d_icp();
+  s->ctx = ctx;
+  s->src = src;
+  s->tgt = tgt;
+  s->params = *params;
+  s->max_dist = max_dist;
+  s->nblocks = terms_blocks(src->n);
+  int rc = dev_alloc(ctx, &s->state, 1);
+  if (!rc) rc = dev_alloc(ctx, &s->keys, std::max<int64_t>(src->n, 1));
+  if (!rc) rc = dev_alloc(ctx, &s->corr, std::max<int64_t>(src->n, 1));
+  if (!rc) rc = dev_alloc(ctx, &s->partials, s->nblocks * kTermSlots);
+  if (!rc) rc = dev_alloc(ctx, &s->sums, kTermSlots);
+  if (rc) {
+    m3d_icp_destroy(s);
+    return rc;
+  }
+  *out = s;
+  return M3D_OK;
+}
+
+void m3d_icp_destroy(m3d_icp* s) {
+  if (!s) return;
+  hipFree(s->state);
+  hipFree(s->keys);
+  hipFree(s->corr);
+  hipFree(s->partials);
+  hipFree(s->sums);
+  delete s;
+}
+
+int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  m3d_ctx* ctx = s->ctx;
+  double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  const double* T = init ? init : I;
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  HIPX(ctx, hipMemsetAsync(s->corr, 0xFF, sizeof(int32_t) * std::max<int64_t>(s->src->n, 1), st));
+  HIPX(ctx, launch_icp_reset(s, T, st));
+  return M3D_OK;
+}
+
+int m3d_icp_step(m3d_icp* s, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  m3d_ctx* ctx = s->ctx;
+  hipStream_t st = S(stream);
+  HIPX(ctx, launch_icp_keyinit(s, 0, st));
+  { KTimer kt(ctx, M3D_KERNEL_NN, st); HIPX(ctx, launch_icp_nn(s, 0, st)); }
+  { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, 0, 0, st)); }
+  HIPX(ctx, launch_icp_reduce(s, s->sums, st));
+  HIPX(ctx, launch_icp_solve(s, s->sums, st));
+  return M3D_OK;
+}
+
+int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* keys, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  m3d_ctx* ctx = s->ctx;
+  CHECK_ARG(ctx, off >= 0, "negative shard offset");
+  hipStream_t st = S(stream);
+  HIPX(ctx, launch_icp_keyinit(s, off, st));
+  { KTimer kt(ctx, M3D_KERNEL_NN, st); HIPX(ctx, launch_icp_nn(s, off, st)); }
+  if (keys && keys != s->keys)
+    HIPX(ctx, hipMemcpyAsync(keys, s->keys, sizeof(int64_t) * s->src->n, hipMemcpyDeviceToDevice, st));
+  return M3D_OK;
+}
+
+int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* keys, double* sums, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  m3d_ctx* ctx = s->ctx;
+  CHECK_ARG(ctx, sums != nullptr, "null sums");
+  hipStream_t st = S(stream);
+  if (keys && keys != s->keys)
+    HIPX(ctx, hipMemcpyAsync(s->keys, keys, sizeof(int64_t) * s->src->n, hipMemcpyDeviceToDevice, st));
+  { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, off, 1, st)); }
+  HIPX(ctx, launch_icp_reduce(s, sums, st));
+  return M3D_OK;
+}
+
+int m3d_icp_solve(m3d_icp* s, const double* sums, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  HIPX(s->ctx, launch_icp_solve(s, sums ? sums : s->sums, S(stream)));
+  return M3D_OK;
+}
+
+int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream) {
+  if (!s || !out) return M3D_ERR_INVALID;
+  m3d_ctx* ctx = s->ctx;
+  IcpState h;
+  HIPX(ctx, hipMemcpyAsync(&h, s->state, sizeof(h), hipMemcpyDeviceToHost, S(stream)));
+  HIPX(ctx, hipStreamSynchronize(S(stream)));
+  for (int k = 0; k < 16; ++k) out->T[k] = h.T[k];
+  out->fitness = h.fitness;
+  out->inlier_rmse = h.rmse;
+  out->num_correspondences = h.count;
+  out->iterations = h.iters;
+  out->converged = h.converged;
+  return M3D_OK;
+}
+
+const int32_t* m3d_icp_corr(const m3d_icp* s) { return s ? s->corr : nullptr; }
+
+int m3d_icp_copy_corr(const m3d_icp* s, int32_t* dst, void* stream) {
+  if (!s || !dst) return M3D_ERR_INVALID;
+  if (s->src->n == 0) return M3D_OK;
+  HIPX(s->ctx, hipMemcpyAsync(dst, s->corr, sizeof(int32_t) * s->src->n, hipMemcpyDeviceToDevice,
+                              S(stream)));
+  return M3D_OK;
+}
+
+int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const double* init,
+                double max_dist, const m3d_icp_params* params, m3d_icp_result* out,
+                int32_t* corr_idx, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, out != nullptr, "null output");
+  m3d_icp* s = nullptr;
+  int rc = m3d_icp_create(ctx, src, tgt, max_dist, params, &s);
+  if (rc) return rc;
+  rc = m3d_icp_reset(s, init, stream);
+  for (int k = 0; !rc && k <= params->max_iteration; ++k) rc = m3d_icp_step(s, stream);
+  if (!rc) rc = m3d_icp_result_get(s, out, stream);
+  if (!rc && corr_idx && src->n > 0) {
+    hipError_t e = hipMemcpyAsync(corr_idx, s->corr, sizeof(int32_t) * src->n,
+                                  hipMemcpyDeviceToDevice, S(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(S(stream));
+    if (e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  }
+  m3d_icp_destroy(s);
+  return rc;
+}
+
+int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const double* T_host,
+            double max_dist, int32_t* idx, double* d2, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, src && tgt && idx, "invalid arguments");
+  CHECK_ARG(ctx, max_dist > 0.0, "max_dist must be > 0");
+  m3d_icp_params p{1e-6, 1e-6, 0, M3D_EST_POINT_TO_POINT};
+  m3d_icp* s = nullptr;
+  int rc = m3d_icp_create(ctx, src, tgt, max_dist, &p, &s);
+  if (rc) return rc;
+  hipStream_t st = S(stream);
+  rc = m3d_icp_reset(s, T_host, stream);
+  hipError_t e = hipSuccess;
+  if (!rc) e = launch_icp_keyinit(s, 0, st);
+  if (e == hipSuccess) e = launch_icp_nn(s, 0, st);
+  if (e == hipSuccess) e = launch_nn_finalize(s, idx, d2, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (!rc && e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  m3d_icp_destroy(s);
+  return rc;
+}
+
+// ------------------------------------------------------------------------------- test hooks
+int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16) {
+  if (!src9 || !tgt9 || !T16) return M3D_ERR_INVALID;
+  double ps[3][3], qs[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) {
+      ps[i][k] = src9[3 * i + k];
+      qs[i][k] = tgt9[3 * i + k];
+    }
+  return kabsch3(ps, qs, T16);
+}
+
+int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6) {
+  if (!A36 || !b6 || !x6) return M3D_ERR_INVALID;
+  ldlt6_solve(A36, b6, x6);
+  return M3D_OK;
+}
+
+}  // extern "C"

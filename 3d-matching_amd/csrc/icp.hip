@@ -1,0 +1,499 @@
+// icp.hip — ICP refinement for gfx950.
+//
+// Reference: src/matcher/icp.py:42-48 → Open3D 0.19 RegistrationICP with
+// TransformationEstimationPointToPlane and ICPConvergenceCriteria(1e-6, 1e-6, 30).
+// One iteration = Eval(T) [1-NN within r, fitness, rmse] + ComputeTransformation + T ← ΔT·T.
+//
+// Kernels per iteration (all device resident, no host round trip):
+//   keyinit  O(Ns)      seeds each query's bound with its previous neighbour (fp32 d²)
+//   nn       O(Ns·Nt)   brute-force scan: queries in VGPRs (kNNQ per lane), targets streamed
+//                       through SGPRs by scalar loads (wave-uniform tile of kNNTile points).
+//                       Fast path per pair: 3 sub + 3 mul/fma + 1 min (v_min3 pairs them);
+//                       argmin bookkeeping only in the rare tiles whose minimum beats the bound.
+//                       The target range is split into slices (grid.y) so the chip is full;
+//                       slices merge with a 64-bit atomicMin on packed (bits(d²) << 32 | idx):
+//                       order independent → deterministic, lowest index wins exact ties.
+//   terms    O(Ns)      fp64: radius test d² < r² (strict, nanoflann), point-to-plane
+//                       J = [p×n ; n], r = (p−q)·n → JTJ(21) JTr(6) Σr²; count; Σd²
+//   reduce   1 block    fixed-order sum of the per-block partials (deterministic)
+//   solve    1 thread   fitness/rmse, convergence test, LDLT(JTJ, −JTr), x → Rz·Ry·Rx|t, T ← ΔT·T
+// The same keys/terms/solve pieces serve the target-sharded multi-GPU path (RCCL MIN on keys,
+// SUM on the 32 term slots between them).
+#include <float.h>
+
+#include "linalg.h"
+#include "m3d_internal.h"
+
+namespace m3d {
+
+constexpr int kNNQ = 2;
+constexpr int kNNTile = 16;
+constexpr int kNNBlock = 256;
+constexpr int kTermsBlock = 256;
+constexpr double kU = 5.9604644775390625e-08;
+
+__device__ __forceinline__ float d2f(float qx, float qy, float qz, float tx, float ty, float tz) {
+  const float dx = qx - tx, dy = qy - ty, dz = qz - tz;
+  return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+}
+
+__device__ __forceinline__ void xform32(const float* Rt, float4 p, float& x, float& y, float& z) {
+  x = fmaf(Rt[0], p.x, fmaf(Rt[1], p.y, fmaf(Rt[2], p.z, Rt[9])));
+  y = fmaf(Rt[3], p.x, fmaf(Rt[4], p.y, fmaf(Rt[5], p.z, Rt[10])));
+  z = fmaf(Rt[6], p.x, fmaf(Rt[7], p.y, fmaf(Rt[8], p.z, Rt[11])));
+}
+
+__device__ __forceinline__ uint64_t make_key(float d2, uint32_t j) {
+  return ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)j;
+}
+
+// ------------------------------------------------------------------------------- state
+// Refresh the fp32 search transform and radius bound for the current T (device side).
+__device__ void refresh_rt32(IcpState* s, const double* cs, const double* ct, double pinf,
+                             double qinf) {
+  double rowl1 = 0.0, tinf = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    const double* r = s->T + 4 * i;
+    const double tp = fma(r[2], cs[2], fma(r[1], cs[1], r[0] * cs[0])) + r[3] - ct[i];
+    for (int j = 0; j < 3; ++j) s->Rt32[3 * i + j] = (float)r[j];
+    s->Rt32[9 + i] = (float)tp;
+    rowl1 = fmax(rowl1, fabs(r[0]) + fabs(r[1]) + fabs(r[2]));
+    tinf = fmax(tinf, fabs(tp));
+  }
+  const double E = 8.0 * kU * (rowl1 * pinf + tinf + qinf);
+  const double r = sqrt(s->r2);
+  const double e = 2.0 * (3.0 * kU * (r + 1.7320508075688772 * E) * (r + 1.7320508075688772 * E) +
+                          2.0 * 1.7320508075688772 * E * r + 3.0 * E * E);
+  float hi = __double2float_ru(s->r2 + e);
+  s->r2_hi = isfinite(hi) ? hi : FLT_MAX;
+}
+
+struct FrameParams {
+  double cs[3], ct[3];
+  double pinf, qinf;
+};
+
+__global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, double T3, double T4,
+                                double T5, double T6, double T7, double T8, double T9, double T10,
+                                double T11, double r2, FrameParams f) {
+  if (threadIdx.x != 0) return;
+  const double T[12] = {T0, T1, T2, T3, T4, T5, T6, T7, T8, T9, T10, T11};
+  for (int k = 0; k < 12; ++k) s->T[k] = T[k];
+  s->T[12] = s->T[13] = s->T[14] = 0.0;
+  s->T[15] = 1.0;
+  s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
+  s->count = 0;
+  s->evals = s->iters = s->done = s->converged = 0;
+  s->r2 = r2;
+  refresh_rt32(s, f.cs, f.ct, f.pinf, f.qinf);
+}
+
+// ------------------------------------------------------------------------------- keyinit
+__global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__ src32, int64_t ns,
+                                                      const float4* __restrict__ tgt32,
+                                                      int64_t nt_shard, int64_t off,
+                                                      const IcpState* __restrict__ s,
+                                                      const int32_t* __restrict__ prev,
+                                                      int64_t* __restrict__ keys) {
+  if (s->done) return;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= ns) return;
+  float Rt[12];
+  for (int k = 0; k < 12; ++k) Rt[k] = s->Rt32[k];
+  int64_t key = kKeyNone;
+  const int64_t j = prev != nullptr ? (int64_t)prev[i] : -1;
+  if (j >= off && j < off + nt_shard) {
+    float x, y, z;
+    xform32(Rt, src32[i], x, y, z);
+    const float4 t = tgt32[j - off];
+    const float d2 = d2f(x, y, z, t.x, t.y, t.z);
+    if (d2 < s->r2_hi) key = (int64_t)make_key(d2, (uint32_t)j);
+  }
+  keys[i] = key;
+}
+
+// ------------------------------------------------------------------------------- NN scan
+__global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__ src32, int64_t ns,
+                                                      const Pt4 M3D_CONST* tgt,
+                                                      int64_t nt_pad, int64_t slice_len,
+                                                      int64_t off, const IcpState* __restrict__ s,
+                                                      int64_t* __restrict__ keys) {
+  if (s->done) return;
+  float Rt[12];
+  for (int k = 0; k < 12; ++k) Rt[k] = s->Rt32[k];
+  const float r2_hi = s->r2_hi;
+  float qx[kNNQ], qy[kNNQ], qz[kNNQ], best[kNNQ];
+  uint32_t bidx[kNNQ];
+  int64_t qi[kNNQ];
+#pragma unroll
+  for (int q = 0; q < kNNQ; ++q) {
+    const int64_t i = (int64_t)blockIdx.x * (kNNBlock * kNNQ) + q * kNNBlock + threadIdx.x;
+    qi[q] = i;
+    if (i < ns) {
+      xform32(Rt, src32[i], qx[q], qy[q], qz[q]);
+      const int64_t key = keys[i];
+      if (key == kKeyNone) {
+        best[q] = r2_hi;
+        bidx[q] = 0xFFFFFFFFu;
+      } else {
+        best[q] = __uint_as_float((uint32_t)((uint64_t)key >> 32));
+        bidx[q] = (uint32_t)key;
+      }
+    } else {
+      qx[q] = qy[q] = qz[q] = 3.0e18f;  // far query: never beats its bound
+      best[q] = 0.0f;
+      bidx[q] = 0xFFFFFFFFu;
+    }
+  }
+  uint32_t bidx0[kNNQ];
+#pragma unroll
+  for (int q = 0; q < kNNQ; ++q) bidx0[q] = bidx[q];
+  const int64_t jb = (int64_t)blockIdx.y * slice_len;
+  const int64_t je = min(nt_pad, jb + slice_len);
+  for (int64_t j0 = jb; j0 < je; j0 += kNNTile) {
+    float m[kNNQ];
+#pragma unroll
+    for (int q = 0; q < kNNQ; ++q) m[q] = best[q];
+#pragma unroll
+    for (int k = 0; k < kNNTile; ++k) {
+      const float tx = tgt[j0 + k].x, ty = tgt[j0 + k].y, tz = tgt[j0 + k].z;
+#pragma unroll
+      for (int q = 0; q < kNNQ; ++q) m[q] = fminf(m[q], d2f(qx[q], qy[q], qz[q], tx, ty, tz));
+    }
+#pragma unroll
+    for (int q = 0; q < kNNQ; ++q) {
+      if (__any(m[q] <= best[q])) {
+#pragma unroll
+        for (int k = 0; k < kNNTile; ++k) {
+          const float tx = tgt[j0 + k].x, ty = tgt[j0 + k].y, tz = tgt[j0 + k].z;
+          const float d2 = d2f(qx[q], qy[q], qz[q], tx, ty, tz);
+          const uint32_t gj = (uint32_t)(off + j0 + k);
+          if (d2 < best[q] || (d2 == best[q] && gj < bidx[q])) {
+            best[q] = d2;
+            bidx[q] = gj;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kNNQ; ++q) {
+    // every improvement changes the index (strict d² or strictly lower index on a tie)
+    if (qi[q] < ns && bidx[q] != bidx0[q]) {
+      atomicMin((unsigned long long*)&keys[qi[q]], (unsigned long long)make_key(best[q], bidx[q]));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- terms
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// est: M3D_EST_POINT_TO_PLANE → slots 0..20 JTJ (upper, row-major), 21..26 JTr, 27 Σr²
+//      M3D_EST_POINT_TO_POINT → slots 0..2 Σp_c, 3..5 Σq_c, 6..14 Σ p_c q_cᵀ (row-major)
+// both: 28 count, 29 Σd²  (c = source centre: identical on every shard)
+__global__ __launch_bounds__(kTermsBlock) void terms_kernel(
+    const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
+    const double* __restrict__ nrm64, int64_t nt_shard, int64_t off,
+    const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
+    int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
+    double* __restrict__ partials) {
+  if (s->done) return;
+  __shared__ double red[kTermSlots][kTermsBlock / kWave];
+  const int64_t i = (int64_t)blockIdx.x * kTermsBlock + threadIdx.x;
+  double acc[30];
+#pragma unroll
+  for (int k = 0; k < 30; ++k) acc[k] = 0.0;
+  if (i < ns) {
+    const int64_t key = keys[i];
+    int32_t out = -1;
+    if (key != kKeyNone) {
+      const int64_t gj = (int64_t)(uint32_t)key;
+      if (sharded) out = (int32_t)gj;  // tentative hint; the owner decides validity
+      if (gj >= off && gj < off + nt_shard) {
+        const double* T = s->T;
+        const double* p = src64 + 3 * i;
+        const double vs[3] = {fma(T[2], p[2], fma(T[1], p[1], T[0] * p[0])) + T[3],
+                              fma(T[6], p[2], fma(T[5], p[1], T[4] * p[0])) + T[7],
+                              fma(T[10], p[2], fma(T[9], p[1], T[8] * p[0])) + T[11]};
+        const double* q = tgt64 + 3 * (gj - off);
+        const double d[3] = {vs[0] - q[0], vs[1] - q[1], vs[2] - q[2]};
+        const double d2 = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+        if (d2 < s->r2) {
+          out = (int32_t)gj;
+          acc[28] = 1.0;
+          acc[29] = d2;
+          if (est == M3D_EST_POINT_TO_PLANE) {
+            const double* n = nrm64 + 3 * (gj - off);
+            const double r = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
+            double J[6];
+            cross3(vs, n, J);
+            J[3] = n[0];
+            J[4] = n[1];
+            J[5] = n[2];
+            int k = 0;
+#pragma unroll
+            for (int a = 0; a < 6; ++a)
+#pragma unroll
+              for (int b = a; b < 6; ++b) acc[k++] = J[a] * J[b];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) acc[21 + a] = J[a] * r;
+            acc[27] = r * r;
+          } else {
+            const double pc[3] = {vs[0] - c0, vs[1] - c1, vs[2] - c2};
+            const double qc[3] = {q[0] - c0, q[1] - c1, q[2] - c2};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+              acc[a] = pc[a];
+              acc[3 + a] = qc[a];
+#pragma unroll
+              for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] = pc[a] * qc[b];
+            }
+          }
+        } else if (!sharded) {
+          out = -1;
+        }
+      }
+    }
+    if (corr != nullptr && (!sharded || out >= 0 || key == kKeyNone)) corr[i] = out;
+  }
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < 30; ++k) {
+    const double v = wave_sum(acc[k]);
+    if (lane == 0) red[k][wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kTermSlots) {
+    double v = 0.0;
+    if (threadIdx.x < 30)
+      for (int w = 0; w < kTermsBlock / kWave; ++w) v += red[threadIdx.x][w];
+    partials[(int64_t)blockIdx.x * kTermSlots + threadIdx.x] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------- reduce
+__global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ partials,
+                                                     int64_t nblocks, double* __restrict__ sums,
+                                                     const IcpState* __restrict__ s) {
+  if (s != nullptr && s->done) return;
+  __shared__ double red[8][kTermSlots];
+  const int slot = threadIdx.x & (kTermSlots - 1);
+  const int g = threadIdx.x / kTermSlots;
+  double v = 0.0;
+  for (int64_t b = g; b < nblocks; b += 8) v += partials[b * kTermSlots + slot];
+  red[g][slot] = v;
+  __syncthreads();
+  if (threadIdx.x < kTermSlots) {
+    double t = 0.0;
+    for (int k = 0; k < 8; ++k) t += red[k][threadIdx.x];
+    sums[threadIdx.x] = t;
+  }
+}
+
+// ------------------------------------------------------------------------------- solve
+struct SolveParams {
+  double rel_fit, rel_rmse;
+  int max_iter, est;
+  int64_t ns;
+  double c[3];  // centre used by point-to-point sums
+  FrameParams f;
+};
+
+__global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
+                             SolveParams sp) {
+  if (threadIdx.x != 0 || s->done) return;
+  const double count = sums[28];
+  const double fit = count > 0.0 ? count / (double)sp.ns : 0.0;
+  const double rmse = count > 0.0 ? sqrt(sums[29] / count) : 0.0;
+  bool stop = false;
+  if (s->evals > 0 && fabs(s->prev_fitness - fit) < sp.rel_fit &&
+      fabs(s->prev_rmse - rmse) < sp.rel_rmse) {
+    s->converged = 1;
+    stop = true;
+  } else if (s->iters >= sp.max_iter) {
+    stop = true;
+  }
+  s->fitness = fit;
+  s->rmse = rmse;
+  s->count = (int64_t)count;
+  s->prev_fitness = fit;
+  s->prev_rmse = rmse;
+  s->evals += 1;
+  if (stop) {
+    s->done = 1;
+    return;
+  }
+  double upd[16];
+  for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  if (count > 0.0) {
+    if (sp.est == M3D_EST_POINT_TO_PLANE) {
+      double A[36], b[6], x[6];
+      int k = 0;
+      for (int a = 0; a < 6; ++a)
+        for (int c = a; c < 6; ++c) {
+          A[a * 6 + c] = sums[k];
+          A[c * 6 + a] = sums[k];
+          ++k;
+        }
+      for (int a = 0; a < 6; ++a) b[a] = -sums[21 + a];
+      ldlt6_solve(A, b, x);
+      vec6_to_matrix(x, upd);
+    } else {
+      const double n = count;
+      double mp[3], mq[3], Hm[9], R[9];
+      for (int a = 0; a < 3; ++a) {
+        mp[a] = sums[a] / n;
+        mq[a] = sums[3 + a] / n;
+      }
+      for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) Hm[3 * a + c] = sums[6 + 3 * a + c] / n - mp[a] * mq[c];
+      rotation_from_cov(Hm, R);
+      for (int a = 0; a < 3; ++a) {
+        const double mpw[3] = {mp[0] + sp.c[0], mp[1] + sp.c[1], mp[2] + sp.c[2]};
+        for (int c = 0; c < 3; ++c) upd[4 * a + c] = R[3 * a + c];
+        upd[4 * a + 3] = (mq[a] + sp.c[a]) - (R[3 * a] * mpw[0] + R[3 * a + 1] * mpw[1] + R[3 * a + 2] * mpw[2]);
+      }
+    }
+  }
+  bool finite = true;
+  for (int k = 0; k < 16; ++k) finite = finite && isfinite(upd[k]);
+  if (!finite)
+    for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  matmul4(upd, s->T, s->T);
+  s->iters += 1;
+  refresh_rt32(s, sp.f.cs, sp.f.ct, sp.f.pinf, sp.f.qinf);
+}
+
+// finalize standalone NN (m3d_nn1): exact radius test in fp64
+__global__ __launch_bounds__(256) void nn_finalize_kernel(const double* __restrict__ src64,
+                                                          int64_t ns,
+                                                          const double* __restrict__ tgt64,
+                                                          const IcpState* __restrict__ s,
+                                                          const int64_t* __restrict__ keys,
+                                                          int32_t* __restrict__ idx,
+                                                          double* __restrict__ d2out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= ns) return;
+  const int64_t key = keys[i];
+  int32_t o = -1;
+  double dd = INFINITY;
+  if (key != kKeyNone) {
+    const int64_t j = (int64_t)(uint32_t)key;
+    const double* T = s->T;
+    const double* p = src64 + 3 * i;
+    const double* q = tgt64 + 3 * j;
+    const double dx = fma(T[2], p[2], fma(T[1], p[1], T[0] * p[0])) + T[3] - q[0];
+    const double dy = fma(T[6], p[2], fma(T[5], p[1], T[4] * p[0])) + T[7] - q[1];
+    const double dz = fma(T[10], p[2], fma(T[9], p[1], T[8] * p[0])) + T[11] - q[2];
+    const double d2 = (dx * dx + dy * dy) + dz * dz;
+    if (d2 < s->r2) {
+      o = (int32_t)j;
+      dd = d2;
+    }
+  }
+  idx[i] = o;
+  if (d2out != nullptr) d2out[i] = dd;
+}
+
+__global__ void keys_to_idx_kernel(const int64_t* __restrict__ keys, int64_t n,
+                                   int32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) idx[i] = keys[i] == kKeyNone ? -1 : (int32_t)(uint32_t)keys[i];
+}
+
+// ------------------------------------------------------------------------------- launchers
+static FrameParams frame_of(const m3d_icp* s) {
+  FrameParams f;
+  for (int k = 0; k < 3; ++k) {
+    f.cs[k] = s->src->center[k];
+    f.ct[k] = s->tgt->center[k];
+  }
+  f.pinf = s->src->rmax;
+  f.qinf = s->tgt->rmax;
+  return f;
+}
+
+hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st) {
+  icp_init_kernel<<<1, 64, 0, st>>>(s->state, T[0], T[1], T[2], T[3], T[4], T[5], T[6], T[7],
+                                    T[8], T[9], T[10], T[11], s->max_dist * s->max_dist,
+                                    frame_of(s));
+  return hipGetLastError();
+}
+
+hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t off, hipStream_t st) {
+  const int64_t ns = s->src->n;
+  if (ns == 0) return hipSuccess;
+  keyinit_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(
+      s->src->xyz32, ns, s->tgt->xyz32, s->tgt->n, off, s->state, s->corr, s->keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
+  const int64_t ns = s->src->n;
+  const int64_t nt_pad = s->tgt->n_pad;
+  if (ns == 0 || s->tgt->n == 0) return hipSuccess;
+  const int64_t bx = (ns + kNNBlock * kNNQ - 1) / (kNNBlock * kNNQ);
+  // fill ≥ 2048 blocks (8 per CU) by splitting the target range; keep slices ≥ 1024 targets
+  int64_t S = (2048 + bx - 1) / bx;
+  const int64_t max_s = nt_pad / 1024 > 0 ? nt_pad / 1024 : 1;
+  if (S > max_s) S = max_s;
+  if (S < 1) S = 1;
+  int64_t slice = (nt_pad + S - 1) / S;
+  slice = (slice + kNNTile - 1) / kNNTile * kNNTile;
+  S = (nt_pad + slice - 1) / slice;
+  dim3 grid((unsigned)bx, (unsigned)S);
+  nn_kernel<<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, (const Pt4 M3D_CONST*)s->tgt->xyz32,
+                                       nt_pad, slice, off, s->state, s->keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hipStream_t st) {
+  const int64_t ns = s->src->n;
+  if (ns == 0) return hipMemsetAsync(s->partials, 0, sizeof(double) * kTermSlots, st);
+  terms_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
+      s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, off, s->state, s->keys, s->corr,
+      s->params.estimation, s->src->center[0], s->src->center[1], s->src->center[2], sharded,
+      s->partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st) {
+  reduce_kernel<<<1, 256, 0, st>>>(s->partials, s->nblocks, sums, s->state);
+  return hipGetLastError();
+}
+
+hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st) {
+  SolveParams sp;
+  sp.rel_fit = s->params.relative_fitness;
+  sp.rel_rmse = s->params.relative_rmse;
+  sp.max_iter = s->params.max_iteration;
+  sp.est = s->params.estimation;
+  sp.ns = s->src->n;
+  for (int k = 0; k < 3; ++k) sp.c[k] = s->src->center[k];
+  sp.f = frame_of(s);
+  solve_kernel<<<1, 64, 0, st>>>(sums, s->state, sp);
+  return hipGetLastError();
+}
+
+hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStream_t st) {
+  const int64_t ns = s->src->n;
+  if (ns == 0) return hipSuccess;
+  nn_finalize_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(s->src->xyz64, ns,
+                                                                   s->tgt->xyz64, s->state,
+                                                                   s->keys, idx, d2);
+  return hipGetLastError();
+}
+
+hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  keys_to_idx_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(keys, n, idx);
+  return hipGetLastError();
+}
+
+int64_t terms_blocks(int64_t ns) { return ns > 0 ? (ns + kTermsBlock - 1) / kTermsBlock : 1; }
+
+}  // namespace m3d

@@ -1,0 +1,182 @@
+// m3d_internal.h — library-private types shared by the HIP translation units and the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/m3d.h"
+
+// Uniform (wave-invariant) loads: a pointer in the constant address space makes the AMDGPU
+// backend emit scalar s_load / s_buffer_load, which put the data in SGPRs and broadcast it to
+// every lane for free (the hypothesis block in scoring, the target tile in the NN scan).
+#define M3D_CONST __attribute__((address_space(4)))
+
+namespace m3d {
+
+constexpr int kWave = 64;
+
+// fp32 hypothesis block for the scoring screen (64 B = one s_load_dwordx16).
+// r: rotation row-major, t: translation in the centred frames (T p + t - q evaluated as
+// R p_c + t' - q_c with p_c = p - c_src, q_c = q - c_tgt), lo/hi: guard band around thr².
+struct alignas(64) HypF32 {
+  float r[9];
+  float t[3];
+  float lo, hi;
+  float pad[2];
+};
+
+// Plain 16-B point for constant-address-space (scalar) loads; HIP's float4 has no
+// address-space-qualified copy constructor.
+struct alignas(16) Pt4 {
+  float x, y, z, w;
+};
+
+// Ambiguous (hypothesis, correspondence chunk) record of the fp32 screen.
+struct AmbRecord {
+  int32_t hyp;    // hypothesis index within the batch
+  int32_t chunk;  // wave chunk (kScoreK*64 correspondences)
+  int32_t lo;     // screen count already added for this chunk
+  int32_t pad;
+};
+
+// Running state of the a4 loop across batches (device resident).
+struct RansacState {
+  double T_best[16];
+  int64_t best_count;
+  int64_t best_index;
+  int64_t iterations;
+  int64_t rechecked;
+  int32_t done;
+  int32_t pad[3];
+};
+
+// ICP loop state (device resident), Open3D RegistrationICP semantics.
+struct IcpState {
+  double T[16];       // current transformation (world frame)
+  float Rt32[12];     // fp32 R (row-major) + t' mapping centred source to centred target
+  double fitness, rmse;
+  double prev_fitness, prev_rmse;
+  int64_t count;      // correspondences of the last evaluation
+  int32_t evals;      // evaluations done
+  int32_t iters;      // updates applied
+  int32_t done;
+  int32_t converged;
+  double r2;          // max_dist² (fp64, strict <)
+  float r2_hi;        // fp32 search bound (≥ r2 plus guard)
+  float pad;
+};
+
+constexpr int kTermSlots = 32;  // 21 JTJ + 6 JTr + r² + count + Σd² (+2 pad)
+constexpr int64_t kKeyNone = 0x7FFFFFFFFFFFFFFFll;
+
+}  // namespace m3d
+
+struct m3d_ctx {
+  int device = 0;
+  std::string err;
+  // kernel timing (m3d_profile_*): event pairs per kernel id
+  bool profiling = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
+  size_t ev_used[4] = {0, 0, 0, 0};
+  // scratch (grown on demand)
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  int64_t* stats = nullptr;  // [8] device counters
+  m3d::RansacState* rstate = nullptr;
+};
+
+struct m3d_corrset {
+  m3d_ctx* ctx = nullptr;
+  int64_t nc = 0, nc_pad = 0;
+  double* p64 = nullptr;  // nc×3 gathered source points (original frame)
+  double* q64 = nullptr;  // nc×3 gathered target points
+  float4* p32 = nullptr;  // nc_pad centred source (w = 0), pad = 0
+  float4* q32 = nullptr;  // nc_pad centred target, pad = far away
+  double cs[3] = {0, 0, 0}, ct[3] = {0, 0, 0};
+  double pmax2 = 0.0;    // max |p_c|∞ (guard-band bound)
+  double qmaxinf = 0.0;  // max |q_c|∞
+};
+
+struct m3d_cloud {
+  m3d_ctx* ctx = nullptr;
+  int64_t n = 0, n_pad = 0;
+  double* xyz64 = nullptr;  // n×3
+  double* nrm64 = nullptr;  // n×3 or null
+  float4* xyz32 = nullptr;  // n_pad centred (pad = far away)
+  double center[3] = {0, 0, 0};
+  double rmax = 0.0;  // max |x_c|∞ (guard-band bound)
+};
+
+struct m3d_icp {
+  m3d_ctx* ctx = nullptr;
+  const m3d_cloud* src = nullptr;
+  const m3d_cloud* tgt = nullptr;
+  m3d_icp_params params{};
+  double max_dist = 0.0;
+  m3d::IcpState* state = nullptr;  // device
+  int64_t* keys = nullptr;         // ns packed NN keys
+  int32_t* corr = nullptr;         // ns current correspondence (-1 none)
+  double* partials = nullptr;      // nblocks × kTermSlots
+  double* sums = nullptr;          // kTermSlots
+  int64_t nblocks = 0;
+};
+
+// error plumbing ------------------------------------------------------------------------
+int m3d_fail(m3d_ctx* ctx, int code, const std::string& msg);
+
+// kernel timing: RAII bracket recording events around one launch when profiling is on
+struct KTimer {
+  m3d_ctx* ctx;
+  int id;
+  hipStream_t st;
+  hipEvent_t end = nullptr;
+  KTimer(m3d_ctx* c, int kid, hipStream_t s);
+  ~KTimer();
+};
+#define M3D_HIP_CHECK(ctx, expr)                                                        \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return m3d_fail((ctx), M3D_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// kernel launchers (defined in the .hip translation units) ------------------------------
+namespace m3d {
+hipError_t launch_pack_corr(const double* src, const double* tgt, const int32_t* corr, int64_t nc,
+                            const double* p_src, const double* p_tgt, double* p64, double* q64,
+                            hipStream_t st);
+hipError_t launch_sum3(const double* a, int64_t n, double* partial /*[blocks*3]*/, int blocks,
+                       hipStream_t st);
+hipError_t launch_center_pack(const double* a, int64_t n, int64_t n_pad, const double c[3],
+                              float4* out, float pad_value, float* maxnorm_partial, int blocks,
+                              int maxinf, hipStream_t st);
+hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_t seed,
+                          int64_t hyp0, int64_t H, double thr_sq, double* T_out, uint8_t* status,
+                          HypF32* hypf, const int32_t* done, hipStream_t st);
+hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
+                              HypF32* hypf, hipStream_t st);
+hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
+                        AmbRecord* amb, int32_t* amb_count, int32_t amb_cap, int32_t* full_flag,
+                        int32_t* full_list, int32_t* full_count, const int32_t* done,
+                        hipStream_t st);
+hipError_t launch_recheck(const m3d_corrset* cs, const double* T, int64_t H, double thr, int mode,
+                          int32_t* counts, const AmbRecord* amb, const int32_t* amb_count,
+                          int32_t amb_cap, const int32_t* full_list, const int32_t* full_count,
+                          int64_t* stats, const int32_t* done, hipStream_t st);
+hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int64_t nc,
+                         int64_t max_iter, int early_stop, double es_thr, double es_conf,
+                         const double* T_batch, RansacState* rs, hipStream_t st);
+hipError_t launch_copy_result(const RansacState* rs, int64_t nc, m3d_ransac_result* out_dev,
+                              hipStream_t st);
+
+// ICP
+hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_t st);
+hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, hipStream_t st);
+hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st);
+hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);
+hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
+}  // namespace m3d

@@ -1,0 +1,555 @@
+// ransac.hip — RANSAC hypothesis generation and inlier scoring for gfx950.
+//
+// Reference path (all CPU, numpy fp64):
+//   compute_step_transformation  src/matcher/ransac.py:104-192   → kabsch3_kernel
+//   evaluate_inlier_ratio[_fast] src/matcher/ransac.py:195-277   → score_kernel + recheck kernels
+//   step-RANSAC loop             _visualize_matcher.py:343-470   → select_kernel (batched, on device)
+//
+// Scoring design (VALU-bound, no dense contraction → no MFMA):
+//   * One lane holds kScoreK = 8 correspondences (centred fp32, 6 VGPRs each) for the whole block;
+//     a block of 4 waves covers 2048 correspondences and sweeps 64 hypotheses.
+//   * The hypothesis block (R, t', guard band: 64 B) is wave-uniform and read with scalar loads
+//     (constant address space) → its 12 floats are SGPR operands of the VALU ops.
+//   * Per (hypothesis, correspondence): 12 ops for d = R p + t' − q, 3 for d², 2 compares.  The
+//     compares are folded into wave masks (v_cmp → s_bcnt1 → s_add): counting is scalar work.
+//   * Exactness: the fp32 screen counts d² < lo (certainly inside) and d² < hi (possibly inside);
+//     lo/hi bracket thr² by a rounding-error bound proven in DESIGN.md §3.2.  Chunks where the two
+//     counts differ are re-evaluated in fp64 with numpy's operation order (recheck kernels), so the
+//     final counts equal an fp64 evaluation of the reference formula.
+//   * Counts are integers: atomics are exact and order-independent → deterministic results.
+#include <float.h>
+
+#include "linalg.h"
+#include "m3d_internal.h"
+
+namespace m3d {
+
+constexpr int kScoreK = 8;
+constexpr int kScoreBlock = 256;
+constexpr int kScoreHyps = 64;
+constexpr int kChunk = kScoreK * kWave;  // 512 correspondences per wave
+constexpr int kBlockCorr = kChunk * 4;   // 2048 per block
+constexpr double kU32 = 5.9604644775390625e-08;  // 2^-24
+
+// ------------------------------------------------------------------------------- packing
+__global__ void pack_corr_kernel(const double* __restrict__ src, const double* __restrict__ tgt,
+                                 const int32_t* __restrict__ corr, int64_t nc,
+                                 const double* __restrict__ p_src, const double* __restrict__ p_tgt,
+                                 double* __restrict__ p64, double* __restrict__ q64) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc) return;
+  const double* a;
+  const double* b;
+  if (corr != nullptr) {
+    a = src + 3 * (int64_t)corr[2 * i];
+    b = tgt + 3 * (int64_t)corr[2 * i + 1];
+  } else {
+    a = p_src + 3 * i;
+    b = p_tgt + 3 * i;
+  }
+  for (int k = 0; k < 3; ++k) {
+    p64[3 * i + k] = a[k];
+    q64[3 * i + k] = b[k];
+  }
+}
+
+// deterministic per-block partial sums of an n×3 f64 array (fixed grid, fixed tree)
+__global__ __launch_bounds__(256) void sum3_kernel(const double* __restrict__ a, int64_t n,
+                                                   double* __restrict__ partial) {
+  __shared__ double s[3][256];
+  double acc[3] = {0.0, 0.0, 0.0};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    for (int k = 0; k < 3; ++k) acc[k] += a[3 * i + k];
+  for (int k = 0; k < 3; ++k) s[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int k = 0; k < 3; ++k) s[k][threadIdx.x] += s[k][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 3; ++k) partial[3 * blockIdx.x + k] = s[k][0];
+}
+
+// centre + convert to padded float4; per-block max of ‖x_c‖₂ (or |x_c|∞)
+__global__ __launch_bounds__(256) void center_pack_kernel(const double* __restrict__ a, int64_t n,
+                                                          int64_t n_pad, double c0, double c1,
+                                                          double c2, float4* __restrict__ out,
+                                                          float pad_value,
+                                                          float* __restrict__ maxpart, int maxinf) {
+  __shared__ float s[256];
+  float m = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad;
+       i += (int64_t)gridDim.x * 256) {
+    float4 v;
+    if (i < n) {
+      double x = a[3 * i] - c0, y = a[3 * i + 1] - c1, z = a[3 * i + 2] - c2;
+      v = make_float4((float)x, (float)y, (float)z, 0.0f);
+      double mm = maxinf ? fmax(fabs(x), fmax(fabs(y), fabs(z))) : sqrt(x * x + y * y + z * z);
+      m = fmaxf(m, (float)mm * (1.0f + 1e-6f));
+    } else {
+      v = make_float4(pad_value, pad_value, pad_value, 0.0f);
+    }
+    out[i] = v;
+  }
+  s[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s[threadIdx.x] = fmaxf(s[threadIdx.x], s[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) maxpart[blockIdx.x] = s[0];
+}
+
+// ------------------------------------------------------------------------------- sampler
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Counter-based sampler; oracle/ransac_oracle.py::native_triples restates it bit for bit.
+__device__ void native_triple(uint64_t seed, int64_t h, int64_t nc, int out[3]) {
+  const uint64_t base = splitmix64(seed ^ ((uint64_t)h * 0x9E3779B97F4A7C15ull));
+  int got = 0;
+  for (uint64_t k = 0; got < 3 && k < (1u << 20); ++k) {
+    const uint64_t v = splitmix64(base + k);
+    const int idx = (int)(((v >> 32) * (uint64_t)nc) >> 32);
+    bool dup = false;
+    for (int j = 0; j < got; ++j) dup |= (out[j] == idx);
+    if (!dup) out[got++] = idx;
+  }
+  for (; got < 3; ++got) out[got] = got;  // unreachable for nc >= 3
+}
+
+// ------------------------------------------------------------------------------- Kabsch
+struct GuardParams {
+  double cs[3], ct[3];
+  double pinf;  // max |p_c|∞
+  double qinf;  // max |q_c|∞
+  double thr_sq;
+};
+
+// fp32 screen block for transform T (row-major 4×4, world frame) with a proven guard band.
+__device__ HypF32 make_hypf(const double* T, const GuardParams& g) {
+  HypF32 hp;
+  double tp[3], rowl1 = 0.0, tinf = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    const double* r = T + 4 * i;
+    tp[i] = fma(r[2], g.cs[2], fma(r[1], g.cs[1], r[0] * g.cs[0])) + r[3] - g.ct[i];
+    for (int j = 0; j < 3; ++j) hp.r[3 * i + j] = (float)r[j];
+    hp.t[i] = (float)tp[i];
+    rowl1 = fmax(rowl1, fabs(r[0]) + fabs(r[1]) + fabs(r[2]));
+    tinf = fmax(tinf, fabs(tp[i]));
+  }
+  // Per-component error of the fp32 evaluation:  E ≤ 8u(‖r‖₁|p|∞ + |t'| + |q|∞)
+  const double E = 8.0 * kU32 * (rowl1 * g.pinf + tinf + g.qinf);
+  const double thr = sqrt(g.thr_sq);
+  double eps = 3.0 * kU32 * (thr + 1.7320508075688772 * E) * (thr + 1.7320508075688772 * E) +
+               2.0 * 1.7320508075688772 * E * thr + 3.0 * E * E;
+  eps = 2.0 * eps + 4.0 * DBL_EPSILON * g.thr_sq;
+  double lo = g.thr_sq - eps, hi = g.thr_sq + eps;
+  if (!(lo > 0.0)) lo = 0.0;
+  hp.lo = __double2float_rd(lo);
+  hp.hi = __double2float_ru(hi);
+  if (!isfinite(hp.hi)) hp.hi = FLT_MAX;
+  hp.pad[0] = hp.pad[1] = 0.0f;
+  return hp;
+}
+
+__global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__ p64,
+                                                      const double* __restrict__ q64, int64_t nc,
+                                                      const int32_t* __restrict__ triples,
+                                                      uint64_t seed, int64_t hyp0, int64_t H,
+                                                      GuardParams g, double* __restrict__ T_out,
+                                                      uint8_t* __restrict__ status,
+                                                      HypF32* __restrict__ hypf,
+                                                      const int32_t* __restrict__ done) {
+  if (done != nullptr && *done) return;
+  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  double T[16];
+  int st = M3D_HYP_OK;
+  if (nc < 3) {  // ransac.py:139-140
+    for (int k = 0; k < 16; ++k) T[k] = (k % 5 == 0) ? 1.0 : 0.0;
+    st = M3D_HYP_DEGENERATE;
+  } else {
+    int id[3];
+    if (triples != nullptr) {
+      for (int k = 0; k < 3; ++k) {
+        int v = triples[3 * h + k];
+        id[k] = (v < 0 || v >= nc) ? 0 : v;
+      }
+    } else {
+      native_triple(seed, hyp0 + h, nc, id);
+    }
+    double ps[3][3], qs[3][3];
+    for (int k = 0; k < 3; ++k)
+      for (int c = 0; c < 3; ++c) {
+        ps[k][c] = p64[3 * (int64_t)id[k] + c];
+        qs[k][c] = q64[3 * (int64_t)id[k] + c];
+      }
+    st = kabsch3(ps, qs, T) ? M3D_HYP_NONFINITE : M3D_HYP_OK;
+  }
+  for (int k = 0; k < 16; ++k) T_out[16 * h + k] = T[k];
+  if (status != nullptr) status[h] = (uint8_t)st;
+  hypf[h] = make_hypf(T, g);
+}
+
+__global__ __launch_bounds__(256) void hypf_from_T_kernel(const double* __restrict__ T, int64_t H,
+                                                          GuardParams g,
+                                                          HypF32* __restrict__ hypf) {
+  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h < H) hypf[h] = make_hypf(T + 16 * h, g);
+}
+
+// ------------------------------------------------------------------------------- fp32 screen
+__global__ __launch_bounds__(kScoreBlock) void score_kernel(
+    const float4* __restrict__ p32, const float4* __restrict__ q32,
+    const HypF32 M3D_CONST* hyp, int64_t H, int64_t hbase, int32_t* __restrict__ counts,
+    AmbRecord* __restrict__ amb, int32_t* __restrict__ amb_count, int32_t amb_cap,
+    int32_t* __restrict__ full_flag, int32_t* __restrict__ full_list,
+    int32_t* __restrict__ full_count, const int32_t* __restrict__ done) {
+  if (done != nullptr && *done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int64_t chunk = (int64_t)blockIdx.x * 4 + wave;
+  float px[kScoreK], py[kScoreK], pz[kScoreK], qx[kScoreK], qy[kScoreK], qz[kScoreK];
+#pragma unroll
+  for (int k = 0; k < kScoreK; ++k) {
+    const int64_t i = chunk * kChunk + k * kWave + lane;  // padded: always in range
+    const float4 a = p32[i];
+    const float4 b = q32[i];
+    px[k] = a.x; py[k] = a.y; pz[k] = a.z;
+    qx[k] = b.x; qy[k] = b.y; qz[k] = b.z;
+  }
+  const int64_t h0 = hbase + (int64_t)blockIdx.y * kScoreHyps;
+  const int nh = (int)((H - h0) < kScoreHyps ? (H - h0) : kScoreHyps);
+  int cnt = 0;
+  for (int hl = 0; hl < nh; ++hl) {
+    const HypF32 M3D_CONST* P = hyp + h0 + hl;
+    const float r0 = P->r[0], r1 = P->r[1], r2 = P->r[2];
+    const float r3 = P->r[3], r4 = P->r[4], r5 = P->r[5];
+    const float r6 = P->r[6], r7 = P->r[7], r8 = P->r[8];
+    const float t0 = P->t[0], t1 = P->t[1], t2 = P->t[2];
+    const float lo_t = P->lo, hi_t = P->hi;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < kScoreK; ++k) {
+      const float dx = fmaf(r0, px[k], fmaf(r1, py[k], fmaf(r2, pz[k], t0 - qx[k])));
+      const float dy = fmaf(r3, px[k], fmaf(r4, py[k], fmaf(r5, pz[k], t1 - qy[k])));
+      const float dz = fmaf(r6, px[k], fmaf(r7, py[k], fmaf(r8, pz[k], t2 - qz[k])));
+      const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+      lo += (uint32_t)__popcll(__ballot(d2 < lo_t));
+      hi += (uint32_t)__popcll(__ballot(d2 < hi_t));
+    }
+    cnt = (lane == hl) ? (int)lo : cnt;
+    if (lo != hi && lane == 0) {
+      const int slot = atomicAdd(amb_count, 1);
+      if (slot < amb_cap) {
+        AmbRecord r;
+        r.hyp = (int32_t)(h0 + hl);
+        r.chunk = (int32_t)chunk;
+        r.lo = (int32_t)lo;
+        r.pad = 0;
+        amb[slot] = r;
+      } else if (atomicExch(&full_flag[h0 + hl], 1) == 0) {
+        full_list[atomicAdd(full_count, 1)] = (int32_t)(h0 + hl);
+      }
+    }
+  }
+  __shared__ int red[4][kWave];
+  red[wave][lane] = cnt;
+  __syncthreads();
+  if (threadIdx.x < nh) {
+    const int t = threadIdx.x;
+    atomicAdd(&counts[h0 + t], red[0][t] + red[1][t] + red[2][t] + red[3][t]);
+  }
+}
+
+// ------------------------------------------------------------------------------- fp64 recheck
+// numpy order (verified in the build container): p @ R.T is fma(r2,z,fma(r1,y,r0*x)), then + t,
+// (.)**2 summed left to right; evaluate_inlier_ratio takes sqrt of the same sum.
+__device__ __forceinline__ bool exact_inlier(const double* T, const double* p, const double* q,
+                                             double thr, int mode) {
+  const double x = fma(T[2], p[2], fma(T[1], p[1], T[0] * p[0])) + T[3];
+  const double y = fma(T[6], p[2], fma(T[5], p[1], T[4] * p[0])) + T[7];
+  const double z = fma(T[10], p[2], fma(T[9], p[1], T[8] * p[0])) + T[11];
+  const double dx = x - q[0], dy = y - q[1], dz = z - q[2];
+  const double s = (dx * dx + dy * dy) + dz * dz;
+  return mode == M3D_SCORE_SQUARED ? (s < thr) : (sqrt(s) < thr);
+}
+
+__global__ __launch_bounds__(256) void recheck_chunk_kernel(
+    const double* __restrict__ p64, const double* __restrict__ q64, int64_t nc,
+    const double* __restrict__ T, double thr, int mode, int32_t* __restrict__ counts,
+    const AmbRecord* __restrict__ amb, const int32_t* __restrict__ amb_count, int32_t amb_cap,
+    int64_t* __restrict__ stats, const int32_t* __restrict__ done) {
+  if (done != nullptr && *done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t nrec = min(*amb_count, amb_cap);
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t r = wid; r < nrec; r += nw) {
+    const AmbRecord rec = amb[r];
+    double Th[12];
+    for (int k = 0; k < 12; ++k) Th[k] = T[16 * (int64_t)rec.hyp + k];
+    int exact = 0;
+    for (int k = 0; k < kScoreK; ++k) {
+      const int64_t i = (int64_t)rec.chunk * kChunk + k * kWave + lane;
+      bool in = false;
+      if (i < nc) in = exact_inlier(Th, p64 + 3 * i, q64 + 3 * i, thr, mode);
+      exact += __popcll(__ballot(in));
+    }
+    if (lane == 0) {
+      atomicAdd(&counts[rec.hyp], exact - rec.lo);
+      atomicAdd((unsigned long long*)&stats[0], (unsigned long long)kChunk);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void recheck_full_kernel(
+    const double* __restrict__ p64, const double* __restrict__ q64, int64_t nc,
+    const double* __restrict__ T, double thr, int mode, int32_t* __restrict__ counts,
+    const int32_t* __restrict__ full_list, const int32_t* __restrict__ full_count,
+    int64_t* __restrict__ stats, const int32_t* __restrict__ done) {
+  if (done != nullptr && *done) return;
+  __shared__ int red[256];
+  const int n = *full_count;
+  for (int e = blockIdx.x; e < n; e += gridDim.x) {
+    const int h = full_list[e];
+    double Th[12];
+    for (int k = 0; k < 12; ++k) Th[k] = T[16 * (int64_t)h + k];
+    int c = 0;
+    for (int64_t i = threadIdx.x; i < nc; i += 256)
+      c += exact_inlier(Th, p64 + 3 * i, q64 + 3 * i, thr, mode) ? 1 : 0;
+    red[threadIdx.x] = c;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      counts[h] = red[0];
+      atomicAdd((unsigned long long*)&stats[1], (unsigned long long)nc);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------- a4 select
+struct BestPair {
+  int64_t c, i;
+};
+__device__ __forceinline__ BestPair combine(BestPair l, BestPair r) { return (r.c > l.c) ? r : l; }
+
+// exact cube (double-double, then one rounding) so r**3 matches a correctly rounded pow(r, 3)
+__device__ __forceinline__ double cube_rn(double r) {
+  const double r2 = r * r;
+  const double e2 = fma(r, r, -r2);
+  const double hi = r2 * r;
+  const double e3 = fma(r2, r, -hi);
+  return hi + (e3 + e2 * r);
+}
+
+__device__ __forceinline__ int64_t required_iters(double ratio, double conf, int64_t max_iter) {
+  if (ratio < 0.01) return max_iter;  // _visualize_matcher.py:367-368
+  const double v = log(1.0 - conf) / log(1.0 - cube_rn(ratio));
+  if (!(v < 9.0e18)) return INT64_MAX;
+  return (int64_t)v;  // int() truncation (v >= 0 here)
+}
+
+__global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict__ counts,
+                                                      int64_t h_begin, int64_t n, int64_t nc,
+                                                      int64_t max_iter, int early, double es_thr,
+                                                      double es_conf,
+                                                      const double* __restrict__ T_batch,
+                                                      RansacState* __restrict__ rs) {
+  __shared__ int64_t sc[1024], si[1024];
+  __shared__ int64_t stop_s[1024];
+  __shared__ int32_t done_s;
+  const int t = threadIdx.x;
+  if (t == 0) done_s = rs->done;
+  __syncthreads();
+  if (done_s) return;
+  const int64_t seg = (n + 1023) / 1024;
+  const int64_t b = (int64_t)t * seg, e = min(n, b + seg);
+  BestPair loc{-1, -1};
+  for (int64_t i = b; i < e; ++i) loc = combine(loc, BestPair{counts[i], h_begin + i});
+  sc[t] = loc.c;
+  si[t] = loc.i;
+  __syncthreads();
+  // inclusive Hillis-Steele scan of (count, index) with the first-max combine
+  for (int off = 1; off < 1024; off <<= 1) {
+    BestPair v{sc[t], si[t]};
+    if (t >= off) v = combine(BestPair{sc[t - off], si[t - off]}, v);
+    __syncthreads();
+    sc[t] = v.c;
+    si[t] = v.i;
+    __syncthreads();
+  }
+  BestPair carry{rs->best_count, rs->best_index};
+  if (t > 0) carry = combine(carry, BestPair{sc[t - 1], si[t - 1]});
+  // second pass: walk own segment with the running best, find first early-stop iteration
+  int64_t stop = INT64_MAX;
+  BestPair at_stop = carry;
+  BestPair cur = carry;
+  if (early) {
+    for (int64_t i = b; i < e; ++i) {
+      cur = combine(cur, BestPair{counts[i], h_begin + i});
+      const double fit = (double)cur.c / (double)nc;
+      if (fit > es_thr) {
+        const int64_t it = h_begin + i + 1;
+        if (it >= required_iters(fit, es_conf, max_iter)) {
+          stop = i;
+          at_stop = cur;
+          break;
+        }
+      }
+    }
+  }
+  stop_s[t] = stop;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if (t < w) stop_s[t] = min(stop_s[t], stop_s[t + w]);
+    __syncthreads();
+  }
+  const int64_t first_stop = stop_s[0];
+  BestPair fin;
+  bool writer;
+  if (first_stop != INT64_MAX) {
+    writer = (stop == first_stop);
+    fin = at_stop;
+  } else {
+    writer = (t == 1023);
+    fin = combine(BestPair{rs->best_count, rs->best_index}, BestPair{sc[1023], si[1023]});
+  }
+  __syncthreads();
+  if (writer) {
+    if (fin.i != rs->best_index && fin.i >= h_begin) {
+      for (int k = 0; k < 16; ++k) rs->T_best[k] = T_batch[16 * (fin.i - h_begin) + k];
+    }
+    rs->best_count = fin.c;
+    rs->best_index = fin.i;
+    if (first_stop != INT64_MAX) {
+      rs->iterations = h_begin + first_stop + 1;
+      rs->done = 1;
+    } else {
+      rs->iterations = h_begin + n;
+      if (rs->iterations >= max_iter) rs->done = 1;
+    }
+  }
+}
+
+__global__ void copy_result_kernel(const RansacState* __restrict__ rs, int64_t nc,
+                                   m3d_ransac_result* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  for (int k = 0; k < 16; ++k) out->T[k] = rs->T_best[k];
+  out->best_count = rs->best_count;
+  out->best_index = rs->best_index;
+  out->iterations = rs->iterations;
+  out->fitness = nc > 0 ? (double)rs->best_count / (double)nc : 0.0;
+  out->rechecked = rs->rechecked;
+}
+
+// ------------------------------------------------------------------------------- launchers
+static inline int blocks_for(int64_t n, int t) { return (int)((n + t - 1) / t); }
+
+hipError_t launch_pack_corr(const double* src, const double* tgt, const int32_t* corr, int64_t nc,
+                            const double* p_src, const double* p_tgt, double* p64, double* q64,
+                            hipStream_t st) {
+  if (nc == 0) return hipSuccess;
+  pack_corr_kernel<<<blocks_for(nc, 256), 256, 0, st>>>(src, tgt, corr, nc, p_src, p_tgt, p64, q64);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum3(const double* a, int64_t n, double* partial, int blocks, hipStream_t st) {
+  sum3_kernel<<<blocks, 256, 0, st>>>(a, n, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_center_pack(const double* a, int64_t n, int64_t n_pad, const double c[3],
+                              float4* out, float pad_value, float* maxnorm_partial, int blocks,
+                              int maxinf, hipStream_t st) {
+  center_pack_kernel<<<blocks, 256, 0, st>>>(a, n, n_pad, c[0], c[1], c[2], out, pad_value,
+                                             maxnorm_partial, maxinf);
+  return hipGetLastError();
+}
+
+static GuardParams guard_of(const m3d_corrset* cs, double thr_sq) {
+  GuardParams g;
+  for (int k = 0; k < 3; ++k) {
+    g.cs[k] = cs->cs[k];
+    g.ct[k] = cs->ct[k];
+  }
+  g.pinf = cs->pmax2;
+  g.qinf = cs->qmaxinf;
+  g.thr_sq = thr_sq;
+  return g;
+}
+
+hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_t seed,
+                          int64_t hyp0, int64_t H, double thr_sq, double* T_out, uint8_t* status,
+                          HypF32* hypf, const int32_t* done, hipStream_t st) {
+  if (H == 0) return hipSuccess;
+  kabsch3_kernel<<<blocks_for(H, 256), 256, 0, st>>>(cs->p64, cs->q64, cs->nc, triples, seed,
+                                                     hyp0, H, guard_of(cs, thr_sq), T_out, status,
+                                                     hypf, done);
+  return hipGetLastError();
+}
+
+hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
+                              HypF32* hypf, hipStream_t st) {
+  if (H == 0) return hipSuccess;
+  hypf_from_T_kernel<<<blocks_for(H, 256), 256, 0, st>>>(T, H, guard_of(cs, thr_sq), hypf);
+  return hipGetLastError();
+}
+
+hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
+                        AmbRecord* amb, int32_t* amb_count, int32_t amb_cap, int32_t* full_flag,
+                        int32_t* full_list, int32_t* full_count, const int32_t* done,
+                        hipStream_t st) {
+  if (H == 0 || cs->nc == 0) return hipSuccess;
+  const int64_t per_launch = (int64_t)65535 * kScoreHyps;  // grid.y limit
+  for (int64_t hb = 0; hb < H; hb += per_launch) {
+    const int64_t nh = (H - hb) < per_launch ? (H - hb) : per_launch;
+    dim3 grid((unsigned)(cs->nc_pad / kBlockCorr), (unsigned)((nh + kScoreHyps - 1) / kScoreHyps));
+    score_kernel<<<grid, kScoreBlock, 0, st>>>(cs->p32, cs->q32, (const HypF32 M3D_CONST*)hypf, H,
+                                               hb, counts, amb, amb_count, amb_cap, full_flag,
+                                               full_list, full_count, done);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_recheck(const m3d_corrset* cs, const double* T, int64_t H, double thr, int mode,
+                          int32_t* counts, const AmbRecord* amb, const int32_t* amb_count,
+                          int32_t amb_cap, const int32_t* full_list, const int32_t* full_count,
+                          int64_t* stats, const int32_t* done, hipStream_t st) {
+  if (H == 0 || cs->nc == 0) return hipSuccess;
+  recheck_chunk_kernel<<<1024, 256, 0, st>>>(cs->p64, cs->q64, cs->nc, T, thr, mode, counts, amb,
+                                             amb_count, amb_cap, stats, done);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  recheck_full_kernel<<<256, 256, 0, st>>>(cs->p64, cs->q64, cs->nc, T, thr, mode, counts,
+                                           full_list, full_count, stats, done);
+  return hipGetLastError();
+}
+
+hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int64_t nc,
+                         int64_t max_iter, int early_stop, double es_thr, double es_conf,
+                         const double* T_batch, RansacState* rs, hipStream_t st) {
+  select_kernel<<<1, 1024, 0, st>>>(counts, h_begin, n, nc, max_iter, early_stop, es_thr, es_conf,
+                                    T_batch, rs);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_result(const RansacState* rs, int64_t nc, m3d_ransac_result* out_dev,
+                              hipStream_t st) {
+  copy_result_kernel<<<1, 64, 0, st>>>(rs, nc, out_dev);
+  return hipGetLastError();
+}
+
+}  // namespace m3d

@@ -1,0 +1,128 @@
+"""ctypes binding of libm3d.so (include/m3d.h).
+
+The library is built in-tree (``make -C 3d-matching_amd/csrc`` or ``__graft_entry__.build()``)
+and loaded from this directory.  There is no fallback: if the shared object or a gfx950 device
+is missing, the product path raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "libm3d.so"
+
+M3D_OK = 0
+M3D_ERR_INVALID = -1
+M3D_ERR_HIP = -2
+M3D_ERR_OOM = -3
+M3D_ERR_NODEVICE = -4
+
+HYP_OK, HYP_DEGENERATE, HYP_NONFINITE = 0, 1, 2
+SCORE_SQUARED, SCORE_NORM = 0, 1
+EST_POINT_TO_POINT, EST_POINT_TO_PLANE = 0, 1
+KERNEL_NN, KERNEL_SCORE, KERNEL_KABSCH, KERNEL_TERMS = 0, 1, 2, 3
+
+vp = C.c_void_p
+i64 = C.c_int64
+u64 = C.c_uint64
+i32 = C.c_int32
+dbl = C.c_double
+
+
+class RansacParams(C.Structure):
+    _fields_ = [("max_iter", i64), ("seed", u64), ("thr", dbl), ("mode", i32),
+                ("early_stop", i32), ("es_threshold", dbl), ("es_confidence", dbl),
+                ("batch", i64), ("hyp0", i64)]
+
+
+class RansacResult(C.Structure):
+    _fields_ = [("T", dbl * 16), ("fitness", dbl), ("best_index", i64), ("iterations", i64),
+                ("best_count", i64), ("rechecked", i64)]
+
+
+class IcpParams(C.Structure):
+    _fields_ = [("relative_fitness", dbl), ("relative_rmse", dbl), ("max_iteration", i32),
+                ("estimation", i32)]
+
+
+class IcpResult(C.Structure):
+    _fields_ = [("T", dbl * 16), ("fitness", dbl), ("inlier_rmse", dbl),
+                ("num_correspondences", i64), ("iterations", i32), ("converged", i32)]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "m3d_abi_version": (C.c_int, []),
+    "m3d_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "m3d_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+    "m3d_destroy": (None, [vp]),
+    "m3d_last_error": (C.c_char_p, [vp]),
+    "m3d_get_stats": (C.c_int, [vp, C.POINTER(i64)]),
+    "m3d_profile_enable": (C.c_int, [vp, C.c_int]),
+    "m3d_profile_read": (C.c_int, [vp, C.c_int, C.POINTER(dbl), C.POINTER(i64)]),
+    "m3d_corrset_create": (C.c_int, [vp, vp, i64, vp, i64, vp, i64, vp, C.POINTER(vp)]),
+    "m3d_corrset_create_gathered": (C.c_int, [vp, vp, vp, i64, vp, C.POINTER(vp)]),
+    "m3d_corrset_destroy": (None, [vp]),
+    "m3d_corrset_size": (i64, [vp]),
+    "m3d_kabsch3_batch": (C.c_int, [vp, vp, vp, u64, i64, i64, vp, vp, vp]),
+    "m3d_ransac_score": (C.c_int, [vp, vp, vp, i64, dbl, C.c_int, vp, vp]),
+    "m3d_ransac_run": (C.c_int, [vp, vp, C.POINTER(RansacParams), vp, C.POINTER(RansacResult), vp]),
+    "m3d_ransac_run_async": (C.c_int, [vp, vp, C.POINTER(RansacParams), vp, vp, vp, vp]),
+    "m3d_replay_triples": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(i32), i64, i64,
+                                     C.POINTER(i32)]),
+    "m3d_cloud_create": (C.c_int, [vp, vp, vp, i64, vp, C.POINTER(vp)]),
+    "m3d_cloud_destroy": (None, [vp]),
+    "m3d_cloud_size": (i64, [vp]),
+    "m3d_nn1": (C.c_int, [vp, vp, vp, C.POINTER(dbl), dbl, vp, vp, vp]),
+    "m3d_icp_run": (C.c_int, [vp, vp, vp, C.POINTER(dbl), dbl, C.POINTER(IcpParams),
+                              C.POINTER(IcpResult), vp, vp]),
+    "m3d_icp_create": (C.c_int, [vp, vp, vp, dbl, C.POINTER(IcpParams), C.POINTER(vp)]),
+    "m3d_icp_destroy": (None, [vp]),
+    "m3d_icp_reset": (C.c_int, [vp, C.POINTER(dbl), vp]),
+    "m3d_icp_step": (C.c_int, [vp, vp]),
+    "m3d_icp_shard_nn": (C.c_int, [vp, i64, vp, vp]),
+    "m3d_icp_shard_terms": (C.c_int, [vp, i64, vp, vp, vp]),
+    "m3d_icp_solve": (C.c_int, [vp, vp, vp]),
+    "m3d_icp_result_get": (C.c_int, [vp, C.POINTER(IcpResult), vp]),
+    "m3d_icp_corr": (vp, [vp]),
+    "m3d_icp_copy_corr": (C.c_int, [vp, vp, vp]),
+    "m3d_debug_kabsch3_host": (C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
+    "m3d_debug_ldlt6_host": (C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
+}
+
+_lib = None
+
+
+class M3DError(RuntimeError):
+    pass
+
+
+def load() -> C.CDLL:
+    """Load libm3d.so (once).  Raises ImportError if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} not built: run `make -C {LIB_PATH.parent.parent / 'csrc'}` "
+                          "(hipcc --offload-arch=gfx950)")
+    lib = C.CDLL(os.fspath(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, ctx=None, what: str = "") -> None:
+    if rc == M3D_OK:
+        return
+    msg = ""
+    if ctx is not None:
+        raw = load().m3d_last_error(ctx)
+        msg = raw.decode() if raw else ""
+    if rc == M3D_ERR_INVALID:
+        raise ValueError(f"{what}: {msg}" if msg else what)
+    raise M3DError(f"{what} failed (code {rc}): {msg}")

@@ -1,0 +1,346 @@
+"""Python host layer over libm3d.so: contexts, device buffers, packed objects, batched calls.
+
+PyTorch-ROCm is used only for device memory and streams (tensors' ``data_ptr()`` are passed
+through the C ABI); every numerical step of the hot path runs in the HIP kernels.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+_tls = threading.local()
+
+
+def _torch():
+    import torch  # deferred: importing torch takes seconds on a cold image
+
+    return torch
+
+
+def require_device():
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise RuntimeError("m3d needs a gfx950 (MI355X) GPU; torch.cuda is not available")
+    return torch
+
+
+class Context:
+    """One m3d context per (host thread, device)."""
+
+    def __init__(self, device: int = 0):
+        lib = _lib.load()
+        require_device()
+        self.device = device
+        h = C.c_void_p()
+        rc = lib.m3d_create(device, C.byref(h))
+        if rc == _lib.M3D_ERR_NODEVICE:
+            raise RuntimeError(f"device {device} is not a gfx950 (MI355X) GPU")
+        check(rc, None, "m3d_create")
+        self.h = h
+        self.lib = lib
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.lib.m3d_destroy(h)
+            self.h = None
+
+    def check(self, rc, what):
+        check(rc, self.h, what)
+
+    def profile(self, enable: bool = True):
+        """Record HIP events around every launch of the timed kernels (m3d_profile_enable)."""
+        self.check(self.lib.m3d_profile_enable(self.h, int(enable)), "m3d_profile_enable")
+
+    def profile_read(self, kernel: int):
+        """(total_ms, launches) of `kernel` since the last read (synchronises)."""
+        ms = C.c_double()
+        n = C.c_int64()
+        self.check(self.lib.m3d_profile_read(self.h, int(kernel), C.byref(ms), C.byref(n)),
+                   "m3d_profile_read")
+        return ms.value, n.value
+
+    def stats(self) -> np.ndarray:
+        out = (C.c_int64 * 8)()
+        self.check(self.lib.m3d_get_stats(self.h, out), "m3d_get_stats")
+        return np.array(out[:], dtype=np.int64)
+
+
+def context(device: int | None = None) -> Context:
+    torch = require_device()
+    dev = torch.cuda.current_device() if device is None else int(device)
+    cache = getattr(_tls, "ctx", None)
+    if cache is None:
+        cache = _tls.ctx = {}
+    if dev not in cache:
+        cache[dev] = Context(dev)
+    return cache[dev]
+
+
+def stream_handle():
+    torch = _torch()
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t) -> C.c_void_p:
+    return C.c_void_p(0 if t is None else t.data_ptr())
+
+
+def to_device(a, dtype="float64", shape_tail=(3,), device=None):
+    """numpy / torch / sequence → contiguous torch tensor on the GPU (no copy if already there)."""
+    torch = require_device()
+    tdt = {"float64": torch.float64, "int32": torch.int32, "int64": torch.int64}[dtype]
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    if isinstance(a, torch.Tensor):
+        t = a.to(device=dev, dtype=tdt)
+    else:
+        arr = np.ascontiguousarray(np.asarray(a), dtype=np.dtype(dtype))
+        t = torch.from_numpy(arr).to(dev)
+    if shape_tail is not None:
+        t = t.reshape(-1, *shape_tail)
+    return t.contiguous()
+
+
+# --------------------------------------------------------------------------------- RANSAC
+class CorrSet:
+    """Packed correspondence set on the device (gathered fp64 pairs + centred fp32 SoA)."""
+
+    def __init__(self, src_points=None, tgt_points=None, corr=None, *, p_src=None, p_tgt=None,
+                 ctx: Context | None = None):
+        self.ctx = ctx or context()
+        lib = self.ctx.lib
+        h = C.c_void_p()
+        st = stream_handle()
+        if p_src is not None:
+            ps = to_device(p_src)
+            pt = to_device(p_tgt)
+            if ps.shape != pt.shape:
+                raise ValueError("p_src and p_tgt must have the same shape")
+            self.nc = ps.shape[0]
+            self._keep = (ps, pt)
+            self.ctx.check(lib.m3d_corrset_create_gathered(self.ctx.h, ptr(ps), ptr(pt), self.nc, st,
+                                                           C.byref(h)), "corrset_create_gathered")
+        else:
+            s = to_device(src_points)
+            t = to_device(tgt_points)
+            c = to_device(corr, "int32", (2,))
+            self.nc = c.shape[0]
+            self._keep = (s, t, c)
+            self.ctx.check(lib.m3d_corrset_create(self.ctx.h, ptr(s), s.shape[0], ptr(t), t.shape[0],
+                                                  ptr(c), self.nc, st, C.byref(h)), "corrset_create")
+        self.h = h
+        self._keep = None  # the corrset holds its own gathered copy
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.ctx.lib.m3d_corrset_destroy(h)
+            self.h = None
+
+    def kabsch3(self, H: int, triples=None, seed: int = 0, hyp0: int = 0):
+        """Batched a1: returns (T (H,4,4) torch f64 cuda, status (H,) uint8)."""
+        torch = _torch()
+        T = torch.empty((H, 4, 4), dtype=torch.float64, device="cuda")
+        status = torch.empty((H,), dtype=torch.uint8, device="cuda")
+        tri = None if triples is None else to_device(triples, "int32", (3,))
+        self.ctx.check(self.ctx.lib.m3d_kabsch3_batch(self.ctx.h, self.h, ptr(tri), seed, hyp0, H,
+                                                      ptr(T), ptr(status), stream_handle()),
+                       "kabsch3_batch")
+        return T, status
+
+    def score(self, T, thr: float, mode: int = _lib.SCORE_SQUARED):
+        """Batched a2/a3: inlier counts (H,) int32 for transforms T (H,4,4)."""
+        torch = _torch()
+        Td = to_device(T, "float64", (4, 4))
+        H = Td.shape[0]
+        counts = torch.empty((H,), dtype=torch.int32, device="cuda")
+        self.ctx.check(self.ctx.lib.m3d_ransac_score(self.ctx.h, self.h, ptr(Td), H, float(thr),
+                                                     int(mode), ptr(counts), stream_handle()),
+                       "ransac_score")
+        return counts
+
+    def run(self, params: "RansacParams", triples=None) -> "RansacOutcome":
+        """a4 on the device: the step-RANSAC loop with best tracking and early stop."""
+        p = params.to_c()
+        res = _lib.RansacResult()
+        tri = None if triples is None else to_device(triples, "int32", (3,))
+        self.ctx.check(self.ctx.lib.m3d_ransac_run(self.ctx.h, self.h, C.byref(p), ptr(tri),
+                                                   C.byref(res), stream_handle()), "ransac_run")
+        return RansacOutcome(np.array(res.T[:]).reshape(4, 4), res.fitness, res.best_index,
+                             res.iterations, res.best_count, self.nc)
+
+
+@dataclass
+class RansacParams:
+    max_iter: int = 10000
+    seed: int = 0
+    thr: float = 0.45 * 0.45
+    mode: int = _lib.SCORE_SQUARED
+    early_stop: bool = True
+    es_threshold: float = 0.5
+    es_confidence: float = 0.99
+    batch: int = 0
+    hyp0: int = 0
+
+    def to_c(self):
+        return _lib.RansacParams(int(self.max_iter), int(self.seed) & ((1 << 64) - 1), float(self.thr),
+                                 int(self.mode), int(bool(self.early_stop)), float(self.es_threshold),
+                                 float(self.es_confidence), int(self.batch), int(self.hyp0))
+
+
+@dataclass
+class RansacOutcome:
+    transformation: np.ndarray
+    fitness: float
+    best_index: int
+    iterations: int
+    best_count: int
+    n_correspondences: int
+
+
+def replay_triples(nc: int, H: int, state=None):
+    """Rows that H successive ``np.random.choice(nc, 3, replace=False)`` calls draw from the
+    legacy MT19937 stream (ransac.py:143).  ``state`` defaults to the global numpy RNG, which is
+    advanced exactly as the reference would advance it.  Returns (H,3) int32."""
+    lib = _lib.load()
+    use_global = state is None
+    st = np.random.get_state() if use_global else state
+    if st[0] != "MT19937":
+        raise ValueError("legacy MT19937 state required")
+    key = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
+    pos = C.c_int32(int(st[2]))
+    out = np.empty((H, 3), dtype=np.int32)
+    rc = lib.m3d_replay_triples(key.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(pos), int(nc),
+                                int(H), out.ctypes.data_as(C.POINTER(C.c_int32)))
+    check(rc, None, "replay_triples")
+    new_state = ("MT19937", key, pos.value, 0, 0.0)
+    if use_global:
+        np.random.set_state(new_state)
+    return out, new_state
+
+
+# --------------------------------------------------------------------------------- ICP
+class Cloud:
+    """Packed point cloud on the device (fp64 AoS + centred fp32 float4, optional normals)."""
+
+    def __init__(self, points, normals=None, ctx: Context | None = None):
+        self.ctx = ctx or context()
+        p = to_device(points)
+        nrm = None if normals is None else to_device(normals)
+        if nrm is not None and nrm.shape != p.shape:
+            raise ValueError("normals must match points")
+        self.n = p.shape[0]
+        h = C.c_void_p()
+        self.ctx.check(self.ctx.lib.m3d_cloud_create(self.ctx.h, ptr(p), ptr(nrm), self.n,
+                                                     stream_handle(), C.byref(h)), "cloud_create")
+        self.h = h
+        self.has_normals = nrm is not None
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.ctx.lib.m3d_cloud_destroy(h)
+            self.h = None
+
+
+def _T16(T):
+    a = np.ascontiguousarray(np.asarray(T, dtype=np.float64).reshape(16))
+    return (C.c_double * 16)(*a.tolist())
+
+
+def nn1(src: Cloud, tgt: Cloud, T, max_dist: float):
+    """Radius-bounded 1-NN of T·src in tgt → (idx int32 (-1 none), d2 f64) torch cuda."""
+    torch = _torch()
+    idx = torch.empty((src.n,), dtype=torch.int32, device="cuda")
+    d2 = torch.empty((src.n,), dtype=torch.float64, device="cuda")
+    src.ctx.check(src.ctx.lib.m3d_nn1(src.ctx.h, src.h, tgt.h, _T16(T), float(max_dist), ptr(idx),
+                                      ptr(d2), stream_handle()), "nn1")
+    return idx, d2
+
+
+@dataclass
+class IcpOutcome:
+    transformation: np.ndarray
+    fitness: float
+    inlier_rmse: float
+    num_correspondences: int
+    iterations: int
+    converged: bool
+    correspondence_set: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.int32))
+
+
+def icp(src: Cloud, tgt: Cloud, max_dist: float, init=None, estimation=_lib.EST_POINT_TO_PLANE,
+        relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30, with_correspondences=True):
+    torch = _torch()
+    p = _lib.IcpParams(float(relative_fitness), float(relative_rmse), int(max_iteration), int(estimation))
+    res = _lib.IcpResult()
+    corr = torch.empty((max(src.n, 1),), dtype=torch.int32, device="cuda") if with_correspondences else None
+    init16 = _T16(np.eye(4) if init is None else init)
+    src.ctx.check(src.ctx.lib.m3d_icp_run(src.ctx.h, src.h, tgt.h, init16, float(max_dist), C.byref(p),
+                                          C.byref(res), ptr(corr), stream_handle()), "icp_run")
+    cs = np.zeros((0, 2), np.int32)
+    if with_correspondences and src.n > 0:
+        j = corr[: src.n].cpu().numpy()
+        i = np.nonzero(j >= 0)[0]
+        cs = np.stack([i, j[i]], axis=1).astype(np.int32)
+    return IcpOutcome(np.array(res.T[:]).reshape(4, 4), res.fitness, res.inlier_rmse,
+                      res.num_correspondences, res.iterations, bool(res.converged), cs)
+
+
+class IcpLoop:
+    """Step-wise device ICP (benchmarks, multi-GPU).  Every call only enqueues work."""
+
+    def __init__(self, src: Cloud, tgt: Cloud, max_dist: float, estimation=_lib.EST_POINT_TO_PLANE,
+                 relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30):
+        self.ctx = src.ctx
+        self.src, self.tgt = src, tgt
+        self.p = _lib.IcpParams(float(relative_fitness), float(relative_rmse), int(max_iteration),
+                                int(estimation))
+        h = C.c_void_p()
+        self.ctx.check(self.ctx.lib.m3d_icp_create(self.ctx.h, src.h, tgt.h, float(max_dist),
+                                                   C.byref(self.p), C.byref(h)), "icp_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            self.ctx.lib.m3d_icp_destroy(h)
+            self.h = None
+
+    def reset(self, init=None):
+        self.ctx.check(self.ctx.lib.m3d_icp_reset(self.h, _T16(np.eye(4) if init is None else init),
+                                                  stream_handle()), "icp_reset")
+
+    def step(self):
+        self.ctx.check(self.ctx.lib.m3d_icp_step(self.h, stream_handle()), "icp_step")
+
+    def shard_nn(self, offset: int, keys):
+        self.ctx.check(self.ctx.lib.m3d_icp_shard_nn(self.h, int(offset), ptr(keys), stream_handle()),
+                       "icp_shard_nn")
+
+    def shard_terms(self, offset: int, keys, sums):
+        self.ctx.check(self.ctx.lib.m3d_icp_shard_terms(self.h, int(offset), ptr(keys), ptr(sums),
+                                                        stream_handle()), "icp_shard_terms")
+
+    def solve(self, sums):
+        self.ctx.check(self.ctx.lib.m3d_icp_solve(self.h, ptr(sums), stream_handle()), "icp_solve")
+
+    def result(self) -> IcpOutcome:
+        r = _lib.IcpResult()
+        self.ctx.check(self.ctx.lib.m3d_icp_result_get(self.h, C.byref(r), stream_handle()), "icp_result")
+        return IcpOutcome(np.array(r.T[:]).reshape(4, 4), r.fitness, r.inlier_rmse,
+                          r.num_correspondences, r.iterations, bool(r.converged))
+
+    def correspondences(self):
+        """Current correspondence target per source point (int32, -1 = none), torch cuda."""
+        torch = _torch()
+        out = torch.empty((max(self.src.n, 1),), dtype=torch.int32, device="cuda")
+        self.ctx.check(self.ctx.lib.m3d_icp_copy_corr(self.h, ptr(out), stream_handle()), "icp_copy_corr")
+        return out[: self.src.n]

@@ -1,0 +1,164 @@
+"""Drop-in replacement of the reference's ``src/matcher/ransac.py`` on MI355X.
+
+Same function names, arguments, defaults, return types and soft-failure behaviour as
+KTC-Security-Circle/3d-matching ``src/matcher/ransac.py``; the arithmetic runs in libm3d.so
+(HIP, gfx950) through the C ABI of ``include/m3d.h``.
+
+* ``compute_step_transformation`` (ransac.py:104-192): draws its 3 rows from the GLOBAL legacy
+  numpy RNG exactly like the reference (``np.random.choice(n, 3, replace=False)``), so a seeded
+  program sees the same hypotheses; the Kabsch estimate runs on the device.
+* ``evaluate_inlier_ratio`` (ransac.py:195-236) and ``evaluate_inlier_ratio_fast``
+  (ransac.py:239-277): exact counts (fp32 screen + fp64 guard-band recheck on the device).
+* ``compute_feature_correspondences`` (ransac.py:62-101): FPFH feature-space NN on the device
+  plus the reference's outlier injection on the global numpy RNG.
+* ``global_registration`` (ransac.py:20-59): see ``m3d.feature_ransac``.
+
+Additions (batched, device-resident): ``ransac`` runs the whole step-RANSAC loop of
+``_visualize_matcher.py:343-470`` on the GPU; ``register`` is the coarse-to-fine façade
+``main.py:34-38`` intends.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from m3d import _lib
+from m3d import cache as _cache
+from m3d.core import CorrSet, RansacParams, replay_triples
+from m3d.types import RegistrationResult
+
+__all__ = [
+    "global_registration",
+    "compute_feature_correspondences",
+    "compute_step_transformation",
+    "evaluate_inlier_ratio",
+    "evaluate_inlier_ratio_fast",
+    "ransac",
+]
+
+
+def _down_points(x) -> np.ndarray:
+    """``src.pcd_down.points`` of a Ply-like (ransac.py:147-148), or the array itself."""
+    if hasattr(x, "pcd_down"):
+        x = x.pcd_down.points
+    elif hasattr(x, "points"):
+        x = x.points
+    return np.asarray(x, dtype=np.float64).reshape(-1, 3)
+
+
+def _corr_array(correspondences) -> np.ndarray:
+    c = np.asarray(correspondences)
+    if c.size == 0:
+        return np.zeros((0, 2), np.int32)
+    return c.reshape(-1, 2)
+
+
+def global_registration(src, tgt, voxel_size: float, iteration: int = 30) -> RegistrationResult:
+    """ransac.py:20-59: feature-matching RANSAC (mutual filter, Point-to-Point, ransac_n=3,
+    EdgeLength(0.9) + Distance(1.5·v) checkers, RANSACConvergenceCriteria(iteration, 0.999))."""
+    from m3d import feature_ransac
+
+    dist_thresh = voxel_size * 1.5
+    return feature_ransac.registration_ransac_based_on_feature_matching(
+        _down_points(src), _down_points(tgt), src.pcd_fpfh, tgt.pcd_fpfh, True, dist_thresh,
+        ransac_n=3, edge_length=0.9, distance=dist_thresh, max_iteration=iteration, confidence=0.999)
+
+
+def compute_feature_correspondences(src, tgt, mutual_filter: bool = False,
+                                    noise_ratio: float = 0.0) -> np.ndarray:
+    """ransac.py:62-101.  Returns an (N,2) int32 array (the Vector2iVector's numpy view)."""
+    from m3d import feature_ransac
+
+    corres_np = feature_ransac.correspondences_from_features(src.pcd_fpfh, tgt.pcd_fpfh, mutual_filter)
+    if noise_ratio > 0:                                         # ransac.py:89-99
+        n_original = len(corres_np)
+        n_noise = int(n_original * noise_ratio)
+        if n_noise > 0:
+            src_indices = np.random.randint(0, len(_down_points(src)), n_noise)
+            tgt_indices = np.random.randint(0, len(_down_points(tgt)), n_noise)
+            noise_corres = np.stack((src_indices, tgt_indices), axis=1)
+            corres_np = np.vstack((corres_np, noise_corres))
+            np.random.shuffle(corres_np)
+    return np.asarray(corres_np, dtype=np.int32)
+
+
+def compute_step_transformation(src, tgt, correspondences) -> RegistrationResult:
+    """ransac.py:104-192 — 3-point Kabsch with identity fallback (fitness stays 0.0)."""
+    corres_np = _corr_array(correspondences)
+    res = RegistrationResult(np.eye(4), 0.0)
+    n_corres = len(corres_np)
+    if n_corres < 3:
+        return res
+    idxs = np.random.choice(n_corres, 3, replace=False)       # same RNG stream as the reference
+    cs = _cache.corrset(_down_points(src), _down_points(tgt), corres_np)
+    T, status = cs.kabsch3(1, triples=np.asarray(idxs, np.int32).reshape(1, 3))
+    if int(status[0].item()) == _lib.HYP_OK:
+        res.transformation = T[0].cpu().numpy()
+    return res
+
+
+def evaluate_inlier_ratio(src, tgt, correspondences, transform, voxel_size) -> float:
+    """ransac.py:195-236 — fraction of pairs with ‖T p − q‖ < 1.5·voxel_size."""
+    dist_thresh = voxel_size * 1.5
+    corres = _corr_array(correspondences)
+    if len(corres) == 0:
+        return 0.0
+    cs = _cache.corrset(_down_points(src), _down_points(tgt), corres)
+    cnt = cs.score(np.asarray(transform, np.float64).reshape(1, 4, 4), dist_thresh, _lib.SCORE_NORM)
+    return np.int64(cnt[0].item()) / len(corres)
+
+
+def evaluate_inlier_ratio_fast(p_src, p_tgt, transform, dist_thresh_sq) -> float:
+    """ransac.py:239-277 — fraction of pre-gathered pairs with Σ(T p − q)² < dist_thresh_sq."""
+    p_src = np.asarray(p_src, np.float64).reshape(-1, 3)
+    if len(p_src) == 0:
+        return 0.0
+    cs = _cache.corrset_gathered(p_src, np.asarray(p_tgt, np.float64).reshape(-1, 3))
+    cnt = cs.score(np.asarray(transform, np.float64).reshape(1, 4, 4), dist_thresh_sq,
+                   _lib.SCORE_SQUARED)
+    return np.int64(cnt[0].item()) / len(p_src)
+
+
+def ransac(src, tgt, correspondences, voxel_size: float = 0.3, max_iter: int = 10000,
+           early_stop: bool = True, early_stop_threshold: float = 0.5,
+           early_stop_confidence: float = 0.99, sampler: str = "replay", seed=None,
+           score: str = "fast"):
+    """The step-RANSAC loop of _visualize_matcher.py:343-470 on the device.
+
+    sampler="replay": the rows come from the global legacy numpy RNG exactly as successive
+    ``compute_step_transformation`` calls would draw them (and the RNG is advanced by the number
+    of iterations actually run), so the result is the reference loop's result.
+    sampler="native": counter-based sampler keyed by ``seed`` (fast; no host RNG work).
+    score="fast" compares Σd² < (1.5·v)² (evaluate_inlier_ratio_fast, the GUI loop);
+    score="norm" compares ‖d‖ < 1.5·v (evaluate_inlier_ratio, benchmark_ransac.py).
+    Returns (RegistrationResult, info dict with best_index / iterations / best_count).
+    """
+    corres = _corr_array(correspondences)
+    nc = len(corres)
+    dist_thresh = voxel_size * 1.5
+    if score == "fast":
+        thr, mode = dist_thresh * dist_thresh, _lib.SCORE_SQUARED
+    elif score == "norm":
+        thr, mode = dist_thresh, _lib.SCORE_NORM
+    else:
+        raise ValueError("score must be 'fast' or 'norm'")
+    cs = _cache.corrset(_down_points(src), _down_points(tgt), corres)
+    params = RansacParams(max_iter=max_iter, thr=thr, mode=mode, early_stop=early_stop,
+                          es_threshold=early_stop_threshold, es_confidence=early_stop_confidence)
+    triples = None
+    state0 = None
+    if sampler == "replay" and nc >= 3:
+        state0 = np.random.get_state()
+        triples, _ = replay_triples(nc, max_iter, state=state0)
+    elif sampler == "native":
+        params.seed = 0 if seed is None else int(seed)
+    elif sampler != "replay":
+        raise ValueError("sampler must be 'replay' or 'native'")
+    out = cs.run(params, triples=triples)
+    if state0 is not None:
+        # advance the global RNG by exactly the iterations the loop consumed
+        _, st = replay_triples(nc, out.iterations, state=state0)
+        np.random.set_state(st)
+    res = RegistrationResult(out.transformation, out.fitness)
+    return res, dict(best_index=out.best_index, iterations=out.iterations, best_count=out.best_count,
+                     n_correspondences=nc)

@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""Benchmark: ICP iterations/s (cfg1) + RANSAC hypotheses/s (cfg2) on synthetic 100k↔100k pairs.
+
+BASELINE.json metric "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pts, 1/2/4/8 GPU".
+
+* step (the timed unit) = one full cfg1 ICP run: 100k source ↔ 100k target points per GPU,
+  50 point-to-plane iterations (convergence disabled → exactly 50 updates, 51 NN evaluations),
+  brute-force radius-bounded NN (r = 0.4·0.3), fp64 terms/solve, all device resident.
+  value = ICP iterations/s summed over ranks (each rank's 100k-target shard is one 100k×100k
+  block; N>1 shards the target over ranks with RCCL MIN on the packed NN keys and SUM on the
+  32 estimation terms per iteration → weak scaling).
+* "ransac": cfg2 — benchmark_ransac.py's loop (a1 sample + Kabsch, a2 ‖d‖ < 1.5·v scoring) at
+  Nc = 1e5, H = 1e5 hypotheses per GPU, counter sampler seed 42, no early stop; N>1 shards the
+  hypothesis ids and all-reduces MAX of the packed (count, ~id) best key.
+* roofline: dominant kernel = ICP NN scan, timed with HIP events recorded by the library on the
+  launch stream around every NN launch inside the timed region; algorithmic cost 8 flop per
+  (source, target) pair; peak = FP32 vector 157.3 TFLOP/s (no MFMA: the scan is
+  a min-reduction, not a contraction).  traffic = HBM bytes per launch from the committed
+  rocprofv3 PMC summary (profiles/), or null.
+* cpu_baseline (rank 0, N = 1): the oracle restatement (oracle/icp_oracle.py: scipy cKDTree on
+  16 threads + numpy point-to-plane) timed on a bounded sample of the same workload.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "3d-matching_amd"))
+
+VALU_FP32_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector)
+HBM_PEAK_GBS = 8000.0
+NN_FLOP_PER_PAIR = 8        # 3 sub + 1 mul + 2 FMA
+SCORE_FLOP_PER_PAIR = 27    # 9 FMA transform + 3 sub + (1 mul + 2 FMA) + 1 cmp
+CPU_THREADS = 16            # the GPU box's CPU share per GPU
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--ns", type=int, default=100_000)
+    ap.add_argument("--nt", type=int, default=100_000, help="target points per GPU")
+    ap.add_argument("--icp-iters", type=int, default=50)
+    ap.add_argument("--nc", type=int, default=100_000)
+    ap.add_argument("--hyps", type=int, default=100_000, help="RANSAC hypotheses per GPU per run")
+    ap.add_argument("--ransac-steps", type=int, default=3)
+    ap.add_argument("--no-ransac", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline leg")
+    return ap.parse_args()
+
+
+def pmc_traffic(kernel_substr: str):
+    """HBM bytes per launch from the newest committed PMC summary (profiles/pmc_*.json)."""
+    files = sorted((ROOT / "profiles").glob("pmc_*.json"))
+    for f in reversed(files):
+        try:
+            d = json.loads(f.read_text())
+        except Exception:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if kernel_substr in k and v.get("hbm_bytes_per_launch") is not None:
+                return float(v["hbm_bytes_per_launch"]), f.name
+    return None, None
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from m3d import _lib, synth
+    from m3d.core import Cloud, CorrSet, IcpLoop, RansacParams, context
+
+    ctx = context()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ------------------------------------------------------------------ cfg1: ICP
+    ns, nt, iters = args.ns, args.nt, args.icp_iters
+    r = 0.4 * 0.3
+    src, tgt_all, nrm_all, T_true = synth.icp_pair(ns, nt * world, seed=0)
+    off = rank * nt
+    src_c = Cloud(src)
+    tgt_c = Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt])
+    loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters)
+    keys = torch.empty(ns, dtype=torch.int64, device=dev)
+    sums = torch.empty(32, dtype=torch.float64, device=dev)
+
+    def icp_run():
+        loop.reset(np.eye(4))
+        for _ in range(iters + 1):
+            if world == 1:
+                loop.step()
+            else:
+                loop.shard_nn(off, keys)
+                dist.all_reduce(keys, op=dist.ReduceOp.MIN)
+                loop.shard_terms(off, keys, sums)
+                dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+                loop.solve(sums)
+
+    for _ in range(args.warmup):
+        icp_run()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_read(_lib.KERNEL_NN)
+    ctx.profile_read(_lib.KERNEL_TERMS)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        icp_run()
+    torch.cuda.synchronize()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    nn_ms, nn_n = ctx.profile_read(_lib.KERNEL_NN)
+    terms_ms, terms_n = ctx.profile_read(_lib.KERNEL_TERMS)
+    ctx.profile(False)
+    res = loop.result()
+    icp_value = world * iters * args.steps / el
+    nn_avg_ms = max_over_ranks(nn_ms / max(nn_n, 1))
+    nn_flop = NN_FLOP_PER_PAIR * ns * nt
+    achieved_tf = nn_flop / (nn_avg_ms * 1e-3) / 1e12
+    err = float(np.abs(res.transformation - T_true).max())
+
+    # ------------------------------------------------------------------ cfg2: RANSAC
+    ransac = None
+    if not args.no_ransac:
+        nc, H = args.nc, args.hyps
+        rs_src, rs_tgt, corr, _ = synth.ransac_pair(nc, seed=42)
+        cs = CorrSet(rs_src, rs_tgt, corr)
+        thr = 0.3 * 1.5
+        params = RansacParams(max_iter=H, seed=42, thr=thr, mode=_lib.SCORE_NORM, early_stop=False,
+                              hyp0=rank * H)
+
+        def ransac_run():
+            out = cs.run(params)
+            if world > 1:
+                key = torch.tensor([out.best_count * (1 << 32) + (0xFFFFFFFF - (rank * H + out.best_index))],
+                                   dtype=torch.int64, device=dev)
+                dist.all_reduce(key, op=dist.ReduceOp.MAX)
+            return out
+
+        ransac_run()
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        ctx.profile_read(_lib.KERNEL_SCORE)
+        ctx.profile_read(_lib.KERNEL_KABSCH)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.ransac_steps):
+            out = ransac_run()
+        torch.cuda.synchronize()
+        barrier()
+        rel = max_over_ranks(time.perf_counter() - t0)
+        sc_ms, sc_n = ctx.profile_read(_lib.KERNEL_SCORE)
+        kb_ms, kb_n = ctx.profile_read(_lib.KERNEL_KABSCH)
+        ctx.profile(False)
+        sc_avg = max_over_ranks(sc_ms / max(sc_n, 1))
+        hyps_per_launch = H / max(sc_n // args.ransac_steps, 1)
+        sc_tf = SCORE_FLOP_PER_PAIR * nc * hyps_per_launch / (sc_avg * 1e-3) / 1e12
+        ransac = {
+            "metric": "RANSAC hypotheses/sec (cfg2: Nc=1e5, a1+a2, no early stop)",
+            "value": world * H * args.ransac_steps / rel, "unit": "hyp/s",
+            "ms_per_run": rel / args.ransac_steps * 1e3, "hyps_per_gpu": H, "nc": nc,
+            "best_fitness": out.fitness,
+            "roofline": {"bound": "valu", "kernel": "score_kernel", "achieved": sc_tf,
+                         "peak": VALU_FP32_PEAK_TF, "unit": "TFLOP/s", "frac": sc_tf / VALU_FP32_PEAK_TF,
+                         "avg_launch_ms": sc_avg, "launches": sc_n, "flop_per_pair": SCORE_FLOP_PER_PAIR},
+            "kabsch_avg_launch_ms": kb_ms / max(kb_n, 1),
+        }
+
+    # ------------------------------------------------------------------ CPU baseline
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(src, tgt_all[:nt], nrm_all[:nt], r, args, ransac is not None)
+
+    traffic, traffic_src = pmc_traffic("nn_kernel")
+    line = {
+        "metric": "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pts, 1/2/4/8 GPU",
+        "value": icp_value,
+        "unit": "ICP iter/s (100k src x 100k tgt per GPU)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 NN screen + f64 terms/solve",
+        "data": "synthetic (m3d.synth: asymmetric closed surface, extent ~10, analytic normals)",
+        "config": {"workload": "cfg1: 100k<->100k synthetic pair, 50 point-to-plane ICP iterations, "
+                               "brute-force NN (r=0.12), 1 GPU" if world == 1 else
+                               f"cfg1 per GPU, target sharded over {world} GPUs (RCCL MIN keys + SUM terms)",
+                   "ns": ns, "nt_per_gpu": nt, "icp_iterations_per_step": iters, "max_corr": r,
+                   "parallelism": "single" if world == 1 else f"target-shard x{world}"},
+        "roofline": {"bound": "valu", "kernel": "nn_kernel", "achieved": achieved_tf,
+                     "peak": VALU_FP32_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / VALU_FP32_PEAK_TF,
+                     "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": nn_avg_ms,
+                     "launches": nn_n, "flop_per_launch": nn_flop,
+                     "terms_avg_launch_ms": terms_ms / max(terms_n, 1)},
+        "ransac": ransac,
+        "cpu_baseline": cpu,
+        "check": {"icp_fitness": res.fitness, "icp_rmse": res.inlier_rmse, "max_abs_err_vs_T_true": err},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(src, tgt, nrm, r, args, with_ransac):
+    """Oracle ('port') on the host: bounded samples of the same two workloads."""
+    import numpy as np
+    from scipy.spatial import cKDTree
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import icp_oracle as I
+    import ransac_oracle as O
+    from m3d import synth
+
+    # ICP: Open3D-semantics iterations (KD-tree built once, like RegistrationICP)
+    tree = cKDTree(tgt)
+    T = np.eye(4)
+    n_it = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_budget and n_it < 200:
+        pcd = I.transform_points(T, src)
+        d, j = tree.query(pcd, k=1, workers=CPU_THREADS)
+        ok = d * d < r * r
+        corr = np.stack([np.nonzero(ok)[0], j[ok]], axis=1)
+        T = I.point_to_plane_update(pcd, tgt, nrm, corr) @ T
+        n_it += 1
+    icp_el = time.perf_counter() - t0
+    out = {"value": n_it / icp_el, "unit": "ICP iter/s (100k src x 100k tgt)", "cores": CPU_THREADS,
+           "kind": "port",
+           "sample": f"{n_it} Open3D-semantics point-to-plane iterations on the cfg1 pair "
+                     f"(oracle/icp_oracle.py: scipy cKDTree workers={CPU_THREADS}, numpy fp64; "
+                     "KD-tree build excluded)"}
+    if with_ransac:
+        src_r, tgt_r, corr_r, _ = synth.ransac_pair(args.nc, seed=42)
+        rng = np.random.RandomState(42)
+        n_h = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_budget and n_h < 5000:
+            Th, _, _ = O.compute_step_transformation(src_r, tgt_r, corr_r, rng=rng)
+            O.evaluate_inlier_ratio(src_r, tgt_r, corr_r, Th, 0.3)
+            n_h += 1
+        rel = time.perf_counter() - t0
+        out["ransac"] = {"value": n_h / rel, "unit": "hyp/s", "cores": 1, "kind": "port",
+                         "sample": f"{n_h} hypotheses of benchmark_ransac.py's loop (a1 + a2, numpy fp64, "
+                                   f"legacy RNG permutation sampling) at Nc={args.nc}"}
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,223 @@
+/*
+ * m3d.h — C ABI of the MI355X-native point-cloud registration core (libm3d.so, gfx950).
+ *
+ * Drop-in boundary for the hot path of KTC-Security-Circle/3d-matching `src/matcher`
+ * (SURVEY.md §8(b)).  The reference has no FFI of its own: its "plugin API" is the Python
+ * functions of `src/matcher/ransac.py` and `src/matcher/icp.py`, which call numpy and the
+ * Open3D 0.19 C++ registration pipeline.  Each entry point below names the reference interface
+ * it replaces; the Python mirror (3d-matching_amd/matcher) binds them through ctypes.
+ *
+ * Conventions
+ *   - Plain C types only; no torch types.  Array arguments marked [device] are caller-owned
+ *     device allocations (e.g. torch.cuda tensors' data_ptr()); [host] are host memory.
+ *   - Point arrays are float64 AoS N×3 (24 B/pt), exactly the layout of Open3D's
+ *     Vector3dVector / numpy (N,3) the reference uses; correspondences are int32 N×2.
+ *   - 4×4 transforms are float64 row-major (numpy order).
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  Every entry point only
+ *     enqueues work on `stream` unless documented as synchronous (the *_run functions and the
+ *     object constructors return host values and synchronise the stream).
+ *   - Return value: M3D_OK (0) or a negative M3D_ERR_*; m3d_last_error(ctx) explains it.
+ *     Numerical failure of a hypothesis is NOT an error: as in the reference
+ *     (ransac.py:134-140,184-192) it yields the identity transform and a per-hypothesis status.
+ *   - One context per (host thread, device).  A context owns its scratch memory; the library
+ *     never frees caller memory.
+ */
+#ifndef M3D_H_
+#define M3D_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define M3D_ABI_VERSION 1
+
+/* return codes */
+#define M3D_OK 0
+#define M3D_ERR_INVALID (-1)  /* bad argument (sizes, null pointers, missing normals, ...) */
+#define M3D_ERR_HIP (-2)      /* HIP runtime error */
+#define M3D_ERR_OOM (-3)      /* device allocation failed */
+#define M3D_ERR_NODEVICE (-4) /* no usable gfx950 device */
+
+/* per-hypothesis status (ransac.py:134-140,184-192) */
+#define M3D_HYP_OK 0
+#define M3D_HYP_DEGENERATE 1 /* fewer than 3 correspondences -> identity */
+#define M3D_HYP_NONFINITE 2  /* NaN/Inf in the estimate -> identity */
+
+/* inlier comparator */
+#define M3D_SCORE_SQUARED 0 /* Σd² < thr   (evaluate_inlier_ratio_fast, ransac.py:274-277) */
+#define M3D_SCORE_NORM 1    /* ‖d‖ < thr    (evaluate_inlier_ratio,      ransac.py:233-236) */
+
+/* ICP estimators (Open3D TransformationEstimation*) */
+#define M3D_EST_POINT_TO_POINT 0
+#define M3D_EST_POINT_TO_PLANE 1
+
+typedef struct m3d_ctx m3d_ctx;
+typedef struct m3d_corrset m3d_corrset; /* packed correspondence set (RANSAC) */
+typedef struct m3d_cloud m3d_cloud;     /* packed point cloud (ICP / NN)      */
+typedef struct m3d_icp m3d_icp;         /* device-resident ICP loop state     */
+
+/* ------------------------------------------------------------------ context */
+int m3d_abi_version(void);
+int m3d_device_count(int* count);
+int m3d_create(int device, m3d_ctx** out);
+void m3d_destroy(m3d_ctx* ctx);
+const char* m3d_last_error(const m3d_ctx* ctx);
+/* Device-side hit counters (cumulative): [0] pairs rechecked by chunk, [1] by full hypothesis. */
+int m3d_get_stats(m3d_ctx* ctx, int64_t* out8 /* [host] 8 values */);
+
+/* Kernel timing with HIP events recorded on the launch stream immediately before and after each
+ * launch of the named kernel (benchmarks / roofline).  Kernel ids: */
+#define M3D_KERNEL_NN 0     /* ICP brute-force NN scan          */
+#define M3D_KERNEL_SCORE 1  /* RANSAC fp32 scoring screen       */
+#define M3D_KERNEL_KABSCH 2 /* RANSAC batched 3-point Kabsch    */
+#define M3D_KERNEL_TERMS 3  /* ICP fp64 estimation terms        */
+int m3d_profile_enable(m3d_ctx* ctx, int enable);
+/* Synchronises, returns Σ launch durations (ms) and launch count since the last read, resets. */
+int m3d_profile_read(m3d_ctx* ctx, int kernel, double* total_ms, int64_t* launches);
+
+/* ------------------------------------------------------------------ RANSAC */
+
+/* Gather + pack a correspondence set: p_i = src[corr[i,0]], q_i = tgt[corr[i,1]].
+ * Replaces the per-call gathers of evaluate_inlier_ratio (ransac.py:223-227) and the
+ * pre-gather of _visualize_matcher.py:376-384.  Synchronous (computes centring offsets).
+ * src_xyz [device] ns×3 f64, tgt_xyz [device] nt×3 f64, corr [device] nc×2 int32. */
+int m3d_corrset_create(m3d_ctx* ctx, const double* src_xyz, int64_t ns, const double* tgt_xyz,
+                       int64_t nt, const int32_t* corr, int64_t nc, void* stream,
+                       m3d_corrset** out);
+/* Same from pre-gathered pairs (the p_src / p_tgt arguments of evaluate_inlier_ratio_fast,
+ * ransac.py:239-244): p_src, p_tgt [device] nc×3 f64. */
+int m3d_corrset_create_gathered(m3d_ctx* ctx, const double* p_src, const double* p_tgt,
+                                int64_t nc, void* stream, m3d_corrset** out);
+void m3d_corrset_destroy(m3d_corrset* cs);
+int64_t m3d_corrset_size(const m3d_corrset* cs);
+
+/* a1, batched: H hypotheses of compute_step_transformation (ransac.py:104-192).
+ * triples [device] H×3 int32 correspondence rows (replay mode: e.g. the rows the reference's
+ * np.random.choice(n,3,replace=False) draws, see m3d_replay_triples), or NULL for the native
+ * counter-based sampler keyed by (seed, hyp0 + h).
+ * T_out [device] H×16 f64 row-major; status [device] H uint8 (may be NULL). */
+int m3d_kabsch3_batch(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triples,
+                      uint64_t seed, int64_t hyp0, int64_t H, double* T_out, uint8_t* status,
+                      void* stream);
+
+/* a2/a3, batched: counts[h] = #{i : dist(T_h p_i, q_i) < thr} for H transforms.
+ * mode M3D_SCORE_SQUARED: thr is the squared threshold (evaluate_inlier_ratio_fast);
+ * mode M3D_SCORE_NORM:    thr is the distance threshold (evaluate_inlier_ratio).
+ * T [device] H×16 f64; counts [device] H int32.  Counts are exact w.r.t. an fp64 evaluation
+ * of the reference formula (fp32 screen + fp64 recheck of pairs inside a proven guard band). */
+int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64_t H, double thr,
+                     int mode, int32_t* counts, void* stream);
+
+/* a4: the step-RANSAC loop (_visualize_matcher.py:343-470; benchmark_ransac.py:87-125 when
+ * early_stop == 0), run on the device in batches with no host round trip per batch. */
+typedef struct {
+  int64_t max_iter;     /* MatcherSettings.ransac_iteration                          */
+  uint64_t seed;        /* native sampler seed (ignored when triples are supplied)   */
+  double thr;           /* comparator threshold (see mode)                           */
+  int32_t mode;         /* M3D_SCORE_SQUARED (GUI loop, a3) or M3D_SCORE_NORM (a2)   */
+  int32_t early_stop;   /* MatcherSettings.early_stop_enabled                        */
+  double es_threshold;  /* MatcherSettings.early_stop_threshold (0.5)                */
+  double es_confidence; /* MatcherSettings.early_stop_confidence (0.99)              */
+  int64_t batch;        /* hypotheses per device batch (0 = automatic)               */
+  int64_t hyp0;         /* first hypothesis id (multi-GPU hypothesis sharding)       */
+} m3d_ransac_params;
+
+typedef struct {
+  double T[16];        /* best transform (row-major)                        */
+  double fitness;      /* best inlier ratio = best_count / nc                */
+  int64_t best_index;  /* 0-based iteration index of the best hypothesis     */
+  int64_t iterations;  /* iter_num at exit (early stop or max_iter)          */
+  int64_t best_count;  /* inlier count of the best hypothesis                */
+  int64_t rechecked;   /* pairs re-evaluated in fp64 (guard band)            */
+} m3d_ransac_result;
+
+/* triples [device] max_iter×3 int32 or NULL (native sampler).  Synchronous. */
+int m3d_ransac_run(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_params* params,
+                   const int32_t* triples, m3d_ransac_result* out, void* stream);
+/* Asynchronous form: per-hypothesis counts of the whole run land in counts_out [device]
+ * (max_iter int32, may be NULL) and the result struct in result_dev [device]. */
+int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_params* params,
+                         const int32_t* triples, int32_t* counts_out, m3d_ransac_result* result_dev,
+                         void* stream);
+
+/* Host-side replay of the reference RNG: the rows H successive
+ * `np.random.choice(nc, 3, replace=False)` calls of the legacy MT19937 RandomState draw
+ * (ransac.py:143 ≡ permutation(nc)[:3]).  mt_key [host] 624 uint32 + *mt_pos is the state
+ * `np.random.get_state()` returns; both are advanced in place exactly as numpy would.
+ * triples_out [host] H×3 int32. */
+int m3d_replay_triples(uint32_t* mt_key, int32_t* mt_pos, int64_t nc, int64_t H,
+                       int32_t* triples_out);
+
+/* ------------------------------------------------------------------ ICP */
+
+/* Pack a cloud for NN / ICP: xyz [device] n×3 f64, normals [device] n×3 f64 or NULL.
+ * Synchronous (computes the centring offset).  Replaces Open3D's PointCloud copy +
+ * KDTreeFlann::SetGeometry (Registration.cpp RegistrationICP). */
+int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                     void* stream, m3d_cloud** out);
+void m3d_cloud_destroy(m3d_cloud* c);
+int64_t m3d_cloud_size(const m3d_cloud* c);
+
+/* Radius-bounded 1-NN (KDTreeFlann::SearchHybrid(p, r, 1) for every source point after T):
+ * idx [device] ns int32 (-1 = no target with d² < r²), d2 [device] ns f64 (may be NULL). */
+int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const double* T_host,
+            double max_dist, int32_t* idx, double* d2, void* stream);
+
+typedef struct {
+  double relative_fitness; /* ICPConvergenceCriteria defaults 1e-6 */
+  double relative_rmse;    /* 1e-6 */
+  int32_t max_iteration;   /* 30 */
+  int32_t estimation;      /* M3D_EST_* */
+} m3d_icp_params;
+
+typedef struct {
+  double T[16];
+  double fitness;
+  double inlier_rmse;
+  int64_t num_correspondences;
+  int32_t iterations; /* updates applied */
+  int32_t converged;
+} m3d_icp_result;
+
+/* registration_icp (icp.py:42-48 → Open3D RegistrationICP).  init [host] 16 f64.
+ * corr_idx [device] ns int32 or NULL: final correspondence target per source (-1 = none).
+ * Synchronous. */
+int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const double* init,
+                double max_dist, const m3d_icp_params* params, m3d_icp_result* out,
+                int32_t* corr_idx, void* stream);
+
+/* Step-wise ICP driver (benchmarks, multi-GPU).  An m3d_icp holds the device-resident loop
+ * state (T, fitness/rmse history, convergence flag); every call only enqueues work. */
+int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
+                   const m3d_icp_params* params, m3d_icp** out);
+void m3d_icp_destroy(m3d_icp* s);
+int m3d_icp_reset(m3d_icp* s, const double* init_host, void* stream);
+/* One full iteration on one device: NN evaluation + estimation terms + solve/update. */
+int m3d_icp_step(m3d_icp* s, void* stream);
+/* Target-sharded pieces (cfg3): `tgt` of m3d_icp_create is this rank's shard whose first
+ * point has global index shard_offset.  keys [device] ns int64: packed (bits(d²)<<32 | idx),
+ * INT64_MAX = none; reduce with MIN across ranks.  sums [device] 32 f64; reduce with SUM. */
+int m3d_icp_shard_nn(m3d_icp* s, int64_t shard_offset, int64_t* keys, void* stream);
+int m3d_icp_shard_terms(m3d_icp* s, int64_t shard_offset, const int64_t* keys, double* sums,
+                        void* stream);
+int m3d_icp_solve(m3d_icp* s, const double* sums, void* stream);
+/* Read the loop state (synchronises the stream). */
+int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream);
+/* Device pointer to the current correspondence index array (ns int32, -1 = none). */
+const int32_t* m3d_icp_corr(const m3d_icp* s);
+/* Copy the current correspondence array to dst [device] (ns int32). */
+int m3d_icp_copy_corr(const m3d_icp* s, int32_t* dst, void* stream);
+
+/* ------------------------------------------------------------------ test hooks
+ * Host-compiled copy of the device 3×3 linear algebra (same source), for CPU-side unit tests
+ * of the math.  Never used by the product path. */
+int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16);
+int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* M3D_H_ */

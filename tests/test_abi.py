@@ -1,0 +1,129 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol include/m3d.h declares,
+and its host-side pieces (MT19937 replay, and the host-compiled copy of the device linear algebra)
+agree with the reference's golden vectors / numpy."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from m3d import _lib
+
+ROOT = Path(__file__).resolve().parents[1]
+P = C.POINTER(C.c_double)
+
+
+def header_symbols():
+    text = (ROOT / "include" / "m3d.h").read_text()
+    return sorted(set(re.findall(r"\b(m3d_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} missing from the ctypes signature table"
+    assert lib.m3d_abi_version() == 1
+
+
+def test_no_device_here_is_reported_not_crashed():
+    lib = _lib.load()
+    n = C.c_int(-1)
+    assert lib.m3d_device_count(C.byref(n)) == 0
+    if n.value == 0:
+        h = C.c_void_p()
+        assert lib.m3d_create(0, C.byref(h)) == _lib.M3D_ERR_NODEVICE
+
+
+@pytest.mark.parametrize("nc", [3, 4, 5, 17, 1000, 65537])
+def test_replay_triples_match_numpy_legacy_choice(nc):
+    from m3d.core import replay_triples
+
+    rs = np.random.RandomState(1234 + nc)
+    st0 = rs.get_state()
+    H = 40 if nc > 10000 else 300
+    tri, st1 = replay_triples(nc, H, state=st0)
+    exp = np.array([rs.choice(nc, 3, replace=False) for _ in range(H)])
+    np.testing.assert_array_equal(tri, exp)
+    st_np = rs.get_state()
+    assert st1[2] == st_np[2]
+    np.testing.assert_array_equal(st1[1], st_np[1])
+
+
+def test_replay_triples_advance_global_rng():
+    from m3d.core import replay_triples
+
+    np.random.seed(42)
+    tri, _ = replay_triples(5000, 10)
+    after = np.random.rand()
+    np.random.seed(42)
+    exp = np.array([np.random.choice(5000, 3, replace=False) for _ in range(10)])
+    np.testing.assert_array_equal(tri, exp)
+    assert np.random.rand() == after
+
+
+def host_kabsch(a, b):
+    lib = _lib.load()
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    T = np.zeros(16)
+    rc = lib.m3d_debug_kabsch3_host(a.ctypes.data_as(P), b.ctypes.data_as(P), T.ctypes.data_as(P))
+    return T.reshape(4, 4), rc
+
+
+def test_host_kabsch_matches_reference_kats(golden):
+    k = golden("crash_kats.npz")
+    for s in range(10):
+        T, rc = host_kabsch(k["minimal_src"][s], k["minimal_tgt"][s])
+        assert rc == 0
+        np.testing.assert_allclose(T, k["minimal_T"][s], atol=1e-12)
+    for name, a, b in (("collinear", "collinear_pts", "collinear_pts"),
+                       ("coplanar", "coplanar_src", "coplanar_tgt"),
+                       ("coplanar_self", "coplanar_src", "coplanar_src"),
+                       ("duplicate", "duplicate_pts", "duplicate_pts")):
+        T, rc = host_kabsch(k[a][:3], k[b][:3])
+        np.testing.assert_allclose(T, k[f"{name}_T"], atol=1e-12, err_msg=name)
+
+
+@pytest.mark.parametrize("seed", (0, 42))
+def test_host_kabsch_matches_reference_5k(golden, pts5k, seed):
+    g = golden(f"ransac_5k_seed{seed}.npz")
+    src, tgt, corr = pts5k["src"], pts5k["tgt"], pts5k["corr_noise"]
+    p, q = src[corr[:, 0]], tgt[corr[:, 1]]
+    tri = g["noise_triples"]
+    worst, n_rank1 = 0.0, 0
+    for h in range(1000):
+        T, rc = host_kabsch(p[tri[h]], q[tri[h]])
+        assert rc == 0
+        if rank_deficient(p[tri[h]], q[tri[h]]):
+            # rotation not unique (LAPACK returns rounding noise): pin properness only
+            n_rank1 += 1
+            R = T[:3, :3]
+            np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-12)
+            assert abs(np.linalg.det(R) - 1) < 1e-12
+            continue
+        worst = max(worst, np.abs(T - g["noise_T"][h]).max())
+    assert worst < 1e-9, worst
+    assert n_rank1 <= 5
+
+
+def rank_deficient(a, b):
+    """3-point sample whose cross-covariance has rank < 2 (collinear or repeated points)."""
+    H = (a - a.mean(0)).T @ (b - b.mean(0))
+    s = np.linalg.svd(H, compute_uv=False)
+    return s[1] <= 1e-10 * s[0]
+
+
+def test_host_ldlt_matches_dense_solve():
+    lib = _lib.load()
+    rng = np.random.default_rng(1)
+    for _ in range(10):
+        J = rng.standard_normal((40, 6))
+        A = np.ascontiguousarray(J.T @ J)
+        b = rng.standard_normal(6)
+        x = np.zeros(6)
+        lib.m3d_debug_ldlt6_host(A.ctypes.data_as(P), b.ctypes.data_as(P), x.ctypes.data_as(P))
+        np.testing.assert_allclose(x, np.linalg.solve(A, b), rtol=1e-9, atol=1e-12)

@@ -1,0 +1,153 @@
+"""GPU parity for the ICP half: the HIP NN + point-to-plane/point-to-point loop vs the CPU oracle
+(Open3D 0.19 semantics restated; parity against Open3D itself is unpinned — SURVEY.md §8(c)).
+
+Tolerances (stated): NN indices equal except where two targets are within fp32 rounding of each
+other (the chosen target's fp64 distance is then within 2e-6·max(d², 1e-6) of the true minimum);
+ICP transforms within 1e-6 (rotation) / 1e-5 (translation) of the oracle; fitness within 2e-4.
+"""
+import numpy as np
+import pytest
+from scipy.spatial import cKDTree
+
+import icp_oracle as I
+from m3d import _lib, synth
+from m3d.core import Cloud, IcpLoop, icp, nn1
+
+pytestmark = pytest.mark.gpu
+
+
+def check_nn(src_t, tgt, r, idx, d2):
+    tree = cKDTree(tgt)
+    dd, jj = tree.query(src_t, k=1)
+    ref_d2 = dd * dd
+    inside = ref_d2 < r * r
+    got = idx >= 0
+    # radius decisions agree except within fp rounding of r²
+    edge = np.abs(ref_d2 - r * r) < 1e-6 * r * r
+    assert np.all((got == inside) | edge)
+    both = got & inside
+    same = idx[both] == jj[both]
+    if not same.all():
+        bi = np.nonzero(both)[0][~same]
+        diff = src_t[bi] - tgt[idx[bi]]
+        mine = np.sum(diff * diff, axis=1)
+        assert np.all(mine <= ref_d2[bi] + 2e-6 * np.maximum(ref_d2[bi], 1e-6))
+    assert same.mean() > 0.999
+    np.testing.assert_allclose(d2[both], np.sum((src_t[both] - tgt[idx[both]]) ** 2, axis=1), rtol=1e-12)
+
+
+@pytest.mark.parametrize("ns,nt", [(1, 1), (5, 3000), (1000, 1000), (20000, 30011), (100_000, 100_000)])
+def test_nn1_matches_kdtree(ns, nt):
+    rng = np.random.default_rng(ns + nt)
+    tgt, _ = synth.surface_points(nt, seed=1)
+    src, _ = synth.surface_points(ns, seed=2)
+    T = synth.random_rigid(3, rot_range=0.02, trans_range=0.05)
+    r = 0.3 if nt < 5000 else 0.12
+    idx, d2 = nn1(Cloud(src), Cloud(tgt), T, r)
+    check_nn(synth.apply(T, src), tgt, r, idx.cpu().numpy(), d2.cpu().numpy())
+    del rng
+
+
+def test_nn1_exact_ties_pick_lowest_index():
+    tgt = np.array([[1.0, 0, 0], [-1.0, 0, 0], [0, 1.0, 0], [1.0, 0, 0]])
+    src = np.zeros((3, 3))
+    idx, d2 = nn1(Cloud(src), Cloud(tgt), np.eye(4), 2.0)
+    assert idx.cpu().numpy().tolist() == [0, 0, 0]
+    idx, _ = nn1(Cloud(src), Cloud(tgt), np.eye(4), 1.0)  # strict d² < r²: none
+    assert idx.cpu().numpy().tolist() == [-1, -1, -1]
+
+
+@pytest.mark.parametrize("estimation", ["point_to_plane", "point_to_point"])
+def test_icp_matches_oracle(estimation):
+    src, tgt, nrm, T_true = synth.icp_pair(20000, seed=5)
+    if estimation == "point_to_point":
+        src = synth.apply(np.linalg.inv(T_true), tgt)[::2]
+    ref = I.registration_icp(src, tgt, 0.12, init=np.eye(4), tgt_normals=nrm, estimation=estimation,
+                             max_iteration=30)
+    est = _lib.EST_POINT_TO_PLANE if estimation == "point_to_plane" else _lib.EST_POINT_TO_POINT
+    out = icp(Cloud(src), Cloud(tgt, nrm if est == _lib.EST_POINT_TO_PLANE else None), 0.12,
+              np.eye(4), estimation=est, max_iteration=30)
+    np.testing.assert_allclose(out.transformation[:3, :3], ref["transformation"][:3, :3], atol=1e-6)
+    np.testing.assert_allclose(out.transformation[:3, 3], ref["transformation"][:3, 3], atol=1e-5)
+    assert abs(out.fitness - ref["fitness"]) < 2e-4
+    assert abs(out.inlier_rmse - ref["inlier_rmse"]) < 1e-4 * ref["inlier_rmse"] + 1e-9
+    assert abs(out.iterations - ref["iterations"]) <= 1
+
+
+def test_refine_registration_api_recovers_pose():
+    from matcher.icp import refine_registration
+    from ply import Ply
+
+    src_pts, tgt_pts, nrm, T_true = synth.icp_pair(100_000, seed=7)
+    src = Ply.from_arrays(src_pts)
+    tgt = Ply.from_arrays(tgt_pts, normals=nrm)
+    res = refine_registration(src, tgt, np.eye(4), 0.3)
+    assert res.fitness > 0.95
+    np.testing.assert_allclose(res.transformation, T_true, atol=5e-4)
+    assert len(res.correspondence_set) == round(res.fitness * len(src_pts))
+
+
+def test_fixed_iterations_and_missing_normals():
+    src, tgt, nrm, _ = synth.icp_pair(5000, seed=9)
+    out = icp(Cloud(src), Cloud(tgt, nrm), 0.12, np.eye(4), relative_fitness=-1, relative_rmse=-1,
+              max_iteration=7)
+    assert out.iterations == 7 and not out.converged
+    from matcher.icp import registration_icp
+
+    with pytest.raises(ValueError):
+        registration_icp(src, tgt, 0.12, np.eye(4), "point_to_plane")
+    with pytest.raises(ValueError):
+        registration_icp(src, tgt, 0.0)
+
+
+def test_no_overlap_gives_identity_and_zero_fitness():
+    src, _ = synth.surface_points(2000, seed=1)
+    tgt, nrm = synth.surface_points(2000, seed=2)
+    out = icp(Cloud(src + 100.0), Cloud(tgt, nrm), 0.12, np.eye(4), max_iteration=5)
+    assert out.fitness == 0.0 and out.inlier_rmse == 0.0
+    np.testing.assert_array_equal(out.transformation, np.eye(4))
+
+
+def test_step_loop_matches_run():
+    src, tgt, nrm, _ = synth.icp_pair(30000, seed=11)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    full = icp(s, t, 0.12, np.eye(4), relative_fitness=-1, relative_rmse=-1, max_iteration=10)
+    loop = IcpLoop(s, t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=10)
+    loop.reset(np.eye(4))
+    for _ in range(11):
+        loop.step()
+    r = loop.result()
+    np.testing.assert_array_equal(r.transformation, full.transformation)
+    assert r.fitness == full.fitness and r.iterations == 10
+
+
+def test_target_sharded_loop_matches_single_device():
+    """The multi-GPU target-shard protocol (MIN on keys, SUM on terms) emulated on one device."""
+    import torch
+
+    src, tgt, nrm, _ = synth.icp_pair(20000, 30000, seed=13)
+    s = Cloud(src)
+    full = icp(s, Cloud(tgt, nrm), 0.12, np.eye(4), relative_fitness=-1, relative_rmse=-1,
+               max_iteration=6)
+    bounds = [0, 7000, 19001, 30000]
+    shards = [Cloud(tgt[a:b], nrm[a:b]) for a, b in zip(bounds[:-1], bounds[1:])]
+    loops = [IcpLoop(s, sh, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=6) for sh in shards]
+    for lp in loops:
+        lp.reset(np.eye(4))
+    ns = len(src)
+    for _ in range(7):
+        keys = [torch.empty(ns, dtype=torch.int64, device="cuda") for _ in loops]
+        for lp, off, k in zip(loops, bounds, keys):
+            lp.shard_nn(off, k)
+        kmin = torch.stack(keys).min(dim=0).values
+        sums = [torch.empty(32, dtype=torch.float64, device="cuda") for _ in loops]
+        for lp, off, sm in zip(loops, bounds, sums):
+            lp.shard_terms(off, kmin, sm)
+        tot = torch.stack(sums).sum(dim=0)
+        for lp in loops:
+            lp.solve(tot)
+    r = loops[0].result()
+    np.testing.assert_allclose(r.transformation, full.transformation, atol=1e-9)
+    assert abs(r.fitness - full.fitness) < 1e-12
+    for lp in loops[1:]:
+        np.testing.assert_array_equal(lp.result().transformation, r.transformation)

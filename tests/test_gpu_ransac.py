@@ -1,0 +1,250 @@
+"""GPU parity: the HIP RANSAC path (through the C ABI) vs the reference's golden vectors and the
+CPU oracle.  Bar: inlier counts bit-exact; Kabsch transforms within 1e-9 (rank-2 samples);
+loop trajectories (best index, best fitness, stop iteration) exact."""
+import numpy as np
+import pytest
+
+import ransac_oracle as O
+from m3d import _lib
+from m3d.core import CorrSet, RansacParams
+
+pytestmark = pytest.mark.gpu
+
+THR = 0.3 * 1.5
+
+
+def rank_deficient(a, b):
+    H = (a - a.mean(0)).T @ (b - b.mean(0))
+    s = np.linalg.svd(H, compute_uv=False)
+    return s[1] <= 1e-10 * s[0]
+
+
+@pytest.fixture(scope="module")
+def sets(pts5k):
+    out = {}
+    for name in ("clean", "noise", "mid"):
+        corr = pts5k[f"corr_{name}"]
+        out[name] = (CorrSet(pts5k["src"], pts5k["tgt"], corr), corr)
+    return out
+
+
+@pytest.mark.parametrize("seed", (0, 1, 42))
+@pytest.mark.parametrize("name", ("clean", "noise"))
+def test_kabsch_replay_matches_reference(golden, pts5k, sets, seed, name):
+    g = golden(f"ransac_5k_seed{seed}.npz")
+    cs, corr = sets[name]
+    T, st = cs.kabsch3(1000, triples=g[f"{name}_triples"])
+    T = T.cpu().numpy()
+    assert (st.cpu().numpy() == _lib.HYP_OK).all()
+    p, q = pts5k["src"][corr[:, 0]], pts5k["tgt"][corr[:, 1]]
+    tri = g[f"{name}_triples"]
+    for h in range(1000):
+        if rank_deficient(p[tri[h]], q[tri[h]]):
+            R = T[h, :3, :3]
+            np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-12)
+            continue
+        np.testing.assert_allclose(T[h], g[f"{name}_T"][h], atol=1e-9, err_msg=f"hyp {h}")
+
+
+@pytest.mark.parametrize("seed", (0, 1, 42))
+@pytest.mark.parametrize("name", ("clean", "noise"))
+def test_scores_exact_on_reference_transforms(golden, sets, seed, name):
+    g = golden(f"ransac_5k_seed{seed}.npz")
+    cs, _ = sets[name]
+    Ts = g[f"{name}_T"]
+    fast = cs.score(Ts, THR * THR, _lib.SCORE_SQUARED).cpu().numpy()
+    slow = cs.score(Ts, THR, _lib.SCORE_NORM).cpu().numpy()
+    np.testing.assert_array_equal(fast, g[f"{name}_count_fast"])
+    np.testing.assert_array_equal(slow, g[f"{name}_count_slow"])
+
+
+def test_native_sampler_matches_oracle(pts5k, sets):
+    cs, corr = sets["noise"]
+    H = 3000
+    T, st = cs.kabsch3(H, seed=42, hyp0=17)
+    T = T.cpu().numpy()
+    tri = O.native_triples(42, 17, H, len(corr))
+    p, q = pts5k["src"][corr[:, 0]], pts5k["tgt"][corr[:, 1]]
+    for h in range(0, H, 3):
+        if rank_deficient(p[tri[h]], q[tri[h]]):
+            continue
+        Tr, _ = O.kabsch3(p[tri[h]], q[tri[h]])
+        np.testing.assert_allclose(T[h], Tr, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ("clean", "noise", "mid"))
+def test_loop_trajectory_matches_reference(golden, sets, name):
+    t = golden("loop_trajectory.npz")
+    cs, corr = sets[name]
+    max_iter = int(t[f"{name}_max_iter"])
+    tri, _ = O.replay_triples(int(t[f"{name}_seed"]), len(corr), max_iter)
+    for batch in (0, 7, 64):
+        out = cs.run(RansacParams(max_iter=max_iter, thr=THR * THR, mode=_lib.SCORE_SQUARED,
+                                  early_stop=True, batch=batch), triples=tri)
+        assert out.best_index == int(t[f"{name}_best_index"])
+        assert out.fitness == float(t[f"{name}_best_fitness"])
+        assert out.iterations == int(t[f"{name}_iterations"])
+
+
+def test_loop_no_early_stop_argmax(pts5k, sets):
+    cs, corr = sets["noise"]
+    H = 5000
+    out = cs.run(RansacParams(max_iter=H, seed=9, thr=THR, mode=_lib.SCORE_NORM, early_stop=False,
+                              batch=1000))
+    T, _ = cs.kabsch3(H, seed=9)
+    counts = cs.score(T, THR, _lib.SCORE_NORM).cpu().numpy()
+    assert out.iterations == H
+    assert out.best_index == int(np.argmax(counts))
+    assert out.best_count == counts.max()
+    np.testing.assert_allclose(out.transformation, T[out.best_index].cpu().numpy(), atol=0)
+
+
+def test_matcher_api_is_drop_in(golden, pts5k):
+    from matcher import ransac as M
+    from ply import Ply
+
+    g = golden("ransac_5k_seed42.npz")
+    corr = pts5k["corr_noise"]
+    src = Ply.from_arrays(pts5k["src"])
+    tgt = Ply.from_arrays(pts5k["tgt"])
+    np.random.seed(42)
+    p, q = pts5k["src"][corr[:, 0]], pts5k["tgt"][corr[:, 1]]
+    for h in range(12):
+        res = M.compute_step_transformation(src, tgt, corr)
+        assert res.fitness == 0.0
+        if not rank_deficient(p[g["noise_triples"][h]], q[g["noise_triples"][h]]):
+            np.testing.assert_allclose(res.transformation, g["noise_T"][h], atol=1e-9)
+        assert M.evaluate_inlier_ratio(src, tgt, corr, g["noise_T"][h], 0.3) == g["noise_ratio_slow"][h]
+        assert M.evaluate_inlier_ratio_fast(p, q, g["noise_T"][h], float(g["thr_sq"])) == \
+            g["noise_ratio_fast"][h]
+    # RNG consumed exactly like the reference's 12 calls
+    np.random.seed(42)
+    for _ in range(12):
+        np.random.choice(len(corr), 3, replace=False)
+    ref_next = np.random.rand()
+    np.random.seed(42)
+    for _ in range(12):
+        M.compute_step_transformation(src, tgt, corr)
+    assert np.random.rand() == ref_next
+
+
+def test_matcher_ransac_replay_equals_reference_loop(golden, pts5k):
+    from matcher import ransac as M
+
+    t = golden("loop_trajectory.npz")
+    corr = pts5k["corr_mid"]
+    np.random.seed(int(t["mid_seed"]))
+    res, info = M.ransac(pts5k["src"], pts5k["tgt"], corr, voxel_size=0.3,
+                         max_iter=int(t["mid_max_iter"]))
+    assert info["iterations"] == int(t["mid_iterations"])
+    assert info["best_index"] == int(t["mid_best_index"])
+    assert res.fitness == float(t["mid_best_fitness"])
+    # the global RNG advanced by exactly the iterations consumed
+    after = np.random.rand()
+    np.random.seed(int(t["mid_seed"]))
+    for _ in range(int(t["mid_iterations"])):
+        np.random.choice(len(corr), 3, replace=False)
+    assert np.random.rand() == after
+
+
+def test_crash_kats_through_api(golden):
+    from matcher import ransac as M
+
+    k = golden("crash_kats.npz")
+    c3 = np.array([[0, 0], [1, 1], [2, 2]], dtype=np.int32)
+    col = k["collinear_pts"]
+    np.random.seed(5)
+    np.testing.assert_allclose(M.compute_step_transformation(col, col, c3).transformation,
+                               k["collinear_T"], atol=1e-12)
+    dup = k["duplicate_pts"]
+    np.random.seed(9)
+    np.testing.assert_allclose(M.compute_step_transformation(dup, dup, c3).transformation,
+                               k["duplicate_T"], atol=1e-12)
+    np.random.seed(8)
+    np.testing.assert_allclose(M.compute_step_transformation(k["coplanar_src"], k["coplanar_tgt"],
+                                                             c3).transformation,
+                               k["coplanar_T"], atol=1e-12)
+    for s in range(10):
+        np.random.seed(200 + s)
+        np.testing.assert_allclose(
+            M.compute_step_transformation(k["minimal_src"][s], k["minimal_tgt"][s], c3).transformation,
+            k["minimal_T"][s], atol=1e-12)
+    ten = np.random.rand(10, 3)
+    assert M.evaluate_inlier_ratio(ten, ten, np.zeros((0, 2), np.int32), np.eye(4), 0.3) == 0.0
+    r = M.compute_step_transformation(ten, ten, c3[:2])
+    np.testing.assert_array_equal(r.transformation, np.eye(4))
+
+
+def test_crash_kat_ratios_through_api(golden, pts5k):
+    from matcher import ransac as M
+
+    k = golden("crash_kats.npz")
+    src, tgt = pts5k["src"], pts5k["tgt"]
+    assert M.evaluate_inlier_ratio(src, tgt, pts5k["corr_clean"], k["large_T"], 0.3) == k["large_ratio_clean"]
+    assert M.evaluate_inlier_ratio(src, tgt, pts5k["corr_clean"], np.eye(4), 0.3) == k["identity_ratio_clean"]
+    assert M.evaluate_inlier_ratio(src, tgt, pts5k["corr_clean"], pts5k["T_true"], 0.3) == k["true_ratio_clean"]
+    assert M.evaluate_inlier_ratio(src, tgt, pts5k["corr_noise"], pts5k["T_true"], 0.3) == k["true_ratio_noise"]
+
+
+def test_negative_and_out_of_range_indices():
+    from matcher import ransac as M
+
+    pts = np.random.default_rng(0).random((10, 3))
+    c = np.array([[-1, -1], [0, 0], [1, 1]], dtype=np.int32)  # numpy wraps -1
+    assert M.evaluate_inlier_ratio(pts, pts, c, np.eye(4), 0.3) == 1.0
+    with pytest.raises(ValueError):
+        M.evaluate_inlier_ratio(pts, pts, np.array([[0, 10]], np.int32), np.eye(4), 0.3)
+
+
+@pytest.mark.parametrize("nc", [1, 2, 3, 5, 63, 2047, 2048, 2049, 10007])
+def test_ragged_sizes_exact(nc):
+    from m3d import synth
+
+    src, tgt, corr, T = synth.ransac_pair(max(nc, 3), seed=nc)
+    corr = corr[:nc]
+    cs = CorrSet(src, tgt, corr)
+    rng = np.random.default_rng(nc)
+    Ts = np.stack([T] + [synth.random_rigid(int(s), rot_range=0.2, trans_range=0.3)
+                         for s in rng.integers(0, 1 << 30, 70)])
+    p, q = src[corr[:, 0]], tgt[corr[:, 1]]
+    for mode, thr in ((_lib.SCORE_SQUARED, THR * THR), (_lib.SCORE_NORM, THR)):
+        got = cs.score(Ts, thr, mode).cpu().numpy()
+        np.testing.assert_array_equal(got, O.inlier_counts(p, q, Ts, thr, mode))
+
+
+def test_guard_band_recheck_is_exercised_and_exact():
+    """Pairs placed within ~1e-7 of the threshold force the fp64 recheck path."""
+    from m3d.core import context
+
+    rng = np.random.default_rng(3)
+    n = 20000
+    p = rng.uniform(-5, 5, (n, 3))
+    d = rng.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    scale = THR * (1 + rng.uniform(-3e-7, 3e-7, n))
+    q = p + d * scale[:, None]
+    cs = CorrSet(p_src=p, p_tgt=q)
+    ctx = context()
+    before = ctx.stats()
+    Ts = np.stack([np.eye(4)] * 5)
+    for mode, thr in ((_lib.SCORE_SQUARED, THR * THR), (_lib.SCORE_NORM, THR)):
+        got = cs.score(Ts, thr, mode).cpu().numpy()
+        np.testing.assert_array_equal(got, O.inlier_counts(p, q, Ts, thr, mode))
+    assert (ctx.stats() - before)[:2].sum() > 0  # rechecks happened
+
+
+def test_full_size_counts_subsample_exact():
+    """cfg2 geometry (Nc = 1e5): native-sampled hypotheses' counts equal the oracle's."""
+    from m3d import synth
+
+    src, tgt, corr, _ = synth.ransac_pair(100_000, seed=42)
+    cs = CorrSet(src, tgt, corr)
+    H = 20_000
+    T, _ = cs.kabsch3(H, seed=42)
+    counts = cs.score(T, THR, _lib.SCORE_NORM).cpu().numpy()
+    Tn = T.cpu().numpy()
+    p, q = src[corr[:, 0]], tgt[corr[:, 1]]
+    pick = np.random.default_rng(0).choice(H, 60, replace=False)
+    np.testing.assert_array_equal(counts[pick], O.inlier_counts(p, q, Tn[pick], THR, 1))
+    out = cs.run(RansacParams(max_iter=H, seed=42, thr=THR, mode=_lib.SCORE_NORM, early_stop=False))
+    assert out.best_count == counts.max() and out.best_index == int(np.argmax(counts))
