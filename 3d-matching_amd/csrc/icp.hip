@@ -151,9 +151,11 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
   const int64_t jb = (int64_t)blockIdx.y * slice_len;
   const int64_t je = min(nt_pad, jb + slice_len);
   for (int64_t j0 = jb; j0 < je; j0 += kNNTile) {
+    // tile minimum from +inf: `m <= best` then means some target of the tile is at least as
+    // close as the current bound (a strict improvement or an exact tie to resolve by index)
     float m[kNNQ];
 #pragma unroll
-    for (int q = 0; q < kNNQ; ++q) m[q] = best[q];
+    for (int q = 0; q < kNNQ; ++q) m[q] = FLT_MAX;
 #pragma unroll
     for (int k = 0; k < kNNTile; ++k) {
       const float tx = tgt[j0 + k].x, ty = tgt[j0 + k].y, tz = tgt[j0 + k].z;

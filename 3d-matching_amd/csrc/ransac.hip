@@ -205,6 +205,16 @@ __global__ __launch_bounds__(256) void hypf_from_T_kernel(const double* __restri
 }
 
 // ------------------------------------------------------------------------------- fp32 screen
+__device__ __forceinline__ void load_hyp(const HypF32 M3D_CONST* P, float v[14]) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) v[k] = P->r[k];
+  v[9] = P->t[0];
+  v[10] = P->t[1];
+  v[11] = P->t[2];
+  v[12] = P->lo;
+  v[13] = P->hi;
+}
+
 __global__ __launch_bounds__(kScoreBlock) void score_kernel(
     const float4* __restrict__ p32, const float4* __restrict__ q32,
     const HypF32 M3D_CONST* hyp, int64_t H, int64_t hbase, int32_t* __restrict__ counts,
@@ -227,25 +237,45 @@ __global__ __launch_bounds__(kScoreBlock) void score_kernel(
   const int64_t h0 = hbase + (int64_t)blockIdx.y * kScoreHyps;
   const int nh = (int)((H - h0) < kScoreHyps ? (H - h0) : kScoreHyps);
   int cnt = 0;
+  // software-prefetched hypothesis block: the scalar load of h+1 is in flight while h computes
+  float cur[14];
+  load_hyp(hyp + h0, cur);
   for (int hl = 0; hl < nh; ++hl) {
-    const HypF32 M3D_CONST* P = hyp + h0 + hl;
-    const float r0 = P->r[0], r1 = P->r[1], r2 = P->r[2];
-    const float r3 = P->r[3], r4 = P->r[4], r5 = P->r[5];
-    const float r6 = P->r[6], r7 = P->r[7], r8 = P->r[8];
-    const float t0 = P->t[0], t1 = P->t[1], t2 = P->t[2];
-    const float lo_t = P->lo, hi_t = P->hi;
-    uint32_t lo = 0, hi = 0;
+    float nxt[14];
+    load_hyp(hyp + h0 + (hl + 1 < nh ? hl + 1 : hl), nxt);
+    const float r0 = cur[0], r1 = cur[1], r2 = cur[2];
+    const float r3 = cur[3], r4 = cur[4], r5 = cur[5];
+    const float r6 = cur[6], r7 = cur[7], r8 = cur[8];
+    const float t0 = cur[9], t1 = cur[10], t2 = cur[11];
+    const float lo_t = cur[12], hi_t = cur[13];
+    // all K distances first (independent chains), then the compares into independent masks,
+    // so the VALU→SGPR→SALU hand-offs overlap instead of serialising on one mask register
+    float d2[kScoreK];
 #pragma unroll
     for (int k = 0; k < kScoreK; ++k) {
       const float dx = fmaf(r0, px[k], fmaf(r1, py[k], fmaf(r2, pz[k], t0 - qx[k])));
       const float dy = fmaf(r3, px[k], fmaf(r4, py[k], fmaf(r5, pz[k], t1 - qy[k])));
       const float dz = fmaf(r6, px[k], fmaf(r7, py[k], fmaf(r8, pz[k], t2 - qz[k])));
-      const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-      lo += (uint32_t)__popcll(__ballot(d2 < lo_t));
-      hi += (uint32_t)__popcll(__ballot(d2 < hi_t));
+      d2[k] = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
     }
+    uint64_t mlo[kScoreK], mband[kScoreK];
+#pragma unroll
+    for (int k = 0; k < kScoreK; ++k) {
+      mlo[k] = __ballot(d2[k] < lo_t);
+      mband[k] = __ballot(d2[k] < hi_t);
+    }
+    uint32_t lo = 0;
+    uint64_t band = 0;
+#pragma unroll
+    for (int k = 0; k < kScoreK; ++k) {
+      lo += (uint32_t)__popcll(mlo[k]);
+      band |= mband[k] & ~mlo[k];
+    }
+    const bool ambiguous = band != 0;
+#pragma unroll
+    for (int k = 0; k < 14; ++k) cur[k] = nxt[k];
     cnt = (lane == hl) ? (int)lo : cnt;
-    if (lo != hi && lane == 0) {
+    if (ambiguous && lane == 0) {
       const int slot = atomicAdd(amb_count, 1);
       if (slot < amb_cap) {
         AmbRecord r;

@@ -2,7 +2,8 @@
 
 Put ``3d-matching_amd`` on ``PYTHONPATH`` where the reference put ``src``
 (`.devcontainer/Dockerfile:39`) and ``from matcher.ransac import ...`` / ``from matcher.icp
-import ...`` resolve to these modules.  ``register(source, target)`` is the coarse-to-fine
+import ...`` resolve to these modules.  (The package namespace keeps ``matcher.ransac`` and
+``matcher.icp`` as the submodules, exactly like the reference's empty ``__init__``.)  ``register(source, target)`` is the coarse-to-fine
 façade the reference's ``main()`` intends (`src/main.py:34-38`).
 """
 
@@ -15,7 +16,7 @@ from .ransac import (
     evaluate_inlier_ratio,
     evaluate_inlier_ratio_fast,
     global_registration,
-    ransac,
+    run_ransac,
 )
 from .register import register
 
@@ -25,7 +26,7 @@ __all__ = [
     "evaluate_inlier_ratio",
     "evaluate_inlier_ratio_fast",
     "global_registration",
-    "ransac",
+    "run_ransac",
     "refine_registration",
     "registration_icp",
     "register",

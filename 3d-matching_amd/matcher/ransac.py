@@ -13,7 +13,7 @@ KTC-Security-Circle/3d-matching ``src/matcher/ransac.py``; the arithmetic runs i
   plus the reference's outlier injection on the global numpy RNG.
 * ``global_registration`` (ransac.py:20-59): see ``m3d.feature_ransac``.
 
-Additions (batched, device-resident): ``ransac`` runs the whole step-RANSAC loop of
+Additions (batched, device-resident): ``run_ransac`` runs the whole step-RANSAC loop of
 ``_visualize_matcher.py:343-470`` on the GPU; ``register`` is the coarse-to-fine façade
 ``main.py:34-38`` intends.
 """
@@ -33,7 +33,7 @@ __all__ = [
     "compute_step_transformation",
     "evaluate_inlier_ratio",
     "evaluate_inlier_ratio_fast",
-    "ransac",
+    "run_ransac",
 ]
 
 
@@ -119,7 +119,7 @@ def evaluate_inlier_ratio_fast(p_src, p_tgt, transform, dist_thresh_sq) -> float
     return np.int64(cnt[0].item()) / len(p_src)
 
 
-def ransac(src, tgt, correspondences, voxel_size: float = 0.3, max_iter: int = 10000,
+def run_ransac(src, tgt, correspondences, voxel_size: float = 0.3, max_iter: int = 10000,
            early_stop: bool = True, early_stop_threshold: float = 0.5,
            early_stop_confidence: float = 0.99, sampler: str = "replay", seed=None,
            score: str = "fast"):

@@ -6,14 +6,14 @@ written).  This façade supplies it (``Ply.voxel_size``, default 
 the same two stages on the device:
 
 1. coarse: ``global_registration`` when both inputs carry FPFH features (``pcd_fpfh``), else the
-   step-RANSAC loop (``ransac``) over the given ``correspondences``;
+   step-RANSAC loop (``run_ransac``) over the given ``correspondences``;
 2. fine: ``refine_registration`` (point-to-plane ICP, radius 0.4·voxel) from the coarse result.
 """
 
 from __future__ import annotations
 
 from .icp import refine_registration
-from .ransac import global_registration, ransac
+from .ransac import global_registration, run_ransac
 
 
 def register(source, target, voxel_size=None, correspondences=None, ransac_iterations: int = 10000,
@@ -24,7 +24,7 @@ def register(source, target, voxel_size=None, correspondences=None, ransac_itera
             and getattr(target, "pcd_fpfh", None) is not None:
         coarse = global_registration(source, target, v)
     elif correspondences is not None:
-        coarse, _ = ransac(source, target, correspondences, voxel_size=v, max_iter=ransac_iterations,
+        coarse, _ = run_ransac(source, target, correspondences, voxel_size=v, max_iter=ransac_iterations,
                            **ransac_kwargs)
     else:
         raise ValueError("register needs FPFH features on both inputs (pcd_fpfh) or correspondences")

@@ -1,0 +1,167 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the N>1 protocols in m3d/dist.py.
+
+The driver (ShardedIcp) is the code bench.py runs over RCCL; here its backend is an oracle-backed
+CPU implementation of the same three calls (shard_nn / shard_terms / solve), so the protocol —
+key packing, MIN/SUM reductions, ownership of terms, identical solve on every rank — is checked
+against the single-process oracle.  The GPU kernels behind the same calls are covered by
+tests/test_gpu_icp.py::test_target_sharded_loop_matches_single_device.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+from scipy.spatial import cKDTree
+
+import icp_oracle as I
+from m3d import dist as D
+from m3d import synth
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class OracleShard:
+    """CPU stand-in for IcpLoop on one target shard (fp64 NN, fp32 keys, fp64 terms)."""
+
+    def __init__(self, src, tgt, nrm, r, max_iteration):
+        self.src, self.tgt, self.nrm, self.r = src, tgt, nrm, r
+        self.tree = cKDTree(tgt)
+        self.max_iteration = max_iteration
+
+    def reset(self, init):
+        self.T = np.array(init, np.float64)
+        self.iters = 0
+        self.evals = 0
+        self.done = False
+        self.fitness = self.rmse = 0.0
+
+    def shard_nn(self, off, keys):
+        if self.done:
+            return
+        pcd = I.transform_points(self.T, self.src)
+        d, j = self.tree.query(pcd, k=1)
+        d2 = d * d
+        ok = d2 < self.r * self.r
+        k = D.pack_nn_key(d2.astype(np.float32), np.where(ok, j + off, -1))
+        keys.copy_(torch.from_numpy(k))
+
+    def shard_terms(self, off, keys, sums):
+        if self.done:
+            return
+        _, idx = D.unpack_nn_key(keys.numpy())
+        mine = (idx >= off) & (idx < off + len(self.tgt))
+        i = np.nonzero(mine)[0]
+        j = idx[mine] - off
+        pcd = I.transform_points(self.T, self.src)
+        out = np.zeros(32)
+        if len(i):
+            JTJ, JTr, r2 = I.point_to_plane_terms(pcd, self.tgt, self.nrm, np.stack([i, j], 1))
+            out[:21] = JTJ[np.triu_indices(6)]
+            out[21:27] = JTr
+            out[27] = r2
+            dd = pcd[i] - self.tgt[j]
+            out[28] = len(i)
+            out[29] = np.sum(dd * dd)
+        sums.copy_(torch.from_numpy(out))
+
+    def solve(self, sums):
+        if self.done:
+            return
+        s = sums.numpy()
+        count = s[28]
+        self.fitness = count / len(self.src)
+        self.rmse = np.sqrt(s[29] / count) if count else 0.0
+        self.evals += 1
+        if self.iters >= self.max_iteration:
+            self.done = True
+            return
+        if count > 0:
+            A = np.zeros((6, 6))
+            A[np.triu_indices(6)] = s[:21]
+            A = A + np.triu(A, 1).T
+            self.T = I.vec6_to_matrix(I.ldlt_solve(A, -s[21:27])) @ self.T
+        self.iters += 1
+
+    def result(self):
+        return self.T, self.fitness, self.rmse, self.iters
+
+
+def _icp_worker(rank, world, port, path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    src, tgt, nrm, _ = synth.icp_pair(4000, 6001, seed=21)
+    off, cnt = D.shard_bounds(len(tgt), world, rank)
+    b = OracleShard(src, tgt[off:off + cnt], nrm[off:off + cnt], 0.12, 8)
+    drv = D.ShardedIcp(b, off, len(src), "cpu")
+    T, fit, rmse, iters = drv.run(np.eye(4), 8)
+    np.savez(f"{path}/rank{rank}.npz", T=T, fit=fit, rmse=rmse, iters=iters)
+    dist.destroy_process_group()
+
+
+def test_sharded_icp_protocol_matches_single_process(tmp_path):
+    world = 2
+    mp.spawn(_icp_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    src, tgt, nrm, _ = synth.icp_pair(4000, 6001, seed=21)
+    ref = I.registration_icp(src, tgt, 0.12, np.eye(4), tgt_normals=nrm, relative_fitness=-1,
+                             relative_rmse=-1, max_iteration=8)
+    r0 = np.load(tmp_path / "rank0.npz")
+    r1 = np.load(tmp_path / "rank1.npz")
+    np.testing.assert_array_equal(r0["T"], r1["T"])  # every rank holds the identical transform
+    np.testing.assert_allclose(r0["T"], ref["transformation"], atol=1e-10)
+    assert abs(float(r0["fit"]) - ref["fitness"]) < 1e-12
+    assert int(r0["iters"]) == 8
+
+
+def _ransac_worker(rank, world, port, path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    counts = np.load(f"{path}/counts.npy")
+    off, cnt = D.shard_bounds(len(counts), world, rank)
+    local = counts[off:off + cnt]
+    li = int(np.argmax(local))  # first max in this shard
+    key = torch.tensor([D.best_key(local[li], off + li)], dtype=torch.int64)
+    dist.all_reduce(key, op=dist.ReduceOp.MAX)
+    np.save(f"{path}/best{rank}.npy", np.array(D.unpack_best_key(int(key.item()))))
+    dist.destroy_process_group()
+
+
+def test_ransac_best_key_allreduce_first_max(tmp_path):
+    rng = np.random.default_rng(0)
+    counts = rng.integers(0, 50, 1001)
+    counts[[100, 700, 900]] = 77  # ties across both shards: the lowest id must win
+    np.save(tmp_path / "counts.npy", counts)
+    mp.spawn(_ransac_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert tuple(np.load(tmp_path / f"best{r}.npy")) == (77, 100)
+
+
+def test_key_packing_is_order_preserving():
+    rng = np.random.default_rng(1)
+    d2 = np.sort(rng.random(1000).astype(np.float32) * 10)
+    idx = rng.integers(0, 1 << 31, 1000)
+    k = D.pack_nn_key(d2, idx)
+    assert np.all(np.diff(k[np.argsort(d2, kind="stable")]) >= 0) or np.all(np.diff(k) >= 0)
+    dd, ii = D.unpack_nn_key(k)
+    np.testing.assert_array_equal(dd, d2)
+    np.testing.assert_array_equal(ii, idx)
+    assert D.pack_nn_key(np.float32(1.0), -1) == D.KEY_NONE
+    # equal distances: lower index wins under MIN
+    a = D.pack_nn_key(np.float32(0.5), 7)
+    b = D.pack_nn_key(np.float32(0.5), 3)
+    assert min(a, b) == b
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (100_000, 8), (7, 8)])
+def test_shard_bounds_cover(n, world):
+    spans = [D.shard_bounds(n, world, r) for r in range(world)]
+    assert spans[0][0] == 0
+    for (o1, c1), (o2, _) in zip(spans, spans[1:]):
+        assert o1 + c1 == o2
+    assert sum(c for _, c in spans) == n

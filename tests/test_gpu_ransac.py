@@ -134,7 +134,7 @@ def test_matcher_ransac_replay_equals_reference_loop(golden, pts5k):
     t = golden("loop_trajectory.npz")
     corr = pts5k["corr_mid"]
     np.random.seed(int(t["mid_seed"]))
-    res, info = M.ransac(pts5k["src"], pts5k["tgt"], corr, voxel_size=0.3,
+    res, info = M.run_ransac(pts5k["src"], pts5k["tgt"], corr, voxel_size=0.3,
                          max_iter=int(t["mid_max_iter"]))
     assert info["iterations"] == int(t["mid_iterations"])
     assert info["best_index"] == int(t["mid_best_index"])
