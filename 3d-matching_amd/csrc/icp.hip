@@ -6,10 +6,13 @@
 //
 // Kernels per iteration (all device resident, no host round trip):
 //   keyinit  O(Ns)      seeds each query's bound with its previous neighbour (fp32 d²)
-//   nn       O(Ns·Nt)   brute-force scan: queries in VGPRs (kNNQ per lane), targets streamed
+//   nn       O(Ns·Nt)   brute-force scan: queries in VGPRs (kNNQ = 4 per lane), targets streamed
 //                       through SGPRs by scalar loads (wave-uniform tile of kNNTile points).
-//                       Fast path per pair: 3 sub + 3 mul/fma + 1 min (v_min3 pairs them);
-//                       argmin bookkeeping only in the rare tiles whose minimum beats the bound.
+//                       Fast path per pair: a screen key |t|² − 2q·t = 3 FMA + ½ v_min3
+//                       (|t|² precomputed in t.w); tiles whose screen minimum cannot reach the
+//                       current bound (proven error bound, refresh_rt32) are skipped, the rest
+//                       take the exact path: direct fp32 d² (3 sub + mul + 2 FMA) with
+//                       lexicographic (d², index) argmin — the same result as a full direct scan.
 //                       The target range is split into slices (grid.y) so the chip is full;
 //                       slices merge with a 64-bit atomicMin on packed (bits(d²) << 32 | idx):
 //                       order independent → deterministic, lowest index wins exact ties.
@@ -20,13 +23,14 @@
 // The same keys/terms/solve pieces serve the target-sharded multi-GPU path (RCCL MIN on keys,
 // SUM on the 32 term slots between them).
 #include <float.h>
+#include <stdlib.h>
 
 #include "linalg.h"
 #include "m3d_internal.h"
 
 namespace m3d {
 
-constexpr int kNNQ = 2;
+constexpr int kNNQDefault = 4;  // queries per lane (M3D_NN_Q=1|2|4 overrides, tuning)
 constexpr int kNNTile = 16;
 constexpr int kNNBlock = 256;
 constexpr int kTermsBlock = 256;
@@ -66,6 +70,13 @@ __device__ void refresh_rt32(IcpState* s, const double* cs, const double* ct, do
                           2.0 * 1.7320508075688772 * E * r + 3.0 * E * E);
   float hi = __double2float_ru(s->r2 + e);
   s->r2_hi = isfinite(hi) ? hi : FLT_MAX;
+  // Screen bound: |fl(|t|² − 2q·t) − (d² − |q|²)| + rounding of thr ≤ eps,
+  // with |t|∞ ≤ qinf (target), |q|∞ ≤ Q = rowl1·pinf + |t'|∞ (query after the transform).
+  const double Q = rowl1 * pinf + tinf;
+  const double E1 = 5.0 * kU * (3.0 * qinf * qinf + 6.0 * Q * qinf);
+  const double es = 2.0 * (E1 + 6.0 * kU * (double)s->r2_hi + 12.0 * kU * Q * Q) + 1e-30;
+  const float esf = __double2float_ru(es);
+  s->screen_eps = isfinite(esf) ? esf : FLT_MAX;
 }
 
 struct FrameParams {
@@ -113,6 +124,7 @@ __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__
 }
 
 // ------------------------------------------------------------------------------- NN scan
+template <int kNNQ>
 __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__ src32, int64_t ns,
                                                       const Pt4 M3D_CONST* tgt,
                                                       int64_t nt_pad, int64_t slice_len,
@@ -122,7 +134,11 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
   float Rt[12];
   for (int k = 0; k < 12; ++k) Rt[k] = s->Rt32[k];
   const float r2_hi = s->r2_hi;
-  float qx[kNNQ], qy[kNNQ], qz[kNNQ], best[kNNQ];
+  const float eps = s->screen_eps;
+  // per query: q (exact-path coordinates), a = −2q (screen), qq = |q|², bound `best` (+ index)
+  // and the screen threshold thr = best − qq + eps.
+  float qx[kNNQ], qy[kNNQ], qz[kNNQ], ax[kNNQ], ay[kNNQ], az[kNNQ], qq[kNNQ], best[kNNQ],
+      thr[kNNQ];
   uint32_t bidx[kNNQ];
   int64_t qi[kNNQ];
 #pragma unroll
@@ -140,10 +156,15 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
         bidx[q] = (uint32_t)key;
       }
     } else {
-      qx[q] = qy[q] = qz[q] = 3.0e18f;  // far query: never beats its bound
-      best[q] = 0.0f;
+      qx[q] = qy[q] = qz[q] = 0.0f;  // inactive lane: negative bound, the screen never fires
+      best[q] = -1.0f;
       bidx[q] = 0xFFFFFFFFu;
     }
+    ax[q] = -2.0f * qx[q];
+    ay[q] = -2.0f * qy[q];
+    az[q] = -2.0f * qz[q];
+    qq[q] = fmaf(qz[q], qz[q], fmaf(qy[q], qy[q], qx[q] * qx[q]));
+    thr[q] = (best[q] - qq[q]) + eps;
   }
   uint32_t bidx0[kNNQ];
 #pragma unroll
@@ -151,20 +172,27 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
   const int64_t jb = (int64_t)blockIdx.y * slice_len;
   const int64_t je = min(nt_pad, jb + slice_len);
   for (int64_t j0 = jb; j0 < je; j0 += kNNTile) {
-    // tile minimum from +inf: `m <= best` then means some target of the tile is at least as
-    // close as the current bound (a strict improvement or an exact tie to resolve by index)
+    // Screen: key = |t|² − 2 q·t (3 FMA per pair, |t|² precomputed in t.w) differs from
+    // d² − |q|² by at most eps, so any target whose exact d² could reach `best` has
+    // key ≤ thr.  Tiles whose screen minimum stays above thr are skipped exactly.
     float m[kNNQ];
 #pragma unroll
     for (int q = 0; q < kNNQ; ++q) m[q] = FLT_MAX;
 #pragma unroll
     for (int k = 0; k < kNNTile; ++k) {
       const float tx = tgt[j0 + k].x, ty = tgt[j0 + k].y, tz = tgt[j0 + k].z;
+      // |t|² as the FMA addend must live in a VGPR (one SGPR operand per VALU op on gfx950):
+      // move it once per target and share it across the kNNQ queries of the lane
+      float tw;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(tw) : "s"(tgt[j0 + k].w));
 #pragma unroll
-      for (int q = 0; q < kNNQ; ++q) m[q] = fminf(m[q], d2f(qx[q], qy[q], qz[q], tx, ty, tz));
+      for (int q = 0; q < kNNQ; ++q)
+        m[q] = fminf(m[q], fmaf(ax[q], tx, fmaf(ay[q], ty, fmaf(az[q], tz, tw))));
     }
 #pragma unroll
     for (int q = 0; q < kNNQ; ++q) {
-      if (__any(m[q] <= best[q])) {
+      if (__any(m[q] <= thr[q])) {
+        // exact path: direct fp32 d², lexicographic (d², index) update
 #pragma unroll
         for (int k = 0; k < kNNTile; ++k) {
           const float tx = tgt[j0 + k].x, ty = tgt[j0 + k].y, tz = tgt[j0 + k].z;
@@ -175,6 +203,7 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
             bidx[q] = gj;
           }
         }
+        thr[q] = (best[q] - qq[q]) + eps;
       }
     }
   }
@@ -438,7 +467,12 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
   const int64_t ns = s->src->n;
   const int64_t nt_pad = s->tgt->n_pad;
   if (ns == 0 || s->tgt->n == 0) return hipSuccess;
-  const int64_t bx = (ns + kNNBlock * kNNQ - 1) / (kNNBlock * kNNQ);
+  static const int Q = [] {
+    const char* e = getenv("M3D_NN_Q");
+    const int v = e ? atoi(e) : kNNQDefault;
+    return (v == 1 || v == 2 || v == 4) ? v : kNNQDefault;
+  }();
+  const int64_t bx = (ns + kNNBlock * Q - 1) / (kNNBlock * Q);
   // fill ≥ 2048 blocks (8 per CU) by splitting the target range; keep slices ≥ 1024 targets
   int64_t S = (2048 + bx - 1) / bx;
   const int64_t max_s = nt_pad / 1024 > 0 ? nt_pad / 1024 : 1;
@@ -448,8 +482,13 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
   slice = (slice + kNNTile - 1) / kNNTile * kNNTile;
   S = (nt_pad + slice - 1) / slice;
   dim3 grid((unsigned)bx, (unsigned)S);
-  nn_kernel<<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, (const Pt4 M3D_CONST*)s->tgt->xyz32,
-                                       nt_pad, slice, off, s->state, s->keys);
+  const Pt4 M3D_CONST* tp = (const Pt4 M3D_CONST*)s->tgt->xyz32;
+  if (Q == 4)
+    nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
+  else if (Q == 2)
+    nn_kernel<2><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
+  else
+    nn_kernel<1><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
   return hipGetLastError();
 }
 

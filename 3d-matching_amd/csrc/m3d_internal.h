@@ -67,7 +67,7 @@ struct IcpState {
   int32_t converged;
   double r2;          // max_dist² (fp64, strict <)
   float r2_hi;        // fp32 search bound (≥ r2 plus guard)
-  float pad;
+  float screen_eps;   // NN screen error bound (icp.hip refresh_rt32)
 };
 
 constexpr int kTermSlots = 32;  // 21 JTJ + 6 JTr + r² + count + Σd² (+2 pad)

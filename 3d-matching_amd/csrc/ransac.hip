@@ -84,11 +84,14 @@ __global__ __launch_bounds__(256) void center_pack_kernel(const double* __restri
     float4 v;
     if (i < n) {
       double x = a[3 * i] - c0, y = a[3 * i + 1] - c1, z = a[3 * i + 2] - c2;
-      v = make_float4((float)x, (float)y, (float)z, 0.0f);
+      const float fx = (float)x, fy = (float)y, fz = (float)z;
+      // w = |x̃|² of the fp32-rounded coordinates (fp64, one rounding): the NN screen's |t|²
+      const double w = (double)fx * fx + (double)fy * fy + (double)fz * fz;
+      v = make_float4(fx, fy, fz, (float)w);
       double mm = maxinf ? fmax(fabs(x), fmax(fabs(y), fabs(z))) : sqrt(x * x + y * y + z * z);
       m = fmaxf(m, (float)mm * (1.0f + 1e-6f));
     } else {
-      v = make_float4(pad_value, pad_value, pad_value, 0.0f);
+      v = make_float4(pad_value, pad_value, pad_value, 3.0f * pad_value * pad_value);
     }
     out[i] = v;
   }
