@@ -31,7 +31,8 @@
 namespace m3d {
 
 constexpr int kNNQDefault = 4;  // queries per lane (M3D_NN_Q=1|2|4 overrides, tuning)
-constexpr int kNNTile = 16;
+constexpr int kNNTile = 16;   // screen sub-tile (one branch per sub-tile)
+constexpr int kNNLds = 512;   // targets per LDS tile (8 KB, double-buffered)
 constexpr int kNNBlock = 256;
 constexpr int kTermsBlock = 256;
 constexpr double kU = 5.9604644775390625e-08;
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__
 // ------------------------------------------------------------------------------- NN scan
 template <int kNNQ>
 __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__ src32, int64_t ns,
-                                                      const Pt4 M3D_CONST* tgt,
+                                                      const float4* __restrict__ tgt,
                                                       int64_t nt_pad, int64_t slice_len,
                                                       int64_t off, const IcpState* __restrict__ s,
                                                       int64_t* __restrict__ keys) {
@@ -169,43 +170,69 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
   uint32_t bidx0[kNNQ];
 #pragma unroll
   for (int q = 0; q < kNNQ; ++q) bidx0[q] = bidx[q];
+  // Targets are staged through LDS (double-buffered tiles of kNNLds points): every wave reads
+  // each target with one broadcast ds_read_b128 into VGPRs, so the FMAs have no SGPR operand
+  // (an SGPR source costs 1.65x issue time on gfx950, tools/ubench_valu.hip).
+  __shared__ float4 tile[2][kNNLds];
   const int64_t jb = (int64_t)blockIdx.y * slice_len;
   const int64_t je = min(nt_pad, jb + slice_len);
-  for (int64_t j0 = jb; j0 < je; j0 += kNNTile) {
-    // Screen: key = |t|² − 2 q·t (3 FMA per pair, |t|² precomputed in t.w) differs from
-    // d² − |q|² by at most eps, so any target whose exact d² could reach `best` has
-    // key ≤ thr.  Tiles whose screen minimum stays above thr are skipped exactly.
-    float m[kNNQ];
 #pragma unroll
-    for (int q = 0; q < kNNQ; ++q) m[q] = FLT_MAX;
+  for (int r = 0; r < kNNLds / kNNBlock; ++r)
+    tile[0][r * kNNBlock + threadIdx.x] = tgt[jb + r * kNNBlock + threadIdx.x];
+  __syncthreads();
+  int buf = 0;
+  for (int64_t j0 = jb; j0 < je; j0 += kNNLds) {
+    // next tile: global loads issued now, written to the other buffer after this tile
+    const bool has_next = j0 + kNNLds < je;
+    float4 pre[kNNLds / kNNBlock];
+    if (has_next) {
 #pragma unroll
-    for (int k = 0; k < kNNTile; ++k) {
-      const float tx = tgt[j0 + k].x, ty = tgt[j0 + k].y, tz = tgt[j0 + k].z;
-      // |t|² as the FMA addend must live in a VGPR (one SGPR operand per VALU op on gfx950):
-      // move it once per target and share it across the kNNQ queries of the lane
-      float tw;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(tw) : "s"(tgt[j0 + k].w));
-#pragma unroll
-      for (int q = 0; q < kNNQ; ++q)
-        m[q] = fminf(m[q], fmaf(ax[q], tx, fmaf(ay[q], ty, fmaf(az[q], tz, tw))));
+      for (int r = 0; r < kNNLds / kNNBlock; ++r) pre[r] = tgt[j0 + kNNLds + r * kNNBlock + threadIdx.x];
     }
+    const float4* tl = tile[buf];
+    for (int sb = 0; sb < kNNLds; sb += kNNTile) {
+      // Screen: key = |t|² − 2 q·t (3 FMA per pair, |t|² precomputed in t.w) differs from
+      // d² − |q|² by at most eps, so any target whose exact d² could reach `best` has
+      // key ≤ thr.  Sub-tiles whose screen minimum stays above thr are skipped exactly.
+      float m[kNNQ];
 #pragma unroll
-    for (int q = 0; q < kNNQ; ++q) {
-      if (__any(m[q] <= thr[q])) {
-        // exact path: direct fp32 d², lexicographic (d², index) update
+      for (int q = 0; q < kNNQ; ++q) m[q] = FLT_MAX;
 #pragma unroll
-        for (int k = 0; k < kNNTile; ++k) {
-          const float tx = tgt[j0 + k].x, ty = tgt[j0 + k].y, tz = tgt[j0 + k].z;
-          const float d2 = d2f(qx[q], qy[q], qz[q], tx, ty, tz);
-          const uint32_t gj = (uint32_t)(off + j0 + k);
-          if (d2 < best[q] || (d2 == best[q] && gj < bidx[q])) {
-            best[q] = d2;
-            bidx[q] = gj;
+      for (int k = 0; k < kNNTile; ++k) {
+        const float4 t = tl[sb + k];
+#pragma unroll
+        for (int q = 0; q < kNNQ; ++q)
+          m[q] = fminf(m[q], fmaf(ax[q], t.x, fmaf(ay[q], t.y, fmaf(az[q], t.z, t.w))));
+      }
+      // one (almost always not-taken) branch per sub-tile for all queries
+      bool hit = false;
+#pragma unroll
+      for (int q = 0; q < kNNQ; ++q) hit = hit || (m[q] <= thr[q]);
+      if (!__any(hit)) continue;
+#pragma unroll
+      for (int q = 0; q < kNNQ; ++q) {
+        if (__any(m[q] <= thr[q])) {
+          // exact path: direct fp32 d², lexicographic (d², index) update
+#pragma unroll
+          for (int k = 0; k < kNNTile; ++k) {
+            const float4 t = tl[sb + k];
+            const float d2 = d2f(qx[q], qy[q], qz[q], t.x, t.y, t.z);
+            const uint32_t gj = (uint32_t)(off + j0 + sb + k);
+            if (d2 < best[q] || (d2 == best[q] && gj < bidx[q])) {
+              best[q] = d2;
+              bidx[q] = gj;
+            }
           }
+          thr[q] = (best[q] - qq[q]) + eps;
         }
-        thr[q] = (best[q] - qq[q]) + eps;
       }
     }
+    if (has_next) {
+#pragma unroll
+      for (int r = 0; r < kNNLds / kNNBlock; ++r) tile[buf ^ 1][r * kNNBlock + threadIdx.x] = pre[r];
+    }
+    __syncthreads();
+    buf ^= 1;
   }
 #pragma unroll
   for (int q = 0; q < kNNQ; ++q) {
@@ -479,10 +506,10 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
   if (S > max_s) S = max_s;
   if (S < 1) S = 1;
   int64_t slice = (nt_pad + S - 1) / S;
-  slice = (slice + kNNTile - 1) / kNNTile * kNNTile;
+  slice = (slice + kNNLds - 1) / kNNLds * kNNLds;
   S = (nt_pad + slice - 1) / slice;
   dim3 grid((unsigned)bx, (unsigned)S);
-  const Pt4 M3D_CONST* tp = (const Pt4 M3D_CONST*)s->tgt->xyz32;
+  const float4* tp = s->tgt->xyz32;
   if (Q == 4)
     nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
   else if (Q == 2)

@@ -15,7 +15,8 @@ from pathlib import Path
 
 
 def short(name):
-    m = re.match(r"(?:m3d::)?([A-Za-z0-9_]+)", name.replace("_ZN3m3d", ""))
+    name = re.sub(r"^void ", "", name.replace("_ZN3m3d", ""))
+    m = re.match(r"(?:m3d::)?([A-Za-z0-9_]+(?:<[0-9]+>)?)", name)
     return m.group(1) if m else name[:40]
 
 
