@@ -8,8 +8,8 @@
 // Scoring design (VALU-bound, no dense contraction → no MFMA):
 //   * One lane holds kScoreK = 8 correspondences (centred fp32, 6 VGPRs each) for the whole block;
 //     a block of 4 waves covers 2048 correspondences and sweeps 64 hypotheses.
-//   * The hypothesis block (R, t', guard band: 64 B) is wave-uniform and read with scalar loads
-//     (constant address space) → its 12 floats are SGPR operands of the VALU ops.
+//   * The block's 64 hypothesis blocks (R, t', guard band: 64 B each) are staged in LDS and read
+//     with broadcast ds_read_b128 → VGPR operands (SGPR operands cost 1.65x issue time).
 //   * Per (hypothesis, correspondence): 12 ops for d = R p + t' − q, 3 for d², 2 compares.  The
 //     compares are folded into wave masks (v_cmp → s_bcnt1 → s_add): counting is scalar work.
 //   * Exactness: the fp32 screen counts d² < lo (certainly inside) and d² < hi (possibly inside);
@@ -208,19 +208,9 @@ __global__ __launch_bounds__(256) void hypf_from_T_kernel(const double* __restri
 }
 
 // ------------------------------------------------------------------------------- fp32 screen
-__device__ __forceinline__ void load_hyp(const HypF32 M3D_CONST* P, float v[14]) {
-#pragma unroll
-  for (int k = 0; k < 9; ++k) v[k] = P->r[k];
-  v[9] = P->t[0];
-  v[10] = P->t[1];
-  v[11] = P->t[2];
-  v[12] = P->lo;
-  v[13] = P->hi;
-}
-
 __global__ __launch_bounds__(kScoreBlock) void score_kernel(
     const float4* __restrict__ p32, const float4* __restrict__ q32,
-    const HypF32 M3D_CONST* hyp, int64_t H, int64_t hbase, int32_t* __restrict__ counts,
+    const float4* __restrict__ hyp4, int64_t H, int64_t hbase, int32_t* __restrict__ counts,
     AmbRecord* __restrict__ amb, int32_t* __restrict__ amb_count, int32_t amb_cap,
     int32_t* __restrict__ full_flag, int32_t* __restrict__ full_list,
     int32_t* __restrict__ full_count, const int32_t* __restrict__ done) {
@@ -240,17 +230,22 @@ __global__ __launch_bounds__(kScoreBlock) void score_kernel(
   const int64_t h0 = hbase + (int64_t)blockIdx.y * kScoreHyps;
   const int nh = (int)((H - h0) < kScoreHyps ? (H - h0) : kScoreHyps);
   int cnt = 0;
-  // software-prefetched hypothesis block: the scalar load of h+1 is in flight while h computes
-  float cur[14];
-  load_hyp(hyp + h0, cur);
+  // The block's 64 hypothesis blocks (4 KB) are staged in LDS once; each wave reads one with
+  // four broadcast ds_read_b128 into VGPRs, so the FMAs have no SGPR operand (an SGPR source
+  // costs 1.65x issue time on gfx950, tools/ubench_valu.hip).
+  __shared__ float4 hs[kScoreHyps * 4];
+  {
+    const int64_t hh = h0 + threadIdx.x / 4;
+    hs[threadIdx.x] = hh < H ? hyp4[hh * 4 + (threadIdx.x & 3)] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
   for (int hl = 0; hl < nh; ++hl) {
-    float nxt[14];
-    load_hyp(hyp + h0 + (hl + 1 < nh ? hl + 1 : hl), nxt);
-    const float r0 = cur[0], r1 = cur[1], r2 = cur[2];
-    const float r3 = cur[3], r4 = cur[4], r5 = cur[5];
-    const float r6 = cur[6], r7 = cur[7], r8 = cur[8];
-    const float t0 = cur[9], t1 = cur[10], t2 = cur[11];
-    const float lo_t = cur[12], hi_t = cur[13];
+    const float4 ha = hs[4 * hl], hb = hs[4 * hl + 1], hc = hs[4 * hl + 2], hd = hs[4 * hl + 3];
+    const float r0 = ha.x, r1 = ha.y, r2 = ha.z;
+    const float r3 = ha.w, r4 = hb.x, r5 = hb.y;
+    const float r6 = hb.z, r7 = hb.w, r8 = hc.x;
+    const float t0 = hc.y, t1 = hc.z, t2 = hc.w;
+    const float lo_t = hd.x, hi_t = hd.y;
     // all K distances first (independent chains), then the compares into independent masks,
     // so the VALU→SGPR→SALU hand-offs overlap instead of serialising on one mask register
     float d2[kScoreK];
@@ -275,8 +270,6 @@ __global__ __launch_bounds__(kScoreBlock) void score_kernel(
       band |= mband[k] & ~mlo[k];
     }
     const bool ambiguous = band != 0;
-#pragma unroll
-    for (int k = 0; k < 14; ++k) cur[k] = nxt[k];
     cnt = (lane == hl) ? (int)lo : cnt;
     if (ambiguous && lane == 0) {
       const int slot = atomicAdd(amb_count, 1);
@@ -548,7 +541,7 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
   for (int64_t hb = 0; hb < H; hb += per_launch) {
     const int64_t nh = (H - hb) < per_launch ? (H - hb) : per_launch;
     dim3 grid((unsigned)(cs->nc_pad / kBlockCorr), (unsigned)((nh + kScoreHyps - 1) / kScoreHyps));
-    score_kernel<<<grid, kScoreBlock, 0, st>>>(cs->p32, cs->q32, (const HypF32 M3D_CONST*)hypf, H,
+    score_kernel<<<grid, kScoreBlock, 0, st>>>(cs->p32, cs->q32, (const float4*)hypf, H,
                                                hb, counts, amb, amb_count, amb_cap, full_flag,
                                                full_list, full_count, done);
     hipError_t e = hipGetLastError();
