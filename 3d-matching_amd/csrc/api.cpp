@@ -352,7 +352,7 @@ int m3d_kabsch3_batch(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triple
   int rc = a.commit();
   if (rc) return rc;
   hipError_t e = launch_kabsch3(cs, triples, seed, hyp0, H, 0.0, T_out, status,
-                                a.at<HypF32>(o_h), nullptr, S(stream));
+                                a.at<HypF32>(o_h), nullptr, ZeroArgs{}, S(stream));
   if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   return M3D_OK;
 }
@@ -396,10 +396,9 @@ double thr_sq_of(double thr, int mode) { return mode == M3D_SCORE_SQUARED ? thr 
 hipError_t score_enqueue(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64_t H,
                          double thr, int mode, int32_t* counts, const ScoreScratch& s,
                          const int32_t* done, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(counts, 0, sizeof(int32_t) * H, st);
-  if (e == hipSuccess) e = hipMemsetAsync(s.ctr, 0, sizeof(int32_t) * 64, st);
-  if (e == hipSuccess) e = hipMemsetAsync(s.full_flag, 0, sizeof(int32_t) * H, st);
-  if (e == hipSuccess) {
+  // counts / full_flag / record counters were zeroed by the preceding kabsch3 or hypf kernel
+  hipError_t e = hipSuccess;
+  {
     KTimer kt(ctx, M3D_KERNEL_SCORE, st);
     e = launch_score(cs, s.hypf, H, counts, s.amb, s.ctr, s.amb_cap, s.full_flag, s.full_list,
                      s.ctr + 1, done, st);
@@ -430,7 +429,8 @@ int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64
   int rc = a.commit();
   if (rc) return rc;
   ScoreScratch s = score_bind(a, o, H);
-  hipError_t e = launch_hypf_from_T(cs, T, H, thr_sq_of(thr, mode), s.hypf, st);
+  hipError_t e = launch_hypf_from_T(cs, T, H, thr_sq_of(thr, mode), s.hypf,
+                                    ZeroArgs{counts, s.full_flag, s.ctr}, st);
   if (e == hipSuccess) e = score_enqueue(ctx, cs, T, H, thr, mode, counts, s, nullptr, st);
   if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   return M3D_OK;
@@ -450,8 +450,8 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   const int64_t max_iter = p->max_iter;
   int64_t B = p->batch;
   if (B <= 0) {
-    // ~2e8 pair evaluations per batch keeps the chip busy; early stop wants small first batches
-    B = nc > 0 ? std::max<int64_t>(1024, (int64_t)2e8 / std::max<int64_t>(nc, 1)) : 1024;
+    // ~1e9 pair evaluations per batch amortise the per-batch launches; early stop caps it
+    B = nc > 0 ? std::max<int64_t>(1024, (int64_t)1e9 / std::max<int64_t>(nc, 1)) : 1024;
     if (p->early_stop) B = std::min<int64_t>(B, 16384);
   }
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(max_iter, 1)));
@@ -482,7 +482,8 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
     hipError_t e;
     {
       KTimer kt(ctx, M3D_KERNEL_KABSCH, st);
-      e = launch_kabsch3(cs, tri, p->seed, p->hyp0 + b0, n, thr_sq, Tb, nullptr, s.hypf, done, st);
+      e = launch_kabsch3(cs, tri, p->seed, p->hyp0 + b0, n, thr_sq, Tb, nullptr, s.hypf, done,
+                         ZeroArgs{cnt, s.full_flag, s.ctr}, st);
     }
     if (e == hipSuccess) {
       if (nc > 0)

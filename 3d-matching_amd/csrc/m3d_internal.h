@@ -39,8 +39,15 @@ struct alignas(16) Pt4 {
 struct AmbRecord {
   int32_t hyp;    // hypothesis index within the batch
   int32_t chunk;  // wave chunk (kScoreK*64 correspondences)
-  int32_t lo;     // screen count already added for this chunk
-  int32_t pad;
+  int32_t lo;     // screen count of the masked groups (already added to the total)
+  int32_t mask;   // bit k: 64-pair group k of the chunk holds a pair inside the guard band
+};
+
+// Per-batch scoring state zeroed by the kernel that runs before the screen.
+struct ZeroArgs {
+  int32_t* counts = nullptr;
+  int32_t* full_flag = nullptr;
+  int32_t* ctr = nullptr;  // [0] ambiguous-record count, [1] full-recheck count
 };
 
 // Running state of the a4 loop across batches (device resident).
@@ -156,9 +163,9 @@ hipError_t launch_center_pack(const double* a, int64_t n, int64_t n_pad, const d
                               int maxinf, hipStream_t st);
 hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_t seed,
                           int64_t hyp0, int64_t H, double thr_sq, double* T_out, uint8_t* status,
-                          HypF32* hypf, const int32_t* done, hipStream_t st);
+                          HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st);
 hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
-                              HypF32* hypf, hipStream_t st);
+                              HypF32* hypf, ZeroArgs z, hipStream_t st);
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
                         AmbRecord* amb, int32_t* amb_count, int32_t amb_cap, int32_t* full_flag,
                         int32_t* full_list, int32_t* full_count, const int32_t* done,

@@ -161,6 +161,16 @@ __device__ HypF32 make_hypf(const double* T, const GuardParams& g) {
   return hp;
 }
 
+// Zero the per-batch scoring state in the kernel that precedes the screen (saves 3 memset
+// launches per batch): counts[h], full_flag[h], and the two record counters.
+__device__ __forceinline__ void zero_scoring_state(const ZeroArgs& z, int64_t h, int64_t H) {
+  if (h < H) {
+    if (z.counts) z.counts[h] = 0;
+    if (z.full_flag) z.full_flag[h] = 0;
+  }
+  if (h == 0 && z.ctr) z.ctr[0] = z.ctr[1] = 0;
+}
+
 __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__ p64,
                                                       const double* __restrict__ q64, int64_t nc,
                                                       const int32_t* __restrict__ triples,
@@ -168,9 +178,11 @@ __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__
                                                       GuardParams g, double* __restrict__ T_out,
                                                       uint8_t* __restrict__ status,
                                                       HypF32* __restrict__ hypf,
-                                                      const int32_t* __restrict__ done) {
+                                                      const int32_t* __restrict__ done,
+                                                      ZeroArgs z) {
   if (done != nullptr && *done) return;
   const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  zero_scoring_state(z, h, H);
   if (h >= H) return;
   double T[16];
   int st = M3D_HYP_OK;
@@ -202,8 +214,9 @@ __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__
 
 __global__ __launch_bounds__(256) void hypf_from_T_kernel(const double* __restrict__ T, int64_t H,
                                                           GuardParams g,
-                                                          HypF32* __restrict__ hypf) {
+                                                          HypF32* __restrict__ hypf, ZeroArgs z) {
   const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  zero_scoring_state(z, h, H);
   if (h < H) hypf[h] = make_hypf(T + 16 * h, g);
 }
 
@@ -272,13 +285,22 @@ __global__ __launch_bounds__(kScoreBlock) void score_kernel(
     const bool ambiguous = band != 0;
     cnt = (lane == hl) ? (int)lo : cnt;
     if (ambiguous && lane == 0) {
+      // rare: record which 64-pair groups hold a band pair and their screen count
+      uint32_t gmask = 0, lo_amb = 0;
+#pragma unroll
+      for (int k = 0; k < kScoreK; ++k) {
+        if (mband[k] & ~mlo[k]) {
+          gmask |= 1u << k;
+          lo_amb += (uint32_t)__popcll(mlo[k]);
+        }
+      }
       const int slot = atomicAdd(amb_count, 1);
       if (slot < amb_cap) {
         AmbRecord r;
         r.hyp = (int32_t)(h0 + hl);
         r.chunk = (int32_t)chunk;
-        r.lo = (int32_t)lo;
-        r.pad = 0;
+        r.lo = (int32_t)lo_amb;
+        r.mask = (int32_t)gmask;
         amb[slot] = r;
       } else if (atomicExch(&full_flag[h0 + hl], 1) == 0) {
         full_list[atomicAdd(full_count, 1)] = (int32_t)(h0 + hl);
@@ -321,16 +343,18 @@ __global__ __launch_bounds__(256) void recheck_chunk_kernel(
     const AmbRecord rec = amb[r];
     double Th[12];
     for (int k = 0; k < 12; ++k) Th[k] = T[16 * (int64_t)rec.hyp + k];
-    int exact = 0;
+    int exact = 0, groups = 0;
     for (int k = 0; k < kScoreK; ++k) {
+      if (!((rec.mask >> k) & 1)) continue;  // group fully decided by the screen
       const int64_t i = (int64_t)rec.chunk * kChunk + k * kWave + lane;
       bool in = false;
       if (i < nc) in = exact_inlier(Th, p64 + 3 * i, q64 + 3 * i, thr, mode);
       exact += __popcll(__ballot(in));
+      ++groups;
     }
     if (lane == 0) {
       atomicAdd(&counts[rec.hyp], exact - rec.lo);
-      atomicAdd((unsigned long long*)&stats[0], (unsigned long long)kChunk);
+      atomicAdd((unsigned long long*)&stats[0], (unsigned long long)(groups * kWave));
     }
   }
 }
@@ -517,18 +541,18 @@ static GuardParams guard_of(const m3d_corrset* cs, double thr_sq) {
 
 hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_t seed,
                           int64_t hyp0, int64_t H, double thr_sq, double* T_out, uint8_t* status,
-                          HypF32* hypf, const int32_t* done, hipStream_t st) {
+                          HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st) {
   if (H == 0) return hipSuccess;
   kabsch3_kernel<<<blocks_for(H, 256), 256, 0, st>>>(cs->p64, cs->q64, cs->nc, triples, seed,
                                                      hyp0, H, guard_of(cs, thr_sq), T_out, status,
-                                                     hypf, done);
+                                                     hypf, done, z);
   return hipGetLastError();
 }
 
 hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
-                              HypF32* hypf, hipStream_t st) {
+                              HypF32* hypf, ZeroArgs z, hipStream_t st) {
   if (H == 0) return hipSuccess;
-  hypf_from_T_kernel<<<blocks_for(H, 256), 256, 0, st>>>(T, H, guard_of(cs, thr_sq), hypf);
+  hypf_from_T_kernel<<<blocks_for(H, 256), 256, 0, st>>>(T, H, guard_of(cs, thr_sq), hypf, z);
   return hipGetLastError();
 }
 
