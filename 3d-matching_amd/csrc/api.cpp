@@ -361,52 +361,23 @@ int m3d_kabsch3_batch(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triple
 namespace {
 struct ScoreScratch {
   HypF32* hypf;
-  AmbRecord* amb;
-  int32_t* ctr;  // [0] amb_count [1] full_count
-  int32_t* full_flag;
-  int32_t* full_list;
-  int32_t amb_cap;
 };
 
-size_t score_layout(Arena& a, int64_t H, size_t* o) {
-  const int64_t Hn = std::max<int64_t>(H, 1);
-  o[0] = a.take(sizeof(HypF32) * Hn);
-  o[1] = a.take(sizeof(AmbRecord) * (size_t)std::min<int64_t>(std::max<int64_t>(4 * Hn, 1 << 16), 1 << 22));
-  o[2] = a.take(sizeof(int32_t) * 64);
-  o[3] = a.take(sizeof(int32_t) * Hn);
-  o[4] = a.take(sizeof(int32_t) * Hn);
-  return 0;
+void score_layout(Arena& a, int64_t H, size_t* o) {
+  o[0] = a.take(sizeof(HypF32) * std::max<int64_t>(H, 1));
 }
 
-ScoreScratch score_bind(const Arena& a, const size_t* o, int64_t H) {
-  const int64_t Hn = std::max<int64_t>(H, 1);
-  ScoreScratch s;
-  s.hypf = a.at<HypF32>(o[0]);
-  s.amb = a.at<AmbRecord>(o[1]);
-  s.ctr = a.at<int32_t>(o[2]);
-  s.full_flag = a.at<int32_t>(o[3]);
-  s.full_list = a.at<int32_t>(o[4]);
-  s.amb_cap = (int32_t)std::min<int64_t>(std::max<int64_t>(4 * Hn, 1 << 16), 1 << 22);
-  return s;
-}
+ScoreScratch score_bind(const Arena& a, const size_t* o) { return ScoreScratch{a.at<HypF32>(o[0])}; }
 
 double thr_sq_of(double thr, int mode) { return mode == M3D_SCORE_SQUARED ? thr : thr * thr; }
 
-// score H transforms T (device) whose fp32 blocks are already in s.hypf
+// score H transforms T (device) whose fp32 blocks are already in s.hypf and whose counts were
+// zeroed by the kernel that produced them
 hipError_t score_enqueue(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64_t H,
                          double thr, int mode, int32_t* counts, const ScoreScratch& s,
                          const int32_t* done, hipStream_t st) {
-  // counts / full_flag / record counters were zeroed by the preceding kabsch3 or hypf kernel
-  hipError_t e = hipSuccess;
-  {
-    KTimer kt(ctx, M3D_KERNEL_SCORE, st);
-    e = launch_score(cs, s.hypf, H, counts, s.amb, s.ctr, s.amb_cap, s.full_flag, s.full_list,
-                     s.ctr + 1, done, st);
-  }
-  if (e == hipSuccess)
-    e = launch_recheck(cs, T, H, thr, mode, counts, s.amb, s.ctr, s.amb_cap, s.full_list, s.ctr + 1,
-                       ctx->stats, done, st);
-  return e;
+  KTimer kt(ctx, M3D_KERNEL_SCORE, st);
+  return launch_score(cs, s.hypf, H, counts, T, thr, mode, ctx->stats, done, st);
 }
 }  // namespace
 
@@ -424,13 +395,12 @@ int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64
     return M3D_OK;
   }
   Arena a(ctx);
-  size_t o[5];
+  size_t o[1];
   score_layout(a, H, o);
   int rc = a.commit();
   if (rc) return rc;
-  ScoreScratch s = score_bind(a, o, H);
-  hipError_t e = launch_hypf_from_T(cs, T, H, thr_sq_of(thr, mode), s.hypf,
-                                    ZeroArgs{counts, s.full_flag, s.ctr}, st);
+  ScoreScratch s = score_bind(a, o);
+  hipError_t e = launch_hypf_from_T(cs, T, H, thr_sq_of(thr, mode), s.hypf, ZeroArgs{counts}, st);
   if (e == hipSuccess) e = score_enqueue(ctx, cs, T, H, thr, mode, counts, s, nullptr, st);
   if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   return M3D_OK;
@@ -456,13 +426,13 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   }
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(max_iter, 1)));
   Arena a(ctx);
-  size_t o[5];
+  size_t o[1];
   score_layout(a, B, o);
   size_t o_T = a.take(sizeof(double) * 16 * B);
   size_t o_c = a.take(sizeof(int32_t) * B);
   int rc = a.commit();
   if (rc) return rc;
-  ScoreScratch s = score_bind(a, o, B);
+  ScoreScratch s = score_bind(a, o);
   double* Tb = a.at<double>(o_T);
   int32_t* cb = a.at<int32_t>(o_c);
   RansacState init;
@@ -473,6 +443,8 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   init.iterations = 0;
   init.done = (max_iter == 0) ? 1 : 0;
   HIPX(ctx, hipMemcpyAsync(ctx->rstate, &init, sizeof(init), hipMemcpyHostToDevice, st));
+  HIPX(ctx, hipMemcpyAsync(&ctx->rstate->rechecked, ctx->stats, sizeof(int64_t),
+                           hipMemcpyDeviceToDevice, st));
   const int32_t* done = &ctx->rstate->done;
   const double thr_sq = thr_sq_of(p->thr, p->mode);
   for (int64_t b0 = 0; b0 < max_iter; b0 += B) {
@@ -483,7 +455,7 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
     {
       KTimer kt(ctx, M3D_KERNEL_KABSCH, st);
       e = launch_kabsch3(cs, tri, p->seed, p->hyp0 + b0, n, thr_sq, Tb, nullptr, s.hypf, done,
-                         ZeroArgs{cnt, s.full_flag, s.ctr}, st);
+                         ZeroArgs{cnt}, st);
     }
     if (e == hipSuccess) {
       if (nc > 0)
@@ -496,7 +468,7 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
                         p->es_threshold, p->es_confidence, Tb, ctx->rstate, st);
     if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   }
-  hipError_t e = launch_copy_result(ctx->rstate, nc, result_dev, st);
+  hipError_t e = launch_copy_result(ctx->rstate, nc, ctx->stats, result_dev, st);
   if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   return M3D_OK;
 }

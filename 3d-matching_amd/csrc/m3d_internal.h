@@ -35,19 +35,9 @@ struct alignas(16) Pt4 {
   float x, y, z, w;
 };
 
-// Ambiguous (hypothesis, correspondence chunk) record of the fp32 screen.
-struct AmbRecord {
-  int32_t hyp;    // hypothesis index within the batch
-  int32_t chunk;  // wave chunk (kScoreK*64 correspondences)
-  int32_t lo;     // screen count of the masked groups (already added to the total)
-  int32_t mask;   // bit k: 64-pair group k of the chunk holds a pair inside the guard band
-};
-
 // Per-batch scoring state zeroed by the kernel that runs before the screen.
 struct ZeroArgs {
   int32_t* counts = nullptr;
-  int32_t* full_flag = nullptr;
-  int32_t* ctr = nullptr;  // [0] ambiguous-record count, [1] full-recheck count
 };
 
 // Running state of the a4 loop across batches (device resident).
@@ -167,18 +157,13 @@ hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_
 hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
                               HypF32* hypf, ZeroArgs z, hipStream_t st);
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
-                        AmbRecord* amb, int32_t* amb_count, int32_t amb_cap, int32_t* full_flag,
-                        int32_t* full_list, int32_t* full_count, const int32_t* done,
-                        hipStream_t st);
-hipError_t launch_recheck(const m3d_corrset* cs, const double* T, int64_t H, double thr, int mode,
-                          int32_t* counts, const AmbRecord* amb, const int32_t* amb_count,
-                          int32_t amb_cap, const int32_t* full_list, const int32_t* full_count,
-                          int64_t* stats, const int32_t* done, hipStream_t st);
+                        const double* T64, double thr, int mode, int64_t* stats,
+                        const int32_t* done, hipStream_t st);
 hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int64_t nc,
                          int64_t max_iter, int early_stop, double es_thr, double es_conf,
                          const double* T_batch, RansacState* rs, hipStream_t st);
-hipError_t launch_copy_result(const RansacState* rs, int64_t nc, m3d_ransac_result* out_dev,
-                              hipStream_t st);
+hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* stats,
+                              m3d_ransac_result* out_dev, hipStream_t st);
 
 // ICP
 hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_t st);

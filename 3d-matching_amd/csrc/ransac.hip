@@ -2,7 +2,7 @@
 //
 // Reference path (all CPU, numpy fp64):
 //   compute_step_transformation  src/matcher/ransac.py:104-192   → kabsch3_kernel
-//   evaluate_inlier_ratio[_fast] src/matcher/ransac.py:195-277   → score_kernel + recheck kernels
+//   evaluate_inlier_ratio[_fast] src/matcher/ransac.py:195-277   → score_kernel (fp64 recheck inline)
 //   step-RANSAC loop             _visualize_matcher.py:343-470   → select_kernel (batched, on device)
 //
 // Scoring design (VALU-bound, no dense contraction → no MFMA):
@@ -12,10 +12,10 @@
 //     with broadcast ds_read_b128 → VGPR operands (SGPR operands cost 1.65x issue time).
 //   * Per (hypothesis, correspondence): 12 ops for d = R p + t' − q, 3 for d², 2 compares.  The
 //     compares are folded into wave masks (v_cmp → s_bcnt1 → s_add): counting is scalar work.
-//   * Exactness: the fp32 screen counts d² < lo (certainly inside) and d² < hi (possibly inside);
-//     lo/hi bracket thr² by a rounding-error bound proven in DESIGN.md §3.2.  Chunks where the two
-//     counts differ are re-evaluated in fp64 with numpy's operation order (recheck kernels), so the
-//     final counts equal an fp64 evaluation of the reference formula.
+//   * Exactness: the fp32 screen counts d² < lo (certainly inside) and flags lo ≤ d² < hi; lo/hi
+//     bracket thr² by a rounding-error bound.  A flagged 64-pair group is
+//     re-evaluated in fp64 with numpy's operation order inside the same kernel (rare branch), so
+//     the counts equal an fp64 evaluation of the reference formula.
 //   * Counts are integers: atomics are exact and order-independent → deterministic results.
 #include <float.h>
 
@@ -146,12 +146,15 @@ __device__ HypF32 make_hypf(const double* T, const GuardParams& g) {
     rowl1 = fmax(rowl1, fabs(r[0]) + fabs(r[1]) + fabs(r[2]));
     tinf = fmax(tinf, fabs(tp[i]));
   }
-  // Per-component error of the fp32 evaluation:  E ≤ 8u(‖r‖₁|p|∞ + |t'| + |q|∞)
-  const double E = 8.0 * kU32 * (rowl1 * g.pinf + tinf + g.qinf);
+  // Per-component error of the fp32 evaluation d = fma(r0,p0,fma(r1,p1,fma(r2,p2,t'−q)))
+  // (DESIGN.md §3.2): inputs (p, q, R, t' rounded to fp32) 2S + |t'| + |q|, the four roundings
+  // |t'−q| + |a1| + |a2| + |d| ≤ 2S + 3(|t'| + |q|) + thr  →  E ≤ u(4S + 4|t'| + 4|q| + thr),
+  // S = Σ|r_j||p_j| ≤ ‖r‖₁|p|∞.  (1 + 1e-3) absorbs the O(u²) terms.
   const double thr = sqrt(g.thr_sq);
+  const double E = kU32 * (4.0 * rowl1 * g.pinf + 4.0 * tinf + 4.0 * g.qinf + thr) * 1.001;
   double eps = 3.0 * kU32 * (thr + 1.7320508075688772 * E) * (thr + 1.7320508075688772 * E) +
                2.0 * 1.7320508075688772 * E * thr + 3.0 * E * E;
-  eps = 2.0 * eps + 4.0 * DBL_EPSILON * g.thr_sq;
+  eps = 1.25 * eps + 4.0 * DBL_EPSILON * g.thr_sq;
   double lo = g.thr_sq - eps, hi = g.thr_sq + eps;
   if (!(lo > 0.0)) lo = 0.0;
   hp.lo = __double2float_rd(lo);
@@ -161,14 +164,9 @@ __device__ HypF32 make_hypf(const double* T, const GuardParams& g) {
   return hp;
 }
 
-// Zero the per-batch scoring state in the kernel that precedes the screen (saves 3 memset
-// launches per batch): counts[h], full_flag[h], and the two record counters.
+// Zero the per-batch counts in the kernel that precedes the screen (saves a memset launch).
 __device__ __forceinline__ void zero_scoring_state(const ZeroArgs& z, int64_t h, int64_t H) {
-  if (h < H) {
-    if (z.counts) z.counts[h] = 0;
-    if (z.full_flag) z.full_flag[h] = 0;
-  }
-  if (h == 0 && z.ctr) z.ctr[0] = z.ctr[1] = 0;
+  if (h < H && z.counts) z.counts[h] = 0;
 }
 
 __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__ p64,
@@ -220,13 +218,34 @@ __global__ __launch_bounds__(256) void hypf_from_T_kernel(const double* __restri
   if (h < H) hypf[h] = make_hypf(T + 16 * h, g);
 }
 
+// ------------------------------------------------------------------------------- fp64 recheck
+// numpy order (verified in the build container): p @ R.T is fma(r2,z,fma(r1,y,r0*x)), then + t,
+// (.)**2 summed left to right; evaluate_inlier_ratio takes sqrt of the same sum.
+__device__ __forceinline__ bool exact_inlier(const double* T, const double* p, const double* q,
+                                             double thr, int mode) {
+  const double x = fma(T[2], p[2], fma(T[1], p[1], T[0] * p[0])) + T[3];
+  const double y = fma(T[6], p[2], fma(T[5], p[1], T[4] * p[0])) + T[7];
+  const double z = fma(T[10], p[2], fma(T[9], p[1], T[8] * p[0])) + T[11];
+  const double dx = x - q[0], dy = y - q[1], dz = z - q[2];
+  const double s = (dx * dx + dy * dy) + dz * dz;
+  return mode == M3D_SCORE_SQUARED ? (s < thr) : (sqrt(s) < thr);
+}
+
 // ------------------------------------------------------------------------------- fp32 screen
+struct ExactArgs {
+  const double* T64;  // [H][16] fp64 transforms of the batch
+  const double* p64;  // [nc][3]
+  const double* q64;  // [nc][3]
+  int64_t nc;
+  double thr;
+  int mode;
+  int64_t* stats;  // [0] pairs re-evaluated in fp64
+};
+
 __global__ __launch_bounds__(kScoreBlock) void score_kernel(
     const float4* __restrict__ p32, const float4* __restrict__ q32,
     const float4* __restrict__ hyp4, int64_t H, int64_t hbase, int32_t* __restrict__ counts,
-    AmbRecord* __restrict__ amb, int32_t* __restrict__ amb_count, int32_t amb_cap,
-    int32_t* __restrict__ full_flag, int32_t* __restrict__ full_list,
-    int32_t* __restrict__ full_count, const int32_t* __restrict__ done) {
+    ExactArgs ex, const int32_t* __restrict__ done) {
   if (done != nullptr && *done) return;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
@@ -282,30 +301,27 @@ __global__ __launch_bounds__(kScoreBlock) void score_kernel(
       lo += (uint32_t)__popcll(mlo[k]);
       band |= mband[k] & ~mlo[k];
     }
-    const bool ambiguous = band != 0;
-    cnt = (lane == hl) ? (int)lo : cnt;
-    if (ambiguous && lane == 0) {
-      // rare: record which 64-pair groups hold a band pair and their screen count
-      uint32_t gmask = 0, lo_amb = 0;
+    if (band != 0) {
+      // rare (wave-uniform): a 64-pair group holds a pair inside the guard band — re-evaluate
+      // that group in fp64 with numpy's operation order and replace its screen count.  The
+      // dependent loads stall only this wave; the SIMD's other waves keep the VALU busy.
+      double Th[12];
+#pragma unroll
+      for (int k = 0; k < 12; ++k) Th[k] = ex.T64[16 * (h0 + hl) + k];
+      int groups = 0;
 #pragma unroll
       for (int k = 0; k < kScoreK; ++k) {
         if (mband[k] & ~mlo[k]) {
-          gmask |= 1u << k;
-          lo_amb += (uint32_t)__popcll(mlo[k]);
+          const int64_t i = chunk * kChunk + k * kWave + lane;
+          const bool in = i < ex.nc && exact_inlier(Th, ex.p64 + 3 * i, ex.q64 + 3 * i, ex.thr, ex.mode);
+          lo += (uint32_t)__popcll(__ballot(in)) - (uint32_t)__popcll(mlo[k]);
+          ++groups;
         }
       }
-      const int slot = atomicAdd(amb_count, 1);
-      if (slot < amb_cap) {
-        AmbRecord r;
-        r.hyp = (int32_t)(h0 + hl);
-        r.chunk = (int32_t)chunk;
-        r.lo = (int32_t)lo_amb;
-        r.mask = (int32_t)gmask;
-        amb[slot] = r;
-      } else if (atomicExch(&full_flag[h0 + hl], 1) == 0) {
-        full_list[atomicAdd(full_count, 1)] = (int32_t)(h0 + hl);
-      }
+      if (lane == 0 && ex.stats)
+        atomicAdd((unsigned long long*)&ex.stats[0], (unsigned long long)(groups * kWave));
     }
+    cnt = (lane == hl) ? (int)lo : cnt;
   }
   __shared__ int red[4][kWave];
   red[wave][lane] = cnt;
@@ -313,78 +329,6 @@ __global__ __launch_bounds__(kScoreBlock) void score_kernel(
   if (threadIdx.x < nh) {
     const int t = threadIdx.x;
     atomicAdd(&counts[h0 + t], red[0][t] + red[1][t] + red[2][t] + red[3][t]);
-  }
-}
-
-// ------------------------------------------------------------------------------- fp64 recheck
-// numpy order (verified in the build container): p @ R.T is fma(r2,z,fma(r1,y,r0*x)), then + t,
-// (.)**2 summed left to right; evaluate_inlier_ratio takes sqrt of the same sum.
-__device__ __forceinline__ bool exact_inlier(const double* T, const double* p, const double* q,
-                                             double thr, int mode) {
-  const double x = fma(T[2], p[2], fma(T[1], p[1], T[0] * p[0])) + T[3];
-  const double y = fma(T[6], p[2], fma(T[5], p[1], T[4] * p[0])) + T[7];
-  const double z = fma(T[10], p[2], fma(T[9], p[1], T[8] * p[0])) + T[11];
-  const double dx = x - q[0], dy = y - q[1], dz = z - q[2];
-  const double s = (dx * dx + dy * dy) + dz * dz;
-  return mode == M3D_SCORE_SQUARED ? (s < thr) : (sqrt(s) < thr);
-}
-
-__global__ __launch_bounds__(256) void recheck_chunk_kernel(
-    const double* __restrict__ p64, const double* __restrict__ q64, int64_t nc,
-    const double* __restrict__ T, double thr, int mode, int32_t* __restrict__ counts,
-    const AmbRecord* __restrict__ amb, const int32_t* __restrict__ amb_count, int32_t amb_cap,
-    int64_t* __restrict__ stats, const int32_t* __restrict__ done) {
-  if (done != nullptr && *done) return;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t nrec = min(*amb_count, amb_cap);
-  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) / kWave;
-  for (int64_t r = wid; r < nrec; r += nw) {
-    const AmbRecord rec = amb[r];
-    double Th[12];
-    for (int k = 0; k < 12; ++k) Th[k] = T[16 * (int64_t)rec.hyp + k];
-    int exact = 0, groups = 0;
-    for (int k = 0; k < kScoreK; ++k) {
-      if (!((rec.mask >> k) & 1)) continue;  // group fully decided by the screen
-      const int64_t i = (int64_t)rec.chunk * kChunk + k * kWave + lane;
-      bool in = false;
-      if (i < nc) in = exact_inlier(Th, p64 + 3 * i, q64 + 3 * i, thr, mode);
-      exact += __popcll(__ballot(in));
-      ++groups;
-    }
-    if (lane == 0) {
-      atomicAdd(&counts[rec.hyp], exact - rec.lo);
-      atomicAdd((unsigned long long*)&stats[0], (unsigned long long)(groups * kWave));
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void recheck_full_kernel(
-    const double* __restrict__ p64, const double* __restrict__ q64, int64_t nc,
-    const double* __restrict__ T, double thr, int mode, int32_t* __restrict__ counts,
-    const int32_t* __restrict__ full_list, const int32_t* __restrict__ full_count,
-    int64_t* __restrict__ stats, const int32_t* __restrict__ done) {
-  if (done != nullptr && *done) return;
-  __shared__ int red[256];
-  const int n = *full_count;
-  for (int e = blockIdx.x; e < n; e += gridDim.x) {
-    const int h = full_list[e];
-    double Th[12];
-    for (int k = 0; k < 12; ++k) Th[k] = T[16 * (int64_t)h + k];
-    int c = 0;
-    for (int64_t i = threadIdx.x; i < nc; i += 256)
-      c += exact_inlier(Th, p64 + 3 * i, q64 + 3 * i, thr, mode) ? 1 : 0;
-    red[threadIdx.x] = c;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      counts[h] = red[0];
-      atomicAdd((unsigned long long*)&stats[1], (unsigned long long)nc);
-    }
-    __syncthreads();
   }
 }
 
@@ -493,6 +437,7 @@ __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict_
 }
 
 __global__ void copy_result_kernel(const RansacState* __restrict__ rs, int64_t nc,
+                                   const int64_t* __restrict__ stats,
                                    m3d_ransac_result* __restrict__ out) {
   if (threadIdx.x != 0) return;
   for (int k = 0; k < 16; ++k) out->T[k] = rs->T_best[k];
@@ -500,7 +445,8 @@ __global__ void copy_result_kernel(const RansacState* __restrict__ rs, int64_t n
   out->best_index = rs->best_index;
   out->iterations = rs->iterations;
   out->fitness = nc > 0 ? (double)rs->best_count / (double)nc : 0.0;
-  out->rechecked = rs->rechecked;
+  // rs->rechecked holds the recheck counter's value when the run started
+  out->rechecked = stats ? stats[0] - rs->rechecked : 0;
 }
 
 // ------------------------------------------------------------------------------- launchers
@@ -557,35 +503,20 @@ hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H,
 }
 
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
-                        AmbRecord* amb, int32_t* amb_count, int32_t amb_cap, int32_t* full_flag,
-                        int32_t* full_list, int32_t* full_count, const int32_t* done,
-                        hipStream_t st) {
+                        const double* T64, double thr, int mode, int64_t* stats,
+                        const int32_t* done, hipStream_t st) {
   if (H == 0 || cs->nc == 0) return hipSuccess;
+  ExactArgs ex{T64, cs->p64, cs->q64, cs->nc, thr, mode, stats};
   const int64_t per_launch = (int64_t)65535 * kScoreHyps;  // grid.y limit
   for (int64_t hb = 0; hb < H; hb += per_launch) {
     const int64_t nh = (H - hb) < per_launch ? (H - hb) : per_launch;
     dim3 grid((unsigned)(cs->nc_pad / kBlockCorr), (unsigned)((nh + kScoreHyps - 1) / kScoreHyps));
-    score_kernel<<<grid, kScoreBlock, 0, st>>>(cs->p32, cs->q32, (const float4*)hypf, H,
-                                               hb, counts, amb, amb_count, amb_cap, full_flag,
-                                               full_list, full_count, done);
+    score_kernel<<<grid, kScoreBlock, 0, st>>>(cs->p32, cs->q32, (const float4*)hypf, H, hb,
+                                               counts, ex, done);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
-}
-
-hipError_t launch_recheck(const m3d_corrset* cs, const double* T, int64_t H, double thr, int mode,
-                          int32_t* counts, const AmbRecord* amb, const int32_t* amb_count,
-                          int32_t amb_cap, const int32_t* full_list, const int32_t* full_count,
-                          int64_t* stats, const int32_t* done, hipStream_t st) {
-  if (H == 0 || cs->nc == 0) return hipSuccess;
-  recheck_chunk_kernel<<<1024, 256, 0, st>>>(cs->p64, cs->q64, cs->nc, T, thr, mode, counts, amb,
-                                             amb_count, amb_cap, stats, done);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  recheck_full_kernel<<<256, 256, 0, st>>>(cs->p64, cs->q64, cs->nc, T, thr, mode, counts,
-                                           full_list, full_count, stats, done);
-  return hipGetLastError();
 }
 
 hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int64_t nc,
@@ -596,9 +527,9 @@ hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int6
   return hipGetLastError();
 }
 
-hipError_t launch_copy_result(const RansacState* rs, int64_t nc, m3d_ransac_result* out_dev,
-                              hipStream_t st) {
-  copy_result_kernel<<<1, 64, 0, st>>>(rs, nc, out_dev);
+hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* stats,
+                              m3d_ransac_result* out_dev, hipStream_t st) {
+  copy_result_kernel<<<1, 64, 0, st>>>(rs, nc, stats, out_dev);
   return hipGetLastError();
 }
 
