@@ -614,6 +614,10 @@ int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int
 
 void m3d_cloud_destroy(m3d_cloud* c) {
   if (!c) return;
+  if (c->grid) {
+    grid_free(c->grid);
+    delete c->grid;
+  }
   hipFree(c->xyz64);
   hipFree(c->nrm64);
   hipFree(c->xyz32);
@@ -623,6 +627,37 @@ void m3d_cloud_destroy(m3d_cloud* c) {
 int64_t m3d_cloud_size(const m3d_cloud* c) { return c ? c->n : -1; }
 
 // ------------------------------------------------------------------------------- ICP
+namespace {
+// uniform grid of a cloud for radius `cell` (built once, synchronously; reused while the
+// requested cell size is unchanged)
+int ensure_grid(m3d_ctx* ctx, const m3d_cloud* c, double cell, hipStream_t st) {
+  if (c->grid && c->grid->cell_req == cell && c->grid->n_pts == c->n) return M3D_OK;
+  if (!c->grid) c->grid = new Grid();
+  hipError_t e = grid_build(c->xyz32, c->n, cell, st, c->grid);
+  if (e != hipSuccess) {
+    grid_free(c->grid);
+    c->grid->cell_req = 0.0;
+    return m3d_fail(ctx, M3D_ERR_HIP, std::string("grid build: ") + hipGetErrorString(e));
+  }
+  c->grid->cell_req = cell;
+  return M3D_OK;
+}
+
+// NN evaluation for the current transform → s->keys (brute: keyinit + scan; grid: one kernel)
+hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st) {
+  m3d_ctx* ctx = s->ctx;
+  if (s->params.nn_method == M3D_NN_GRID) {
+    KTimer kt(ctx, M3D_KERNEL_NN, st);
+    return launch_grid_nn(s->src->xyz32, s->src->n, s->qorder, s->tgt->grid, off, s->state,
+                          s->keys, st);
+  }
+  hipError_t e = launch_icp_keyinit(s, off, st);
+  if (e != hipSuccess) return e;
+  KTimer kt(ctx, M3D_KERNEL_NN, st);
+  return launch_icp_nn(s, off, st);
+}
+}  // namespace
+
 int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
                    const m3d_icp_params* params, m3d_icp** out) {
   if (!ctx) return M3D_ERR_INVALID;
@@ -635,7 +670,16 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
             "TransformationEstimationPointToPlane requires pre-computed normal vectors for target "
             "PointCloud.");
   CHECK_ARG(ctx, params->max_iteration >= 0, "max_iteration must be >= 0");
+  CHECK_ARG(ctx, params->nn_method == M3D_NN_BRUTE || params->nn_method == M3D_NN_GRID,
+            "unknown nn_method");
   hipSetDevice(ctx->device);
+  if (params->nn_method == M3D_NN_GRID) {
+    // cell ≈ the search radius: a query visits 3 cells per axis
+    const double cell = max_dist * 1.001;
+    int grc = ensure_grid(ctx, tgt, cell, nullptr);
+    if (!grc) grc = ensure_grid(ctx, src, cell, nullptr);
+    if (grc) return grc;
+  }
   m3d_icp* s = new m3d_icp();
   s->ctx = ctx;
   s->src = src;
@@ -643,6 +687,7 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   s->params = *params;
   s->max_dist = max_dist;
   s->nblocks = terms_blocks(src->n);
+  if (params->nn_method == M3D_NN_GRID) s->qorder = src->grid->order;
   int rc = dev_alloc(ctx, &s->state, 1);
   if (!rc) rc = dev_alloc(ctx, &s->keys, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->corr, std::max<int64_t>(src->n, 1));
@@ -682,8 +727,7 @@ int m3d_icp_step(m3d_icp* s, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;
   hipStream_t st = S(stream);
-  HIPX(ctx, launch_icp_keyinit(s, 0, st));
-  { KTimer kt(ctx, M3D_KERNEL_NN, st); HIPX(ctx, launch_icp_nn(s, 0, st)); }
+  HIPX(ctx, enqueue_nn(s, 0, st));
   { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, 0, 0, st)); }
   HIPX(ctx, launch_icp_reduce(s, s->sums, st));
   HIPX(ctx, launch_icp_solve(s, s->sums, st));
@@ -695,8 +739,7 @@ int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* keys, void* stream) {
   m3d_ctx* ctx = s->ctx;
   CHECK_ARG(ctx, off >= 0, "negative shard offset");
   hipStream_t st = S(stream);
-  HIPX(ctx, launch_icp_keyinit(s, off, st));
-  { KTimer kt(ctx, M3D_KERNEL_NN, st); HIPX(ctx, launch_icp_nn(s, off, st)); }
+  HIPX(ctx, enqueue_nn(s, off, st));
   if (keys && keys != s->keys)
     HIPX(ctx, hipMemcpyAsync(keys, s->keys, sizeof(int64_t) * s->src->n, hipMemcpyDeviceToDevice, st));
   return M3D_OK;
@@ -767,19 +810,18 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
 }
 
 int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const double* T_host,
-            double max_dist, int32_t* idx, double* d2, void* stream) {
+            double max_dist, int32_t nn_method, int32_t* idx, double* d2, void* stream) {
   if (!ctx) return M3D_ERR_INVALID;
   CHECK_ARG(ctx, src && tgt && idx, "invalid arguments");
   CHECK_ARG(ctx, max_dist > 0.0, "max_dist must be > 0");
-  m3d_icp_params p{1e-6, 1e-6, 0, M3D_EST_POINT_TO_POINT};
+  m3d_icp_params p{1e-6, 1e-6, 0, M3D_EST_POINT_TO_POINT, nn_method, 0};
   m3d_icp* s = nullptr;
   int rc = m3d_icp_create(ctx, src, tgt, max_dist, &p, &s);
   if (rc) return rc;
   hipStream_t st = S(stream);
   rc = m3d_icp_reset(s, T_host, stream);
   hipError_t e = hipSuccess;
-  if (!rc) e = launch_icp_keyinit(s, 0, st);
-  if (e == hipSuccess) e = launch_icp_nn(s, 0, st);
+  if (!rc) e = enqueue_nn(s, 0, st);
   if (e == hipSuccess) e = launch_nn_finalize(s, idx, d2, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (!rc && e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));

@@ -1,0 +1,298 @@
+// grid.hip — radius-bounded uniform-grid 1-NN for gfx950.
+//
+// Reference semantics: Open3D KDTreeFlann::SearchHybrid(p, r, max_nn = 1) inside
+// GetRegistrationResultAndCorrespondences (a8).  The brute-force scan (icp.hip nn_kernel) and
+// this path return the SAME key for every query: the lexicographic (fp32 d², index) minimum over
+// the targets with d² ≤ r2_hi, where d² is the identical fp32 expression (d2f) of the identical
+// fp32 query (xform32).  The grid only restricts which targets are visited, and it provably
+// visits every target that can satisfy d² ≤ r2_hi:
+//   * cell coordinate c(x) = trunc(clamp((x − o)·inv_h, 0, n−1)) is monotone in x (fp32
+//     subtraction and multiplication by a positive constant are monotone under rounding);
+//   * d2f(q, t) ≤ r2_hi ⇒ |q_k − t_k| ≤ R = 1.001·√r2_hi for every axis (each rounding of the
+//     three-term sum shrinks by at most (1 − u)⁵ ≫ 1/1.001²);
+//   * |q_k − t_k| ≤ R ⇒ fl(q_k − R) ≤ t_k ≤ fl(q_k + R) (t_k is representable) ⇒
+//     c(fl(q_k − R)) ≤ c(t_k) ≤ c(fl(q_k + R)).
+// So the cell box [c(q − R), c(q + R)] contains every candidate whatever the cell size; the cell
+// size (≈ r) only sets how many cells a query visits (3 per axis).
+//
+// Layout in HBM: targets sorted by cell (row-major x fastest) as float4 (x, y, z, index bits),
+// one int32 start offset per cell (+1).  For a query the cells of one (y, z) row are contiguous
+// in the sorted array: ≤ 9 contiguous runs per query.  Queries are visited in the source cloud's
+// own cell order (spatially coherent waves → the 9 runs of neighbouring lanes overlap in L2).
+// Build: per-axis bounds (min/max reduction), cell ids, hipcub radix sort of (cell, index)
+// pairs (stable → deterministic layout), cell starts by binary search, gather.
+#include <float.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include <hipcub/hipcub.hpp>
+
+#include "m3d_internal.h"
+
+namespace m3d {
+
+constexpr int kGridBlock = 256;
+constexpr int64_t kMaxCells = (int64_t)1 << 25;
+
+__device__ __forceinline__ int grid_coord(float x, float o, float inv_h, int n) {
+  float f = (x - o) * inv_h;
+  f = fminf(fmaxf(f, 0.0f), (float)(n - 1));
+  return (int)f;
+}
+
+__global__ __launch_bounds__(kGridBlock) void minmax3_kernel(const float4* __restrict__ p, int64_t n,
+                                                             float* __restrict__ part) {
+  __shared__ float s[6][kGridBlock];
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int64_t i = (int64_t)blockIdx.x * kGridBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGridBlock) {
+    const float4 v = p[i];
+    const float c[3] = {v.x, v.y, v.z};
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = fminf(lo[k], c[k]);
+      hi[k] = fmaxf(hi[k], c[k]);
+    }
+  }
+  for (int k = 0; k < 3; ++k) {
+    s[k][threadIdx.x] = lo[k];
+    s[3 + k][threadIdx.x] = hi[k];
+  }
+  __syncthreads();
+  for (int w = kGridBlock / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int k = 0; k < 3; ++k) {
+        s[k][threadIdx.x] = fminf(s[k][threadIdx.x], s[k][threadIdx.x + w]);
+        s[3 + k][threadIdx.x] = fmaxf(s[3 + k][threadIdx.x], s[3 + k][threadIdx.x + w]);
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) part[6 * blockIdx.x + threadIdx.x] = s[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(kGridBlock) void cell_id_kernel(const float4* __restrict__ p, int64_t n,
+                                                             GridDev g, uint32_t* __restrict__ key,
+                                                             int32_t* __restrict__ val) {
+  const int64_t i = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (i >= n) return;
+  const float4 v = p[i];
+  const int cx = grid_coord(v.x, g.o[0], g.inv_h, g.n[0]);
+  const int cy = grid_coord(v.y, g.o[1], g.inv_h, g.n[1]);
+  const int cz = grid_coord(v.z, g.o[2], g.inv_h, g.n[2]);
+  key[i] = (uint32_t)(((int64_t)cz * g.n[1] + cy) * g.n[0] + cx);
+  val[i] = (int32_t)i;
+}
+
+// start[c] = first sorted position whose cell ≥ c (c = 0 .. ncells)
+__global__ __launch_bounds__(kGridBlock) void cell_start_kernel(const uint32_t* __restrict__ key,
+                                                                int64_t n, int64_t ncells,
+                                                                int32_t* __restrict__ start) {
+  const int64_t c = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (c > ncells) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)key[mid] < c)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  start[c] = (int32_t)lo;
+}
+
+__global__ __launch_bounds__(kGridBlock) void grid_gather_kernel(const float4* __restrict__ p,
+                                                                 const int32_t* __restrict__ val,
+                                                                 int64_t n,
+                                                                 float4* __restrict__ pts) {
+  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (k >= n) return;
+  const int32_t j = val[k];
+  const float4 v = p[j];
+  pts[k] = make_float4(v.x, v.y, v.z, __int_as_float(j));
+}
+
+// ------------------------------------------------------------------------------- query
+__device__ __forceinline__ float gd2f(float qx, float qy, float qz, float tx, float ty, float tz) {
+  const float dx = qx - tx, dy = qy - ty, dz = qz - tz;  // == icp.hip d2f
+  return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+}
+
+// kGridLanes lanes cooperate on one query: the query's cell rows (contiguous runs of the sorted
+// array) are dealt round-robin to the lanes, each lane keeps its packed (bits(d²) << 32 | index)
+// minimum, and the lanes combine with shuffles.  A key compare is exactly the lexicographic
+// (d², index) compare of the brute-force scan (d² ≥ +0, so the float bits order as the values;
+// NaN bits order above every finite bound and are never selected).  16 lanes per query keep
+// ~16x more loads in flight than one lane per query: the scan is latency-bound, not bandwidth.
+constexpr int kGridLanes = 16;
+
+__global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __restrict__ src32,
+                                                             int64_t ns,
+                                                             const int32_t* __restrict__ order,
+                                                             GridDev g, int64_t off,
+                                                             const IcpState* __restrict__ s,
+                                                             int64_t* __restrict__ keys) {
+  if (s->done) return;
+  const int64_t t = ((int64_t)blockIdx.x * kGridBlock + threadIdx.x) / kGridLanes;
+  const int sub = threadIdx.x & (kGridLanes - 1);
+  const float r2_hi = s->r2_hi;
+  const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
+  uint64_t key = key0;
+  int64_t i = 0;
+  if (t < ns) {
+    i = order != nullptr ? (int64_t)order[t] : t;
+    const float* Rt = s->Rt32;
+    const float4 p = src32[i];
+    // == icp.hip xform32
+    const float qx = fmaf(Rt[0], p.x, fmaf(Rt[1], p.y, fmaf(Rt[2], p.z, Rt[9])));
+    const float qy = fmaf(Rt[3], p.x, fmaf(Rt[4], p.y, fmaf(Rt[5], p.z, Rt[10])));
+    const float qz = fmaf(Rt[6], p.x, fmaf(Rt[7], p.y, fmaf(Rt[8], p.z, Rt[11])));
+    if (g.ncells > 0) {
+      const float R = sqrtf(r2_hi) * 1.001f;
+      const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
+      const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
+      const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
+      const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
+      const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
+      const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
+      const int ny = y1 - y0 + 1;
+      const int rows = ny * (z1 - z0 + 1);
+      for (int r = sub; r < rows; r += kGridLanes) {
+        const int cz = z0 + r / ny, cy = y0 + r % ny;
+        const int64_t row = ((int64_t)cz * g.n[1] + cy) * g.n[0];
+        const int32_t j0 = g.start[row + x0], j1 = g.start[row + x1 + 1];
+        for (int32_t j = j0; j < j1; ++j) {
+          const float4 v = g.pts[j];
+          const float d2 = gd2f(qx, qy, qz, v.x, v.y, v.z);
+          const uint64_t kc = ((uint64_t)__float_as_uint(d2) << 32) |
+                              (uint64_t)(uint32_t)(off + __float_as_int(v.w));
+          key = kc < key ? kc : key;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = kGridLanes / 2; o > 0; o >>= 1) {
+    const uint32_t hi = __shfl_xor((uint32_t)(key >> 32), o, kGridLanes);
+    const uint32_t lo = __shfl_xor((uint32_t)key, o, kGridLanes);
+    const uint64_t other = ((uint64_t)hi << 32) | lo;
+    key = other < key ? other : key;
+  }
+  if (t < ns && sub == 0) keys[i] = key == key0 ? kKeyNone : (int64_t)key;
+}
+
+// ------------------------------------------------------------------------------- host side
+static hipError_t grid_fail(hipError_t e, void* a, void* b, void* c, void* d, void* tmp) {
+  hipFree(a);
+  hipFree(b);
+  hipFree(c);
+  hipFree(d);
+  hipFree(tmp);
+  return e;
+}
+
+hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g) {
+  g->n_pts = n;
+  g->cell = cell;
+  GridDev& d = g->dev;
+  d.ncells = 0;
+  if (n == 0) return hipSuccess;
+  // per-axis bounds
+  const int nb = (int)std::min<int64_t>(1024, (n + kGridBlock - 1) / kGridBlock);
+  float* part = nullptr;
+  hipError_t e = hipMalloc(&part, sizeof(float) * 6 * nb);
+  if (e != hipSuccess) return e;
+  minmax3_kernel<<<nb, kGridBlock, 0, st>>>(xyz32, n, part);
+  std::vector<float> hp(6 * (size_t)nb);
+  e = hipMemcpyAsync(hp.data(), part, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipFree(part);
+  if (e != hipSuccess) return e;
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int b = 0; b < nb; ++b)
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], hp[6 * b + k]);
+      hi[k] = std::max(hi[k], hp[6 * b + 3 + k]);
+    }
+  // cell size: requested, grown until the dense grid has at most kMaxCells cells
+  double h = cell > 0.0 && std::isfinite(cell) ? cell : 1.0;
+  int64_t nn[3], total = 0;
+  for (;;) {
+    total = 1;
+    for (int k = 0; k < 3; ++k) {
+      const double ext = std::isfinite((double)hi[k] - lo[k]) ? (double)hi[k] - lo[k] : 0.0;
+      nn[k] = (int64_t)std::floor(ext / h) + 1;
+      total *= nn[k];
+      if (total > kMaxCells) break;
+    }
+    if (total <= kMaxCells) break;
+    h *= 1.26;
+  }
+  for (int k = 0; k < 3; ++k) {
+    d.o[k] = lo[k];
+    d.n[k] = (int)nn[k];
+  }
+  d.inv_h = (float)(1.0 / h);
+  d.ncells = total;
+  g->cell = h;
+  // (cell, index) pairs → stable radix sort
+  uint32_t *kin = nullptr, *kout = nullptr;
+  int32_t *vin = nullptr, *vout = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  int bits = 1;
+  while (bits < 32 && ((int64_t)1 << bits) < total) ++bits;
+  if ((e = hipMalloc(&kin, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&kout, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&vin, sizeof(int32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&vout, sizeof(int32_t) * n)) != hipSuccess)
+    return grid_fail(e, kin, kout, vin, vout, tmp);
+  const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
+  cell_id_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, n, d, kin, vin);
+  if ((e = hipGetLastError()) != hipSuccess) return grid_fail(e, kin, kout, vin, vout, tmp);
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, bits, st);
+  if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 1));
+  if (e == hipSuccess)
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, bits, st);
+  if (e != hipSuccess) return grid_fail(e, kin, kout, vin, vout, tmp);
+  hipFree(g->start);
+  hipFree(g->pts);
+  hipFree(g->order);
+  g->start = nullptr;
+  g->pts = nullptr;
+  g->order = nullptr;
+  if ((e = hipMalloc(&g->start, sizeof(int32_t) * (total + 1))) != hipSuccess ||
+      (e = hipMalloc(&g->pts, sizeof(float4) * n)) != hipSuccess)
+    return grid_fail(e, kin, kout, vin, vout, tmp);
+  cell_start_kernel<<<(unsigned)((total + 1 + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
+      kout, n, total, g->start);
+  grid_gather_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, vout, n, g->pts);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  g->order = vout;  // sorted point indices: the cloud's cell order
+  vout = nullptr;
+  d.start = g->start;
+  d.pts = g->pts;
+  return grid_fail(e, kin, kout, vin, vout, tmp);
+}
+
+void grid_free(Grid* g) {
+  if (!g) return;
+  hipFree(g->start);
+  hipFree(g->pts);
+  hipFree(g->order);
+  g->start = nullptr;
+  g->pts = nullptr;
+  g->order = nullptr;
+}
+
+hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
+                          int64_t off, const IcpState* s, int64_t* keys, hipStream_t st) {
+  if (ns == 0) return hipSuccess;
+  const int64_t threads = ns * kGridLanes;
+  grid_nn_kernel<<<(unsigned)((threads + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
+      src32, ns, order, g->dev, off, s, keys);
+  return hipGetLastError();
+}
+
+}  // namespace m3d

@@ -6,8 +6,8 @@
 //
 // Kernels per iteration (all device resident, no host round trip):
 //   keyinit  O(Ns)      seeds each query's bound with its previous neighbour (fp32 d²)
-//   nn       O(Ns·Nt)   brute-force scan: queries in VGPRs (kNNQ = 4 per lane), targets streamed
-//                       through SGPRs by scalar loads (wave-uniform tile of kNNTile points).
+//   nn       O(Ns·Nt)   brute-force scan: queries in VGPRs (kNNQ = 4 per lane), targets staged
+//                       through double-buffered LDS tiles and read with broadcast ds_read_b128.
 //                       Fast path per pair: a screen key |t|² − 2q·t = 3 FMA + ½ v_min3
 //                       (|t|² precomputed in t.w); tiles whose screen minimum cannot reach the
 //                       current bound (proven error bound, refresh_rt32) are skipped, the rest
@@ -110,8 +110,7 @@ __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__
   if (s->done) return;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= ns) return;
-  float Rt[12];
-  for (int k = 0; k < 12; ++k) Rt[k] = s->Rt32[k];
+  const float* Rt = s->Rt32;  // uniform → scalar loads (a local copy went to scratch)
   int64_t key = kKeyNone;
   const int64_t j = prev != nullptr ? (int64_t)prev[i] : -1;
   if (j >= off && j < off + nt_shard) {
@@ -132,8 +131,7 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
                                                       int64_t off, const IcpState* __restrict__ s,
                                                       int64_t* __restrict__ keys) {
   if (s->done) return;
-  float Rt[12];
-  for (int k = 0; k < 12; ++k) Rt[k] = s->Rt32[k];
+  const float* Rt = s->Rt32;  // uniform → scalar loads (a local copy went to scratch)
   const float r2_hi = s->r2_hi;
   const float eps = s->screen_eps;
   // per query: q (exact-path coordinates), a = −2q (screen), qq = |q|², bound `best` (+ index)
@@ -334,20 +332,24 @@ __global__ __launch_bounds__(kTermsBlock) void terms_kernel(
 }
 
 // ------------------------------------------------------------------------------- reduce
-__global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ partials,
-                                                     int64_t nblocks, double* __restrict__ sums,
-                                                     const IcpState* __restrict__ s) {
+// 32 groups × 32 slots: group g sums blocks g, g+32, … (independent loads in flight), then the
+// 32 group sums are added in group order — a fixed order, so the result is deterministic.
+constexpr int kReduceGroups = 32;
+__global__ __launch_bounds__(kReduceGroups * kTermSlots) void reduce_kernel(
+    const double* __restrict__ partials, int64_t nblocks, double* __restrict__ sums,
+    const IcpState* __restrict__ s) {
   if (s != nullptr && s->done) return;
-  __shared__ double red[8][kTermSlots];
+  __shared__ double red[kReduceGroups][kTermSlots];
   const int slot = threadIdx.x & (kTermSlots - 1);
   const int g = threadIdx.x / kTermSlots;
   double v = 0.0;
-  for (int64_t b = g; b < nblocks; b += 8) v += partials[b * kTermSlots + slot];
+#pragma unroll 4
+  for (int64_t b = g; b < nblocks; b += kReduceGroups) v += partials[b * kTermSlots + slot];
   red[g][slot] = v;
   __syncthreads();
   if (threadIdx.x < kTermSlots) {
     double t = 0.0;
-    for (int k = 0; k < 8; ++k) t += red[k][threadIdx.x];
+    for (int k = 0; k < kReduceGroups; ++k) t += red[k][threadIdx.x];
     sums[threadIdx.x] = t;
   }
 }
@@ -530,7 +532,7 @@ hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hip
 }
 
 hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st) {
-  reduce_kernel<<<1, 256, 0, st>>>(s->partials, s->nblocks, sums, s->state);
+  reduce_kernel<<<1, kReduceGroups * kTermSlots, 0, st>>>(s->partials, s->nblocks, sums, s->state);
   return hipGetLastError();
 }
 

@@ -170,50 +170,85 @@ M3D_HD int kabsch3(const double ps[3][3], const double qs[3][3], double T[16]) {
   return 0;
 }
 
+M3D_HD void swapd(double& a, double& b) {
+  const double t = a;
+  a = b;
+  b = t;
+}
+
 // Eigen::LDLT-style solve of a symmetric 6×6 system A x = b (A row-major, full).
+// Every loop is unrolled and the pivot swap is predicated on compile-time row indices, so on
+// the device the factorisation lives in registers (a dynamically indexed pivot row would put
+// M, L and the permutation in scratch memory: 720 B and ~10 µs of serial scratch latency).
 M3D_HD void ldlt6_solve(const double A_in[36], const double b_in[6], double x[6]) {
   double M[6][6], L[6][6], D[6], y[6];
   int perm[6];
+#pragma unroll
   for (int i = 0; i < 6; ++i) {
     perm[i] = i;
+#pragma unroll
     for (int j = 0; j < 6; ++j) {
       M[i][j] = A_in[i * 6 + j];
       L[i][j] = (i == j) ? 1.0 : 0.0;
     }
   }
   const double tiny = 2.2250738585072014e-308;
+#pragma unroll
   for (int k = 0; k < 6; ++k) {
     int p = k;
     double best = fabs(M[k][k]);
+#pragma unroll
     for (int i = k + 1; i < 6; ++i)
       if (fabs(M[i][i]) > best) {
         best = fabs(M[i][i]);
         p = i;
       }
-    if (p != k) {
-      for (int j = 0; j < 6; ++j) { double t = M[k][j]; M[k][j] = M[p][j]; M[p][j] = t; }
-      for (int i = 0; i < 6; ++i) { double t = M[i][k]; M[i][k] = M[i][p]; M[i][p] = t; }
-      for (int j = 0; j < k; ++j) { double t = L[k][j]; L[k][j] = L[p][j]; L[p][j] = t; }
-      int t = perm[k]; perm[k] = perm[p]; perm[p] = t;
+#pragma unroll
+    for (int q = k + 1; q < 6; ++q) {
+      if (q == p) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) swapd(M[k][j], M[q][j]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) swapd(M[i][k], M[i][q]);
+#pragma unroll
+        for (int j = 0; j < k; ++j) swapd(L[k][j], L[q][j]);
+        const int t = perm[k];
+        perm[k] = perm[q];
+        perm[q] = t;
+      }
     }
     D[k] = M[k][k];
     const bool ok = fabs(D[k]) > tiny;
+#pragma unroll
     for (int i = k + 1; i < 6; ++i) L[i][k] = ok ? M[i][k] / D[k] : 0.0;
+#pragma unroll
     for (int i = k + 1; i < 6; ++i)
+#pragma unroll
       for (int j = k + 1; j < 6; ++j) M[i][j] -= L[i][k] * M[k][j];
   }
+#pragma unroll
   for (int i = 0; i < 6; ++i) {
-    double s = b_in[perm[i]];
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s = (perm[i] == j) ? b_in[j] : s;  // b[perm[i]]
+#pragma unroll
     for (int j = 0; j < i; ++j) s -= L[i][j] * y[j];
     y[i] = s;
   }
+#pragma unroll
   for (int i = 0; i < 6; ++i) y[i] = (fabs(D[i]) > tiny) ? y[i] / D[i] : 0.0;
+#pragma unroll
   for (int i = 5; i >= 0; --i) {
     double s = y[i];
+#pragma unroll
     for (int j = i + 1; j < 6; ++j) s -= L[j][i] * y[j];
     y[i] = s;
   }
-  for (int i = 0; i < 6; ++i) x[perm[i]] = y[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if (perm[i] == j) x[j] = y[i];
 }
 
 // Open3D TransformVector6dToMatrix4d: R = Rz(x2) Ry(x1) Rx(x0), t = x[3..5].

@@ -67,6 +67,26 @@ struct IcpState {
   float screen_eps;   // NN screen error bound (icp.hip refresh_rt32)
 };
 
+// Uniform grid over a cloud's centred fp32 points (grid.hip): kernel view + owner.
+struct GridDev {
+  float o[3];
+  float inv_h;
+  int n[3];
+  int64_t ncells = 0;
+  const int32_t* start = nullptr;  // ncells + 1 sorted-array offsets
+  const float4* pts = nullptr;     // points sorted by cell, w = index bits
+};
+
+struct Grid {
+  GridDev dev;
+  int32_t* start = nullptr;
+  float4* pts = nullptr;
+  int32_t* order = nullptr;  // point indices in cell order
+  int64_t n_pts = 0;
+  double cell = 0.0;      // cell size used
+  double cell_req = 0.0;  // cell size requested
+};
+
 constexpr int kTermSlots = 32;  // 21 JTJ + 6 JTr + r² + count + Σd² (+2 pad)
 constexpr int64_t kKeyNone = 0x7FFFFFFFFFFFFFFFll;
 
@@ -106,6 +126,7 @@ struct m3d_cloud {
   float4* xyz32 = nullptr;  // n_pad centred (pad = far away)
   double center[3] = {0, 0, 0};
   double rmax = 0.0;  // max |x_c|∞ (guard-band bound)
+  mutable m3d::Grid* grid = nullptr;  // built on demand (grid NN)
 };
 
 struct m3d_icp {
@@ -120,6 +141,7 @@ struct m3d_icp {
   double* partials = nullptr;      // nblocks × kTermSlots
   double* sums = nullptr;          // kTermSlots
   int64_t nblocks = 0;
+  const int32_t* qorder = nullptr;  // grid NN: source visit order (source cell order)
 };
 
 // error plumbing ------------------------------------------------------------------------
@@ -170,5 +192,9 @@ hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_
 hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, hipStream_t st);
 hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st);
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);
+hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g);
+void grid_free(Grid* g);
+hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
+                          int64_t off, const IcpState* s, int64_t* keys, hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
 }  // namespace m3d

@@ -23,6 +23,9 @@ HYP_OK, HYP_DEGENERATE, HYP_NONFINITE = 0, 1, 2
 SCORE_SQUARED, SCORE_NORM = 0, 1
 EST_POINT_TO_POINT, EST_POINT_TO_PLANE = 0, 1
 KERNEL_NN, KERNEL_SCORE, KERNEL_KABSCH, KERNEL_TERMS = 0, 1, 2, 3
+NN_BRUTE, NN_GRID = 0, 1
+NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
+ABI_VERSION = 2
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -44,7 +47,7 @@ class RansacResult(C.Structure):
 
 class IcpParams(C.Structure):
     _fields_ = [("relative_fitness", dbl), ("relative_rmse", dbl), ("max_iteration", i32),
-                ("estimation", i32)]
+                ("estimation", i32), ("nn_method", i32), ("reserved", i32)]
 
 
 class IcpResult(C.Structure):
@@ -75,7 +78,7 @@ SIGNATURES = {
     "m3d_cloud_create": (C.c_int, [vp, vp, vp, i64, vp, C.POINTER(vp)]),
     "m3d_cloud_destroy": (None, [vp]),
     "m3d_cloud_size": (i64, [vp]),
-    "m3d_nn1": (C.c_int, [vp, vp, vp, C.POINTER(dbl), dbl, vp, vp, vp]),
+    "m3d_nn1": (C.c_int, [vp, vp, vp, C.POINTER(dbl), dbl, i32, vp, vp, vp]),
     "m3d_icp_run": (C.c_int, [vp, vp, vp, C.POINTER(dbl), dbl, C.POINTER(IcpParams),
                               C.POINTER(IcpResult), vp, vp]),
     "m3d_icp_create": (C.c_int, [vp, vp, vp, dbl, C.POINTER(IcpParams), C.POINTER(vp)]),
@@ -108,6 +111,9 @@ def load() -> C.CDLL:
         raise ImportError(f"{LIB_PATH} not built: run `make -C {LIB_PATH.parent.parent / 'csrc'}` "
                           "(hipcc --offload-arch=gfx950)")
     lib = C.CDLL(os.fspath(LIB_PATH))
+    lib.m3d_abi_version.restype = C.c_int
+    if lib.m3d_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI {lib.m3d_abi_version()} != {ABI_VERSION}; rebuild it")
     for name, (res, args) in SIGNATURES.items():
         f = getattr(lib, name)
         f.restype = res

@@ -255,13 +255,23 @@ def _T16(T):
     return (C.c_double * 16)(*a.tolist())
 
 
-def nn1(src: Cloud, tgt: Cloud, T, max_dist: float):
-    """Radius-bounded 1-NN of T·src in tgt → (idx int32 (-1 none), d2 f64) torch cuda."""
+def _nn_method(nn: str) -> int:
+    try:
+        return _lib.NN_METHODS[nn]
+    except KeyError:
+        raise ValueError(f"nn must be one of {sorted(_lib.NN_METHODS)}, got {nn!r}") from None
+
+
+def nn1(src: Cloud, tgt: Cloud, T, max_dist: float, nn: str = "grid"):
+    """Radius-bounded 1-NN of T·src in tgt → (idx int32 (-1 none), d2 f64) torch cuda.
+
+    nn="brute" scans every target, nn="grid" only the uniform-grid cells within the radius;
+    both return the identical result (grid.hip header)."""
     torch = _torch()
     idx = torch.empty((src.n,), dtype=torch.int32, device="cuda")
     d2 = torch.empty((src.n,), dtype=torch.float64, device="cuda")
-    src.ctx.check(src.ctx.lib.m3d_nn1(src.ctx.h, src.h, tgt.h, _T16(T), float(max_dist), ptr(idx),
-                                      ptr(d2), stream_handle()), "nn1")
+    src.ctx.check(src.ctx.lib.m3d_nn1(src.ctx.h, src.h, tgt.h, _T16(T), float(max_dist),
+                                      _nn_method(nn), ptr(idx), ptr(d2), stream_handle()), "nn1")
     return idx, d2
 
 
@@ -277,9 +287,11 @@ class IcpOutcome:
 
 
 def icp(src: Cloud, tgt: Cloud, max_dist: float, init=None, estimation=_lib.EST_POINT_TO_PLANE,
-        relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30, with_correspondences=True):
+        relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30, with_correspondences=True,
+        nn: str = "grid"):
     torch = _torch()
-    p = _lib.IcpParams(float(relative_fitness), float(relative_rmse), int(max_iteration), int(estimation))
+    p = _lib.IcpParams(float(relative_fitness), float(relative_rmse), int(max_iteration), int(estimation),
+                       _nn_method(nn), 0)
     res = _lib.IcpResult()
     corr = torch.empty((max(src.n, 1),), dtype=torch.int32, device="cuda") if with_correspondences else None
     init16 = _T16(np.eye(4) if init is None else init)
@@ -298,11 +310,11 @@ class IcpLoop:
     """Step-wise device ICP (benchmarks, multi-GPU).  Every call only enqueues work."""
 
     def __init__(self, src: Cloud, tgt: Cloud, max_dist: float, estimation=_lib.EST_POINT_TO_PLANE,
-                 relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30):
+                 relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30, nn: str = "brute"):
         self.ctx = src.ctx
         self.src, self.tgt = src, tgt
         self.p = _lib.IcpParams(float(relative_fitness), float(relative_rmse), int(max_iteration),
-                                int(estimation))
+                                int(estimation), _nn_method(nn), 0)
         h = C.c_void_p()
         self.ctx.check(self.ctx.lib.m3d_icp_create(self.ctx.h, src.h, tgt.h, float(max_dist),
                                                    C.byref(self.p), C.byref(h)), "icp_create")

@@ -17,6 +17,10 @@ BASELINE.json metric "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pt
   (source, target) pair; peak = FP32 vector 157.3 TFLOP/s (no MFMA: the scan is
   a min-reduction, not a contraction).  traffic = HBM bytes per launch from the committed
   rocprofv3 PMC summary (profiles/), or null.
+* "icp_grid": the same cfg1 workload with the radius-bounded uniform-grid NN (SURVEY §8(f)
+  rank 1; identical correspondences, tests/test_gpu_icp.py) — HBM/latency-bound, so its
+  roofline is priced in GB/s on 28·Ns + 16·Nt algorithmic bytes per launch (query float4 +
+  visit order + key write, each target read once).
 * cpu_baseline (rank 0, N = 1): the oracle restatement (oracle/icp_oracle.py: scipy cKDTree on
   16 threads + numpy point-to-plane) timed on a bounded sample of the same workload.
 """
@@ -52,6 +56,7 @@ def parse():
     ap.add_argument("--hyps", type=int, default=100_000, help="RANSAC hypotheses per GPU per run")
     ap.add_argument("--ransac-steps", type=int, default=3)
     ap.add_argument("--no-ransac", action="store_true")
+    ap.add_argument("--no-grid", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline leg")
     return ap.parse_args()
@@ -110,45 +115,72 @@ def main():
     off = rank * nt
     src_c = Cloud(src)
     tgt_c = Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt])
-    loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters)
     keys = torch.empty(ns, dtype=torch.int64, device=dev)
     sums = torch.empty(32, dtype=torch.float64, device=dev)
 
-    def icp_run():
-        loop.reset(np.eye(4))
-        for _ in range(iters + 1):
-            if world == 1:
-                loop.step()
-            else:
-                loop.shard_nn(off, keys)
-                dist.all_reduce(keys, op=dist.ReduceOp.MIN)
-                loop.shard_terms(off, keys, sums)
-                dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-                loop.solve(sums)
+    def time_icp(nn: str):
+        loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters,
+                       nn=nn)
 
-    for _ in range(args.warmup):
-        icp_run()
-    torch.cuda.synchronize()
-    ctx.profile(True)
-    ctx.profile_read(_lib.KERNEL_NN)
-    ctx.profile_read(_lib.KERNEL_TERMS)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        icp_run()
-    torch.cuda.synchronize()
-    barrier()
-    el = max_over_ranks(time.perf_counter() - t0)
-    nn_ms, nn_n = ctx.profile_read(_lib.KERNEL_NN)
-    terms_ms, terms_n = ctx.profile_read(_lib.KERNEL_TERMS)
-    ctx.profile(False)
-    res = loop.result()
+        def icp_run():
+            loop.reset(np.eye(4))
+            for _ in range(iters + 1):
+                if world == 1:
+                    loop.step()
+                else:
+                    loop.shard_nn(off, keys)
+                    dist.all_reduce(keys, op=dist.ReduceOp.MIN)
+                    loop.shard_terms(off, keys, sums)
+                    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+                    loop.solve(sums)
+
+        for _ in range(args.warmup):
+            icp_run()
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        ctx.profile_read(_lib.KERNEL_NN)
+        ctx.profile_read(_lib.KERNEL_TERMS)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            icp_run()
+        torch.cuda.synchronize()
+        barrier()
+        el = max_over_ranks(time.perf_counter() - t0)
+        nn_ms, nn_n = ctx.profile_read(_lib.KERNEL_NN)
+        terms_ms, terms_n = ctx.profile_read(_lib.KERNEL_TERMS)
+        ctx.profile(False)
+        return (el, max_over_ranks(nn_ms / max(nn_n, 1)), nn_n, terms_ms / max(terms_n, 1),
+                loop.result())
+
+    el, nn_avg_ms, nn_n, terms_avg_ms, res = time_icp("brute")
     icp_value = world * iters * args.steps / el
-    nn_avg_ms = max_over_ranks(nn_ms / max(nn_n, 1))
     nn_flop = NN_FLOP_PER_PAIR * ns * nt
     achieved_tf = nn_flop / (nn_avg_ms * 1e-3) / 1e12
     err = float(np.abs(res.transformation - T_true).max())
+
+    # ------------------------------------------------------------------ cfg1 with the grid NN
+    icp_grid = None
+    if not args.no_grid:
+        tg0 = time.perf_counter()
+        IcpLoop(src_c, tgt_c, r, max_iteration=0, nn="grid")  # builds both clouds' grids once
+        torch.cuda.synchronize()
+        build_ms = (time.perf_counter() - tg0) * 1e3
+        gel, g_ms, g_n, g_terms_ms, gres = time_icp("grid")
+        g_bytes = 28 * ns + 16 * nt
+        g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
+        icp_grid = {
+            "metric": "ICP iterations/sec (cfg1 workload, uniform-grid radius NN)",
+            "value": world * iters * args.steps / gel, "unit": "ICP iter/s (100k src x 100k tgt per GPU)",
+            "ms_per_step": gel / args.steps * 1e3, "grid_build_ms": build_ms,
+            "same_result_as_brute": bool(np.array_equal(gres.transformation, res.transformation)),
+            "roofline": {"bound": "hbm", "kernel": "grid_nn_kernel", "achieved": g_gbs,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic("grid_nn_kernel")[0], "avg_launch_ms": g_ms,
+                         "launches": g_n, "bytes_per_launch": g_bytes,
+                         "terms_avg_launch_ms": g_terms_ms},
+        }
 
     # ------------------------------------------------------------------ cfg2: RANSAC
     ransac = None
@@ -226,7 +258,8 @@ def main():
                      "peak": VALU_FP32_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / VALU_FP32_PEAK_TF,
                      "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": nn_avg_ms,
                      "launches": nn_n, "flop_per_launch": nn_flop,
-                     "terms_avg_launch_ms": terms_ms / max(terms_n, 1)},
+                     "terms_avg_launch_ms": terms_avg_ms},
+        "icp_grid": icp_grid,
         "ransac": ransac,
         "cpu_baseline": cpu,
         "check": {"icp_fitness": res.fitness, "icp_rmse": res.inlier_rmse, "max_abs_err_vs_T_true": err},

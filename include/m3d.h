@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 1
+#define M3D_ABI_VERSION 2
 
 /* return codes */
 #define M3D_OK 0
@@ -161,16 +161,24 @@ int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int
 void m3d_cloud_destroy(m3d_cloud* c);
 int64_t m3d_cloud_size(const m3d_cloud* c);
 
+/* Nearest-neighbour search method.  Both return the identical (d², index) result: BRUTE scans
+ * every target (cfg1's LDS-tiled brute force), GRID visits only the uniform-grid cells that can
+ * hold a target within the radius. */
+#define M3D_NN_BRUTE 0
+#define M3D_NN_GRID 1
+
 /* Radius-bounded 1-NN (KDTreeFlann::SearchHybrid(p, r, 1) for every source point after T):
  * idx [device] ns int32 (-1 = no target with d² < r²), d2 [device] ns f64 (may be NULL). */
 int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const double* T_host,
-            double max_dist, int32_t* idx, double* d2, void* stream);
+            double max_dist, int32_t nn_method, int32_t* idx, double* d2, void* stream);
 
 typedef struct {
   double relative_fitness; /* ICPConvergenceCriteria defaults 1e-6 */
   double relative_rmse;    /* 1e-6 */
   int32_t max_iteration;   /* 30 */
   int32_t estimation;      /* M3D_EST_* */
+  int32_t nn_method;       /* M3D_NN_* */
+  int32_t reserved;        /* 0 */
 } m3d_icp_params;
 
 typedef struct {

@@ -16,7 +16,7 @@ from m3d.core import Cloud, IcpLoop, icp, nn1
 pytestmark = pytest.mark.gpu
 
 
-def check_nn(src_t, tgt, r, idx, d2):
+def check_nn(src_t, tgt, r, idx, d2, min_same=0.999):
     tree = cKDTree(tgt)
     dd, jj = tree.query(src_t, k=1)
     ref_d2 = dd * dd
@@ -32,20 +32,69 @@ def check_nn(src_t, tgt, r, idx, d2):
         diff = src_t[bi] - tgt[idx[bi]]
         mine = np.sum(diff * diff, axis=1)
         assert np.all(mine <= ref_d2[bi] + 2e-6 * np.maximum(ref_d2[bi], 1e-6))
-    assert same.size == 0 or same.mean() > 0.999
+    assert same.size == 0 or same.mean() > min_same
     np.testing.assert_allclose(d2[both], np.sum((src_t[both] - tgt[idx[both]]) ** 2, axis=1), rtol=1e-12)
 
 
+@pytest.mark.parametrize("nn", ["brute", "grid"])
 @pytest.mark.parametrize("ns,nt", [(1, 1), (5, 3000), (1000, 1000), (20000, 30011), (100_000, 100_000)])
-def test_nn1_matches_kdtree(ns, nt):
-    rng = np.random.default_rng(ns + nt)
+def test_nn1_matches_kdtree(ns, nt, nn):
     tgt, _ = synth.surface_points(nt, seed=1)
     src, _ = synth.surface_points(ns, seed=2)
     T = synth.random_rigid(3, rot_range=0.02, trans_range=0.05)
     r = 0.3 if nt < 5000 else 0.12
-    idx, d2 = nn1(Cloud(src), Cloud(tgt), T, r)
+    idx, d2 = nn1(Cloud(src), Cloud(tgt), T, r, nn=nn)
     check_nn(synth.apply(T, src), tgt, r, idx.cpu().numpy(), d2.cpu().numpy())
-    del rng
+
+
+def _grid_cases():
+    rng = np.random.default_rng(21)
+    sph, _ = synth.surface_points(30000, seed=3)
+    plane = np.c_[rng.uniform(-3, 3, (20000, 2)), np.zeros(20000)]  # zero extent along z
+    line = np.c_[np.linspace(-1, 1, 5000), np.zeros((5000, 2))]
+    dup = np.repeat(rng.normal(size=(50, 3)), 40, axis=0)  # exact duplicates → index ties
+    wide = rng.uniform(-5e3, 5e3, (40000, 3))  # cell-count cap (r ≪ extent)
+    offset = sph + np.array([1e5, -2e5, 3e4])  # large absolute coordinates
+    return {
+        "sphere": (sph[::3] * 1.002, sph, 0.12),
+        "sphere_big_r": (sph[::7], sph, 50.0),  # radius larger than the cloud
+        "sphere_tiny_r": (sph[::5] + 1e-4, sph, 1e-3),
+        "plane": (plane[::4] + [0, 0, 0.01], plane, 0.05),
+        "line": (line + [0.0001, 0.02, 0], line, 0.03),
+        "duplicates": (dup + 1e-3, dup, 0.5),
+        "wide": (wide[::2] + 0.3, wide, 0.01),
+        "offset": (offset[::3] * 1.0000001, offset, 0.12),
+        "far": (sph[:100] + 1e3, sph, 0.12),
+        "single_target": (sph[:500], sph[:1], 10.0),
+    }
+
+
+@pytest.mark.parametrize("case", list(_grid_cases()))
+def test_grid_nn_identical_to_brute_force(case):
+    """Grid and brute-force NN return bit-identical (index, d²) for every query (grid.hip proof)."""
+    src, tgt, r = _grid_cases()[case]
+    T = synth.random_rigid(17, rot_range=0.01, trans_range=0.01)
+    s, t = Cloud(src), Cloud(tgt)
+    ib, db = nn1(s, t, T, r, nn="brute")
+    ig, dg = nn1(s, t, T, r, nn="grid")
+    np.testing.assert_array_equal(ig.cpu().numpy(), ib.cpu().numpy())
+    np.testing.assert_array_equal(dg.cpu().numpy(), db.cpu().numpy())
+    if case != "wide":  # kd-tree cross-check (the wide case has ~no neighbours by design)
+        # exact duplicates: the kd-tree picks any of the tied targets (distances still checked)
+        check_nn(synth.apply(T, src), tgt, r, ig.cpu().numpy(), dg.cpu().numpy(),
+                 min_same=0.0 if case == "duplicates" else 0.999)
+
+
+@pytest.mark.parametrize("estimation", [_lib.EST_POINT_TO_PLANE, _lib.EST_POINT_TO_POINT])
+def test_icp_grid_identical_to_brute_force(estimation):
+    src, tgt, nrm, _ = synth.icp_pair(50000, 60000, seed=19)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=12, estimation=estimation)
+    a = icp(s, t, 0.12, np.eye(4), nn="brute", **kw)
+    b = icp(s, t, 0.12, np.eye(4), nn="grid", **kw)
+    np.testing.assert_array_equal(b.transformation, a.transformation)
+    assert (b.fitness, b.inlier_rmse, b.iterations) == (a.fitness, a.inlier_rmse, a.iterations)
+    np.testing.assert_array_equal(b.correspondence_set, a.correspondence_set)
 
 
 def test_nn1_exact_ties_pick_lowest_index():
@@ -121,17 +170,19 @@ def test_step_loop_matches_run():
     assert r.fitness == full.fitness and r.iterations == 10
 
 
-def test_target_sharded_loop_matches_single_device():
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_target_sharded_loop_matches_single_device(nn):
     """The multi-GPU target-shard protocol (MIN on keys, SUM on terms) emulated on one device."""
     import torch
 
     src, tgt, nrm, _ = synth.icp_pair(20000, 30000, seed=13)
     s = Cloud(src)
     full = icp(s, Cloud(tgt, nrm), 0.12, np.eye(4), relative_fitness=-1, relative_rmse=-1,
-               max_iteration=6)
+               max_iteration=6, nn="brute")
     bounds = [0, 7000, 19001, 30000]
     shards = [Cloud(tgt[a:b], nrm[a:b]) for a, b in zip(bounds[:-1], bounds[1:])]
-    loops = [IcpLoop(s, sh, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=6) for sh in shards]
+    loops = [IcpLoop(s, sh, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=6, nn=nn)
+             for sh in shards]
     for lp in loops:
         lp.reset(np.eye(4))
     ns = len(src)

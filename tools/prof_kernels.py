@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Short, fixed workload for rocprofv3 runs (kernel trace / PMC counters).
 
-ICP: cfg1 geometry (100k↔100k), `--icp-iters` iterations from identity.
+ICP: cfg1 geometry (100k↔100k), `--icp-iters` iterations from identity, brute-force NN and
+then the uniform-grid NN (`--nn brute|grid|both`).
 RANSAC: cfg2 geometry (Nc = 1e5), `--hyps` native hypotheses, no early stop.
 """
 import argparse
@@ -19,6 +20,7 @@ def main():
     ap.add_argument("--hyps", type=int, default=20_000)
     ap.add_argument("--skip-ransac", action="store_true")
     ap.add_argument("--skip-icp", action="store_true")
+    ap.add_argument("--nn", default="both", choices=["brute", "grid", "both"])
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -29,13 +31,15 @@ def main():
     torch.cuda.set_device(0)
     if not a.skip_icp:
         src, tgt, nrm, _ = synth.icp_pair(a.n, seed=0)
-        loop = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
-                       max_iteration=a.icp_iters)
-        loop.reset(np.eye(4))
-        for _ in range(a.icp_iters + 1):
-            loop.step()
-        r = loop.result()
-        print("icp", r.fitness, r.iterations)
+        sc, tc = Cloud(src), Cloud(tgt, nrm)
+        for nn in (["brute", "grid"] if a.nn == "both" else [a.nn]):
+            loop = IcpLoop(sc, tc, 0.12, relative_fitness=-1, relative_rmse=-1,
+                           max_iteration=a.icp_iters, nn=nn)
+            loop.reset(np.eye(4))
+            for _ in range(a.icp_iters + 1):
+                loop.step()
+            r = loop.result()
+            print("icp", nn, r.fitness, r.iterations)
     if not a.skip_ransac:
         s, t, c, _ = synth.ransac_pair(a.n, seed=42)
         cs = CorrSet(s, t, c)
