@@ -1,0 +1,198 @@
+"""PLY / STL point I/O (host side, feeds cfg4).
+
+Replaces the two readers the reference path touches:
+
+* ``o3d.io.read_point_cloud(path)`` for ``.ply`` (``src/ply/ply.py:80``): vertex positions
+  ``x y z`` and, when present, normals ``nx ny nz``.  Formats: ``ascii 1.0``,
+  ``binary_little_endian 1.0``, ``binary_big_endian 1.0``; every PLY scalar type
+  (``char/int8 … double/float64``) for any vertex property; list properties and other elements
+  (faces, edges) are parsed only as far as needed to skip them.
+* ``convert_stl-ply.py`` (trimesh 4.11.1, not installed — parity unpinned): STL (binary or
+  ASCII) → unique vertices → ASCII PLY point cloud.  Vertices are merged on exact equality and
+  kept in first-occurrence order (trimesh merges within 1e-8; scans never differ by less).
+
+Readers return fp64 arrays (N×3) — the reference converts to ``Vector3dVector`` (fp64).
+Binary payloads are decoded with one numpy structured-dtype view, so a 1M-point file reads in
+milliseconds.
+"""
+
+from __future__ import annotations
+
+import re
+from pathlib import Path
+
+import numpy as np
+
+_PLY_TYPES = {
+    "char": "i1", "int8": "i1", "uchar": "u1", "uint8": "u1",
+    "short": "i2", "int16": "i2", "ushort": "u2", "uint16": "u2",
+    "int": "i4", "int32": "i4", "uint": "u4", "uint32": "u4",
+    "float": "f4", "float32": "f4", "double": "f8", "float64": "f8",
+}
+
+
+class PlyError(ValueError):
+    pass
+
+
+def _parse_header(f):
+    first = f.readline()
+    if first.strip() != b"ply":
+        raise PlyError("not a PLY file (missing 'ply' magic)")
+    fmt = None
+    elements = []  # [name, count, [(prop, type) | (prop, ('list', count_type, item_type))]]
+    while True:
+        line = f.readline()
+        if not line:
+            raise PlyError("PLY header has no end_header")
+        tok = line.decode("ascii", "replace").split()
+        if not tok or tok[0] in ("comment", "obj_info"):
+            continue
+        if tok[0] == "format":
+            fmt = tok[1]
+            if fmt not in ("ascii", "binary_little_endian", "binary_big_endian"):
+                raise PlyError(f"unsupported PLY format {fmt!r}")
+        elif tok[0] == "element":
+            elements.append([tok[1], int(tok[2]), []])
+        elif tok[0] == "property":
+            if not elements:
+                raise PlyError("property before element")
+            if tok[1] == "list":
+                elements[-1][2].append((tok[4], ("list", _ptype(tok[2]), _ptype(tok[3]))))
+            else:
+                elements[-1][2].append((tok[2], _ptype(tok[1])))
+        elif tok[0] == "end_header":
+            break
+    if fmt is None:
+        raise PlyError("PLY header has no format line")
+    return fmt, elements
+
+
+def _ptype(name):
+    try:
+        return _PLY_TYPES[name]
+    except KeyError:
+        raise PlyError(f"unknown PLY property type {name!r}") from None
+
+
+def _skip_binary_element(f, count, props, endian):
+    if all(not isinstance(t, tuple) for _, t in props):
+        f.seek(count * sum(np.dtype(t).itemsize for _, t in props), 1)
+        return
+    for _ in range(count):  # list properties: variable length rows
+        for _, t in props:
+            if isinstance(t, tuple):
+                n = int(np.frombuffer(f.read(np.dtype(t[1]).itemsize), endian + t[1])[0])
+                f.seek(n * np.dtype(t[2]).itemsize, 1)
+            else:
+                f.seek(np.dtype(t).itemsize, 1)
+
+
+def read_ply(path):
+    """Read vertices of a PLY file → ``(points N×3 f64, normals N×3 f64 or None)``."""
+    path = Path(path)
+    with open(path, "rb") as f:
+        fmt, elements = _parse_header(f)
+        endian = {"binary_little_endian": "<", "binary_big_endian": ">"}.get(fmt, "")
+        for name, count, props in elements:
+            if name == "vertex":
+                names = [p for p, _ in props]
+                if not all(k in names for k in ("x", "y", "z")):
+                    raise PlyError("vertex element has no x/y/z properties")
+                if fmt == "ascii":
+                    cols = _read_ascii_vertices(f, count, props)
+                else:
+                    if any(isinstance(t, tuple) for _, t in props):
+                        raise PlyError("list properties in the vertex element are not supported")
+                    dt = np.dtype([(p, endian + t) for p, t in props])
+                    raw = f.read(dt.itemsize * count)
+                    if len(raw) != dt.itemsize * count:
+                        raise PlyError("PLY file truncated in the vertex element")
+                    arr = np.frombuffer(raw, dt)
+                    cols = {p: arr[p] for p in names}
+                pts = np.stack([cols["x"], cols["y"], cols["z"]], axis=1).astype(np.float64)
+                nrm = None
+                if all(k in names for k in ("nx", "ny", "nz")):
+                    nrm = np.stack([cols["nx"], cols["ny"], cols["nz"]], axis=1).astype(np.float64)
+                return pts, nrm
+            # an element before the vertices: skip it
+            if fmt == "ascii":
+                for _ in range(count):
+                    f.readline()
+            else:
+                _skip_binary_element(f, count, props, endian)
+    raise PlyError("PLY file has no vertex element")
+
+
+def _read_ascii_vertices(f, count, props):
+    rows = []
+    while len(rows) < count:
+        line = f.readline()
+        if not line:
+            raise PlyError("PLY file truncated in the vertex element")
+        if line.strip():
+            rows.append(line)
+    if any(isinstance(t, tuple) for _, t in props):
+        raise PlyError("list properties in the vertex element are not supported")
+    data = np.loadtxt(rows, dtype=np.float64, ndmin=2) if count else np.zeros((0, len(props)))
+    if data.shape[1] < len(props):
+        raise PlyError("ASCII vertex rows shorter than the declared properties")
+    return {p: data[:, k] for k, (p, _) in enumerate(props)}
+
+
+def write_ply(path, points, normals=None, binary: bool = False, dtype="double"):
+    """Write a PLY point cloud (x y z [nx ny nz]); ``dtype`` "double" or "float"."""
+    pts = np.asarray(points, np.float64).reshape(-1, 3)
+    cols = [pts]
+    names = ["x", "y", "z"]
+    if normals is not None:
+        cols.append(np.asarray(normals, np.float64).reshape(-1, 3))
+        names += ["nx", "ny", "nz"]
+    data = np.concatenate(cols, axis=1)
+    np_t = {"double": "f8", "float": "f4"}[dtype]
+    head = ["ply", f"format {'binary_little_endian' if binary else 'ascii'} 1.0",
+            f"element vertex {len(pts)}"] + [f"property {dtype} {n}" for n in names] + ["end_header"]
+    with open(path, "wb") as f:
+        f.write(("\n".join(head) + "\n").encode("ascii"))
+        if binary:
+            f.write(np.ascontiguousarray(data.astype("<" + np_t)).tobytes())
+        else:
+            fmt = "%.17g" if dtype == "double" else "%.9g"
+            np.savetxt(f, data.astype(np_t), fmt=fmt)
+
+
+_STL_VERTEX = re.compile(rb"vertex\s+(\S+)\s+(\S+)\s+(\S+)")
+
+
+def read_stl(path):
+    """Read an STL mesh → ``(vertices V×3 f64 unique, faces F×3 int64)``."""
+    raw = Path(path).read_bytes()
+    tri = None
+    if len(raw) >= 84:
+        n = int(np.frombuffer(raw[80:84], "<u4")[0])
+        if len(raw) == 84 + 50 * n:  # binary: exact size match
+            rec = np.frombuffer(raw[84:], np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)),
+                                                    ("a", "<u2")]), count=n)
+            tri = rec["v"].astype(np.float64)
+    if tri is None:
+        if not raw.lstrip().startswith(b"solid"):
+            raise ValueError(f"{path}: neither binary nor ASCII STL")
+        v = np.array(_STL_VERTEX.findall(raw), dtype=np.float64)
+        if len(v) % 3:
+            raise ValueError(f"{path}: ASCII STL vertex count is not a multiple of 3")
+        tri = v.reshape(-1, 3, 3)
+    flat = tri.reshape(-1, 3)
+    _, first, inverse = np.unique(flat, axis=0, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")     # unique vertices in first-occurrence order
+    rank = np.empty_like(order)
+    rank[order] = np.arange(len(order))
+    verts = flat[np.sort(first)]
+    faces = rank[inverse.reshape(-1)].reshape(-1, 3)
+    return verts, faces
+
+
+def convert_stl_to_ply(stl_path, ply_path):
+    """convert_stl-ply.py: STL mesh vertices → ASCII PLY point cloud."""
+    verts, _ = read_stl(stl_path)
+    write_ply(ply_path, verts, binary=False, dtype="double")
+    return len(verts)

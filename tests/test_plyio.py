@@ -1,0 +1,122 @@
+"""PLY / STL I/O (m3d.plyio): round trips and hand-written files of every supported layout.
+
+Reference readers (Open3D read_point_cloud, trimesh) are not installed — parity unpinned; the
+files here are written byte by byte from the PLY/STL specifications.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from m3d import plyio
+
+
+@pytest.mark.parametrize("binary", [False, True])
+@pytest.mark.parametrize("dtype", ["double", "float"])
+@pytest.mark.parametrize("with_normals", [False, True])
+def test_round_trip(tmp_path, binary, dtype, with_normals):
+    rng = np.random.default_rng(0)
+    pts = rng.normal(size=(257, 3)) * 10
+    nrm = rng.normal(size=(257, 3)) if with_normals else None
+    p = tmp_path / "a.ply"
+    plyio.write_ply(p, pts, nrm, binary=binary, dtype=dtype)
+    got, gn = plyio.read_ply(p)
+    cast = np.float64 if dtype == "double" else np.float32
+    # binary float → the float32 value; ASCII values parse as double (as rply/strtod do), so a
+    # printed float32 re-rounds to that float32
+    np.testing.assert_array_equal(got.astype(cast), pts.astype(cast))
+    if with_normals:
+        np.testing.assert_array_equal(gn.astype(cast), nrm.astype(cast))
+    else:
+        assert gn is None
+
+
+def test_big_endian_with_extra_props_and_faces(tmp_path):
+    pts = np.array([[1.5, -2.0, 3.25], [0.0, 1.0, 2.0], [4.0, 5.0, 6.0]])
+    head = ("ply\nformat binary_big_endian 1.0\ncomment made by hand\n"
+            "element vertex 3\nproperty float x\nproperty float y\nproperty float z\n"
+            "property uchar red\nproperty uchar green\nproperty uchar blue\n"
+            "element face 1\nproperty list uchar int vertex_indices\nend_header\n").encode()
+    body = b"".join(struct.pack(">fffBBB", *p, 1, 2, 3) for p in pts)
+    body += struct.pack(">Biii", 3, 0, 1, 2)
+    (tmp_path / "b.ply").write_bytes(head + body)
+    got, nrm = plyio.read_ply(tmp_path / "b.ply")
+    np.testing.assert_array_equal(got, pts)
+    assert nrm is None
+
+
+def test_element_before_vertices_is_skipped(tmp_path):
+    head = ("ply\nformat binary_little_endian 1.0\nelement camera 2\nproperty list uchar float k\n"
+            "property int id\nelement vertex 2\nproperty double x\nproperty double y\n"
+            "property double z\nproperty double nx\nproperty double ny\nproperty double nz\n"
+            "end_header\n").encode()
+    body = struct.pack("<Bffi", 2, 1.0, 2.0, 7) + struct.pack("<Bi", 0, 8)
+    body += struct.pack("<6d", 1, 2, 3, 0, 0, 1) + struct.pack("<6d", 4, 5, 6, 1, 0, 0)
+    (tmp_path / "c.ply").write_bytes(head + body)
+    pts, nrm = plyio.read_ply(tmp_path / "c.ply")
+    np.testing.assert_array_equal(pts, [[1, 2, 3], [4, 5, 6]])
+    np.testing.assert_array_equal(nrm, [[0, 0, 1], [1, 0, 0]])
+
+
+def test_ascii_int_coordinates_and_blank_lines(tmp_path):
+    text = ("ply\nformat ascii 1.0\nelement vertex 3\nproperty int x\nproperty int y\n"
+            "property int z\nelement face 0\nproperty list uchar int vertex_indices\nend_header\n"
+            "1 2 3\n\n4 5 6\n7 8 9\n")
+    (tmp_path / "d.ply").write_text(text)
+    pts, _ = plyio.read_ply(tmp_path / "d.ply")
+    np.testing.assert_array_equal(pts, np.arange(1, 10).reshape(3, 3))
+
+
+@pytest.mark.parametrize("text,err", [
+    ("plx\n", "magic"),
+    ("ply\nformat ascii 1.0\nelement face 0\nend_header\n", "no vertex"),
+    ("ply\nformat binary_little_endian 1.0\nelement vertex 5\nproperty float x\nproperty float y\n"
+     "property float z\nend_header\n", "truncated"),
+    ("ply\nformat ascii 1.0\nelement vertex 1\nproperty float x\nend_header\n1\n", "x/y/z"),
+])
+def test_malformed_files_raise(tmp_path, text, err):
+    (tmp_path / "e.ply").write_bytes(text.encode())
+    with pytest.raises(plyio.PlyError, match=err):
+        plyio.read_ply(tmp_path / "e.ply")
+
+
+def _tetra():
+    v = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]], np.float64)
+    f = np.array([[0, 2, 1], [0, 1, 3], [0, 3, 2], [1, 2, 3]])
+    return v, f
+
+
+def test_binary_stl_merges_shared_vertices(tmp_path):
+    v, f = _tetra()
+    raw = b"\0" * 80 + struct.pack("<I", len(f))
+    for tri in f:
+        raw += struct.pack("<3f", 0, 0, 0) + struct.pack("<9f", *v[tri].ravel()) + b"\0\0"
+    (tmp_path / "t.stl").write_bytes(raw)
+    verts, faces = plyio.read_stl(tmp_path / "t.stl")
+    assert len(verts) == 4
+    np.testing.assert_array_equal(verts[faces], v[f])       # faces reference the merged vertices
+    np.testing.assert_array_equal(verts, v[[0, 2, 1, 3]])   # first-occurrence order
+
+
+def test_ascii_stl_and_convert(tmp_path):
+    v, f = _tetra()
+    lines = ["solid t"]
+    for tri in f:
+        lines += ["facet normal 0 0 0", "outer loop"] + [f"vertex {a} {b} {c}" for a, b, c in v[tri]]
+        lines += ["endloop", "endfacet"]
+    lines.append("endsolid t")
+    (tmp_path / "t.stl").write_text("\n".join(lines))
+    n = plyio.convert_stl_to_ply(tmp_path / "t.stl", tmp_path / "t.ply")
+    assert n == 4
+    pts, _ = plyio.read_ply(tmp_path / "t.ply")
+    assert sorted(map(tuple, pts)) == sorted(map(tuple, v))
+
+
+def test_ply_class_checks_like_reference(tmp_path):
+    from ply import Ply
+
+    with pytest.raises(FileNotFoundError):
+        Ply(tmp_path / "missing.ply")
+    (tmp_path / "x.txt").write_text("x")
+    with pytest.raises(TypeError):
+        Ply(tmp_path / "x.txt")
