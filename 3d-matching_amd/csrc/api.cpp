@@ -614,9 +614,9 @@ int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int
 
 void m3d_cloud_destroy(m3d_cloud* c) {
   if (!c) return;
-  if (c->grid) {
-    grid_free(c->grid);
-    delete c->grid;
+  for (Grid* g : c->grids) {
+    grid_free(g);
+    delete g;
   }
   hipFree(c->xyz64);
   hipFree(c->nrm64);
@@ -628,18 +628,24 @@ int64_t m3d_cloud_size(const m3d_cloud* c) { return c ? c->n : -1; }
 
 // ------------------------------------------------------------------------------- ICP
 namespace {
-// uniform grid of a cloud for radius `cell` (built once, synchronously; reused while the
-// requested cell size is unchanged)
-int ensure_grid(m3d_ctx* ctx, const m3d_cloud* c, double cell, hipStream_t st) {
-  if (c->grid && c->grid->cell_req == cell && c->grid->n_pts == c->n) return M3D_OK;
-  if (!c->grid) c->grid = new Grid();
-  hipError_t e = grid_build(c->xyz32, c->n, cell, st, c->grid);
+// uniform grid of a cloud for cell size `cell` (built once, synchronously, and cached on the
+// cloud per cell size)
+int ensure_grid(m3d_ctx* ctx, const m3d_cloud* c, double cell, hipStream_t st, const Grid** out) {
+  for (Grid* g : c->grids)
+    if (g->cell_req == cell && g->n_pts == c->n) {
+      *out = g;
+      return M3D_OK;
+    }
+  Grid* g = new Grid();
+  hipError_t e = grid_build(c->xyz32, c->n, cell, st, g);
   if (e != hipSuccess) {
-    grid_free(c->grid);
-    c->grid->cell_req = 0.0;
+    grid_free(g);
+    delete g;
     return m3d_fail(ctx, M3D_ERR_HIP, std::string("grid build: ") + hipGetErrorString(e));
   }
-  c->grid->cell_req = cell;
+  g->cell_req = cell;
+  c->grids.push_back(g);
+  *out = g;
   return M3D_OK;
 }
 
@@ -648,8 +654,8 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st) {
   m3d_ctx* ctx = s->ctx;
   if (s->params.nn_method == M3D_NN_GRID) {
     KTimer kt(ctx, M3D_KERNEL_NN, st);
-    return launch_grid_nn(s->src->xyz32, s->src->n, s->qorder, s->tgt->grid, off, s->state,
-                          s->keys, st);
+    return launch_grid_nn(s->src->xyz32, s->src->n, s->qorder, s->tgrid, off, s->state, s->keys,
+                          st);
   }
   hipError_t e = launch_icp_keyinit(s, off, st);
   if (e != hipSuccess) return e;
@@ -673,11 +679,12 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   CHECK_ARG(ctx, params->nn_method == M3D_NN_BRUTE || params->nn_method == M3D_NN_GRID,
             "unknown nn_method");
   hipSetDevice(ctx->device);
+  const Grid *tg = nullptr, *sg = nullptr;
   if (params->nn_method == M3D_NN_GRID) {
     // cell ≈ the search radius: a query visits 3 cells per axis
     const double cell = max_dist * 1.001;
-    int grc = ensure_grid(ctx, tgt, cell, nullptr);
-    if (!grc) grc = ensure_grid(ctx, src, cell, nullptr);
+    int grc = ensure_grid(ctx, tgt, cell, nullptr, &tg);
+    if (!grc) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
     if (grc) return grc;
   }
   m3d_icp* s = new m3d_icp();
@@ -687,7 +694,10 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   s->params = *params;
   s->max_dist = max_dist;
   s->nblocks = terms_blocks(src->n);
-  if (params->nn_method == M3D_NN_GRID) s->qorder = src->grid->order;
+  if (params->nn_method == M3D_NN_GRID) {
+    s->tgrid = tg;
+    s->qorder = sg->order;
+  }
   int rc = dev_alloc(ctx, &s->state, 1);
   if (!rc) rc = dev_alloc(ctx, &s->keys, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->corr, std::max<int64_t>(src->n, 1));
@@ -827,6 +837,209 @@ int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const doub
   if (!rc && e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   m3d_icp_destroy(s);
   return rc;
+}
+
+// ------------------------------------------------------------------------------- preprocessing
+extern "C++" {
+namespace {
+// device scratch released on scope exit (after the synchronous entry point has synchronised)
+template <class T>
+struct DevTmp {
+  T* p = nullptr;
+  ~DevTmp() { hipFree(p); }
+};
+
+// hybrid neighbourhoods of every point of `c` (grid cell = radius)
+int neighbourhoods(m3d_ctx* ctx, const m3d_cloud* c, double radius, int k, hipStream_t st,
+                   DevTmp<int32_t>& idx, DevTmp<double>& d2, DevTmp<int32_t>& cnt) {
+  const Grid* g = nullptr;
+  int rc = ensure_grid(ctx, c, radius, st, &g);
+  if (rc) return rc;
+  const int64_t n = std::max<int64_t>(c->n, 1);
+  rc = dev_alloc(ctx, &idx.p, n * k);
+  if (!rc) rc = dev_alloc(ctx, &d2.p, n * k);
+  if (!rc) rc = dev_alloc(ctx, &cnt.p, n);
+  if (rc) return rc;
+  HIPX(ctx, hybrid_search(c, g, radius, k, idx.p, d2.p, cnt.p, st));
+  return M3D_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int m3d_voxel_down_sample(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                          double voxel_size, double* out_xyz, double* out_normals, int64_t* out_n,
+                          void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, out_n != nullptr && n >= 0 && n < ((int64_t)1 << 31), "invalid arguments");
+  CHECK_ARG(ctx, voxel_size > 0.0, "voxel_size <= 0.");
+  CHECK_ARG(ctx, n == 0 || (xyz && out_xyz), "null device pointer");
+  hipSetDevice(ctx->device);
+  std::string why;
+  hipError_t e = voxel_down_sample(xyz, normals, n, voxel_size, out_xyz, normals ? out_normals : nullptr,
+                                   out_n, S(stream), &why);
+  if (e != hipSuccess)
+    return m3d_fail(ctx, why.empty() ? M3D_ERR_HIP : M3D_ERR_INVALID,
+                    why.empty() ? std::string("voxel_down_sample: ") + hipGetErrorString(e) : why);
+  return M3D_OK;
+}
+
+int m3d_hybrid_search(m3d_ctx* ctx, const m3d_cloud* cloud, double radius, int32_t max_nn,
+                      int32_t* idx, double* d2, int32_t* count, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, cloud && idx && d2 && count, "invalid arguments");
+  CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  const Grid* g = nullptr;
+  int rc = ensure_grid(ctx, cloud, radius, st, &g);
+  if (rc) return rc;
+  HIPX(ctx, hybrid_search(cloud, g, radius, max_nn, idx, d2, count, st));
+  HIPX(ctx, hipStreamSynchronize(st));
+  return M3D_OK;
+}
+
+int m3d_estimate_normals(m3d_ctx* ctx, const m3d_cloud* cloud, double radius, int32_t max_nn,
+                         double* normals_out, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, cloud && (normals_out || cloud->n == 0), "invalid arguments");
+  CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  DevTmp<int32_t> idx, cnt;
+  DevTmp<double> d2;
+  int rc = neighbourhoods(ctx, cloud, radius, max_nn, st, idx, d2, cnt);
+  if (rc) return rc;
+  HIPX(ctx, launch_normals(cloud, idx.p, max_nn, cnt.p, cloud->nrm64, normals_out, st));
+  HIPX(ctx, hipStreamSynchronize(st));
+  return M3D_OK;
+}
+
+int m3d_compute_fpfh(m3d_ctx* ctx, const m3d_cloud* cloud, const double* normals, double radius,
+                     int32_t max_nn, double* fpfh_out, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, cloud && ((normals && fpfh_out) || cloud->n == 0),
+            "Failed because input point cloud has no normal.");
+  CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  DevTmp<int32_t> idx, cnt;
+  DevTmp<double> d2, spfh;
+  int rc = neighbourhoods(ctx, cloud, radius, max_nn, st, idx, d2, cnt);
+  if (!rc) rc = dev_alloc(ctx, &spfh.p, std::max<int64_t>(cloud->n, 1) * 33);
+  if (rc) return rc;
+  HIPX(ctx, launch_fpfh(cloud, normals, idx.p, d2.p, max_nn, cnt.p, spfh.p, fpfh_out, st));
+  HIPX(ctx, hipStreamSynchronize(st));
+  return M3D_OK;
+}
+
+// ------------------------------------------------------------------------------- feature matching
+int m3d_feature_correspondences(m3d_ctx* ctx, const double* f_src, int64_t ns, const double* f_tgt,
+                                int64_t nt, int32_t dim, int32_t mutual_filter,
+                                double mutual_consistent_ratio, int32_t* corr_out, int64_t* n_out,
+                                void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, dim == 33, "feature dimension must be 33 (FPFH)");
+  CHECK_ARG(ctx, n_out && ns >= 0 && nt >= 0 && ns < ((int64_t)1 << 31) && nt < ((int64_t)1 << 31),
+            "invalid arguments");
+  CHECK_ARG(ctx, (ns == 0 || (f_src && corr_out)) && (nt == 0 || f_tgt), "null device pointer");
+  hipSetDevice(ctx->device);
+  HIPX(ctx, feature_correspondences(f_src, ns, f_tgt, nt, mutual_filter, mutual_consistent_ratio,
+                                    corr_out, n_out, S(stream)));
+  return M3D_OK;
+}
+
+int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt,
+                                  const int32_t* corr, int64_t nc,
+                                  const m3d_feature_ransac_params* p,
+                                  m3d_feature_ransac_result* out, int32_t* corr_set_out,
+                                  void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, src && tgt && p && out, "invalid arguments");
+  CHECK_ARG(ctx, p->ransac_n <= 3, "ransac_n > 3 is not supported (the reference uses 3)");
+  CHECK_ARG(ctx, p->max_iteration >= 0, "max_iteration must be >= 0");
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  memset(out, 0, sizeof(*out));
+  for (int k = 0; k < 16; ++k) out->T[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  out->best_index = -1;
+  const int64_t ns = src->n;
+  if (corr_set_out && ns > 0) HIPX(ctx, hipMemsetAsync(corr_set_out, 0xFF, 4 * ns, st));
+  // Open3D returns an empty RegistrationResult for these (Registration.cpp)
+  if (p->ransac_n < 3 || nc < p->ransac_n || !(p->max_correspondence_distance > 0.0) ||
+      p->max_iteration == 0 || ns == 0 || tgt->n == 0) {
+    HIPX(ctx, hipStreamSynchronize(st));
+    return M3D_OK;
+  }
+  CHECK_ARG(ctx, corr != nullptr, "null correspondence pointer");
+  const int64_t H = p->max_iteration;
+  DevTmp<double> T, sums;
+  DevTmp<int32_t> pass;
+  int rc = dev_alloc(ctx, &T.p, 16 * H);
+  if (!rc) rc = dev_alloc(ctx, &pass.p, H);
+  if (!rc) rc = dev_alloc(ctx, &sums.p, kTermSlots * H);
+  if (rc) return rc;
+  HIPX(ctx, launch_feat_hyp(src->xyz64, tgt->xyz64, corr, nc, p->seed, H, p->edge_length,
+                            p->distance, T.p, pass.p, st));
+  std::vector<int32_t> hpass(H);
+  HIPX(ctx, hipMemcpyAsync(hpass.data(), pass.p, 4 * H, hipMemcpyDeviceToHost, st));
+  HIPX(ctx, hipStreamSynchronize(st));
+  m3d_icp_params ip{1e-6, 1e-6, 0, M3D_EST_POINT_TO_POINT, M3D_NN_GRID, 0};
+  m3d_icp* s = nullptr;
+  rc = m3d_icp_create(ctx, src, tgt, p->max_correspondence_distance, &ip, &s);
+  if (rc) return rc;
+  // validation of every hypothesis that passed the checkers (≤ max_iteration); the sequential
+  // early-exit selection below decides which of them Open3D would have validated
+  hipError_t e = hipSuccess;
+  for (int64_t h = 0; h < H && e == hipSuccess; ++h) {
+    if (!hpass[h]) continue;
+    e = launch_icp_set_T(s, T.p + 16 * h, st);
+    if (e == hipSuccess) e = enqueue_nn(s, 0, st);
+    if (e == hipSuccess) e = launch_icp_terms_mode(s, 0, 0, st);
+    if (e == hipSuccess) e = launch_icp_reduce(s, sums.p + kTermSlots * h, st);
+  }
+  std::vector<double> hs((size_t)kTermSlots * H);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(hs.data(), sums.p, sizeof(double) * kTermSlots * H, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    m3d_icp_destroy(s);
+    return m3d_fail(ctx, M3D_ERR_HIP, std::string("feature RANSAC: ") + hipGetErrorString(e));
+  }
+  int64_t est_k = H, best = -1;
+  double best_fit = 0.0, best_rmse = 0.0;
+  for (int64_t h = 0; h < H && h < est_k; ++h) {
+    if (!hpass[h]) continue;
+    out->validations += 1;
+    const double cnt = hs[kTermSlots * h + 28], se = hs[kTermSlots * h + 29];
+    const double fit = cnt > 0.0 ? cnt / (double)ns : 0.0;
+    const double rmse = cnt > 0.0 ? std::sqrt(se / cnt) : 0.0;
+    if (fit > best_fit || (fit == best_fit && rmse < best_rmse)) {  // IsBetterRANSACThan
+      best = h;
+      best_fit = fit;
+      best_rmse = rmse;
+      const double k = fit < 1.0 ? std::ceil(std::log(1.0 - p->confidence) /
+                                             std::log(1.0 - std::pow(fit, (double)p->ransac_n)))
+                                 : 0.0;
+      if (k < (double)est_k) est_k = (int64_t)k;
+    }
+  }
+  if (best >= 0) {
+    e = hipMemcpyAsync(out->T, T.p + 16 * best, sizeof(double) * 16, hipMemcpyDeviceToHost, st);
+    out->fitness = best_fit;
+    out->inlier_rmse = best_rmse;
+    out->best_index = best;
+    if (e == hipSuccess && corr_set_out) {
+      e = launch_icp_set_T(s, T.p + 16 * best, st);
+      if (e == hipSuccess) e = enqueue_nn(s, 0, st);
+      if (e == hipSuccess) e = launch_icp_terms_mode(s, 0, 0, st);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(corr_set_out, s->corr, 4 * ns, hipMemcpyDeviceToDevice, st);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
+  m3d_icp_destroy(s);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  return M3D_OK;
 }
 
 // ------------------------------------------------------------------------------- test hooks

@@ -100,6 +100,17 @@ __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, do
   refresh_rt32(s, f.cs, f.ct, f.pinf, f.qinf);
 }
 
+// state for evaluating transform T (device, row-major 4×4): feature-RANSAC validation (a6)
+__global__ void icp_set_T_kernel(IcpState* s, const double* __restrict__ T, double r2, FrameParams f) {
+  if (threadIdx.x != 0) return;
+  for (int k = 0; k < 16; ++k) s->T[k] = T[k];
+  s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
+  s->count = 0;
+  s->evals = s->iters = s->done = s->converged = 0;
+  s->r2 = r2;
+  refresh_rt32(s, f.cs, f.ct, f.pinf, f.qinf);
+}
+
 // ------------------------------------------------------------------------------- keyinit
 __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__ src32, int64_t ns,
                                                       const float4* __restrict__ tgt32,
@@ -481,6 +492,11 @@ hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st) {
   icp_init_kernel<<<1, 64, 0, st>>>(s->state, T[0], T[1], T[2], T[3], T[4], T[5], T[6], T[7],
                                     T[8], T[9], T[10], T[11], s->max_dist * s->max_dist,
                                     frame_of(s));
+  return hipGetLastError();
+}
+
+hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st) {
+  icp_set_T_kernel<<<1, 64, 0, st>>>(s->state, T_dev, s->max_dist * s->max_dist, frame_of(s));
   return hipGetLastError();
 }
 

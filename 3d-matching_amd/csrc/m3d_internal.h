@@ -126,7 +126,7 @@ struct m3d_cloud {
   float4* xyz32 = nullptr;  // n_pad centred (pad = far away)
   double center[3] = {0, 0, 0};
   double rmax = 0.0;  // max |x_c|∞ (guard-band bound)
-  mutable m3d::Grid* grid = nullptr;  // built on demand (grid NN)
+  mutable std::vector<m3d::Grid*> grids;  // uniform grids built on demand, one per cell size
 };
 
 struct m3d_icp {
@@ -142,6 +142,7 @@ struct m3d_icp {
   double* sums = nullptr;          // kTermSlots
   int64_t nblocks = 0;
   const int32_t* qorder = nullptr;  // grid NN: source visit order (source cell order)
+  const m3d::Grid* tgrid = nullptr;  // grid NN: the target's grid (owned by the target cloud)
 };
 
 // error plumbing ------------------------------------------------------------------------
@@ -197,4 +198,24 @@ void grid_free(Grid* g);
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
                           int64_t off, const IcpState* s, int64_t* keys, hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
+hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st);
+
+// preprocessing (prep.hip) and feature matching (feat.hip)
+hipError_t voxel_down_sample(const double* xyz, const double* nrm, int64_t n, double voxel,
+                             double* out_xyz, double* out_nrm, int64_t* out_n, hipStream_t st,
+                             std::string* why);
+hipError_t hybrid_search(const m3d_cloud* c, const Grid* g, double radius, int k, int32_t* idx,
+                         double* d2, int32_t* cnt, hipStream_t st);
+hipError_t launch_normals(const m3d_cloud* c, const int32_t* nbr, int k, const int32_t* cnt,
+                          const double* prev, double* out, hipStream_t st);
+hipError_t launch_fpfh(const m3d_cloud* c, const double* nrm, const int32_t* nbr, const double* d2,
+                       int k, const int32_t* cnt, double* spfh, double* out, hipStream_t st);
+hipError_t feature_nn(const double* fq, int64_t nq, const double* fr, int64_t nr, int32_t* out,
+                      hipStream_t st);
+hipError_t feature_correspondences(const double* fs, int64_t ns, const double* ft, int64_t nt,
+                                   int mutual, double ratio, int32_t* corr_out, int64_t* n_out,
+                                   hipStream_t st);
+hipError_t launch_feat_hyp(const double* src, const double* tgt, const int32_t* corr, int64_t nc,
+                           uint64_t seed, int64_t H, double edge, double dist, double* T_out,
+                           int32_t* pass, hipStream_t st);
 }  // namespace m3d

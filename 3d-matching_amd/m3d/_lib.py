@@ -50,6 +50,16 @@ class IcpParams(C.Structure):
                 ("estimation", i32), ("nn_method", i32), ("reserved", i32)]
 
 
+class FeatureRansacParams(C.Structure):
+    _fields_ = [("max_correspondence_distance", dbl), ("confidence", dbl), ("edge_length", dbl),
+                ("distance", dbl), ("seed", u64), ("max_iteration", i32), ("ransac_n", i32)]
+
+
+class FeatureRansacResult(C.Structure):
+    _fields_ = [("T", dbl * 16), ("fitness", dbl), ("inlier_rmse", dbl), ("best_index", i64),
+                ("validations", i64)]
+
+
 class IcpResult(C.Structure):
     _fields_ = [("T", dbl * 16), ("fitness", dbl), ("inlier_rmse", dbl),
                 ("num_correspondences", i64), ("iterations", i32), ("converged", i32)]
@@ -91,7 +101,15 @@ SIGNATURES = {
     "m3d_icp_result_get": (C.c_int, [vp, C.POINTER(IcpResult), vp]),
     "m3d_icp_corr": (vp, [vp]),
     "m3d_icp_copy_corr": (C.c_int, [vp, vp, vp]),
-    "m3d_debug_kabsch3_host": (C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
+    "m3d_voxel_down_sample": (C.c_int, [vp, vp, vp, i64, dbl, vp, vp, C.POINTER(i64), vp]),
+    "m3d_hybrid_search": (C.c_int, [vp, vp, dbl, i32, vp, vp, vp, vp]),
+    "m3d_estimate_normals": (C.c_int, [vp, vp, dbl, i32, vp, vp]),
+    "m3d_compute_fpfh": (C.c_int, [vp, vp, vp, dbl, i32, vp, vp]),
+    "m3d_feature_correspondences": (C.c_int, [vp, vp, i64, vp, i64, i32, i32, dbl, vp,
+                                              C.POINTER(i64), vp]),
+    "m3d_ransac_on_correspondences": (C.c_int, [vp, vp, vp, vp, i64, C.POINTER(FeatureRansacParams),
+                                                C.POINTER(FeatureRansacResult), vp, vp]),
+    "m3d_debug_kabsch3_host":(C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
     "m3d_debug_ldlt6_host": (C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }
 

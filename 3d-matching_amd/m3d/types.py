@@ -25,6 +25,19 @@ class RegistrationResult:
                 f"and correspondence_set size of {len(self.correspondence_set)}")
 
 
+class Feature:
+    """Open3D ``pipelines.registration.Feature``: ``data`` is dimension × N (33×N for FPFH)."""
+
+    def __init__(self, data=None):
+        self.data = np.zeros((33, 0)) if data is None else np.asarray(data, np.float64)
+
+    def dimension(self) -> int:
+        return self.data.shape[0]
+
+    def num(self) -> int:
+        return self.data.shape[1]
+
+
 class PointCloud:
     def __init__(self, points=None, normals=None):
         self.points = np.zeros((0, 3)) if points is None else np.asarray(points, np.float64).reshape(-1, 3)

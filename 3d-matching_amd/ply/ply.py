@@ -1,11 +1,19 @@
-"""Point-cloud data holder mirroring the reference's ``src/ply/ply.py`` layout.
+"""Point-cloud data holder mirroring the reference's ``src/ply/ply.py``.
 
-The hot path only needs the reference ``Ply``'s LAYOUT: ``pcd`` (full-resolution
-points + normals, used by ICP), ``pcd_down`` (down-sampled points, used by RANSAC), ``pcd_fpfh``
-(33×N features) and ``voxel_size``.  ``Ply.from_arrays`` builds one from arrays (synthetic
-clouds, tests, benchmarks).  ``Ply(path, voxel_size)`` reads a PLY file (ASCII or binary
-little-endian, float/double x y z [nx ny nz]) with ``m3d.plyio``; on-device preprocessing
-(voxel down-sampling, normals, FPFH — SURVEY.md §8(f) rows 2-3) is applied when available.
+``Ply(path, voxel_size)`` follows ply.py:32-135 step by step, with every Open3D call replaced
+by the device path of ``m3d.prep``:
+
+1. read the PLY (``m3d.plyio``; Open3D ``read_point_cloud``)                       ply.py:80
+2. ``pcd_down`` = voxel down-sample (voxel_size)                                     ply.py:106
+3. ``pcd_down`` normals: hybrid search (2·v, 30)                                     ply.py:110-112
+4. ``pcd_fpfh`` = FPFH on ``pcd_down`` (hybrid 5·v, 100) — an Open3D-style ``Feature``
+   (``.data`` 33×N)                                                                  ply.py:117-120
+5. Gaussian noise N(0, 0.05²) on ``pcd_down`` points from the GLOBAL numpy RNG, after the
+   features (the reference's robustness test)                                        ply.py:61-62
+6. ``pcd`` normals: hybrid search (2·v, 30), oriented by normals read from the file  ply.py:65,133
+
+``Ply.from_arrays`` builds one from arrays (synthetic clouds, tests, benchmarks) without any
+preprocessing unless ``preprocess=True``.
 """
 
 from __future__ import annotations
@@ -14,7 +22,7 @@ from pathlib import Path
 
 import numpy as np
 
-from m3d.types import PointCloud
+from m3d.types import Feature, PointCloud
 
 
 class Ply:
@@ -31,15 +39,31 @@ class Ply:
         if len(pts) == 0:
             raise ValueError(f"Point cloud is empty: {self.path}")          # ply.py:81-84
         self.pcd = PointCloud(pts, nrm)
-        self.pcd_down = PointCloud(pts.copy())
-        self.pcd_fpfh = None
+        self._preprocess(voxel_size)
+
+    def _preprocess(self, voxel_size: float) -> None:
+        from m3d import prep
+
+        v = voxel_size
+        down, _ = prep.voxel_down_sample(self.pcd.points, v)
+        down_n = prep.estimate_normals(down, 2 * v, 30)
+        self.pcd_down = PointCloud(down, down_n)
+        self.pcd_fpfh = Feature(prep.compute_fpfh(down, down_n, 5 * v, 100).T)
+        noise = 0.05 * np.random.randn(*self.pcd_down.points.shape)      # ply.py:61-62
+        self.pcd_down.points = self.pcd_down.points + noise
+        prev = self.pcd.normals if self.pcd.has_normals() else None
+        self.pcd.normals = prep.estimate_normals(self.pcd.points, 2 * v, 30, normals=prev)
 
     @classmethod
-    def from_arrays(cls, points, normals=None, points_down=None, fpfh=None, voxel_size: float = 0.3):
+    def from_arrays(cls, points, normals=None, points_down=None, fpfh=None, voxel_size: float = 0.3,
+                    preprocess: bool = False):
         obj = cls.__new__(cls)
         obj.path = None
         obj.voxel_size = voxel_size
         obj.pcd = PointCloud(points, normals)
+        if preprocess:
+            obj._preprocess(voxel_size)
+            return obj
         obj.pcd_down = PointCloud(points if points_down is None else points_down)
-        obj.pcd_fpfh = None if fpfh is None else np.asarray(fpfh, np.float64)
+        obj.pcd_fpfh = None if fpfh is None else Feature(np.asarray(fpfh, np.float64))
         return obj

@@ -219,6 +219,72 @@ const int32_t* m3d_icp_corr(const m3d_icp* s);
 /* Copy the current correspondence array to dst [device] (ns int32). */
 int m3d_icp_copy_corr(const m3d_icp* s, int32_t* dst, void* stream);
 
+/* ------------------------------------------------------------------ preprocessing
+ * Open3D 0.19 semantics restated (oracle/prep_oracle.py); all fp64. */
+
+/* PointCloud::VoxelDownSample (src/ply/ply.py:106).  xyz [device] n×3, normals [device] n×3 or
+ * NULL; out_xyz / out_normals [device] with room for n×3; *out_n [host] = voxels.  Voxels come in
+ * ascending (ix, iy, iz) order (Open3D: unordered_map order, unspecified).  Synchronous. */
+int m3d_voxel_down_sample(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                          double voxel_size, double* out_xyz, double* out_normals, int64_t* out_n,
+                          void* stream);
+/* KDTreeFlann::SearchHybrid(p_i, radius, max_nn) for every point of the cloud (strict d² < r²,
+ * ascending (d², index)).  idx [device] n×max_nn int32 (-1 pad), d2 [device] n×max_nn f64,
+ * count [device] n int32.  Synchronous. */
+int m3d_hybrid_search(m3d_ctx* ctx, const m3d_cloud* cloud, double radius, int32_t max_nn,
+                      int32_t* idx, double* d2, int32_t* count, void* stream);
+/* PointCloud::EstimateNormals(KDTreeSearchParamHybrid(radius, max_nn)) (ply.py:110-112,133-135):
+ * covariance of the hybrid neighbourhood → FastEigen3x3; the cloud's own normals, if any, orient
+ * the result.  normals_out [device] n×3.  Synchronous. */
+int m3d_estimate_normals(m3d_ctx* ctx, const m3d_cloud* cloud, double radius, int32_t max_nn,
+                         double* normals_out, void* stream);
+/* ComputeFPFHFeature(cloud, KDTreeSearchParamHybrid(radius, max_nn)) (ply.py:117-120).
+ * normals [device] n×3; fpfh_out [device] n×33 row-major (Open3D's Feature.data is 33×n).
+ * Synchronous. */
+int m3d_compute_fpfh(m3d_ctx* ctx, const m3d_cloud* cloud, const double* normals, double radius,
+                     int32_t max_nn, double* fpfh_out, void* stream);
+
+/* ------------------------------------------------------------------ feature matching (a5, a6) */
+
+/* CorrespondencesFromFeatures (src/matcher/ransac.py:85): exact fp64 1-NN in feature space
+ * (lowest index on ties), optional mutual filter with Open3D's fallback to the one-directional
+ * set below mutual_consistent_ratio·ns pairs.  f_src [device] ns×dim, f_tgt [device] nt×dim
+ * (dim = 33), corr_out [device] room for ns×2 int32, *n_out [host].  Synchronous. */
+int m3d_feature_correspondences(m3d_ctx* ctx, const double* f_src, int64_t ns, const double* f_tgt,
+                                int64_t nt, int32_t dim, int32_t mutual_filter,
+                                double mutual_consistent_ratio, int32_t* corr_out, int64_t* n_out,
+                                void* stream);
+
+typedef struct {
+  double max_correspondence_distance; /* ransac.py:41 1.5·v */
+  double confidence;                  /* RANSACConvergenceCriteria.confidence (0.999) */
+  double edge_length;                 /* CorrespondenceCheckerBasedOnEdgeLength (0.9); <= 0 off */
+  double distance;                    /* CorrespondenceCheckerBasedOnDistance (1.5·v); <= 0 off */
+  uint64_t seed;                      /* counter sampler seed */
+  int32_t max_iteration;              /* RANSACConvergenceCriteria.max_iteration (30) */
+  int32_t ransac_n;                   /* 3 (only value supported; < 3 → empty result) */
+} m3d_feature_ransac_params;
+
+typedef struct {
+  double T[16];
+  double fitness;
+  double inlier_rmse;
+  int64_t best_index;  /* hypothesis id of the best, -1 = none */
+  int64_t validations; /* hypotheses that passed the checkers and were validated */
+} m3d_feature_ransac_result;
+
+/* RegistrationRANSACBasedOnCorrespondence (ransac.py:44-58 → Open3D): PointToPoint (no scaling),
+ * rows drawn with replacement by the counter sampler, checkers, validation over all source
+ * points (1-NN within max_correspondence_distance), IsBetterRANSACThan, early exit
+ * k = ceil(log(1-c)/log(1-fitness^3)).  corr [device] nc×2 int32 (source, target) rows.
+ * corr_set_out [device] ns int32 or NULL: the best transform's correspondence per source point
+ * (-1 none).  Synchronous. */
+int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt,
+                                  const int32_t* corr, int64_t nc,
+                                  const m3d_feature_ransac_params* params,
+                                  m3d_feature_ransac_result* out, int32_t* corr_set_out,
+                                  void* stream);
+
 /* ------------------------------------------------------------------ test hooks
  * Host-compiled copy of the device 3×3 linear algebra (same source), for CPU-side unit tests
  * of the math.  Never used by the product path. */

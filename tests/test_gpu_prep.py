@@ -1,0 +1,143 @@
+"""GPU parity of the preprocessing / feature-matching path (prep.hip, feat.hip) against the CPU
+oracle (oracle/prep_oracle.py; Open3D semantics restated, parity with Open3D itself unpinned).
+
+Bars (stated):
+* voxel down-sampling, hybrid neighbourhoods, feature correspondences: bit-exact (same fp64
+  operations in the same order; ties by index on both sides);
+* normals: within 1e-9 (the device's acos/cos may differ from the host libm by an ulp);
+* FPFH: within 1e-6 on ≥ 99.5 % of points (a pair feature that lands exactly on a bin edge
+  may switch bins when an ulp differs); every group of every row sums to 200 (or 0);
+* feature RANSAC: same best hypothesis, transform within 1e-9, fitness within 1e-3 (the
+  validation NN is the fp32-screened grid search).
+"""
+import numpy as np
+import pytest
+
+import prep_oracle as P
+from m3d import prep, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,voxel,with_normals", [(1, 0.3, False), (7, 10.0, True), (5000, 0.3, True),
+                                                  (60000, 0.3, False), (20000, 0.05, True)])
+def test_voxel_down_sample_exact(n, voxel, with_normals):
+    rng = np.random.default_rng(n)
+    pts = rng.uniform(-5, 5, (n, 3)) + np.array([100.0, -50.0, 3.0])
+    nrm = rng.normal(size=(n, 3)) if with_normals else None
+    got, gn = prep.voxel_down_sample(pts, voxel, nrm)
+    ref, rn = P.voxel_down_sample(pts, voxel, nrm)
+    np.testing.assert_array_equal(got, ref)
+    if with_normals:
+        np.testing.assert_array_equal(gn, rn)
+
+
+def test_voxel_down_sample_rejects_bad_voxel():
+    with pytest.raises(ValueError):
+        prep.voxel_down_sample(np.zeros((3, 3)), 0.0)
+    with pytest.raises(ValueError):
+        prep.voxel_down_sample(np.array([[0.0, 0, 0], [1e9, 0, 0]]), 1e-3)
+
+
+@pytest.mark.parametrize("case", ["surface", "duplicates", "plane", "offset"])
+def test_hybrid_search_exact(case):
+    rng = np.random.default_rng(3)
+    if case == "surface":
+        pts, _ = synth.surface_points(8000, seed=1)
+    elif case == "duplicates":
+        pts = np.repeat(rng.normal(size=(400, 3)), 5, axis=0)
+    elif case == "plane":
+        pts = np.c_[rng.uniform(-2, 2, (5000, 2)), np.zeros(5000)]
+    else:
+        pts = synth.surface_points(5000, seed=2)[0] + np.array([2e4, -1e4, 5e3])
+    for radius, k in [(0.6, 30), (1.5, 100)]:
+        gi, gd, gc = prep.hybrid_search(pts, radius, k)
+        ri, rd, rc = P.hybrid_search(pts, radius, k)
+        np.testing.assert_array_equal(gc, rc)
+        np.testing.assert_array_equal(gi, ri)
+        np.testing.assert_array_equal(gd, rd)
+
+
+def test_normals_match_oracle():
+    pts, true = synth.surface_points(6000, seed=4)
+    got = prep.estimate_normals(pts, 0.6, 30)
+    ref = P.estimate_normals(pts, 0.6, 30)
+    np.testing.assert_allclose(got, ref, atol=1e-9)
+    got = prep.estimate_normals(pts, 0.6, 30, normals=true)  # oriented like the file's normals
+    assert np.all(np.sum(got * true, axis=1) > 0)
+    # fewer than 3 neighbours → identity covariance → (0, 0, 1)
+    lone = np.array([[0.0, 0, 0], [10.0, 0, 0], [20.0, 0, 0]])
+    np.testing.assert_array_equal(prep.estimate_normals(lone, 1.0, 30), [[0, 0, 1]] * 3)
+
+
+def test_fpfh_matches_oracle():
+    pts, _ = synth.surface_points(2500, seed=5)
+    nrm = P.estimate_normals(pts, 0.8, 30)
+    got = prep.compute_fpfh(pts, nrm, 2.0, 100)
+    ref = P.compute_fpfh(pts, nrm, 2.0, 100)
+    row_ok = np.all(np.abs(got - ref) <= 1e-6 * np.maximum(1.0, np.abs(ref)), axis=1)
+    assert row_ok.mean() >= 0.995, row_ok.mean()
+    sums = got.reshape(-1, 3, 11).sum(axis=2)
+    assert np.all((np.abs(sums - 200.0) < 1e-9) | (sums == 0.0))
+
+
+@pytest.mark.parametrize("mutual", [False, True])
+def test_feature_correspondences_exact(mutual):
+    pts, _ = synth.surface_points(3000, seed=6)
+    nrm = P.estimate_normals(pts, 0.8, 30)
+    f = P.compute_fpfh(pts, nrm, 2.0, 100)
+    T = synth.random_rigid(2, rot_range=0.4, trans_range=0.5)
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(len(pts))
+    ft = f[perm] + rng.normal(scale=0.5, size=f.shape)
+    got = prep.feature_correspondences(f, ft, mutual)
+    ref = P.correspondences_from_features(f, ft, mutual)
+    np.testing.assert_array_equal(got, ref)
+    del T
+
+
+def test_feature_ransac_matches_oracle():
+    src, _ = synth.surface_points(4000, seed=8)
+    T = synth.random_rigid(3, rot_range=0.5, trans_range=1.0)
+    tgt = synth.apply(T, src) + np.random.default_rng(1).normal(scale=0.01, size=src.shape)
+    rng = np.random.default_rng(2)
+    corr = np.c_[np.arange(4000), np.arange(4000)]
+    bad = rng.random(4000) < 0.6
+    corr[bad, 1] = rng.integers(0, 4000, int(bad.sum()))
+    kw = dict(max_iteration=300, confidence=0.999, edge_length=0.9, distance=0.45)
+    got = prep.ransac_on_correspondences(src, tgt, corr, 0.45, seed=11, **kw)
+    ref = P.ransac_feature(src, tgt, corr, 0.45, lambda h: P.native_rows(11, h, len(corr)), **kw)
+    assert got.best_index == ref["best_index"]
+    assert got.validations == ref["validations"]
+    np.testing.assert_allclose(got.transformation, ref["transformation"], atol=1e-9)
+    assert abs(got.fitness - ref["fitness"]) < 1e-3
+    np.testing.assert_allclose(got.transformation, T, atol=2e-2)
+    assert len(got.correspondence_set) == round(got.fitness * len(src))
+
+
+def test_feature_ransac_empty_cases():
+    pts, _ = synth.surface_points(100, seed=1)
+    out = prep.ransac_on_correspondences(pts, pts, np.zeros((2, 2), np.int32), 0.45)
+    assert out.fitness == 0.0 and out.best_index == -1
+    np.testing.assert_array_equal(out.transformation, np.eye(4))
+
+
+def test_ply_pipeline_registers_synthetic_scan(tmp_path):
+    """Ply(path) → global_registration → refine_registration on a synthetic scan pair
+    (cfg4's pipeline; the reference ships no scans)."""
+    from m3d import plyio
+    from matcher.icp import refine_registration
+    from matcher.ransac import global_registration
+    from ply import Ply
+
+    pts, nrm = synth.surface_points(40000, seed=21)
+    T = synth.random_rigid(22, rot_range=0.5, trans_range=0.5)
+    plyio.write_ply(tmp_path / "src.ply", synth.apply(np.linalg.inv(T), pts), binary=True)
+    plyio.write_ply(tmp_path / "tgt.ply", synth.surface_points(40000, seed=23)[0], binary=False)
+    np.random.seed(0)
+    src, tgt = Ply(tmp_path / "src.ply", 0.3), Ply(tmp_path / "tgt.ply", 0.3)
+    assert src.pcd_fpfh.data.shape == (33, len(src.pcd_down.points))
+    coarse = global_registration(src, tgt, 0.3, iteration=30000)
+    assert coarse.fitness > 0.3
+    fine = refine_registration(src, tgt, coarse.transformation, 0.3)
+    np.testing.assert_allclose(fine.transformation, T, atol=5e-3)
