@@ -604,6 +604,12 @@ int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int
   }
   rc = device_mean3(ctx, c->xyz64, n, c->center, st);
   if (!rc) rc = center_pack(ctx, c->xyz64, n, c->n_pad, c->center, c->xyz32, kFar, &c->rmax, st);
+  if (!rc) {
+    // fp16 screen operand scale: a power of two with |S·x|∞ ≤ 32 (icp.hip pack16_sorted)
+    int ex = 0;
+    std::frexp(std::max(c->rmax, 1e-30) / 32.0, &ex);
+    c->s16 = std::ldexp(1.0, -std::min(std::max(ex, -100), 100));
+  }
   if (rc) {
     m3d_cloud_destroy(c);
     return rc;
@@ -680,11 +686,18 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
             "unknown nn_method");
   hipSetDevice(ctx->device);
   const Grid *tg = nullptr, *sg = nullptr;
-  if (params->nn_method == M3D_NN_GRID) {
-    // cell ≈ the search radius: a query visits 3 cells per axis
+  {
+    // Grid NN: cell ≈ the search radius, a query visits 3 cells per axis.  Brute force: the
+    // same grids only ORDER the points (targets and queries in cell order make the MFMA
+    // screen's 32-target sub-tiles and 64-query waves spatially compact); every pair is still
+    // screened.
     const double cell = max_dist * 1.001;
     int grc = ensure_grid(ctx, tgt, cell, nullptr, &tg);
     if (!grc) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
+    if (!grc && params->nn_method == M3D_NN_BRUTE && tg->mf16 == nullptr) {
+      hipError_t e = build_mfma_tiles(tgt, const_cast<Grid*>(tg), nullptr);
+      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("mfma tiles: ") + hipGetErrorString(e));
+    }
     if (grc) return grc;
   }
   m3d_icp* s = new m3d_icp();
@@ -694,10 +707,8 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   s->params = *params;
   s->max_dist = max_dist;
   s->nblocks = terms_blocks(src->n);
-  if (params->nn_method == M3D_NN_GRID) {
-    s->tgrid = tg;
-    s->qorder = sg->order;
-  }
+  s->tgrid = tg;
+  s->qorder = sg->order;
   int rc = dev_alloc(ctx, &s->state, 1);
   if (!rc) rc = dev_alloc(ctx, &s->keys, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->corr, std::max<int64_t>(src->n, 1));

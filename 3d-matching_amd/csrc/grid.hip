@@ -281,9 +281,14 @@ void grid_free(Grid* g) {
   hipFree(g->start);
   hipFree(g->pts);
   hipFree(g->order);
+  hipFree(g->mf16);
+  hipFree(g->mf32);
   g->start = nullptr;
   g->pts = nullptr;
   g->order = nullptr;
+  g->mf16 = nullptr;
+  g->mf32 = nullptr;
+  g->mf_npad = 0;
 }
 
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,

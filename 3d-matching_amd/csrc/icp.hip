@@ -53,9 +53,17 @@ __device__ __forceinline__ uint64_t make_key(float d2, uint32_t j) {
 }
 
 // ------------------------------------------------------------------------------- state
+struct FrameParams {
+  double cs[3], ct[3];
+  double pinf, qinf;
+  double s16;  // the target cloud's fp16 operand scale (power of two)
+};
+
 // Refresh the fp32 search transform and radius bound for the current T (device side).
-__device__ void refresh_rt32(IcpState* s, const double* cs, const double* ct, double pinf,
-                             double qinf) {
+__device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
+  const double* cs = f.cs;
+  const double* ct = f.ct;
+  const double pinf = f.pinf, qinf = f.qinf;
   double rowl1 = 0.0, tinf = 0.0;
   for (int i = 0; i < 3; ++i) {
     const double* r = s->T + 4 * i;
@@ -78,12 +86,29 @@ __device__ void refresh_rt32(IcpState* s, const double* cs, const double* ct, do
   const double es = 2.0 * (E1 + 6.0 * kU * (double)s->r2_hi + 12.0 * kU * Q * Q) + 1e-30;
   const float esf = __double2float_ru(es);
   s->screen_eps = isfinite(esf) ? esf : FLT_MAX;
+  // MFMA screen (nn_mfma_kernel): the same key from fp16 hi/lo operands scaled
+  // by S = s16, in S² units.  Per coordinate a = −2Sq, t = St split as x = xh + xl + r with
+  // |r| ≤ u16²|x| + 2σ (u16 = 2⁻¹¹, σ = 2⁻²⁵ fp16 subnormal half-spacing); the dropped al·tl and
+  // the split remainders cost ≤ 3u16²|a||t| + 4σ(|a| + |t|) per coordinate, the w = S²|t|² split
+  // u16²|w| + 2σ; the 11 exact fp16 products are accumulated in fp32 by the MFMA in an
+  // unspecified order: ≤ 32·u·Σ|products| (a bound for ≤ 16 additions even if each rounds by a
+  // full ulp).  Back in unscaled units (÷ S²) plus the stored-|t|² rounding u·|t|².
+  const double S = f.s16;
+  const double As = 2.0 * Q * S, Ts = qinf * S;
+  const double Ws = 3.0 * Ts * Ts * (1.0 + 1e-6);
+  const double u16 = 4.8828125e-04, sig = 2.98023223876953125e-08;
+  const double P = 3.0 * As * Ts;
+  const double Esplit = 3.0 * u16 * u16 * P + 4.0 * sig * 3.0 * (As + Ts) + u16 * u16 * Ws + 2.0 * sig;
+  const double Eacc = 32.0 * kU * 1.01 * (P + Ws);
+  const double E1m = 1.05 * (Esplit + Eacc) / (S * S) + kU * 3.0 * qinf * qinf;
+  const double esm = 2.0 * (E1m + 6.0 * kU * (double)s->r2_hi + 12.0 * kU * Q * Q) + 1e-30;
+  const float esmf = __double2float_ru(esm);
+  s->screen_eps_m = isfinite(esmf) ? esmf : FLT_MAX;
+  s->mfma_scale = (float)S;
+  // operands must stay well inside the fp16 range (max 65504) and the bound finite
+  s->mfma_ok = (As < 16384.0 && Ts < 16384.0 && Ws < 16384.0 && isfinite(esmf) &&
+                s->r2_hi < FLT_MAX && esmf < 0.25f * FLT_MAX) ? 1 : 0;
 }
-
-struct FrameParams {
-  double cs[3], ct[3];
-  double pinf, qinf;
-};
 
 __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, double T3, double T4,
                                 double T5, double T6, double T7, double T8, double T9, double T10,
@@ -97,7 +122,7 @@ __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, do
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
   s->r2 = r2;
-  refresh_rt32(s, f.cs, f.ct, f.pinf, f.qinf);
+  refresh_rt32(s, f);
 }
 
 // state for evaluating transform T (device, row-major 4×4): feature-RANSAC validation (a6)
@@ -108,7 +133,7 @@ __global__ void icp_set_T_kernel(IcpState* s, const double* __restrict__ T, doub
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
   s->r2 = r2;
-  refresh_rt32(s, f.cs, f.ct, f.pinf, f.qinf);
+  refresh_rt32(s, f);
 }
 
 // ------------------------------------------------------------------------------- keyinit
@@ -140,8 +165,8 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
                                                       const float4* __restrict__ tgt,
                                                       int64_t nt_pad, int64_t slice_len,
                                                       int64_t off, const IcpState* __restrict__ s,
-                                                      int64_t* __restrict__ keys) {
-  if (s->done) return;
+                                                      int64_t* __restrict__ keys, int mfma_on) {
+  if (s->done || (mfma_on && s->mfma_ok)) return;  // the MFMA screen runs instead
   const float* Rt = s->Rt32;  // uniform → scalar loads (a local copy went to scratch)
   const float r2_hi = s->r2_hi;
   const float eps = s->screen_eps;
@@ -250,6 +275,215 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
       atomicMin((unsigned long long*)&keys[qi[q]], (unsigned long long)make_key(best[q], bidx[q]));
     }
   }
+}
+
+// ------------------------------------------------------------------------------- NN, MFMA screen
+// The screen key |t|² − 2q·t is a rank-4 contraction over (x, y, z, 1): here it runs on the
+// matrix cores.  One v_mfma_f32_32x32x16_f16 computes S²·key for 32 targets (A rows) × 32
+// queries (B columns) from fp16 hi/lo splits of the S-scaled operands, K = 16:
+//   A (target) = [xh, xh, xl, yh, yh, yl, zh, zh | zl, wh, wl, 0, 0, 0, 0, 0]
+//   B (query)  = [ah, al, ah, bh, bl, bh, ch, cl | ch, 1,  1,  0, 0, 0, 0, 0]   (a,b,c) = −2S·q
+// Products of fp16 are exact in fp32; the bound on the whole key error is screen_eps_m
+// (refresh_rt32).  A lane holds column c = lane & 31 (its query) and 16 of the 32 rows; the
+// lane pair (c, c + 32) covers all 32.  Per MFMA the lane takes the minimum of its 16 values
+// (v_min3) and tests it against its query's threshold; a sub-tile that hits anywhere in the
+// wave runs the fp32 exact path of nn_kernel (direct d², lexicographic (d², index)) over the
+// lane's 16 rows, and the pair merges its two states with one shuffle.  Result: the same key
+// as nn_kernel and the grid search, at ~1/16 of the fp32 VALU screen's issue cost per pair.
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMG = 2;        // 32-query groups per wave
+constexpr int kMTile = 256;   // targets per LDS tile: fp16 operands 8 KB + fp32 coordinates 4 KB
+constexpr int kMBlock = 256;  // 4 waves × kMG × 32 = 256 queries per block
+constexpr int kMQueries = 4 * kMG * 32;
+
+__device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+
+union H8 {
+  uint4 u;
+  half8 h;
+};
+
+// MFMA screen operands of a cloud in its grid's cell order (A rows of nn_mfma_kernel):
+// mf16 = fp16 split, mf32 = (x, y, z, original index bits).  Pads: key 65504 (never hit),
+// far-away coordinates (never accepted by the exact path).
+__global__ __launch_bounds__(256) void pack16_sorted_kernel(const float4* __restrict__ sorted,
+                                                            const float4* __restrict__ xyz32,
+                                                            int64_t n, int64_t n_pad, float S,
+                                                            uint4* __restrict__ mf16,
+                                                            float4* __restrict__ mf32) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n_pad) return;
+  H8 a, b;
+  a.u = make_uint4(0, 0, 0, 0);
+  b.u = make_uint4(0, 0, 0, 0);
+  if (k < n) {
+    const int32_t idx = __float_as_int(sorted[k].w);
+    const float4 t = xyz32[idx];  // w = |t|² (center_pack)
+    _Float16 xh, xl, yh, yl, zh, zl, wh, wl;
+    split16(t.x * S, xh, xl);
+    split16(t.y * S, yh, yl);
+    split16(t.z * S, zh, zl);
+    split16(t.w * (S * S), wh, wl);
+    a.h = half8{xh, xh, xl, yh, yh, yl, zh, zh};
+    b.h = half8{zl, wh, wl, (_Float16)0, (_Float16)0, (_Float16)0, (_Float16)0, (_Float16)0};
+    mf32[k] = make_float4(t.x, t.y, t.z, __int_as_float(idx));
+  } else {
+    b.h[1] = (_Float16)65504.0f;
+    mf32[k] = make_float4(1.0e18f, 1.0e18f, 1.0e18f, __int_as_float(-1));
+  }
+  mf16[2 * k] = a.u;
+  mf16[2 * k + 1] = b.u;
+}
+
+hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st) {
+  const int64_t n = c->n;
+  const int64_t n_pad = std::max<int64_t>((n + kMTile - 1) / kMTile * kMTile, kMTile);
+  hipError_t e = hipMalloc(&g->mf16, sizeof(uint4) * 2 * n_pad);
+  if (e == hipSuccess) e = hipMalloc(&g->mf32, sizeof(float4) * n_pad);
+  if (e != hipSuccess) return e;
+  g->mf_npad = n_pad;
+  pack16_sorted_kernel<<<(unsigned)((n_pad + 255) / 256), 256, 0, st>>>(
+      g->pts, c->xyz32, n, n_pad, (float)c->s16, g->mf16, g->mf32);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  return e;
+}
+
+__global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restrict__ src32,
+                                                          int64_t ns,
+                                                          const int32_t* __restrict__ order,
+                                                          const uint4* __restrict__ tgt16,
+                                                          const float4* __restrict__ tgt32,
+                                                          int64_t nt_pad, int64_t slice_len,
+                                                          int64_t off,
+                                                          const IcpState* __restrict__ s,
+                                                          int64_t* __restrict__ keys) {
+  if (s->done || !s->mfma_ok) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const float* Rt = s->Rt32;
+  const float r2_hi = s->r2_hi, eps = s->screen_eps_m, S = s->mfma_scale;
+  const float S2 = S * S;
+  float qx[kMG], qy[kMG], qz[kMG], qq[kMG], best[kMG], thr[kMG];
+  uint32_t bidx[kMG], bidx0[kMG];
+  int64_t qi[kMG];
+  half8 bq[kMG];
+#pragma unroll
+  for (int g = 0; g < kMG; ++g) {
+    const int64_t slot = (int64_t)blockIdx.x * kMQueries + (wave * kMG + g) * 32 + c;
+    const int64_t i = slot < ns ? (order != nullptr ? (int64_t)order[slot] : slot) : ns;
+    qi[g] = i;
+    if (i < ns) {
+      xform32(Rt, src32[i], qx[g], qy[g], qz[g]);
+      const int64_t key = keys[i];
+      if (key == kKeyNone) {
+        best[g] = r2_hi;
+        bidx[g] = 0xFFFFFFFFu;
+      } else {
+        best[g] = __uint_as_float((uint32_t)((uint64_t)key >> 32));
+        bidx[g] = (uint32_t)key;
+      }
+    } else {
+      qx[g] = qy[g] = qz[g] = 0.0f;  // inactive: negative threshold, never hits
+      best[g] = -1.0f;
+      bidx[g] = 0xFFFFFFFFu;
+    }
+    bidx0[g] = bidx[g];
+    qq[g] = fmaf(qz[g], qz[g], fmaf(qy[g], qy[g], qx[g] * qx[g]));
+    thr[g] = ((best[g] - qq[g]) + eps) * S2;  // × power of two: exact
+    _Float16 ah, al, bh, bl, ch, cl;
+    split16(-2.0f * S * qx[g], ah, al);
+    split16(-2.0f * S * qy[g], bh, bl);
+    split16(-2.0f * S * qz[g], ch, cl);
+    const _Float16 one = (_Float16)1.0f, zero = (_Float16)0.0f;
+    bq[g] = h == 0 ? half8{ah, al, ah, bh, bl, bh, ch, cl} : half8{ch, one, one, zero, zero, zero, zero, zero};
+  }
+  const floatx16 zacc = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
+                         0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  // [buffer][lane half][target]: a half-wave's 32 ds_read_b128 hit 32 consecutive 16-B slots
+  __shared__ uint4 t16[2][2][kMTile];
+  __shared__ float4 t32[2][kMTile];
+  const int64_t jb = (int64_t)blockIdx.y * slice_len;
+  const int64_t je = min(nt_pad, jb + slice_len);
+  t16[0][0][threadIdx.x] = tgt16[2 * (jb + threadIdx.x)];
+  t16[0][1][threadIdx.x] = tgt16[2 * (jb + threadIdx.x) + 1];
+  t32[0][threadIdx.x] = tgt32[jb + threadIdx.x];
+  __syncthreads();
+  int buf = 0;
+  for (int64_t j0 = jb; j0 < je; j0 += kMTile) {
+    const bool has_next = j0 + kMTile < je;
+    uint4 p0, p1;
+    float4 p2;
+    if (has_next) {
+      const int64_t jn = j0 + kMTile + threadIdx.x;
+      p0 = tgt16[2 * jn];
+      p1 = tgt16[2 * jn + 1];
+      p2 = tgt32[jn];
+    }
+    for (int sb = 0; sb < kMTile; sb += 32) {
+      H8 av;
+      av.u = t16[buf][h][sb + c];
+      bool hit[kMG];
+      bool any_hit = false;
+#pragma unroll
+      for (int g = 0; g < kMG; ++g) {
+        const floatx16 k = __builtin_amdgcn_mfma_f32_32x32x16_f16(av.h, bq[g], zacc, 0, 0, 0);
+        float m = fminf(fminf(k[0], k[1]), k[2]);
+        m = fminf(fminf(m, k[3]), k[4]);
+        m = fminf(fminf(m, k[5]), k[6]);
+        m = fminf(fminf(m, k[7]), k[8]);
+        m = fminf(fminf(m, k[9]), k[10]);
+        m = fminf(fminf(m, k[11]), k[12]);
+        m = fminf(fminf(m, k[13]), k[14]);
+        m = fminf(m, k[15]);
+        hit[g] = m <= thr[g];
+        any_hit = any_hit || hit[g];
+      }
+      if (!__any(any_hit)) continue;
+#pragma unroll
+      for (int g = 0; g < kMG; ++g) {
+        const bool hp = hit[g] || (__shfl_xor((int)hit[g], 32) != 0);
+        if (!__any(hp)) continue;
+        if (hp) {
+          // exact path over this lane's 16 rows (the partner lane holds the other 16)
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int r = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const float4 t = t32[buf][sb + r];
+            const float d2 = d2f(qx[g], qy[g], qz[g], t.x, t.y, t.z);
+            const uint32_t gj = (uint32_t)(off + __float_as_int(t.w));  // pads: d² ~ 1e36
+            if (d2 < best[g] || (d2 == best[g] && gj < bidx[g])) {
+              best[g] = d2;
+              bidx[g] = gj;
+            }
+          }
+        }
+        const float ob = __shfl_xor(best[g], 32);
+        const uint32_t oi = (uint32_t)__shfl_xor((int)bidx[g], 32);
+        if (ob < best[g] || (ob == best[g] && oi < bidx[g])) {
+          best[g] = ob;
+          bidx[g] = oi;
+        }
+        thr[g] = ((best[g] - qq[g]) + eps) * S2;
+      }
+    }
+    if (has_next) {
+      t16[buf ^ 1][0][threadIdx.x] = p0;
+      t16[buf ^ 1][1][threadIdx.x] = p1;
+      t32[buf ^ 1][threadIdx.x] = p2;
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int g = 0; g < kMG; ++g)
+    if (h == 0 && qi[g] < ns && bidx[g] != bidx0[g])
+      atomicMin((unsigned long long*)&keys[qi[g]], (unsigned long long)make_key(best[g], bidx[g]));
 }
 
 // ------------------------------------------------------------------------------- terms
@@ -436,7 +670,7 @@ __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restri
     for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
   matmul4(upd, s->T, s->T);
   s->iters += 1;
-  refresh_rt32(s, sp.f.cs, sp.f.ct, sp.f.pinf, sp.f.qinf);
+  refresh_rt32(s, sp.f);
 }
 
 // finalize standalone NN (m3d_nn1): exact radius test in fp64
@@ -485,6 +719,7 @@ static FrameParams frame_of(const m3d_icp* s) {
   }
   f.pinf = s->src->rmax;
   f.qinf = s->tgt->rmax;
+  f.s16 = s->tgt->s16;
   return f;
 }
 
@@ -508,6 +743,20 @@ hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t off, hipStream_t st) {
   return hipGetLastError();
 }
 
+// target slices over grid.y so that ≥ ~2048 blocks fill the chip; slices ≥ 1024 targets and a
+// multiple of `mult`
+static dim3 nn_grid(int64_t bx, int64_t nt_pad, int64_t mult, int64_t* slice_out) {
+  int64_t S = (2048 + bx - 1) / bx;
+  const int64_t max_s = nt_pad / 1024 > 0 ? nt_pad / 1024 : 1;
+  if (S > max_s) S = max_s;
+  if (S < 1) S = 1;
+  int64_t slice = (nt_pad + S - 1) / S;
+  slice = (slice + mult - 1) / mult * mult;
+  S = (nt_pad + slice - 1) / slice;
+  *slice_out = slice;
+  return dim3((unsigned)bx, (unsigned)S);
+}
+
 hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
   const int64_t ns = s->src->n;
   const int64_t nt_pad = s->tgt->n_pad;
@@ -517,23 +766,28 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
     const int v = e ? atoi(e) : kNNQDefault;
     return (v == 1 || v == 2 || v == 4) ? v : kNNQDefault;
   }();
-  const int64_t bx = (ns + kNNBlock * Q - 1) / (kNNBlock * Q);
-  // fill ≥ 2048 blocks (8 per CU) by splitting the target range; keep slices ≥ 1024 targets
-  int64_t S = (2048 + bx - 1) / bx;
-  const int64_t max_s = nt_pad / 1024 > 0 ? nt_pad / 1024 : 1;
-  if (S > max_s) S = max_s;
-  if (S < 1) S = 1;
-  int64_t slice = (nt_pad + S - 1) / S;
-  slice = (slice + kNNLds - 1) / kNNLds * kNNLds;
-  S = (nt_pad + slice - 1) / slice;
-  dim3 grid((unsigned)bx, (unsigned)S);
+  static const bool mfma_env = [] {
+    const char* e = getenv("M3D_NN_MFMA");
+    return !(e && atoi(e) == 0);
+  }();
+  // The MFMA screen runs when the scaled operands fit fp16 (decided on the device by
+  // refresh_rt32); the fp32 VALU screen is launched behind it and exits at once in that case.
+  const Grid* tg = s->tgrid;
+  const int mfma_on = (mfma_env && tg != nullptr && tg->mf16 != nullptr) ? 1 : 0;
+  int64_t slice = 0;
+  if (mfma_on) {
+    const dim3 gm = nn_grid((ns + kMQueries - 1) / kMQueries, tg->mf_npad, kMTile, &slice);
+    nn_mfma_kernel<<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
+                                           tg->mf_npad, slice, off, s->state, s->keys);
+  }
+  const dim3 grid = nn_grid((ns + kNNBlock * Q - 1) / (kNNBlock * Q), nt_pad, kNNLds, &slice);
   const float4* tp = s->tgt->xyz32;
   if (Q == 4)
-    nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
+    nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, mfma_on);
   else if (Q == 2)
-    nn_kernel<2><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
+    nn_kernel<2><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, mfma_on);
   else
-    nn_kernel<1><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
+    nn_kernel<1><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, mfma_on);
   return hipGetLastError();
 }
 

@@ -65,6 +65,10 @@ struct IcpState {
   double r2;          // max_dist² (fp64, strict <)
   float r2_hi;        // fp32 search bound (≥ r2 plus guard)
   float screen_eps;   // NN screen error bound (icp.hip refresh_rt32)
+  float screen_eps_m; // NN screen error bound of the fp16-split MFMA screen
+  float mfma_scale;   // power-of-two scale of the fp16 operands (the target cloud's s16)
+  int32_t mfma_ok;    // scaled query magnitudes fit fp16: the MFMA screen may run
+  int32_t pad_;
 };
 
 // Uniform grid over a cloud's centred fp32 points (grid.hip): kernel view + owner.
@@ -85,6 +89,11 @@ struct Grid {
   int64_t n_pts = 0;
   double cell = 0.0;      // cell size used
   double cell_req = 0.0;  // cell size requested
+  // brute-force MFMA screen operands in this grid's cell order (icp.hip pack16_sorted), padded
+  // to mf_npad: fp16 hi/lo split (2 × uint4 per point) + fp32 (x, y, z, original index bits)
+  uint4* mf16 = nullptr;
+  float4* mf32 = nullptr;
+  int64_t mf_npad = 0;
 };
 
 constexpr int kTermSlots = 32;  // 21 JTJ + 6 JTr + r² + count + Σd² (+2 pad)
@@ -126,6 +135,7 @@ struct m3d_cloud {
   float4* xyz32 = nullptr;  // n_pad centred (pad = far away)
   double center[3] = {0, 0, 0};
   double rmax = 0.0;  // max |x_c|∞ (guard-band bound)
+  double s16 = 1.0;  // power-of-two scale of the fp16 MFMA screen operands (|s16·x|∞ ≤ 32)
   mutable std::vector<m3d::Grid*> grids;  // uniform grids built on demand, one per cell size
 };
 
@@ -199,6 +209,7 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order,
                           int64_t off, const IcpState* s, int64_t* keys, hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
 hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st);
+hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st);
 
 // preprocessing (prep.hip) and feature matching (feat.hip)
 hipError_t voxel_down_sample(const double* xyz, const double* nrm, int64_t n, double voxel,
