@@ -293,10 +293,12 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int kMG = 2;        // 32-query groups per wave
+constexpr int kMGDefault = 2;  // 32-query groups per wave (M3D_NN_MG = 1|2|4 overrides, tuning)
 constexpr int kMTile = 256;   // targets per LDS tile: fp16 operands 8 KB + fp32 coordinates 4 KB
-constexpr int kMBlock = 256;  // 4 waves × kMG × 32 = 256 queries per block
-constexpr int kMQueries = 4 * kMG * 32;
+constexpr int kMBlock = 512;  // 8 waves × kMG × 32 = 512 queries per block: every target tile
+                              // staged in LDS serves 512 queries (L2→LDS traffic per pair halved)
+template <int kMG>
+constexpr int mqueries() { return (kMBlock / 64) * kMG * 32; }
 
 __device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
   hi = (_Float16)x;
@@ -307,6 +309,10 @@ union H8 {
   uint4 u;
   half8 h;
 };
+
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
 
 // MFMA screen operands of a cloud in its grid's cell order (A rows of nn_mfma_kernel):
 // mf16 = fp16 split, mf32 = (x, y, z, original index bits).  Pads: key 65504 (never hit),
@@ -336,8 +342,8 @@ __global__ __launch_bounds__(256) void pack16_sorted_kernel(const float4* __rest
     b.h[1] = (_Float16)65504.0f;
     mf32[k] = make_float4(1.0e18f, 1.0e18f, 1.0e18f, __int_as_float(-1));
   }
-  mf16[2 * k] = a.u;
-  mf16[2 * k + 1] = b.u;
+  mf16[k] = a.u;  // two planes: elements 0-7 (lane half 0), elements 8-15 (lane half 1)
+  mf16[n_pad + k] = b.u;
 }
 
 hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st) {
@@ -354,6 +360,7 @@ hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st) {
   return e;
 }
 
+template <int kMG>
 __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restrict__ src32,
                                                           int64_t ns,
                                                           const int32_t* __restrict__ order,
@@ -375,7 +382,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   half8 bq[kMG];
 #pragma unroll
   for (int g = 0; g < kMG; ++g) {
-    const int64_t slot = (int64_t)blockIdx.x * kMQueries + (wave * kMG + g) * 32 + c;
+    const int64_t slot = (int64_t)blockIdx.x * mqueries<kMG>() + (wave * kMG + g) * 32 + c;
     const int64_t i = slot < ns ? (order != nullptr ? (int64_t)order[slot] : slot) : ns;
     qi[g] = i;
     if (i < ns) {
@@ -405,62 +412,64 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   }
   const floatx16 zacc = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
                          0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  // [buffer][lane half][target]: a half-wave's 32 ds_read_b128 hit 32 consecutive 16-B slots
+  // [buffer][lane half][target]: a half-wave's 32 ds_read_b128 hit 32 consecutive 16-B slots.
+  // Thread t stages element plane t / kMTile of target t % kMTile (mf16 is stored as two
+  // planes, so the loads are coalesced).  The fp32 coordinates are read from global memory by
+  // the (rare) exact path only.
+  static_assert(kMBlock == 2 * kMTile, "one 16-B operand half per thread per tile");
   __shared__ uint4 t16[2][2][kMTile];
-  __shared__ float4 t32[2][kMTile];
+  const int sp = threadIdx.x / kMTile, sk = threadIdx.x % kMTile;
   const int64_t jb = (int64_t)blockIdx.y * slice_len;
   const int64_t je = min(nt_pad, jb + slice_len);
-  t16[0][0][threadIdx.x] = tgt16[2 * (jb + threadIdx.x)];
-  t16[0][1][threadIdx.x] = tgt16[2 * (jb + threadIdx.x) + 1];
-  t32[0][threadIdx.x] = tgt32[jb + threadIdx.x];
+  t16[0][sp][sk] = tgt16[sp * nt_pad + jb + sk];
   __syncthreads();
   int buf = 0;
   for (int64_t j0 = jb; j0 < je; j0 += kMTile) {
     const bool has_next = j0 + kMTile < je;
-    uint4 p0, p1;
-    float4 p2;
-    if (has_next) {
-      const int64_t jn = j0 + kMTile + threadIdx.x;
-      p0 = tgt16[2 * jn];
-      p1 = tgt16[2 * jn + 1];
-      p2 = tgt32[jn];
+    uint4 pre;
+    if (has_next) pre = tgt16[sp * nt_pad + j0 + kMTile + sk];
+    // Sweep: MFMA + minimum + threshold test for the tile's 8 sub-tiles, branch-free; a
+    // sub-tile that hits anywhere in the wave sets a bit of the wave-uniform mask (SALU).
+    // Software-pipelined: the MFMA of step t+1 is issued before the minimum of step t is taken,
+    // so a wave never waits on its own MFMA result (two accumulator sets live).
+    uint32_t hm = 0;
+    constexpr int kSteps = (kMTile / 32) * kMG;  // (sub-tile, group) steps of this tile
+    H8 av[kMTile / 32];
+#pragma unroll
+    for (int sub = 0; sub < kMTile / 32; ++sub) av[sub].u = t16[buf][h][sub * 32 + c];
+    floatx16 kc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0].h, bq[0], zacc, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < kSteps; ++t) {
+      floatx16 kn;
+      if (t + 1 < kSteps)
+        kn = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[(t + 1) / kMG].h, bq[(t + 1) % kMG], zacc, 0, 0, 0);
+      // depth-3 tree of v_minimum3_f32 (IEEE minimum: no canonicalising v_max in front, as
+      // fminf needs; the keys are finite — fp16 operands — so NaN propagation never occurs)
+      const float m0 = vmin3(kc[0], kc[1], kc[2]), m1 = vmin3(kc[3], kc[4], kc[5]);
+      const float m2 = vmin3(kc[6], kc[7], kc[8]), m3 = vmin3(kc[9], kc[10], kc[11]);
+      const float m4 = vmin3(kc[12], kc[13], kc[14]);
+      const float m = __builtin_elementwise_minimum(vmin3(m0, m1, m2), vmin3(m3, m4, kc[15]));
+      const int g = t % kMG, sub = t / kMG;
+      if (__any(m <= thr[g])) hm |= 1u << (g * 8 + sub);
+      if (t + 1 < kSteps) kc = kn;
     }
-    for (int sb = 0; sb < kMTile; sb += 32) {
-      H8 av;
-      av.u = t16[buf][h][sb + c];
-      bool hit[kMG];
-      bool any_hit = false;
+    // Exact path for the flagged (group, sub-tile) pairs, every lane (exact for any lane): direct
+    // fp32 d² over the lane's 16 rows, then the lane pair (c, c + 32) merges its two states.
 #pragma unroll
-      for (int g = 0; g < kMG; ++g) {
-        const floatx16 k = __builtin_amdgcn_mfma_f32_32x32x16_f16(av.h, bq[g], zacc, 0, 0, 0);
-        float m = fminf(fminf(k[0], k[1]), k[2]);
-        m = fminf(fminf(m, k[3]), k[4]);
-        m = fminf(fminf(m, k[5]), k[6]);
-        m = fminf(fminf(m, k[7]), k[8]);
-        m = fminf(fminf(m, k[9]), k[10]);
-        m = fminf(fminf(m, k[11]), k[12]);
-        m = fminf(fminf(m, k[13]), k[14]);
-        m = fminf(m, k[15]);
-        hit[g] = m <= thr[g];
-        any_hit = any_hit || hit[g];
-      }
-      if (!__any(any_hit)) continue;
+    for (int g = 0; g < kMG; ++g) {
+      uint32_t m8 = (hm >> (g * 8)) & 0xFFu;
+      while (m8 != 0) {
+        const int sub = __builtin_ctz(m8);
+        m8 &= m8 - 1;
 #pragma unroll
-      for (int g = 0; g < kMG; ++g) {
-        const bool hp = hit[g] || (__shfl_xor((int)hit[g], 32) != 0);
-        if (!__any(hp)) continue;
-        if (hp) {
-          // exact path over this lane's 16 rows (the partner lane holds the other 16)
-#pragma unroll
-          for (int reg = 0; reg < 16; ++reg) {
-            const int r = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            const float4 t = t32[buf][sb + r];
-            const float d2 = d2f(qx[g], qy[g], qz[g], t.x, t.y, t.z);
-            const uint32_t gj = (uint32_t)(off + __float_as_int(t.w));  // pads: d² ~ 1e36
-            if (d2 < best[g] || (d2 == best[g] && gj < bidx[g])) {
-              best[g] = d2;
-              bidx[g] = gj;
-            }
+        for (int reg = 0; reg < 16; ++reg) {
+          const int r = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          const float4 t = tgt32[j0 + sub * 32 + r];
+          const float d2 = d2f(qx[g], qy[g], qz[g], t.x, t.y, t.z);
+          const uint32_t gj = (uint32_t)(off + __float_as_int(t.w));  // pads: d² ~ 1e36
+          if (d2 < best[g] || (d2 == best[g] && gj < bidx[g])) {
+            best[g] = d2;
+            bidx[g] = gj;
           }
         }
         const float ob = __shfl_xor(best[g], 32);
@@ -469,14 +478,10 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
           best[g] = ob;
           bidx[g] = oi;
         }
-        thr[g] = ((best[g] - qq[g]) + eps) * S2;
       }
+      thr[g] = ((best[g] - qq[g]) + eps) * S2;
     }
-    if (has_next) {
-      t16[buf ^ 1][0][threadIdx.x] = p0;
-      t16[buf ^ 1][1][threadIdx.x] = p1;
-      t32[buf ^ 1][threadIdx.x] = p2;
-    }
+    if (has_next) t16[buf ^ 1][sp][sk] = pre;
     __syncthreads();
     buf ^= 1;
   }
@@ -776,9 +781,22 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
   const int mfma_on = (mfma_env && tg != nullptr && tg->mf16 != nullptr) ? 1 : 0;
   int64_t slice = 0;
   if (mfma_on) {
-    const dim3 gm = nn_grid((ns + kMQueries - 1) / kMQueries, tg->mf_npad, kMTile, &slice);
-    nn_mfma_kernel<<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                           tg->mf_npad, slice, off, s->state, s->keys);
+    static const int MG = [] {
+      const char* e = getenv("M3D_NN_MG");
+      const int v = e ? atoi(e) : kMGDefault;
+      return (v == 1 || v == 2 || v == 4) ? v : kMGDefault;
+    }();
+    const int64_t mq = MG == 4 ? mqueries<4>() : (MG == 2 ? mqueries<2>() : mqueries<1>());
+    const dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, kMTile, &slice);
+    if (MG == 4)
+      nn_mfma_kernel<4><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
+                                                tg->mf_npad, slice, off, s->state, s->keys);
+    else if (MG == 2)
+      nn_mfma_kernel<2><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
+                                                tg->mf_npad, slice, off, s->state, s->keys);
+    else
+      nn_mfma_kernel<1><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
+                                                tg->mf_npad, slice, off, s->state, s->keys);
   }
   const dim3 grid = nn_grid((ns + kNNBlock * Q - 1) / (kNNBlock * Q), nt_pad, kNNLds, &slice);
   const float4* tp = s->tgt->xyz32;

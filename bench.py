@@ -12,11 +12,15 @@ BASELINE.json metric "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pt
 * "ransac": cfg2 — benchmark_ransac.py's loop (a1 sample + Kabsch, a2 ‖d‖ < 1.5·v scoring) at
   Nc = 1e5, H = 1e5 hypotheses per GPU, counter sampler seed 42, no early stop; N>1 shards the
   hypothesis ids and all-reduces MAX of the packed (count, ~id) best key.
-* roofline: dominant kernel = ICP NN scan, timed with HIP events recorded by the library on the
-  launch stream around every NN launch inside the timed region; algorithmic cost 8 flop per
-  (source, target) pair; peak = FP32 vector 157.3 TFLOP/s (no MFMA: the scan is
-  a min-reduction, not a contraction).  traffic = HBM bytes per launch from the committed
-  rocprofv3 PMC summary (profiles/), or null.
+* roofline: dominant kernel = the ICP NN scan (nn_mfma_kernel), timed with HIP events recorded
+  by the library on the launch stream around every NN launch inside the timed region.  Its
+  screen key |t|² − 2q·t is a rank-4 contraction run on the matrix cores as one
+  v_mfma_f32_32x32x16_f16 per 32×32 (target, query) block: 16 fp16 MACs = 32 flop per pair
+  (K = 16 fp16 hi/lo split terms, 11 non-zero), so bound = "mfma" against the
+  dense FP16 MFMA peak 2.5 PFLOP/s, achieved = 32 flop × Ns × Nt / launch time.  The SURVEY's
+  8-flop-per-pair algorithmic figure is reported beside it against the FP32 vector roof
+  (157.3 TFLOP/s) that a VALU implementation is bounded by.  traffic = HBM bytes per launch
+  from the committed rocprofv3 PMC summary (profiles/), or null.
 * "icp_grid": the same cfg1 workload with the radius-bounded uniform-grid NN (SURVEY §8(f)
   rank 1; identical correspondences, tests/test_gpu_icp.py) — HBM/latency-bound, so its
   roofline is priced in GB/s on 28·Ns + 16·Nt algorithmic bytes per launch (query float4 +
@@ -39,7 +43,9 @@ sys.path.insert(0, str(ROOT / "3d-matching_amd"))
 
 VALU_FP32_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector)
 HBM_PEAK_GBS = 8000.0
-NN_FLOP_PER_PAIR = 8        # 3 sub + 1 mul + 2 FMA
+MFMA_F16_PEAK_TF = 2500.0   # MI355X_MICROARCH.md: Peak BF16/FP16 MFMA, dense
+NN_FLOP_PER_PAIR = 8        # 3 sub + 1 mul + 2 FMA (SURVEY §8(d), fp32 VALU formulation)
+NN_MFMA_FLOP_PER_PAIR = 32  # 16 fp16 MACs per (target, query) pair in v_mfma_f32_32x32x16_f16
 SCORE_FLOP_PER_PAIR = 27    # 9 FMA transform + 3 sub + (1 mul + 2 FMA) + 1 cmp
 CPU_THREADS = 16            # the GPU box's CPU share per GPU
 
@@ -156,8 +162,9 @@ def main():
 
     el, nn_avg_ms, nn_n, terms_avg_ms, res = time_icp("brute")
     icp_value = world * iters * args.steps / el
-    nn_flop = NN_FLOP_PER_PAIR * ns * nt
+    nn_flop = NN_MFMA_FLOP_PER_PAIR * ns * nt
     achieved_tf = nn_flop / (nn_avg_ms * 1e-3) / 1e12
+    algo_tf = NN_FLOP_PER_PAIR * ns * nt / (nn_avg_ms * 1e-3) / 1e12
     err = float(np.abs(res.transformation - T_true).max())
 
     # ------------------------------------------------------------------ cfg1 with the grid NN
@@ -235,7 +242,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(src, tgt_all[:nt], nrm_all[:nt], r, args, ransac is not None)
 
-    traffic, traffic_src = pmc_traffic("nn_kernel")
+    traffic, traffic_src = pmc_traffic("nn_mfma_kernel")
     line = {
         "metric": "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pts, 1/2/4/8 GPU",
         "value": icp_value,
@@ -247,17 +254,20 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32 NN screen + f64 terms/solve",
+        "dtype": "f16-split MFMA NN screen (exact f32 NN result) + f64 terms/solve",
         "data": "synthetic (m3d.synth: asymmetric closed surface, extent ~10, analytic normals)",
         "config": {"workload": "cfg1: 100k<->100k synthetic pair, 50 point-to-plane ICP iterations, "
                                "brute-force NN (r=0.12), 1 GPU" if world == 1 else
                                f"cfg1 per GPU, target sharded over {world} GPUs (RCCL MIN keys + SUM terms)",
                    "ns": ns, "nt_per_gpu": nt, "icp_iterations_per_step": iters, "max_corr": r,
                    "parallelism": "single" if world == 1 else f"target-shard x{world}"},
-        "roofline": {"bound": "valu", "kernel": "nn_kernel", "achieved": achieved_tf,
-                     "peak": VALU_FP32_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / VALU_FP32_PEAK_TF,
+        "roofline": {"bound": "mfma", "kernel": "nn_mfma_kernel", "achieved": achieved_tf,
+                     "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F16_PEAK_TF,
                      "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": nn_avg_ms,
                      "launches": nn_n, "flop_per_launch": nn_flop,
+                     "flop_per_pair": NN_MFMA_FLOP_PER_PAIR,
+                     "algorithmic_8flop_per_pair_tflops": algo_tf,
+                     "vs_fp32_valu_roof": algo_tf / VALU_FP32_PEAK_TF,
                      "terms_avg_launch_ms": terms_avg_ms},
         "icp_grid": icp_grid,
         "ransac": ransac,
