@@ -784,6 +784,14 @@ int m3d_icp_solve(m3d_icp* s, const double* sums, void* stream) {
   return M3D_OK;
 }
 
+int m3d_icp_set_source_total(m3d_icp* s, int64_t ns_total) {
+  if (!s) return M3D_ERR_INVALID;
+  CHECK_ARG(s->ctx, ns_total >= 0 && (ns_total == 0 || ns_total >= s->src->n),
+            "source total must be 0 or at least the shard's source count");
+  s->ns_total = ns_total;
+  return M3D_OK;
+}
+
 int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream) {
   if (!s || !out) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;

@@ -830,7 +830,7 @@ hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st
   sp.rel_rmse = s->params.relative_rmse;
   sp.max_iter = s->params.max_iteration;
   sp.est = s->params.estimation;
-  sp.ns = s->src->n;
+  sp.ns = s->ns_total > 0 ? s->ns_total : s->src->n;
   for (int k = 0; k < 3; ++k) sp.c[k] = s->src->center[k];
   sp.f = frame_of(s);
   solve_kernel<<<1, 64, 0, st>>>(sums, s->state, sp);

@@ -153,6 +153,7 @@ struct m3d_icp {
   int64_t nblocks = 0;
   const int32_t* qorder = nullptr;  // grid NN: source visit order (source cell order)
   const m3d::Grid* tgrid = nullptr;  // grid NN: the target's grid (owned by the target cloud)
+  int64_t ns_total = 0;  // source-sharded multi-GPU: sources over all ranks (fitness denominator)
 };
 
 // error plumbing ------------------------------------------------------------------------

@@ -99,6 +99,7 @@ SIGNATURES = {
     "m3d_icp_shard_terms": (C.c_int, [vp, i64, vp, vp, vp]),
     "m3d_icp_solve": (C.c_int, [vp, vp, vp]),
     "m3d_icp_result_get": (C.c_int, [vp, C.POINTER(IcpResult), vp]),
+    "m3d_icp_set_source_total": (C.c_int, [vp, i64]),
     "m3d_icp_corr": (vp, [vp]),
     "m3d_icp_copy_corr": (C.c_int, [vp, vp, vp]),
     "m3d_voxel_down_sample": (C.c_int, [vp, vp, vp, i64, dbl, vp, vp, C.POINTER(i64), vp]),

@@ -344,6 +344,10 @@ class IcpLoop:
     def solve(self, sums):
         self.ctx.check(self.ctx.lib.m3d_icp_solve(self.h, ptr(sums), stream_handle()), "icp_solve")
 
+    def set_source_total(self, ns_total: int):
+        """Source-sharded runs: fitness denominator = sources over all ranks."""
+        self.ctx.check(self.ctx.lib.m3d_icp_set_source_total(self.h, int(ns_total)), "icp_set_source_total")
+
     def result(self) -> IcpOutcome:
         r = _lib.IcpResult()
         self.ctx.check(self.ctx.lib.m3d_icp_result_get(self.h, C.byref(r), stream_handle()), "icp_result")

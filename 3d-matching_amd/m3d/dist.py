@@ -1,6 +1,8 @@
 """Multi-GPU protocols over torch.distributed (backend "nccl" = RCCL over xGMI; "gloo" in tests).
 
-One process per GPU.  Two hot-path shardings:
+One process per GPU.  Hot-path shardings; the source-sharded ICP variant
+(``SourceShardedIcp``: sources split, target replicated, one 256-B SUM per iteration) is the
+cheaper exchange whenever the target fits one GPU; the target-sharded one is the north-star's:
 
 * ICP, target-sharded (cfg3).  Rank r owns target points [off_r, off_r + n_r) (points + normals)
   and a replica of the source.  Per iteration:
@@ -84,6 +86,36 @@ class ShardedIcp:
 
     def run(self, init, max_iteration: int):
         """Open3D loop structure: Eval + up to max_iteration updates (max_iteration + 1 passes)."""
+        self.b.reset(init)
+        for _ in range(max_iteration + 1):
+            self.iteration()
+        return self.b.result()
+
+
+class SourceShardedIcp:
+    """Source-sharded ICP driver (SURVEY §8(e) "ICP alternative"): rank r owns sources
+    [off_r, off_r + n_r) and the whole target.  Per iteration: local NN + local terms →
+    all_reduce(sums, SUM) (256 B, the only exchange) → identical solve on every rank, whose
+    fitness denominator is the global source count (backend.set_source_total)."""
+
+    def __init__(self, backend, ns_local: int, ns_total: int, device, group=None):
+        import torch
+
+        self.b = backend
+        self.group = group
+        self.b.set_source_total(ns_total)
+        self.keys = torch.empty(ns_local, dtype=torch.int64, device=device)
+        self.sums = torch.empty(32, dtype=torch.float64, device=device)
+
+    def iteration(self):
+        import torch.distributed as dist
+
+        self.b.shard_nn(0, self.keys)
+        self.b.shard_terms(0, self.keys, self.sums)
+        dist.all_reduce(self.sums, op=dist.ReduceOp.SUM, group=self.group)
+        self.b.solve(self.sums)
+
+    def run(self, init, max_iteration: int):
         self.b.reset(init)
         for _ in range(max_iteration + 1):
             self.iteration()

@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--ransac-steps", type=int, default=3)
     ap.add_argument("--no-ransac", action="store_true")
     ap.add_argument("--no-grid", action="store_true")
+    ap.add_argument("--shard", choices=["target", "source"], default="target",
+                    help="N>1 ICP sharding: target (north-star: RCCL MIN keys + SUM terms) or "
+                         "source (target replicated, SUM terms only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline leg")
     return ap.parse_args()
@@ -117,22 +120,36 @@ def main():
     # ------------------------------------------------------------------ cfg1: ICP
     ns, nt, iters = args.ns, args.nt, args.icp_iters
     r = 0.4 * 0.3
-    src, tgt_all, nrm_all, T_true = synth.icp_pair(ns, nt * world, seed=0)
-    off = rank * nt
+    source_shard = world > 1 and args.shard == "source"
+    if source_shard:  # weak scaling: ns sources per rank against the whole (replicated) target
+        src_all, tgt_all, nrm_all, T_true = synth.icp_pair(ns * world, nt, seed=0)
+        src = src_all[rank * ns:(rank + 1) * ns]
+        off = 0
+        tgt_c = Cloud(tgt_all, nrm_all)
+    else:  # target-sharded: nt targets per rank, sources replicated
+        src, tgt_all, nrm_all, T_true = synth.icp_pair(ns, nt * world, seed=0)
+        off = rank * nt
+        tgt_c = Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt])
     src_c = Cloud(src)
-    tgt_c = Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt])
     keys = torch.empty(ns, dtype=torch.int64, device=dev)
     sums = torch.empty(32, dtype=torch.float64, device=dev)
 
     def time_icp(nn: str):
         loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters,
                        nn=nn)
+        if source_shard:
+            loop.set_source_total(ns * world)
 
         def icp_run():
             loop.reset(np.eye(4))
             for _ in range(iters + 1):
                 if world == 1:
                     loop.step()
+                elif source_shard:
+                    loop.shard_nn(0, keys)
+                    loop.shard_terms(0, keys, sums)
+                    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+                    loop.solve(sums)
                 else:
                     loop.shard_nn(off, keys)
                     dist.all_reduce(keys, op=dist.ReduceOp.MIN)
@@ -258,9 +275,11 @@ def main():
         "data": "synthetic (m3d.synth: asymmetric closed surface, extent ~10, analytic normals)",
         "config": {"workload": "cfg1: 100k<->100k synthetic pair, 50 point-to-plane ICP iterations, "
                                "brute-force NN (r=0.12), 1 GPU" if world == 1 else
-                               f"cfg1 per GPU, target sharded over {world} GPUs (RCCL MIN keys + SUM terms)",
+                               (f"cfg1 per GPU, sources sharded over {world} GPUs, target replicated (RCCL SUM terms)"
+                                if source_shard else
+                                f"cfg1 per GPU, target sharded over {world} GPUs (RCCL MIN keys + SUM terms)"),
                    "ns": ns, "nt_per_gpu": nt, "icp_iterations_per_step": iters, "max_corr": r,
-                   "parallelism": "single" if world == 1 else f"target-shard x{world}"},
+                   "parallelism": "single" if world == 1 else f"{args.shard}-shard x{world}"},
         "roofline": {"bound": "mfma", "kernel": "nn_mfma_kernel", "achieved": achieved_tf,
                      "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F16_PEAK_TF,
                      "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": nn_avg_ms,

@@ -212,6 +212,12 @@ int m3d_icp_shard_nn(m3d_icp* s, int64_t shard_offset, int64_t* keys, void* stre
 int m3d_icp_shard_terms(m3d_icp* s, int64_t shard_offset, const int64_t* keys, double* sums,
                         void* stream);
 int m3d_icp_solve(m3d_icp* s, const double* sums, void* stream);
+/* Source-sharded pieces (SURVEY §8(e) "ICP alternative"): `src` of m3d_icp_create is this
+ * rank's source shard, `tgt` the whole target; per iteration m3d_icp_shard_nn(s, 0, ...) +
+ * m3d_icp_shard_terms(s, 0, ...) on the shard, SUM of the 32 term slots across ranks, then
+ * m3d_icp_solve.  The fitness denominator is the source count over all ranks, set here
+ * (0 = this shard's own count). */
+int m3d_icp_set_source_total(m3d_icp* s, int64_t ns_total);
 /* Read the loop state (synchronises the stream). */
 int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream);
 /* Device pointer to the current correspondence index array (ns int32, -1 = none). */

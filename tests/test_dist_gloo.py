@@ -34,6 +34,10 @@ class OracleShard:
         self.src, self.tgt, self.nrm, self.r = src, tgt, nrm, r
         self.tree = cKDTree(tgt)
         self.max_iteration = max_iteration
+        self.ns_total = len(src)
+
+    def set_source_total(self, n):
+        self.ns_total = n
 
     def reset(self, init):
         self.T = np.array(init, np.float64)
@@ -76,7 +80,7 @@ class OracleShard:
             return
         s = sums.numpy()
         count = s[28]
-        self.fitness = count / len(self.src)
+        self.fitness = count / self.ns_total
         self.rmse = np.sqrt(s[29] / count) if count else 0.0
         self.evals += 1
         if self.iters >= self.max_iteration:
@@ -116,6 +120,33 @@ def test_sharded_icp_protocol_matches_single_process(tmp_path):
     np.testing.assert_array_equal(r0["T"], r1["T"])  # every rank holds the identical transform
     np.testing.assert_allclose(r0["T"], ref["transformation"], atol=1e-10)
     assert abs(float(r0["fit"]) - ref["fitness"]) < 1e-12
+    assert int(r0["iters"]) == 8
+
+
+def _icp_source_worker(rank, world, port, path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    src, tgt, nrm, _ = synth.icp_pair(4001, 6000, seed=22)
+    off, cnt = D.shard_bounds(len(src), world, rank)
+    b = OracleShard(src[off:off + cnt], tgt, nrm, 0.12, 8)
+    drv = D.SourceShardedIcp(b, cnt, len(src), "cpu")
+    T, fit, rmse, iters = drv.run(np.eye(4), 8)
+    np.savez(f"{path}/rank{rank}.npz", T=T, fit=fit, rmse=rmse, iters=iters)
+    dist.destroy_process_group()
+
+
+def test_source_sharded_icp_protocol_matches_single_process(tmp_path):
+    world = 2
+    mp.spawn(_icp_source_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    src, tgt, nrm, _ = synth.icp_pair(4001, 6000, seed=22)
+    ref = I.registration_icp(src, tgt, 0.12, np.eye(4), tgt_normals=nrm, relative_fitness=-1,
+                             relative_rmse=-1, max_iteration=8)
+    r0 = np.load(tmp_path / "rank0.npz")
+    r1 = np.load(tmp_path / "rank1.npz")
+    np.testing.assert_array_equal(r0["T"], r1["T"])
+    np.testing.assert_allclose(r0["T"], ref["transformation"], atol=1e-10)
+    assert abs(float(r0["fit"]) - ref["fitness"]) < 1e-12  # global denominator
+    assert abs(float(r0["rmse"]) - ref["inlier_rmse"]) < 1e-12
     assert int(r0["iters"]) == 8
 
 

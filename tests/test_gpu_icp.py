@@ -171,6 +171,40 @@ def test_step_loop_matches_run():
 
 
 @pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_source_sharded_loop_matches_single_device(nn):
+    """The source-sharded protocol (local NN + terms, SUM of the 32 term slots, global fitness
+    denominator) emulated with three source shards on one device."""
+    import torch
+
+    src, tgt, nrm, _ = synth.icp_pair(30001, 20000, seed=14)
+    t = Cloud(tgt, nrm)
+    full = icp(Cloud(src), t, 0.12, np.eye(4), relative_fitness=-1, relative_rmse=-1,
+               max_iteration=6, nn="brute")
+    bounds = [0, 9000, 21000, 30001]
+    loops = [IcpLoop(Cloud(src[a:b]), t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=6,
+                     nn=nn) for a, b in zip(bounds[:-1], bounds[1:])]
+    for lp in loops:
+        lp.set_source_total(len(src))
+        lp.reset(np.eye(4))
+    for _ in range(7):
+        sums = []
+        for lp in loops:
+            k = torch.empty(lp.src.n, dtype=torch.int64, device="cuda")
+            sm = torch.empty(32, dtype=torch.float64, device="cuda")
+            lp.shard_nn(0, k)
+            lp.shard_terms(0, k, sm)
+            sums.append(sm)
+        tot = torch.stack(sums).sum(dim=0)
+        for lp in loops:
+            lp.solve(tot)
+    r = loops[0].result()
+    np.testing.assert_allclose(r.transformation, full.transformation, atol=1e-9)
+    assert abs(r.fitness - full.fitness) < 1e-12
+    for lp in loops[1:]:
+        np.testing.assert_array_equal(lp.result().transformation, r.transformation)
+
+
+@pytest.mark.parametrize("nn", ["brute", "grid"])
 def test_target_sharded_loop_matches_single_device(nn):
     """The multi-GPU target-shard protocol (MIN on keys, SUM on terms) emulated on one device."""
     import torch
