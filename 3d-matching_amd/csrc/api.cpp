@@ -15,6 +15,7 @@
 namespace m3d {
 hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st);
 hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hipStream_t st);
+hipError_t launch_icp_terms_solve(const m3d_icp* s, hipStream_t st);
 hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStream_t st);
 int64_t terms_blocks(int64_t ns);
 }  // namespace m3d
@@ -748,7 +749,16 @@ int m3d_icp_step(m3d_icp* s, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;
   hipStream_t st = S(stream);
+  static const bool fused = [] {
+    const char* e = getenv("M3D_ICP_FUSED");
+    return !(e && atoi(e) == 0);
+  }();
   HIPX(ctx, enqueue_nn(s, 0, st));
+  if (fused) {
+    KTimer kt(ctx, M3D_KERNEL_TERMS, st);
+    HIPX(ctx, launch_icp_terms_solve(s, st));
+    return M3D_OK;
+  }
   { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, 0, 0, st)); }
   HIPX(ctx, launch_icp_reduce(s, s->sums, st));
   HIPX(ctx, launch_icp_solve(s, s->sums, st));

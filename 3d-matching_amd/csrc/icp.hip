@@ -121,6 +121,7 @@ __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, do
   s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
+  s->ticket = 0;
   s->r2 = r2;
   refresh_rt32(s, f);
 }
@@ -132,6 +133,7 @@ __global__ void icp_set_T_kernel(IcpState* s, const double* __restrict__ T, doub
   s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
+  s->ticket = 0;
   s->r2 = r2;
   refresh_rt32(s, f);
 }
@@ -492,22 +494,57 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
 }
 
 // ------------------------------------------------------------------------------- terms
-__device__ __forceinline__ double wave_sum(double v) {
+// Transposing wave reduction of 32 per-lane slots: each butterfly step halves the slots a lane
+// keeps (the partner gets the other half), so 32 slots cost 31 pair exchanges instead of
+// 32 × 6 full butterflies.  Steps 32 and 16 use the gfx950 permlane swaps (no selects);
+// 8, 4, 2 exchange by shuffles; the last step adds the two lanes of a pair.  Afterwards lanes
+// 2k and 2k+1 both hold the wave's sum of slot k.  A fixed tree: deterministic.
+template <bool k32>
+__device__ __forceinline__ double swap_add(double a, double b) {
+  const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+  const uint32_t alo = (uint32_t)ua, ahi = (uint32_t)(ua >> 32);
+  const uint32_t blo = (uint32_t)ub, bhi = (uint32_t)(ub >> 32);
+  const auto rl = k32 ? __builtin_amdgcn_permlane32_swap(alo, blo, false, false)
+                      : __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+  const auto rh = k32 ? __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false)
+                      : __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+  const double na = __longlong_as_double((long long)(((uint64_t)rh[0] << 32) | rl[0]));
+  const double nb = __longlong_as_double((long long)(((uint64_t)rh[1] << 32) | rl[1]));
+  return na + nb;  // lanes of bit 0: a-slot over both halves; bit 1: b-slot
+}
+
+template <int kOff>
+__device__ __forceinline__ double xchg_add(double a, double b, int lane) {
+  const bool hi = (lane & kOff) != 0;
+  const double keep = hi ? b : a, send = hi ? a : b;
+  return keep + __shfl_xor(send, kOff, kWave);
+}
+
+__device__ __forceinline__ double wave_transpose_sum32(const double (&v)[32], int lane) {
+  double w16[16], w8[8], w4[4], w2[2];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+  for (int j = 0; j < 16; ++j) w16[j] = swap_add<true>(v[j], v[j + 16]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w8[j] = swap_add<false>(w16[j], w16[j + 8]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w4[j] = xchg_add<8>(w8[j], w8[j + 4], lane);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) w2[j] = xchg_add<4>(w4[j], w4[j + 2], lane);
+  const double w1 = xchg_add<2>(w2[0], w2[1], lane);
+  return w1 + __shfl_xor(w1, 1, kWave);  // slot lane >> 1
 }
 
 // est: M3D_EST_POINT_TO_PLANE → slots 0..20 JTJ (upper, row-major), 21..26 JTr, 27 Σr²
 //      M3D_EST_POINT_TO_POINT → slots 0..2 Σp_c, 3..5 Σq_c, 6..14 Σ p_c q_cᵀ (row-major)
 // both: 28 count, 29 Σd²  (c = source centre: identical on every shard)
-__global__ __launch_bounds__(kTermsBlock) void terms_kernel(
+// kWT: write the block partial through to memory (sc1 store) for the fused last-block reduce
+template <bool kWT>
+__device__ __forceinline__ void terms_block(
     const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
     const double* __restrict__ nrm64, int64_t nt_shard, int64_t off,
     const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
     int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
     double* __restrict__ partials) {
-  if (s->done) return;
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
   const int64_t i = (int64_t)blockIdx.x * kTermsBlock + threadIdx.x;
   double acc[30];
@@ -567,24 +604,50 @@ __global__ __launch_bounds__(kTermsBlock) void terms_kernel(
     if (corr != nullptr && (!sharded || out >= 0 || key == kKeyNone)) corr[i] = out;
   }
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  {
+    double v[32];
 #pragma unroll
-  for (int k = 0; k < 30; ++k) {
-    const double v = wave_sum(acc[k]);
-    if (lane == 0) red[k][wave] = v;
+    for (int k = 0; k < 32; ++k) v[k] = k < 30 ? acc[k] : 0.0;
+    const double w = wave_transpose_sum32(v, lane);
+    if ((lane & 1) == 0) red[lane >> 1][wave] = w;
   }
   __syncthreads();
   if (threadIdx.x < kTermSlots) {
     double v = 0.0;
     if (threadIdx.x < 30)
       for (int w = 0; w < kTermsBlock / kWave; ++w) v += red[threadIdx.x][w];
-    partials[(int64_t)blockIdx.x * kTermSlots + threadIdx.x] = v;
+    double* dst = partials + (int64_t)blockIdx.x * kTermSlots + threadIdx.x;
+    if (kWT)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), __double_as_longlong(v),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      *dst = v;
   }
+}
+
+__global__ __launch_bounds__(kTermsBlock) void terms_kernel(
+    const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
+    const double* __restrict__ nrm64, int64_t nt_shard, int64_t off,
+    const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
+    int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
+    double* __restrict__ partials) {
+  if (s->done) return;
+  terms_block<false>(src64, ns, tgt64, nrm64, nt_shard, off, s, keys, corr, est, c0, c1, c2,
+                     sharded, partials);
 }
 
 // ------------------------------------------------------------------------------- reduce
 // 32 groups × 32 slots: group g sums blocks g, g+32, … (independent loads in flight), then the
 // 32 group sums are added in group order — a fixed order, so the result is deterministic.
 constexpr int kReduceGroups = 32;
+__device__ __forceinline__ double group_sum(const double* __restrict__ partials, int64_t nblocks,
+                                            int g, int slot) {
+  double v = 0.0;
+#pragma unroll 4
+  for (int64_t b = g; b < nblocks; b += kReduceGroups) v += partials[b * kTermSlots + slot];
+  return v;
+}
+
 __global__ __launch_bounds__(kReduceGroups * kTermSlots) void reduce_kernel(
     const double* __restrict__ partials, int64_t nblocks, double* __restrict__ sums,
     const IcpState* __restrict__ s) {
@@ -592,10 +655,7 @@ __global__ __launch_bounds__(kReduceGroups * kTermSlots) void reduce_kernel(
   __shared__ double red[kReduceGroups][kTermSlots];
   const int slot = threadIdx.x & (kTermSlots - 1);
   const int g = threadIdx.x / kTermSlots;
-  double v = 0.0;
-#pragma unroll 4
-  for (int64_t b = g; b < nblocks; b += kReduceGroups) v += partials[b * kTermSlots + slot];
-  red[g][slot] = v;
+  red[g][slot] = group_sum(partials, nblocks, g, slot);
   __syncthreads();
   if (threadIdx.x < kTermSlots) {
     double t = 0.0;
@@ -613,9 +673,18 @@ struct SolveParams {
   FrameParams f;
 };
 
-__global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
-                             SolveParams sp) {
-  if (threadIdx.x != 0 || s->done) return;
+// vec6_to_matrix with the three sincos evaluated in lanes 0..2 at once (whole wave calls it)
+__device__ __forceinline__ void vec6_to_matrix_wave(const double x[6], double T[16]) {
+  const int lane = threadIdx.x & (kWave - 1);
+  double sn, cs;
+  sincos(lane == 0 ? x[0] : (lane == 1 ? x[1] : x[2]), &sn, &cs);
+  vec6_to_matrix_sc(x, __shfl(cs, 0, kWave), __shfl(sn, 0, kWave), __shfl(cs, 1, kWave),
+                    __shfl(sn, 1, kWave), __shfl(cs, 2, kWave), __shfl(sn, 2, kWave), T);
+}
+
+// One evaluation + update from the reduced sums.  Run by one whole wave: every lane computes
+// the same values (so its stores to *s agree) except the three sincos of vec6_to_matrix_wave.
+__device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp) {
   const double count = sums[28];
   const double fit = count > 0.0 ? count / (double)sp.ns : 0.0;
   const double rmse = count > 0.0 ? sqrt(sums[29] / count) : 0.0;
@@ -651,7 +720,7 @@ __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restri
         }
       for (int a = 0; a < 6; ++a) b[a] = -sums[21 + a];
       ldlt6_solve(A, b, x);
-      vec6_to_matrix(x, upd);
+      vec6_to_matrix_wave(x, upd);
     } else {
       const double n = count;
       double mp[3], mq[3], Hm[9], R[9];
@@ -676,6 +745,80 @@ __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restri
   matmul4(upd, s->T, s->T);
   s->iters += 1;
   refresh_rt32(s, sp.f);
+}
+
+__global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
+                             SolveParams sp) {
+  if (threadIdx.x >= kWave || s->done) return;
+  solve_state(sums, s, sp);
+}
+
+// Fused single-device iteration tail: terms → block partial → the last block to finish (ticket)
+// reduces all partials in reduce_kernel's exact order and runs solve_state.  Cross-XCD hand-off
+// (MI355X_MICROARCH.md, visibility table, "last adder" row): each block stores its partial
+// write-through (sc1), drains it (vmcnt(0)) and one lane adds to the agent-scope ticket; the
+// block whose add returned nblocks − 1 reads every partial with sc1 loads.  No L2 write-back or
+// invalidate fences are needed.
+__global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
+    const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
+    const double* __restrict__ nrm64, int64_t nt, IcpState* s, const int64_t* __restrict__ keys,
+    int32_t* __restrict__ corr, double* partials, int64_t nblocks, double* __restrict__ sums,
+    SolveParams sp) {
+  if (s->done) return;
+  terms_block<true>(src64, ns, tgt64, nrm64, nt, 0, s, keys, corr, sp.est, sp.c[0], sp.c[1],
+                    sp.c[2], 0, partials);
+  __shared__ double red[kReduceGroups][kTermSlots];
+  __shared__ int last;
+  // the partial went out write-through (sc1): drain it, then one lane takes the ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t =
+        __hip_atomic_fetch_add(&s->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == (uint32_t)(nblocks - 1));
+  }
+  __syncthreads();
+  if (!last) return;
+  // every load of the other blocks' partials is an sc1 load (L2-coherent, bypasses L1)
+  const int slot = threadIdx.x & (kTermSlots - 1);
+  constexpr int kG = kReduceGroups / (kTermsBlock / kTermSlots);  // groups per thread
+  double gv[kG];
+#pragma unroll
+  for (int u = 0; u < kG; ++u) gv[u] = 0.0;
+  const int g0 = threadIdx.x / kTermSlots;
+  constexpr int kR = 4;  // rounds of kReduceGroups blocks in flight per batch (kR·kG loads)
+  for (int64_t b0 = 0; b0 < nblocks; b0 += kR * kReduceGroups) {
+    double t[kR][kG];
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+#pragma unroll
+      for (int u = 0; u < kG; ++u) {
+        const int64_t b = b0 + r * kReduceGroups + g0 + u * (kTermsBlock / kTermSlots);
+        t[r][u] = b < nblocks
+                      ? __longlong_as_double(__hip_atomic_load(
+                            reinterpret_cast<unsigned long long*>(partials + b * kTermSlots + slot),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                      : 0.0;
+      }
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+#pragma unroll
+      for (int u = 0; u < kG; ++u) gv[u] += t[r][u];
+  }
+#pragma unroll
+  for (int u = 0; u < kG; ++u) red[g0 + u * (kTermsBlock / kTermSlots)][slot] = gv[u];
+  __syncthreads();
+  if (threadIdx.x < kTermSlots) {
+    double t = 0.0;
+    for (int k = 0; k < kReduceGroups; ++k) t += red[k][threadIdx.x];
+    red[0][threadIdx.x] = t;  // row 0 is consumed by this thread only before the overwrite
+    sums[threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < kWave) {
+    if (threadIdx.x == 0) s->ticket = 0;
+    solve_state(red[0], s, sp);
+  }
 }
 
 // finalize standalone NN (m3d_nn1): exact radius test in fp64
@@ -824,7 +967,7 @@ hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st) {
+static SolveParams solve_params(const m3d_icp* s) {
   SolveParams sp;
   sp.rel_fit = s->params.relative_fitness;
   sp.rel_rmse = s->params.relative_rmse;
@@ -833,7 +976,24 @@ hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st
   sp.ns = s->ns_total > 0 ? s->ns_total : s->src->n;
   for (int k = 0; k < 3; ++k) sp.c[k] = s->src->center[k];
   sp.f = frame_of(s);
-  solve_kernel<<<1, 64, 0, st>>>(sums, s->state, sp);
+  return sp;
+}
+
+hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st) {
+  solve_kernel<<<1, 64, 0, st>>>(sums, s->state, solve_params(s));
+  return hipGetLastError();
+}
+
+hipError_t launch_icp_terms_solve(const m3d_icp* s, hipStream_t st) {
+  const int64_t ns = s->src->n;
+  if (ns == 0) {  // no blocks to take tickets: the unfused tail handles the empty source
+    hipError_t e = launch_icp_terms_mode(s, 0, 0, st);
+    if (e == hipSuccess) e = launch_icp_reduce(s, s->sums, st);
+    return e == hipSuccess ? launch_icp_solve(s, s->sums, st) : e;
+  }
+  terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
+      s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
+      s->partials, s->nblocks, s->sums, solve_params(s));
   return hipGetLastError();
 }
 

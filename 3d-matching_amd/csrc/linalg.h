@@ -252,10 +252,9 @@ M3D_HD void ldlt6_solve(const double A_in[36], const double b_in[6], double x[6]
 }
 
 // Open3D TransformVector6dToMatrix4d: R = Rz(x2) Ry(x1) Rx(x0), t = x[3..5].
-M3D_HD void vec6_to_matrix(const double x[6], double T[16]) {
-  const double ca = cos(x[0]), sa = sin(x[0]);
-  const double cb = cos(x[1]), sb = sin(x[1]);
-  const double cc = cos(x[2]), sc = sin(x[2]);
+// (the sines/cosines of x[0..2] given: the device solve computes them in three lanes at once)
+M3D_HD void vec6_to_matrix_sc(const double x[6], double ca, double sa, double cb, double sb,
+                              double cc, double sc, double T[16]) {
   const double rx[9] = {1, 0, 0, 0, ca, -sa, 0, sa, ca};
   const double ry[9] = {cb, 0, sb, 0, 1, 0, -sb, 0, cb};
   const double rz[9] = {cc, -sc, 0, sc, cc, 0, 0, 0, 1};
@@ -270,6 +269,10 @@ M3D_HD void vec6_to_matrix(const double x[6], double T[16]) {
   }
   T[12] = T[13] = T[14] = 0.0;
   T[15] = 1.0;
+}
+
+M3D_HD void vec6_to_matrix(const double x[6], double T[16]) {
+  vec6_to_matrix_sc(x, cos(x[0]), sin(x[0]), cos(x[1]), sin(x[1]), cos(x[2]), sin(x[2]), T);
 }
 
 // C = A · B for row-major 4×4.

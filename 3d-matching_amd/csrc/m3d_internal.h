@@ -68,7 +68,7 @@ struct IcpState {
   float screen_eps_m; // NN screen error bound of the fp16-split MFMA screen
   float mfma_scale;   // power-of-two scale of the fp16 operands (the target cloud's s16)
   int32_t mfma_ok;    // scaled query magnitudes fit fp16: the MFMA screen may run
-  int32_t pad_;
+  uint32_t ticket;    // fused terms→reduce→solve: blocks done this iteration (last one resets)
 };
 
 // Uniform grid over a cloud's centred fp32 points (grid.hip): kernel view + owner.

@@ -170,6 +170,30 @@ def test_step_loop_matches_run():
     assert r.fitness == full.fitness and r.iterations == 10
 
 
+@pytest.mark.parametrize("estimation", [_lib.EST_POINT_TO_PLANE, _lib.EST_POINT_TO_POINT])
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_fused_tail_matches_separate_kernels(nn, estimation):
+    """m3d_icp_step fuses terms → reduce → solve into one launch (last-block ticket, ~400 blocks
+    spread over all XCDs); the separate shard_terms / solve launches must give the same bits."""
+    import torch
+
+    src, tgt, nrm, _ = synth.icp_pair(100000, 90000, seed=23)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=8, estimation=estimation, nn=nn)
+    full = icp(s, t, 0.12, np.eye(4), **kw)
+    lp = IcpLoop(s, t, 0.12, **kw)
+    lp.reset(np.eye(4))
+    k = torch.empty(len(src), dtype=torch.int64, device="cuda")
+    sm = torch.empty(32, dtype=torch.float64, device="cuda")
+    for _ in range(9):
+        lp.shard_nn(0, k)
+        lp.shard_terms(0, k, sm)
+        lp.solve(sm)
+    r = lp.result()
+    np.testing.assert_array_equal(r.transformation, full.transformation)
+    assert (r.fitness, r.inlier_rmse, r.iterations) == (full.fitness, full.inlier_rmse, 8)
+
+
 @pytest.mark.parametrize("nn", ["brute", "grid"])
 def test_source_sharded_loop_matches_single_device(nn):
     """The source-sharded protocol (local NN + terms, SUM of the 32 term slots, global fitness

@@ -17,5 +17,7 @@ if l:
       d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], r.get('value', 0),
       (r.get('roofline') or {}).get('avg_launch_ms', 0), (r.get('roofline') or {}).get('frac', 0),
       d['check']['max_abs_err_vs_T_true']))
+    g=d.get('icp_grid')
+    if g: print('grid icp it/s %.1f same %s nn ms %.4f terms ms %.4f' % (g['value'], g['same_result_as_brute'], g['roofline']['avg_launch_ms'], g['roofline']['terms_avg_launch_ms']))
 PY
 exit $rc
