@@ -167,8 +167,8 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
                                                       const float4* __restrict__ tgt,
                                                       int64_t nt_pad, int64_t slice_len,
                                                       int64_t off, const IcpState* __restrict__ s,
-                                                      int64_t* __restrict__ keys, int mfma_on) {
-  if (s->done || (mfma_on && s->mfma_ok)) return;  // the MFMA screen runs instead
+                                                      int64_t* __restrict__ keys) {
+  if (s->done) return;
   const float* Rt = s->Rt32;  // uniform → scalar loads (a local copy went to scratch)
   const float r2_hi = s->r2_hi;
   const float eps = s->screen_eps;
@@ -362,6 +362,41 @@ hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st) {
   return e;
 }
 
+// Exact fallback of nn_mfma_kernel when the scaled operands do not fit fp16 (mfma_ok == 0, a
+// far-off transform): the same lexicographic (fp32 d², index) minimum over the block's slice by
+// a plain scan, one thread per query.  Keeps the fp32 VALU kernel off the launch path.
+template <int kMG>
+__device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
+                              const int32_t* __restrict__ order, const float4* __restrict__ tgt32,
+                              int64_t jb, int64_t je, int64_t off, const IcpState* __restrict__ s,
+                              int64_t* __restrict__ keys) {
+  const float* Rt = s->Rt32;
+  const float r2_hi = s->r2_hi;
+  for (int qs = threadIdx.x; qs < mqueries<kMG>(); qs += kMBlock) {
+    const int64_t slot = (int64_t)blockIdx.x * mqueries<kMG>() + qs;
+    if (slot >= ns) return;
+    const int64_t i = order != nullptr ? (int64_t)order[slot] : slot;
+    float qx, qy, qz;
+    xform32(Rt, src32[i], qx, qy, qz);
+    const int64_t key = keys[i];  // keyinit_kernel's starting key
+    float best = key == kKeyNone ? r2_hi : __uint_as_float((uint32_t)((uint64_t)key >> 32));
+    uint32_t bidx = key == kKeyNone ? 0xFFFFFFFFu : (uint32_t)key;
+    const uint32_t bidx0 = bidx;
+    for (int64_t j = jb; j < je; ++j) {
+      const float4 t = tgt32[j];
+      if (__float_as_int(t.w) < 0) continue;  // pad
+      const float d2 = d2f(qx, qy, qz, t.x, t.y, t.z);
+      const uint32_t gj = (uint32_t)(off + __float_as_int(t.w));
+      if (d2 < best || (d2 == best && gj < bidx)) {
+        best = d2;
+        bidx = gj;
+      }
+    }
+    if (bidx != bidx0)
+      atomicMin((unsigned long long*)&keys[i], (unsigned long long)make_key(best, bidx));
+  }
+}
+
 template <int kMG>
 __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restrict__ src32,
                                                           int64_t ns,
@@ -372,7 +407,12 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           int64_t off,
                                                           const IcpState* __restrict__ s,
                                                           int64_t* __restrict__ keys) {
-  if (s->done || !s->mfma_ok) return;
+  if (s->done) return;
+  if (!s->mfma_ok) {
+    const int64_t jb = (int64_t)blockIdx.y * slice_len;
+    nn_slice_scan<kMG>(src32, ns, order, tgt32, jb, min(nt_pad, jb + slice_len), off, s, keys);
+    return;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const float* Rt = s->Rt32;
@@ -905,6 +945,17 @@ static dim3 nn_grid(int64_t bx, int64_t nt_pad, int64_t mult, int64_t* slice_out
   return dim3((unsigned)bx, (unsigned)S);
 }
 
+static bool icp_nn_uses_mfma(const m3d_icp* s) {
+  static const bool mfma_env = [] {
+    const char* e = getenv("M3D_NN_MFMA");
+    return !(e && atoi(e) == 0);
+  }();
+  return mfma_env && s->tgrid != nullptr && s->tgrid->mf16 != nullptr;
+}
+
+// Brute-force NN into s->keys (after launch_icp_keyinit).  MFMA tiles present: nn_mfma_kernel
+// alone (its exact in-kernel scan covers transforms whose operands do not fit fp16); otherwise
+// the fp32 VALU nn_kernel.
 hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
   const int64_t ns = s->src->n;
   const int64_t nt_pad = s->tgt->n_pad;
@@ -914,16 +965,9 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
     const int v = e ? atoi(e) : kNNQDefault;
     return (v == 1 || v == 2 || v == 4) ? v : kNNQDefault;
   }();
-  static const bool mfma_env = [] {
-    const char* e = getenv("M3D_NN_MFMA");
-    return !(e && atoi(e) == 0);
-  }();
-  // The MFMA screen runs when the scaled operands fit fp16 (decided on the device by
-  // refresh_rt32); the fp32 VALU screen is launched behind it and exits at once in that case.
   const Grid* tg = s->tgrid;
-  const int mfma_on = (mfma_env && tg != nullptr && tg->mf16 != nullptr) ? 1 : 0;
   int64_t slice = 0;
-  if (mfma_on) {
+  if (icp_nn_uses_mfma(s)) {
     static const int MG = [] {
       const char* e = getenv("M3D_NN_MG");
       const int v = e ? atoi(e) : kMGDefault;
@@ -940,17 +984,19 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
     else
       nn_mfma_kernel<1><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
                                                 tg->mf_npad, slice, off, s->state, s->keys);
+    return hipGetLastError();
   }
   const dim3 grid = nn_grid((ns + kNNBlock * Q - 1) / (kNNBlock * Q), nt_pad, kNNLds, &slice);
   const float4* tp = s->tgt->xyz32;
   if (Q == 4)
-    nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, mfma_on);
+    nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
   else if (Q == 2)
-    nn_kernel<2><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, mfma_on);
+    nn_kernel<2><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
   else
-    nn_kernel<1><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, mfma_on);
+    nn_kernel<1><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
   return hipGetLastError();
 }
+
 
 hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hipStream_t st) {
   const int64_t ns = s->src->n;

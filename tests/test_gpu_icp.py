@@ -55,6 +55,9 @@ def _grid_cases():
     dup = np.repeat(rng.normal(size=(50, 3)), 40, axis=0)  # exact duplicates → index ties
     wide = rng.uniform(-5e3, 5e3, (40000, 3))  # cell-count cap (r ≪ extent)
     offset = sph + np.array([1e5, -2e5, 3e4])  # large absolute coordinates
+    # a few far outliers make the fp16-scaled queries overflow: the MFMA kernel's exact scan
+    outl = sph[::3].copy()
+    outl[::500] += 2e4
     return {
         "sphere": (sph[::3] * 1.002, sph, 0.12),
         "sphere_big_r": (sph[::7], sph, 50.0),  # radius larger than the cloud
@@ -65,6 +68,7 @@ def _grid_cases():
         "wide": (wide[::2] + 0.3, wide, 0.01),
         "offset": (offset[::3] * 1.0000001, offset, 0.12),
         "far": (sph[:100] + 1e3, sph, 0.12),
+        "outliers": (outl * 1.002, sph, 0.12),
         "single_target": (sph[:500], sph[:1], 10.0),
     }
 
@@ -95,6 +99,20 @@ def test_icp_grid_identical_to_brute_force(estimation):
     np.testing.assert_array_equal(b.transformation, a.transformation)
     assert (b.fitness, b.inlier_rmse, b.iterations) == (a.fitness, a.inlier_rmse, a.iterations)
     np.testing.assert_array_equal(b.correspondence_set, a.correspondence_set)
+
+
+def test_icp_with_far_outliers_grid_identical_to_brute_force():
+    """Far source outliers switch the brute-force NN to the MFMA kernel's exact in-kernel scan
+    (operands beyond fp16); the fused loop must still match the grid path bit for bit."""
+    src, tgt, nrm, _ = synth.icp_pair(30000, 40000, seed=29)
+    src = src.copy()
+    src[::1000] += 3e4
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=4)
+    a = icp(s, t, 0.12, np.eye(4), nn="brute", **kw)
+    b = icp(s, t, 0.12, np.eye(4), nn="grid", **kw)
+    np.testing.assert_array_equal(a.transformation, b.transformation)
+    assert (a.fitness, a.inlier_rmse) == (b.fitness, b.inlier_rmse) and a.fitness > 0.5
 
 
 def test_nn1_exact_ties_pick_lowest_index():
