@@ -406,7 +406,10 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           int64_t nt_pad, int64_t slice_len,
                                                           int64_t off,
                                                           const IcpState* __restrict__ s,
-                                                          int64_t* __restrict__ keys) {
+                                                          int64_t* __restrict__ keys,
+                                                          uint32_t exp_mask) {
+  // exp_mask: 0xFF always; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
+  // (profiling experiment only: the keys are then wrong)
   if (s->done) return;
   if (!s->mfma_ok) {
     const int64_t jb = (int64_t)blockIdx.y * slice_len;
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   // [buffer][lane half][target]: a half-wave's 32 ds_read_b128 hit 32 consecutive 16-B slots.
   // Thread t stages element plane t / kMTile of target t % kMTile (mf16 is stored as two
   // planes, so the loads are coalesced).  The fp32 coordinates are read from global memory by
-  // the (rare) exact path only.
+  // the (rare) exact path only (staging them in LDS as well cost the sweep more than it saved).
   static_assert(kMBlock == 2 * kMTile, "one 16-B operand half per thread per tile");
   __shared__ uint4 t16[2][2][kMTile];
   const int sp = threadIdx.x / kMTile, sk = threadIdx.x % kMTile;
@@ -499,7 +502,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
     // fp32 d² over the lane's 16 rows, then the lane pair (c, c + 32) merges its two states.
 #pragma unroll
     for (int g = 0; g < kMG; ++g) {
-      uint32_t m8 = (hm >> (g * 8)) & 0xFFu;
+      uint32_t m8 = (hm >> (g * 8)) & 0xFFu & exp_mask;
       while (m8 != 0) {
         const int sub = __builtin_ctz(m8);
         m8 &= m8 - 1;
@@ -973,17 +976,21 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
       const int v = e ? atoi(e) : kMGDefault;
       return (v == 1 || v == 2 || v == 4) ? v : kMGDefault;
     }();
+    static const uint32_t exp_mask = [] {
+      const char* e = getenv("M3D_NN_EXP");
+      return (e && atoi(e) == 1) ? 0u : 0xFFu;
+    }();
     const int64_t mq = MG == 4 ? mqueries<4>() : (MG == 2 ? mqueries<2>() : mqueries<1>());
     const dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, kMTile, &slice);
     if (MG == 4)
       nn_mfma_kernel<4><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys);
+                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask);
     else if (MG == 2)
       nn_mfma_kernel<2><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys);
+                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask);
     else
       nn_mfma_kernel<1><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys);
+                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask);
     return hipGetLastError();
   }
   const dim3 grid = nn_grid((ns + kNNBlock * Q - 1) / (kNNBlock * Q), nt_pad, kNNLds, &slice);
