@@ -765,6 +765,16 @@ int m3d_icp_step(m3d_icp* s, void* stream) {
   return M3D_OK;
 }
 
+int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  CHECK_ARG(s->ctx, n >= 0, "n must be >= 0");
+  for (int32_t k = 0; k < n; ++k) {
+    const int rc = m3d_icp_step(s, stream);
+    if (rc) return rc;
+  }
+  return M3D_OK;
+}
+
 int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* keys, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;

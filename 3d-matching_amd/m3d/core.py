@@ -333,6 +333,10 @@ class IcpLoop:
     def step(self):
         self.ctx.check(self.ctx.lib.m3d_icp_step(self.h, stream_handle()), "icp_step")
 
+    def steps(self, n: int):
+        """n iterations enqueued by the library in one call (m3d_icp_steps)."""
+        self.ctx.check(self.ctx.lib.m3d_icp_steps(self.h, int(n), stream_handle()), "icp_steps")
+
     def shard_nn(self, offset: int, keys):
         self.ctx.check(self.ctx.lib.m3d_icp_shard_nn(self.h, int(offset), ptr(keys), stream_handle()),
                        "icp_shard_nn")

@@ -13,7 +13,9 @@ BASELINE.json metric "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pt
   Nc = 1e5, H = 1e5 hypotheses per GPU, counter sampler seed 42, no early stop; N>1 shards the
   hypothesis ids and all-reduces MAX of the packed (count, ~id) best key.
 * roofline: dominant kernel = the ICP NN scan (nn_mfma_kernel), timed with HIP events recorded
-  by the library on the launch stream around every NN launch inside the timed region.  Its
+  by the library on the launch stream around every NN launch during a second timed pass of the
+  same K steps (an event record costs ~4 us between dependent kernels — tools/loop_overhead.py —
+  so `value` comes from the pass without them; both step times are in the line).  Its
   screen key |t|² − 2q·t is a rank-4 contraction run on the matrix cores as one
   v_mfma_f32_32x32x16_f16 per 32×32 (target, query) block: 16 fp16 MACs = 32 flop per pair
   (K = 16 fp16 hi/lo split terms, 11 non-zero), so bound = "mfma" against the
@@ -142,10 +144,11 @@ def main():
 
         def icp_run():
             loop.reset(np.eye(4))
+            if world == 1:
+                loop.steps(iters + 1)  # the library enqueues the 51 iterations natively
+                return
             for _ in range(iters + 1):
-                if world == 1:
-                    loop.step()
-                elif source_shard:
+                if source_shard:
                     loop.shard_nn(0, keys)
                     loop.shard_terms(0, keys, sums)
                     dist.all_reduce(sums, op=dist.ReduceOp.SUM)
@@ -157,27 +160,35 @@ def main():
                     dist.all_reduce(sums, op=dist.ReduceOp.SUM)
                     loop.solve(sums)
 
+        def timed(events: bool):
+            ctx.profile(events)
+            ctx.profile_read(_lib.KERNEL_NN)
+            ctx.profile_read(_lib.KERNEL_TERMS)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                icp_run()
+            torch.cuda.synchronize()
+            barrier()
+            el = max_over_ranks(time.perf_counter() - t0)
+            nn_ms, nn_n = ctx.profile_read(_lib.KERNEL_NN)
+            terms_ms, terms_n = ctx.profile_read(_lib.KERNEL_TERMS)
+            ctx.profile(False)
+            return el, nn_ms, nn_n, terms_ms, terms_n
+
         for _ in range(args.warmup):
             icp_run()
         torch.cuda.synchronize()
-        ctx.profile(True)
-        ctx.profile_read(_lib.KERNEL_NN)
-        ctx.profile_read(_lib.KERNEL_TERMS)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            icp_run()
-        torch.cuda.synchronize()
-        barrier()
-        el = max_over_ranks(time.perf_counter() - t0)
-        nn_ms, nn_n = ctx.profile_read(_lib.KERNEL_NN)
-        terms_ms, terms_n = ctx.profile_read(_lib.KERNEL_TERMS)
-        ctx.profile(False)
+        # value: the K steps with nothing else on the stream.  Kernel durations: the same K steps
+        # again with the library's HIP events around every NN and terms launch (each event record
+        # costs ~4 us of stream time between dependent kernels: tools/loop_overhead.py).
+        el, _, _, _, _ = timed(False)
+        el_ev, nn_ms, nn_n, terms_ms, terms_n = timed(True)
         return (el, max_over_ranks(nn_ms / max(nn_n, 1)), nn_n, terms_ms / max(terms_n, 1),
-                loop.result())
+                loop.result(), el_ev)
 
-    el, nn_avg_ms, nn_n, terms_avg_ms, res = time_icp("brute")
+    el, nn_avg_ms, nn_n, terms_avg_ms, res, el_ev = time_icp("brute")
     icp_value = world * iters * args.steps / el
     nn_flop = NN_MFMA_FLOP_PER_PAIR * ns * nt
     achieved_tf = nn_flop / (nn_avg_ms * 1e-3) / 1e12
@@ -191,13 +202,14 @@ def main():
         IcpLoop(src_c, tgt_c, r, max_iteration=0, nn="grid")  # builds both clouds' grids once
         torch.cuda.synchronize()
         build_ms = (time.perf_counter() - tg0) * 1e3
-        gel, g_ms, g_n, g_terms_ms, gres = time_icp("grid")
+        gel, g_ms, g_n, g_terms_ms, gres, gel_ev = time_icp("grid")
         g_bytes = 28 * ns + 16 * nt
         g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
         icp_grid = {
             "metric": "ICP iterations/sec (cfg1 workload, uniform-grid radius NN)",
             "value": world * iters * args.steps / gel, "unit": "ICP iter/s (100k src x 100k tgt per GPU)",
             "ms_per_step": gel / args.steps * 1e3, "grid_build_ms": build_ms,
+            "ms_per_step_with_kernel_events": gel_ev / args.steps * 1e3,
             "same_result_as_brute": bool(np.array_equal(gres.transformation, res.transformation)),
             "roofline": {"bound": "hbm", "kernel": "grid_nn_kernel", "achieved": g_gbs,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
@@ -226,27 +238,35 @@ def main():
 
         ransac_run()
         torch.cuda.synchronize()
-        ctx.profile(True)
-        ctx.profile_read(_lib.KERNEL_SCORE)
-        ctx.profile_read(_lib.KERNEL_KABSCH)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.ransac_steps):
-            out = ransac_run()
-        torch.cuda.synchronize()
-        barrier()
-        rel = max_over_ranks(time.perf_counter() - t0)
-        sc_ms, sc_n = ctx.profile_read(_lib.KERNEL_SCORE)
-        kb_ms, kb_n = ctx.profile_read(_lib.KERNEL_KABSCH)
-        ctx.profile(False)
+
+        def ransac_timed(events: bool):
+            ctx.profile(events)
+            ctx.profile_read(_lib.KERNEL_SCORE)
+            ctx.profile_read(_lib.KERNEL_KABSCH)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.ransac_steps):
+                out = ransac_run()
+            torch.cuda.synchronize()
+            barrier()
+            el = max_over_ranks(time.perf_counter() - t0)
+            sc = ctx.profile_read(_lib.KERNEL_SCORE)
+            kb = ctx.profile_read(_lib.KERNEL_KABSCH)
+            ctx.profile(False)
+            return el, sc, kb, out
+
+        rel, _, _, out = ransac_timed(False)  # value: no events on the stream
+        rel_ev, (sc_ms, sc_n), (kb_ms, kb_n), _ = ransac_timed(True)  # kernel durations
         sc_avg = max_over_ranks(sc_ms / max(sc_n, 1))
         hyps_per_launch = H / max(sc_n // args.ransac_steps, 1)
         sc_tf = SCORE_FLOP_PER_PAIR * nc * hyps_per_launch / (sc_avg * 1e-3) / 1e12
         ransac = {
             "metric": "RANSAC hypotheses/sec (cfg2: Nc=1e5, a1+a2, no early stop)",
             "value": world * H * args.ransac_steps / rel, "unit": "hyp/s",
-            "ms_per_run": rel / args.ransac_steps * 1e3, "hyps_per_gpu": H, "nc": nc,
+            "ms_per_run": rel / args.ransac_steps * 1e3,
+            "ms_per_run_with_kernel_events": rel_ev / args.ransac_steps * 1e3,
+            "hyps_per_gpu": H, "nc": nc,
             "best_fitness": out.fitness,
             "roofline": {"bound": "valu", "kernel": "score_kernel", "achieved": sc_tf,
                          "peak": VALU_FP32_PEAK_TF, "unit": "TFLOP/s", "frac": sc_tf / VALU_FP32_PEAK_TF,
@@ -268,6 +288,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3,
+        "ms_per_step_with_kernel_events": el_ev / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 2
+#define M3D_ABI_VERSION 3
 
 /* return codes */
 #define M3D_OK 0
@@ -205,6 +205,9 @@ void m3d_icp_destroy(m3d_icp* s);
 int m3d_icp_reset(m3d_icp* s, const double* init_host, void* stream);
 /* One full iteration on one device: NN evaluation + estimation terms + solve/update. */
 int m3d_icp_step(m3d_icp* s, void* stream);
+/* n iterations (n × m3d_icp_step, enqueued from native code: no per-iteration host binding
+ * overhead).  Iterations after convergence / max_iteration are device no-ops. */
+int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream);
 /* Target-sharded pieces (cfg3): `tgt` of m3d_icp_create is this rank's shard whose first
  * point has global index shard_offset.  keys [device] ns int64: packed (bits(d²)<<32 | idx),
  * INT64_MAX = none; reduce with MIN across ranks.  sums [device] 32 f64; reduce with SUM. */

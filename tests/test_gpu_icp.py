@@ -186,6 +186,11 @@ def test_step_loop_matches_run():
     r = loop.result()
     np.testing.assert_array_equal(r.transformation, full.transformation)
     assert r.fitness == full.fitness and r.iterations == 10
+    loop.reset(np.eye(4))
+    loop.steps(13)  # native loop; the two extra iterations are device no-ops after the last
+    r2 = loop.result()
+    np.testing.assert_array_equal(r2.transformation, full.transformation)
+    assert r2.fitness == full.fitness and r2.iterations == 10
 
 
 @pytest.mark.parametrize("estimation", [_lib.EST_POINT_TO_PLANE, _lib.EST_POINT_TO_POINT])
