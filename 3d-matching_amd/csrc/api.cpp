@@ -302,6 +302,10 @@ static int corrset_build(m3d_ctx* ctx, const double* src, int64_t ns, const doub
   // pad: source 0, target far away → padded pairs are never inliers nor ambiguous
   if (!rc) rc = center_pack(ctx, cs->p64, nc, cs->nc_pad, cs->cs, cs->p32, 0.0f, &cs->pmax2, st);
   if (!rc) rc = center_pack(ctx, cs->q64, nc, cs->nc_pad, cs->ct, cs->q32, kFar, &cs->qmaxinf, st);
+  if (!rc) {
+    hipError_t e2 = launch_corr16(cs, st);  // MFMA scoring operands (ransac.hip)
+    if (e2 != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e2));
+  }
   if (corr_tmp) {
     hipStreamSynchronize(st);
     hipFree(corr_tmp);
@@ -336,6 +340,7 @@ void m3d_corrset_destroy(m3d_corrset* cs) {
   hipFree(cs->q64);
   hipFree(cs->p32);
   hipFree(cs->q32);
+  hipFree(cs->ca16);
   delete cs;
 }
 
@@ -360,15 +365,28 @@ int m3d_kabsch3_batch(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triple
 
 // ------------------------------------------------------------------------------- a2/a3
 namespace {
+extern "C++" {
 struct ScoreScratch {
   HypF32* hypf;
+  ScoreMf mf;
 };
 
+constexpr int kScoreSlots = 3;
 void score_layout(Arena& a, int64_t H, size_t* o) {
+  const int64_t hp = score_mf_hpad(std::max<int64_t>(H, 1));
   o[0] = a.take(sizeof(HypF32) * std::max<int64_t>(H, 1));
+  o[1] = a.take(sizeof(uint4) * 6 * hp);
+  o[2] = a.take(sizeof(float) * hp);
 }
 
-ScoreScratch score_bind(const Arena& a, const size_t* o) { return ScoreScratch{a.at<HypF32>(o[0])}; }
+ScoreScratch score_bind(const Arena& a, const size_t* o) {
+  ScoreScratch s;
+  s.hypf = a.at<HypF32>(o[0]);
+  s.mf.hb16 = a.at<uint4>(o[1]);
+  s.mf.heps = a.at<float>(o[2]);
+  return s;
+}
+}  // extern "C++"
 
 double thr_sq_of(double thr, int mode) { return mode == M3D_SCORE_SQUARED ? thr : thr * thr; }
 
@@ -377,8 +395,10 @@ double thr_sq_of(double thr, int mode) { return mode == M3D_SCORE_SQUARED ? thr 
 hipError_t score_enqueue(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64_t H,
                          double thr, int mode, int32_t* counts, const ScoreScratch& s,
                          const int32_t* done, hipStream_t st) {
+  hipError_t e = launch_score_prep(cs, T, H, thr, mode, s.mf, st);
+  if (e != hipSuccess) return e;
   KTimer kt(ctx, M3D_KERNEL_SCORE, st);
-  return launch_score(cs, s.hypf, H, counts, T, thr, mode, ctx->stats, done, st);
+  return launch_score(cs, s.hypf, H, counts, T, thr, mode, ctx->stats, done, s.mf, st);
 }
 }  // namespace
 
@@ -396,7 +416,7 @@ int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64
     return M3D_OK;
   }
   Arena a(ctx);
-  size_t o[1];
+  size_t o[kScoreSlots];
   score_layout(a, H, o);
   int rc = a.commit();
   if (rc) return rc;
@@ -427,7 +447,7 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   }
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(max_iter, 1)));
   Arena a(ctx);
-  size_t o[1];
+  size_t o[kScoreSlots];
   score_layout(a, B, o);
   size_t o_T = a.take(sizeof(double) * 16 * B);
   size_t o_c = a.take(sizeof(int32_t) * B);

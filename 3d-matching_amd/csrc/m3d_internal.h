@@ -125,6 +125,10 @@ struct m3d_corrset {
   double cs[3] = {0, 0, 0}, ct[3] = {0, 0, 0};
   double pmax2 = 0.0;    // max |p_c|∞ (guard-band bound)
   double qmaxinf = 0.0;  // max |q_c|∞
+  // MFMA scoring operands (ransac.hip score_mfma_kernel): 4 planes × nc_pad of fp16 hi/lo
+  // splits of S·p_c / S·q_c (plane 0: the p part, planes 1-3: the q_x / q_y / q_z parts)
+  uint4* ca16 = nullptr;
+  double s16 = 0.0;  // the power-of-two scale S (0: MFMA scoring unavailable)
 };
 
 struct m3d_cloud {
@@ -190,9 +194,20 @@ hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_
                           HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st);
 hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
                               HypF32* hypf, ZeroArgs z, hipStream_t st);
+// MFMA scoring (score_mfma_kernel): per-batch hypothesis operands built from the fp64
+// transforms; null hb16 → the fp32 VALU screen (score_kernel)
+struct ScoreMf {
+  uint4* hb16 = nullptr;  // 6 planes × h_pad (fp16 hi/lo splits of R rows and S·t')
+  float* heps = nullptr;  // h_pad: guard band of v = S²(thr² − d²) per hypothesis (< 0: none)
+  int64_t h_pad = 0;
+};
+int64_t score_mf_hpad(int64_t H);
+hipError_t launch_corr16(m3d_corrset* cs, hipStream_t st);  // cs->ca16, cs->s16
+hipError_t launch_score_prep(const m3d_corrset* cs, const double* T64, int64_t H, double thr,
+                             int mode, const ScoreMf& mf, hipStream_t st);
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
                         const double* T64, double thr, int mode, int64_t* stats,
-                        const int32_t* done, hipStream_t st);
+                        const int32_t* done, const ScoreMf& mf, hipStream_t st);
 hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int64_t nc,
                          int64_t max_iter, int early_stop, double es_thr, double es_conf,
                          const double* T_batch, RansacState* rs, hipStream_t st);

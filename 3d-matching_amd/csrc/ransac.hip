@@ -2,10 +2,12 @@
 //
 // Reference path (all CPU, numpy fp64):
 //   compute_step_transformation  src/matcher/ransac.py:104-192   → kabsch3_kernel
-//   evaluate_inlier_ratio[_fast] src/matcher/ransac.py:195-277   → score_kernel (fp64 recheck inline)
+//   evaluate_inlier_ratio[_fast] src/matcher/ransac.py:195-277   → score_mfma_kernel (matrix cores,
+//                                                                   see "MFMA screen" below) or the
+//                                                                   fp32 VALU score_kernel
 //   step-RANSAC loop             _visualize_matcher.py:343-470   → select_kernel (batched, on device)
 //
-// Scoring design (VALU-bound, no dense contraction → no MFMA):
+// fp32 VALU scoring design (score_kernel: the fallback, and M3D_SCORE_MFMA=0):
 //   * One lane holds kScoreK = 8 correspondences (centred fp32, 6 VGPRs each) for the whole block;
 //     a block of 4 waves covers 2048 correspondences and sweeps 64 hypotheses.
 //   * The block's 64 hypothesis blocks (R, t', guard band: 64 B each) are staged in LDS and read
@@ -18,6 +20,7 @@
 //     the counts equal an fp64 evaluation of the reference formula.
 //   * Counts are integers: atomics are exact and order-independent → deterministic results.
 #include <float.h>
+#include <stdlib.h>
 
 #include "linalg.h"
 #include "m3d_internal.h"
@@ -332,6 +335,317 @@ __global__ __launch_bounds__(kScoreBlock) void score_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------- MFMA screen
+// The residual VECTOR d = R p_c + t' − q_c per (correspondence, hypothesis) is three rank-13
+// contractions, one v_mfma_f32_32x32x16_f16 per component and 32 × 32 block, from fp16 hi/lo
+// splits of the power-of-two-scaled operands (S = cs->s16, |S·p_c|∞, |S·q_c|∞ ≤ 1024):
+//   A (correspondence row i, component c): [ph0, pl0, ph0, ph1, pl1, ph1, ph2, pl2 |
+//                                           ph2, 1, 1, qh_c, ql_c, 0, 0, 0]
+//   B (hypothesis column j, component c):  [Rh0, Rh0, Rl0, Rh1, Rh1, Rl1, Rh2, Rh2 |
+//                                           Rl2, th_c, tl_c, −1, −1, 0, 0, 0]
+// (R = row c of the rotation, t = S·t'_c; Rl·pl is dropped).  The VALU then forms
+// v = S²thr² − dx² − dy² − dz² (3 packed FMAs per 2 pairs) and counts sign bits per lane (a lane
+// owns one hypothesis column): 3.5 VALU per pair against ≈ 9 for the fp32 screen.  Exactness:
+// |v − S²(thr² − d²)| < ε_j (per hypothesis, hyp16_kernel: split remainders, the MFMA's fp32
+// accumulation of 13 exact products with cancellation, the three FMA roundings, thr² rounding
+// and the fp64 reference's own rounding), so pairs with |v| ≥ ε_j are classified exactly and the
+// rest are re-evaluated in fp64 with numpy's operation order (exact_inlier) — the counts equal
+// the fp32 screen's and the reference formula's.
+typedef _Float16 s_half8 __attribute__((ext_vector_type(8)));
+typedef float s_floatx16 __attribute__((ext_vector_type(16)));
+typedef float s_float2 __attribute__((ext_vector_type(2)));
+union SH8 {
+  uint4 u;
+  s_half8 h;
+};
+
+constexpr int kSMG = 2;                       // 32-hypothesis groups per wave
+constexpr int kSBlock = 512;                  // 8 waves
+constexpr int kSHyps = (kSBlock / 64) * kSMG * 32;  // 512 hypotheses per block
+constexpr int kSTile = 256;                   // correspondences per LDS tile
+constexpr double kU16 = 4.8828125e-04;        // 2^-11
+constexpr double kSig16 = 2.98023223876953125e-08;  // 2^-25: half the fp16 subnormal spacing
+constexpr float kPadQ = 30000.0f;             // padded rows: q far away (exact in fp16)
+constexpr float kFarT = 16384.0f;             // hypotheses that cannot have inliers
+constexpr int kSQueue = 1024;                 // guard-band pairs queued per block (8 KB LDS)
+
+__device__ __forceinline__ void split16d(double x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (double)hi);
+}
+
+__global__ __launch_bounds__(256) void corr16_kernel(const double* __restrict__ p64,
+                                                     const double* __restrict__ q64, int64_t nc,
+                                                     int64_t nc_pad, double cs0, double cs1,
+                                                     double cs2, double ct0, double ct1,
+                                                     double ct2, double S,
+                                                     uint4* __restrict__ ca16) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nc_pad) return;
+  const _Float16 one = (_Float16)1.0f, zero = (_Float16)0.0f;
+  SH8 P, Q[3];
+  if (i < nc) {
+    _Float16 h[3], l[3];
+    split16d(S * (p64[3 * i] - cs0), h[0], l[0]);
+    split16d(S * (p64[3 * i + 1] - cs1), h[1], l[1]);
+    split16d(S * (p64[3 * i + 2] - cs2), h[2], l[2]);
+    P.h = s_half8{h[0], l[0], h[0], h[1], l[1], h[1], h[2], l[2]};
+    const double qc[3] = {q64[3 * i] - ct0, q64[3 * i + 1] - ct1, q64[3 * i + 2] - ct2};
+    for (int c = 0; c < 3; ++c) {
+      _Float16 qh, ql;
+      split16d(S * qc[c], qh, ql);
+      Q[c].h = s_half8{h[2], one, one, qh, ql, zero, zero, zero};
+    }
+  } else {
+    P.u = make_uint4(0, 0, 0, 0);
+    for (int c = 0; c < 3; ++c)
+      Q[c].h = s_half8{zero, one, one, (_Float16)kPadQ, zero, zero, zero, zero};
+  }
+  ca16[i] = P.u;
+  for (int c = 0; c < 3; ++c) ca16[(1 + c) * nc_pad + i] = Q[c].u;
+}
+
+struct Mf16Params {
+  double cs[3], ct[3];
+  double S, pinf, qinf, thr_sq;
+};
+
+// B operands + guard band of hypotheses [0, h_pad) of a batch (fp64 transforms T64).
+__global__ __launch_bounds__(256) void hyp16_kernel(const double* __restrict__ T64, int64_t H,
+                                                    int64_t h_pad, Mf16Params m,
+                                                    uint4* __restrict__ hb16,
+                                                    float* __restrict__ heps) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= h_pad) return;
+  const _Float16 zero = (_Float16)0.0f, mone = (_Float16)-1.0f;
+  SH8 B0[3], B1[3];
+  float eps = -1.0f;  // no guard band: v is never inside (−1, 1)·ε
+  bool far = true, general = false;
+  if (j < H) {
+    const double* T = T64 + 16 * j;
+    double tp[3], rowl1 = 0.0, tinf = 0.0;
+    bool finite = true;
+    for (int c = 0; c < 3; ++c) {
+      const double* r = T + 4 * c;
+      tp[c] = fma(r[2], m.cs[2], fma(r[1], m.cs[1], r[0] * m.cs[0])) + r[3] - m.ct[c];
+      rowl1 = fmax(rowl1, fabs(r[0]) + fabs(r[1]) + fabs(r[2]));
+      tinf = fmax(tinf, fabs(tp[c]));
+      finite = finite && isfinite(r[0]) && isfinite(r[1]) && isfinite(r[2]) && isfinite(tp[c]);
+    }
+    const double thr = sqrt(m.thr_sq);
+    // |d|∞ ≥ |t'|∞ − ‖R‖∞|p_c|∞ − |q_c|∞: beyond thr (with margin) no correspondence is an
+    // inlier, in any arithmetic — such a hypothesis gets count 0 (NaN transforms too, as the
+    // fp32 screen and numpy's comparisons give)
+    far = !finite || tinf > 1.01 * (rowl1 * m.pinf + m.qinf + thr) + 1e-30;
+    // not a rotation (only m3d_ransac_score takes arbitrary transforms): no fp16 operands for
+    // R — every pair of the hypothesis goes to the fp64 re-evaluation
+    general = !far && rowl1 > 2.0;
+    if (general) {
+      for (int c = 0; c < 3; ++c) {
+        B0[c].u = make_uint4(0, 0, 0, 0);
+        B1[c].h = s_half8{zero, zero, zero, mone, mone, zero, zero, zero};
+      }
+      eps = FLT_MAX;  // v = S²thr² − |S·q_c|² is finite: |v| < ε for every pair
+    } else if (!far) {
+      const double S = m.S;
+      for (int c = 0; c < 3; ++c) {
+        const double* r = T + 4 * c;
+        _Float16 rh[3], rl[3], th, tl;
+        for (int k = 0; k < 3; ++k) split16d(r[k], rh[k], rl[k]);
+        split16d(S * tp[c], th, tl);
+        B0[c].h = s_half8{rh[0], rh[0], rl[0], rh[1], rh[1], rl[1], rh[2], rh[2]};
+        B1[c].h = s_half8{rl[2], th, tl, mone, mone, zero, zero, zero};
+      }
+      // per-component error of the scaled d (see the section comment): products exact in fp32,
+      // accumulation ≤ 32u·Σ|terms| in any order even with truncating adds, split remainders
+      // 3u16²|R||p| + 4σ(|R| + 3|p|) summed over the row, u16²|x| + σ for t and q
+      const double Pt = S * m.pinf, Qt = S * m.qinf, Tt = S * tinf;
+      const double sum_terms = (rowl1 * Pt + Tt + Qt) * (1.0 + 4.0 * kU16);
+      const double Ed = 1.05 * (32.0 * kU32 * sum_terms + 3.0 * kU16 * kU16 * rowl1 * Pt +
+                                4.0 * kSig16 * (rowl1 + 3.0 * Pt) + kU16 * kU16 * (Tt + Qt) +
+                                4.0 * kSig16);
+      const double Ts = S * thr, T2 = S * S * m.thr_sq;
+      const double dm = Ts + 1.7320508075688772 * Ed;       // |d| of a pair that could flip
+      const double dc = Ts + 2.0 * 1.7320508075688772 * Ed;  // its computed |d|
+      const double e = kU32 * T2 + 2.0 * 1.7320508075688772 * dm * Ed + 3.0 * Ed * Ed +
+                       3.0 * kU32 * (T2 + dc * dc);
+      eps = __double2float_ru(1.25 * e + 8.0 * DBL_EPSILON * T2);
+    }
+  }
+  if (far) {
+    for (int c = 0; c < 3; ++c) {
+      B0[c].u = make_uint4(0, 0, 0, 0);
+      B1[c].h = s_half8{zero, (_Float16)kFarT, zero, mone, mone, zero, zero, zero};
+    }
+  }
+  for (int c = 0; c < 3; ++c) {
+    hb16[c * h_pad + j] = B0[c].u;
+    hb16[(3 + c) * h_pad + j] = B1[c].u;
+  }
+  heps[j] = eps;
+}
+
+__device__ __forceinline__ float vmin3a(float a, float b, float c) {
+  return __builtin_elementwise_minimum(__builtin_elementwise_minimum(fabsf(a), fabsf(b)), fabsf(c));
+}
+
+// grid: x = hypothesis blocks of kSHyps, y = correspondence slices of slice_len (multiple of
+// kSTile); block = 8 waves, wave w owns hypotheses hb + (w·kSMG + g)·32 + (lane & 31).
+__global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
+    const uint4* __restrict__ ca16, int64_t nc_pad, const uint4* __restrict__ hb16,
+    const float* __restrict__ heps, int64_t h_pad, int64_t H, int64_t slice_len, float T2,
+    int32_t* __restrict__ counts, ExactArgs ex, const int32_t* __restrict__ done, float band_on) {
+  // band_on: 1; M3D_SCORE_EXP=1 passes −1 to time the screen without the fp64 band path
+  // (profiling experiment only: counts are then those of the screen alone)
+  if (done != nullptr && *done) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  s_half8 bx[kSMG], by[kSMG], bz[kSMG];
+  float eps[kSMG];
+  uint32_t outl[kSMG];
+  int64_t hyp[kSMG];
+#pragma unroll
+  for (int g = 0; g < kSMG; ++g) {
+    const int64_t j = (int64_t)blockIdx.x * kSHyps + (wave * kSMG + g) * 32 + c;  // < h_pad
+    hyp[g] = j;
+    SH8 t;
+    t.u = hb16[(3 * h + 0) * h_pad + j];
+    bx[g] = t.h;
+    t.u = hb16[(3 * h + 1) * h_pad + j];
+    by[g] = t.h;
+    t.u = hb16[(3 * h + 2) * h_pad + j];
+    bz[g] = t.h;
+    eps[g] = heps[j] * band_on;
+    outl[g] = 0;
+  }
+  const s_floatx16 zacc = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
+                           0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  // the threshold as a VGPR operand (a uniform value would be kept in SGPRs, and an SGPR source
+  // costs 1.65x VALU issue time on gfx950: tools/ubench_valu.hip)
+  float t2r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t2r) : "s"(T2));
+  const s_float2 t2v = {t2r, t2r};
+  // [buffer][plane][correspondence]: plane 0 = p part (lane half 0 of every component),
+  // planes 1-3 = the q_x / q_y / q_z parts (lane half 1).  Thread t stages two of the tile's
+  // 4 × 256 16-B operands.
+  __shared__ uint4 a16[2][4][kSTile];
+  __shared__ uint32_t qn;                 // guard-band queue: entries used
+  __shared__ uint2 qbuf[kSQueue];         // (correspondence, hypothesis | screen sign << 31)
+  if (threadIdx.x == 0) qn = 0;
+  const int64_t jb = (int64_t)blockIdx.y * slice_len;
+  const int64_t je = min(nc_pad, jb + slice_len);
+  const int p0 = threadIdx.x / kSTile, k0 = threadIdx.x % kSTile;  // planes p0 and p0 + 2
+#pragma unroll
+  for (int u = 0; u < 2; ++u) a16[0][p0 + 2 * u][k0] = ca16[(p0 + 2 * u) * nc_pad + jb + k0];
+  __syncthreads();
+  int buf = 0;
+  const int pa = h == 0 ? 0 : 1;  // planes read by this lane for x, y, z: pa·(1 + comp)
+  for (int64_t j0 = jb; j0 < je; j0 += kSTile) {
+    const bool has_next = j0 + kSTile < je;
+    uint4 pre[2];
+    if (has_next) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) pre[u] = ca16[(p0 + 2 * u) * nc_pad + j0 + kSTile + k0];
+    }
+#pragma unroll 2
+    for (int sub = 0; sub < kSTile / 32; ++sub) {
+      SH8 ax, ay, az;
+      ax.u = a16[buf][pa * 1][sub * 32 + c];
+      ay.u = a16[buf][pa * 2][sub * 32 + c];
+      az.u = a16[buf][pa * 3][sub * 32 + c];
+#pragma unroll
+      for (int g = 0; g < kSMG; ++g) {
+        const s_floatx16 dx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax.h, bx[g], zacc, 0, 0, 0);
+        const s_floatx16 dy = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay.h, by[g], zacc, 0, 0, 0);
+        const s_floatx16 dz = __builtin_amdgcn_mfma_f32_32x32x16_f16(az.h, bz[g], zacc, 0, 0, 0);
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const s_float2 x = {dx[r], dx[r + 1]}, y = {dy[r], dy[r + 1]}, z = {dz[r], dz[r + 1]};
+          s_float2 w = __builtin_elementwise_fma(-x, x, t2v);
+          w = __builtin_elementwise_fma(-y, y, w);
+          w = __builtin_elementwise_fma(-z, z, w);
+          v[r] = w[0];
+          v[r + 1] = w[1];
+        }
+        // v > 0 ⇔ inlier (outside the band): count sign bits (outliers) per lane
+        uint32_t s = 0;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2)
+          s += (__float_as_uint(v[r]) >> 31) + (__float_as_uint(v[r + 1]) >> 31);
+        outl[g] += s;
+        const float m0 = vmin3a(v[0], v[1], v[2]), m1 = vmin3a(v[3], v[4], v[5]);
+        const float m2 = vmin3a(v[6], v[7], v[8]), m3 = vmin3a(v[9], v[10], v[11]);
+        const float m4 = vmin3a(v[12], v[13], v[14]);
+        const float m = __builtin_elementwise_minimum(
+            __builtin_elementwise_minimum(__builtin_elementwise_minimum(m0, m1),
+                                          __builtin_elementwise_minimum(m2, m3)),
+            __builtin_elementwise_minimum(m4, fabsf(v[15])));
+        if (__any(m < eps[g])) {
+          // rare (wave-uniform): pairs inside their hypothesis's guard band.  They are queued in
+          // LDS (correspondence, hypothesis, screen sign) and re-evaluated in fp64 by the whole
+          // block after the sweep, so no wave waits on the dependent fp64 loads here; a full
+          // queue falls back to evaluating in place.
+          uint32_t bm = 0, sm = 0;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            bm |= (fabsf(v[r]) < eps[g] ? 1u : 0u) << r;
+            sm |= (__float_as_uint(v[r]) >> 31) << r;
+          }
+          const uint32_t nb = __builtin_popcount(bm);
+          uint32_t slot = nb ? atomicAdd(&qn, nb) : 0u;
+          while (bm != 0) {
+            const int r = __builtin_ctz(bm);
+            bm &= bm - 1;
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t i = j0 + sub * 32 + row;  // < nc (pads are never in a band)
+            const uint32_t sgn = (sm >> r) & 1u;
+            if (slot < kSQueue) {
+              qbuf[slot] = make_uint2((uint32_t)i, (uint32_t)hyp[g] | (sgn << 31));
+            } else {
+              const bool in = hyp[g] < H && i < ex.nc &&
+                              exact_inlier(ex.T64 + 16 * hyp[g], ex.p64 + 3 * i, ex.q64 + 3 * i,
+                                           ex.thr, ex.mode);
+              outl[g] += (in ? 0u : 1u) - sgn;
+            }
+            ++slot;
+          }
+        }
+      }
+    }
+    if (has_next) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) a16[buf ^ 1][p0 + 2 * u][k0] = pre[u];
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  // inliers of hypothesis column c over this slice: rows − outliers, the two lane halves summed
+  const uint32_t rows = (uint32_t)(je - jb) / 2;  // each lane half sees half of every 32-row block
+#pragma unroll
+  for (int g = 0; g < kSMG; ++g) {
+    const uint32_t in = 2 * rows - (outl[g] + (uint32_t)__shfl_xor((int)outl[g], 32));
+    if (h == 0 && hyp[g] < H && in != 0) atomicAdd(&counts[hyp[g]], (int32_t)in);
+  }
+  // the queued guard-band pairs, one per thread: fp64 in numpy order, count correction
+  // (screen sign − exact outlier flag) for that hypothesis
+  const uint32_t nq = min(qn, (uint32_t)kSQueue);  // the last barrier of the loop published qn
+  for (uint32_t e = threadIdx.x; e < nq; e += kSBlock) {
+    const uint2 q = qbuf[e];
+    const int64_t i = (int64_t)q.x;
+    const int64_t j = (int64_t)(q.y & 0x7FFFFFFFu);
+    const int sgn = (int)(q.y >> 31);
+    const bool in = j < H && i < ex.nc &&
+                    exact_inlier(ex.T64 + 16 * j, ex.p64 + 3 * i, ex.q64 + 3 * i, ex.thr, ex.mode);
+    const int corr = sgn - (in ? 0 : 1);  // +1: a screen outlier is an inlier, −1: the reverse
+    if (corr != 0 && j < H) atomicAdd(&counts[j], corr);
+  }
+  if (threadIdx.x == 0 && ex.stats && qn != 0)
+    atomicAdd((unsigned long long*)&ex.stats[0], (unsigned long long)qn);
+}
+
+int64_t score_mf_hpad(int64_t H) { return (H + kSHyps - 1) / kSHyps * kSHyps; }
+
 // ------------------------------------------------------------------------------- a4 select
 struct BestPair {
   int64_t c, i;
@@ -502,11 +816,83 @@ hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H,
   return hipGetLastError();
 }
 
+hipError_t launch_corr16(m3d_corrset* cs, hipStream_t st) {
+  cs->s16 = 0.0;
+  if (cs->nc == 0) return hipSuccess;
+  const double mx = fmax(cs->pmax2, cs->qmaxinf);
+  if (!(mx < 1e30)) return hipSuccess;  // non-finite input: the fp32 screen handles it
+  double S = 1.0;
+  if (mx > 0.0) S = exp2(floor(log2(1024.0 / mx)));
+  S = fmin(fmax(S, 0x1p-40), 0x1p40);
+  hipError_t e = hipMalloc(&cs->ca16, sizeof(uint4) * 4 * cs->nc_pad);
+  if (e != hipSuccess) {
+    cs->ca16 = nullptr;
+    return e;
+  }
+  corr16_kernel<<<blocks_for(cs->nc_pad, 256), 256, 0, st>>>(
+      cs->p64, cs->q64, cs->nc, cs->nc_pad, cs->cs[0], cs->cs[1], cs->cs[2], cs->ct[0], cs->ct[1],
+      cs->ct[2], S, cs->ca16);
+  e = hipGetLastError();
+  if (e == hipSuccess) cs->s16 = S;
+  return e;
+}
+
+// MFMA scoring applies when the operands exist and the threshold stays inside the cloud's
+// scaled range (S·thr ≤ 1024: thresholds beyond the cloud extent use the fp32 screen)
+static bool use_mfma_score(const m3d_corrset* cs, const ScoreMf& mf, double thr_sq) {
+  static const bool env = [] {
+    const char* e = getenv("M3D_SCORE_MFMA");
+    return !(e && atoi(e) == 0);
+  }();
+  return env && mf.hb16 != nullptr && cs->ca16 != nullptr && cs->s16 > 0.0 &&
+         cs->s16 * sqrt(thr_sq) <= 1024.0;
+}
+
+static double thr_sq_mode(double thr, int mode) { return mode == M3D_SCORE_SQUARED ? thr : thr * thr; }
+
+hipError_t launch_score_prep(const m3d_corrset* cs, const double* T64, int64_t H, double thr,
+                             int mode, const ScoreMf& mf, hipStream_t st) {
+  const double thr_sq = thr_sq_mode(thr, mode);
+  if (H == 0 || cs->nc == 0 || !use_mfma_score(cs, mf, thr_sq)) return hipSuccess;
+  Mf16Params m;
+  for (int k = 0; k < 3; ++k) {
+    m.cs[k] = cs->cs[k];
+    m.ct[k] = cs->ct[k];
+  }
+  m.S = cs->s16;
+  m.pinf = cs->pmax2;
+  m.qinf = cs->qmaxinf;
+  m.thr_sq = thr_sq;
+  const int64_t hp = score_mf_hpad(H);
+  hyp16_kernel<<<blocks_for(hp, 256), 256, 0, st>>>(T64, H, hp, m, mf.hb16, mf.heps);
+  return hipGetLastError();
+}
+
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
                         const double* T64, double thr, int mode, int64_t* stats,
-                        const int32_t* done, hipStream_t st) {
+                        const int32_t* done, const ScoreMf& mf, hipStream_t st) {
   if (H == 0 || cs->nc == 0) return hipSuccess;
   ExactArgs ex{T64, cs->p64, cs->q64, cs->nc, thr, mode, stats};
+  const double thr_sq = thr_sq_mode(thr, mode);
+  if (use_mfma_score(cs, mf, thr_sq)) {
+    const int64_t hp = score_mf_hpad(H);
+    const int64_t bx = hp / kSHyps;
+    // correspondence slices over grid.y so that ≥ ~2048 blocks fill the chip
+    int64_t sy = (2048 + bx - 1) / bx;
+    const int64_t tiles = cs->nc_pad / kSTile;
+    if (sy > tiles) sy = tiles;
+    if (sy < 1) sy = 1;
+    const int64_t slice = (tiles + sy - 1) / sy * kSTile;
+    sy = (cs->nc_pad + slice - 1) / slice;
+    const float T2 = (float)(cs->s16 * cs->s16 * thr_sq);
+    static const float band_on = [] {
+      const char* e = getenv("M3D_SCORE_EXP");
+      return (e && atoi(e) == 1) ? -1.0f : 1.0f;
+    }();
+    score_mfma_kernel<<<dim3((unsigned)bx, (unsigned)sy), kSBlock, 0, st>>>(
+        cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H, slice, T2, counts, ex, done, band_on);
+    return hipGetLastError();
+  }
   const int64_t per_launch = (int64_t)65535 * kScoreHyps;  // grid.y limit
   for (int64_t hb = 0; hb < H; hb += per_launch) {
     const int64_t nh = (H - hb) < per_launch ? (H - hb) : per_launch;

@@ -248,3 +248,27 @@ def test_full_size_counts_subsample_exact():
     np.testing.assert_array_equal(counts[pick], O.inlier_counts(p, q, Tn[pick], THR, 1))
     out = cs.run(RansacParams(max_iter=H, seed=42, thr=THR, mode=_lib.SCORE_NORM, early_stop=False))
     assert out.best_count == counts.max() and out.best_index == int(np.argmax(counts))
+
+
+def test_score_edge_transforms_exact():
+    """Transforms outside the MFMA screen's rigid/near regime keep exact counts: a scaled
+    (non-rigid) matrix (every pair re-evaluated in fp64), NaN entries and far translations
+    (count 0 by the |d|∞ bound), and a threshold beyond the cloud extent (fp32 screen)."""
+    from m3d import synth
+
+    src, tgt, corr, T = synth.ransac_pair(5000, seed=8)
+    cs = CorrSet(src, tgt, corr)
+    p, q = src[corr[:, 0]], tgt[corr[:, 1]]
+    scaled = T.copy()
+    scaled[:3, :3] *= 1.5
+    nan = T.copy()
+    nan[0, 1] = np.nan
+    far = T.copy()
+    far[:3, 3] += 1e4
+    near_far = T.copy()
+    near_far[:3, 3] += 12.0  # just past the extent: the bound must not reject possible inliers
+    Ts = np.stack([T, scaled, nan, far, near_far, np.eye(4)])
+    for mode, thr in ((_lib.SCORE_SQUARED, THR * THR), (_lib.SCORE_NORM, THR),
+                      (_lib.SCORE_NORM, 50.0), (_lib.SCORE_SQUARED, 1e-12)):
+        got = cs.score(Ts, thr, mode).cpu().numpy()
+        np.testing.assert_array_equal(got, O.inlier_counts(p, q, Ts, thr, mode))
