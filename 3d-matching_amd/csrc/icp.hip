@@ -6,22 +6,22 @@
 //
 // Kernels per iteration (all device resident, no host round trip):
 //   keyinit  O(Ns)      seeds each query's bound with its previous neighbour (fp32 d²)
-//   nn       O(Ns·Nt)   brute-force scan: queries in VGPRs (kNNQ = 4 per lane), targets staged
-//                       through double-buffered LDS tiles and read with broadcast ds_read_b128.
-//                       Fast path per pair: a screen key |t|² − 2q·t = 3 FMA + ½ v_min3
-//                       (|t|² precomputed in t.w); tiles whose screen minimum cannot reach the
-//                       current bound (proven error bound, refresh_rt32) are skipped, the rest
-//                       take the exact path: direct fp32 d² (3 sub + mul + 2 FMA) with
-//                       lexicographic (d², index) argmin — the same result as a full direct scan.
-//                       The target range is split into slices (grid.y) so the chip is full;
-//                       slices merge with a 64-bit atomicMin on packed (bits(d²) << 32 | idx):
-//                       order independent → deterministic, lowest index wins exact ties.
-//   terms    O(Ns)      fp64: radius test d² < r² (strict, nanoflann), point-to-plane
-//                       J = [p×n ; n], r = (p−q)·n → JTJ(21) JTr(6) Σr²; count; Σd²
-//   reduce   1 block    fixed-order sum of the per-block partials (deterministic)
-//   solve    1 thread   fitness/rmse, convergence test, LDLT(JTJ, −JTr), x → Rz·Ry·Rx|t, T ← ΔT·T
-// The same keys/terms/solve pieces serve the target-sharded multi-GPU path (RCCL MIN on keys,
-// SUM on the 32 term slots between them).
+//   nn       O(Ns·Nt)   brute-force scan, nn_mfma_kernel: screen key |t|² − 2q·t on the matrix
+//                       cores (fp16 hi/lo split operands, proven error bound, refresh_rt32),
+//                       v_minimum3 tree per 32×32 block, flagged sub-tiles take the exact path:
+//                       direct fp32 d² with lexicographic (d², index) argmin — the same result as
+//                       a full direct scan (nn_kernel: the fp32 VALU form of the same screen,
+//                       used when a target has no MFMA tiles).  The target range is split into
+//                       slices (grid.y); slices merge with a 64-bit atomicMin on packed
+//                       (bits(d²) << 32 | idx): order independent → deterministic, lowest index
+//                       wins exact ties.  (grid.hip: the radius-bounded grid search, same key.)
+//   terms_solve O(Ns)   fp64: radius test d² < r² (strict, nanoflann), point-to-plane
+//                       J = [p×n ; n], r = (p−q)·n → JTJ(21) JTr(6) Σr²; count; Σd² → block
+//                       partials; the last block reduces them in a fixed order and one wave runs
+//                       the solve (fitness/rmse, convergence test, LDLT(JTJ, −JTr),
+//                       x → Rz·Ry·Rx|t, T ← ΔT·T).
+// The multi-GPU paths use the same pieces as separate launches (terms_kernel, reduce_kernel,
+// solve_kernel) with the RCCL MIN on keys / SUM on the 32 term slots between them.
 #include <float.h>
 #include <stdlib.h>
 

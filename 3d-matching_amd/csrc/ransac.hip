@@ -359,9 +359,11 @@ union SH8 {
   s_half8 h;
 };
 
-constexpr int kSMG = 2;                       // 32-hypothesis groups per wave
+constexpr int kSMGDefault = 2;                // 32-hypothesis groups per wave (M3D_SCORE_MG)
 constexpr int kSBlock = 512;                  // 8 waves
-constexpr int kSHyps = (kSBlock / 64) * kSMG * 32;  // 512 hypotheses per block
+template <int kSMG>
+constexpr int shyps() { return (kSBlock / 64) * kSMG * 32; }  // hypotheses per block
+constexpr int kSHypPad = shyps<4>();          // batch padding: a multiple of every variant's
 constexpr int kSTile = 256;                   // correspondences per LDS tile
 constexpr double kU16 = 4.8828125e-04;        // 2^-11
 constexpr double kSig16 = 2.98023223876953125e-08;  // 2^-25: half the fp16 subnormal spacing
@@ -489,8 +491,9 @@ __device__ __forceinline__ float vmin3a(float a, float b, float c) {
   return __builtin_elementwise_minimum(__builtin_elementwise_minimum(fabsf(a), fabsf(b)), fabsf(c));
 }
 
-// grid: x = hypothesis blocks of kSHyps, y = correspondence slices of slice_len (multiple of
-// kSTile); block = 8 waves, wave w owns hypotheses hb + (w·kSMG + g)·32 + (lane & 31).
+// grid: x = hypothesis blocks of shyps<kSMG>(), y = correspondence slices of slice_len (multiple
+// of kSTile); block = 8 waves, wave w owns hypotheses hb + (w·kSMG + g)·32 + (lane & 31).
+template <int kSMG>
 __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
     const uint4* __restrict__ ca16, int64_t nc_pad, const uint4* __restrict__ hb16,
     const float* __restrict__ heps, int64_t h_pad, int64_t H, int64_t slice_len, float T2,
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   int64_t hyp[kSMG];
 #pragma unroll
   for (int g = 0; g < kSMG; ++g) {
-    const int64_t j = (int64_t)blockIdx.x * kSHyps + (wave * kSMG + g) * 32 + c;  // < h_pad
+    const int64_t j = (int64_t)blockIdx.x * shyps<kSMG>() + (wave * kSMG + g) * 32 + c;  // < h_pad
     hyp[g] = j;
     SH8 t;
     t.u = hb16[(3 * h + 0) * h_pad + j];
@@ -644,7 +647,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
     atomicAdd((unsigned long long*)&ex.stats[0], (unsigned long long)qn);
 }
 
-int64_t score_mf_hpad(int64_t H) { return (H + kSHyps - 1) / kSHyps * kSHyps; }
+int64_t score_mf_hpad(int64_t H) { return (H + kSHypPad - 1) / kSHypPad * kSHypPad; }
 
 // ------------------------------------------------------------------------------- a4 select
 struct BestPair {
@@ -875,8 +878,13 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
   ExactArgs ex{T64, cs->p64, cs->q64, cs->nc, thr, mode, stats};
   const double thr_sq = thr_sq_mode(thr, mode);
   if (use_mfma_score(cs, mf, thr_sq)) {
+    static const int MG = [] {
+      const char* e = getenv("M3D_SCORE_MG");
+      const int v = e ? atoi(e) : kSMGDefault;
+      return (v == 1 || v == 2 || v == 4) ? v : kSMGDefault;
+    }();
     const int64_t hp = score_mf_hpad(H);
-    const int64_t bx = hp / kSHyps;
+    const int64_t bx = hp / (MG == 4 ? shyps<4>() : (MG == 2 ? shyps<2>() : shyps<1>()));
     // correspondence slices over grid.y so that ≥ ~2048 blocks fill the chip
     int64_t sy = (2048 + bx - 1) / bx;
     const int64_t tiles = cs->nc_pad / kSTile;
@@ -889,8 +897,16 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
       const char* e = getenv("M3D_SCORE_EXP");
       return (e && atoi(e) == 1) ? -1.0f : 1.0f;
     }();
-    score_mfma_kernel<<<dim3((unsigned)bx, (unsigned)sy), kSBlock, 0, st>>>(
-        cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H, slice, T2, counts, ex, done, band_on);
+    const dim3 grid((unsigned)bx, (unsigned)sy);
+    if (MG == 4)
+      score_mfma_kernel<4><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
+                                                     slice, T2, counts, ex, done, band_on);
+    else if (MG == 2)
+      score_mfma_kernel<2><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
+                                                     slice, T2, counts, ex, done, band_on);
+    else
+      score_mfma_kernel<1><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
+                                                     slice, T2, counts, ex, done, band_on);
     return hipGetLastError();
   }
   const int64_t per_launch = (int64_t)65535 * kScoreHyps;  // grid.y limit

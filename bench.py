@@ -11,7 +11,10 @@ BASELINE.json metric "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pt
   32 estimation terms per iteration → weak scaling).
 * "ransac": cfg2 — benchmark_ransac.py's loop (a1 sample + Kabsch, a2 ‖d‖ < 1.5·v scoring) at
   Nc = 1e5, H = 1e5 hypotheses per GPU, counter sampler seed 42, no early stop; N>1 shards the
-  hypothesis ids and all-reduces MAX of the packed (count, ~id) best key.
+  hypothesis ids and all-reduces MAX of the packed (count, ~id) best key.  Its roofline prices
+  score_mfma_kernel (three v_mfma_f32_32x32x16_f16 per 32×32 (correspondence, hypothesis)
+  block = 96 flop per pair) against the FP16 MFMA peak; the 27-flop algorithmic figure is given
+  beside it against the FP32 vector roof.
 * roofline: dominant kernel = the ICP NN scan (nn_mfma_kernel), timed with HIP events recorded
   by the library on the launch stream around every NN launch during a second timed pass of the
   same K steps (an event record costs ~4 us between dependent kernels — tools/loop_overhead.py —
@@ -49,6 +52,7 @@ MFMA_F16_PEAK_TF = 2500.0   # MI355X_MICROARCH.md: Peak BF16/FP16 MFMA, dense
 NN_FLOP_PER_PAIR = 8        # 3 sub + 1 mul + 2 FMA (SURVEY §8(d), fp32 VALU formulation)
 NN_MFMA_FLOP_PER_PAIR = 32  # 16 fp16 MACs per (target, query) pair in v_mfma_f32_32x32x16_f16
 SCORE_FLOP_PER_PAIR = 27    # 9 FMA transform + 3 sub + (1 mul + 2 FMA) + 1 cmp
+SCORE_MFMA_FLOP_PER_PAIR = 96  # 3 x v_mfma_f32_32x32x16_f16 (16 fp16 MACs each) per pair
 CPU_THREADS = 16            # the GPU box's CPU share per GPU
 
 
@@ -260,7 +264,8 @@ def main():
         rel_ev, (sc_ms, sc_n), (kb_ms, kb_n), _ = ransac_timed(True)  # kernel durations
         sc_avg = max_over_ranks(sc_ms / max(sc_n, 1))
         hyps_per_launch = H / max(sc_n // args.ransac_steps, 1)
-        sc_tf = SCORE_FLOP_PER_PAIR * nc * hyps_per_launch / (sc_avg * 1e-3) / 1e12
+        sc_tf = SCORE_MFMA_FLOP_PER_PAIR * nc * hyps_per_launch / (sc_avg * 1e-3) / 1e12
+        sc_algo_tf = SCORE_FLOP_PER_PAIR * nc * hyps_per_launch / (sc_avg * 1e-3) / 1e12
         ransac = {
             "metric": "RANSAC hypotheses/sec (cfg2: Nc=1e5, a1+a2, no early stop)",
             "value": world * H * args.ransac_steps / rel, "unit": "hyp/s",
@@ -268,9 +273,12 @@ def main():
             "ms_per_run_with_kernel_events": rel_ev / args.ransac_steps * 1e3,
             "hyps_per_gpu": H, "nc": nc,
             "best_fitness": out.fitness,
-            "roofline": {"bound": "valu", "kernel": "score_kernel", "achieved": sc_tf,
-                         "peak": VALU_FP32_PEAK_TF, "unit": "TFLOP/s", "frac": sc_tf / VALU_FP32_PEAK_TF,
-                         "avg_launch_ms": sc_avg, "launches": sc_n, "flop_per_pair": SCORE_FLOP_PER_PAIR},
+            "roofline": {"bound": "mfma", "kernel": "score_mfma_kernel", "achieved": sc_tf,
+                         "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s", "frac": sc_tf / MFMA_F16_PEAK_TF,
+                         "avg_launch_ms": sc_avg, "launches": sc_n,
+                         "flop_per_pair": SCORE_MFMA_FLOP_PER_PAIR,
+                         "algorithmic_27flop_per_pair_tflops": sc_algo_tf,
+                         "vs_fp32_valu_roof": sc_algo_tf / VALU_FP32_PEAK_TF},
             "kabsch_avg_launch_ms": kb_ms / max(kb_n, 1),
         }
 

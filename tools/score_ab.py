@@ -33,7 +33,7 @@ def main():
         dt = time.perf_counter() - t0
         s1 = ctx.stats()[0]
     c = counts.cpu().numpy()
-    print(f"mfma={os.environ.get('M3D_SCORE_MFMA', '1')} nc={nc} H={H} ms={dt * 1e3:.3f} "
+    print(f"{os.environ.get('AB_TAG', '')} mfma={os.environ.get('M3D_SCORE_MFMA', '1')} mg={os.environ.get('M3D_SCORE_MG', '2')} nc={nc} H={H} ms={dt * 1e3:.3f} "
           f"sum={int(c.sum())} mean_fit={c.mean() / nc:.4f} rechecked={int(s1 - s0)} "
           f"hash={hash(c.tobytes()) & 0xffffffff:08x}")
     np.save(f"gpurun_out/counts_{os.environ.get('M3D_SCORE_MFMA', '1')}.npy", c)
