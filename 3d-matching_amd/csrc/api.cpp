@@ -597,10 +597,18 @@ int m3d_replay_triples(uint32_t* mt_key, int32_t* mt_pos, int64_t nc, int64_t H,
 // ------------------------------------------------------------------------------- clouds
 int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
                      void* stream, m3d_cloud** out) {
+  return m3d_cloud_create_framed(ctx, xyz, normals, n, nullptr, stream, out);
+}
+
+int m3d_cloud_create_framed(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                            const double* center, void* stream, m3d_cloud** out) {
   if (!ctx) return M3D_ERR_INVALID;
   CHECK_ARG(ctx, out != nullptr, "null output");
   CHECK_ARG(ctx, n >= 0 && n < (int64_t)1 << 31, "point count out of range");
   CHECK_ARG(ctx, n == 0 || xyz != nullptr, "null device pointer");
+  CHECK_ARG(ctx, center == nullptr || (std::isfinite(center[0]) && std::isfinite(center[1]) &&
+                                       std::isfinite(center[2])),
+            "non-finite centre");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
   m3d_cloud* c = new m3d_cloud();
@@ -623,7 +631,13 @@ int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int
       return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
     }
   }
-  rc = device_mean3(ctx, c->xyz64, n, c->center, st);
+  if (center != nullptr) {
+    for (int k = 0; k < 3; ++k) c->center[k] = center[k];
+    c->center_given = 1;
+    rc = M3D_OK;
+  } else {
+    rc = device_mean3(ctx, c->xyz64, n, c->center, st);
+  }
   if (!rc) rc = center_pack(ctx, c->xyz64, n, c->n_pad, c->center, c->xyz32, kFar, &c->rmax, st);
   if (!rc) {
     // fp16 screen operand scale: a power of two with |S·x|∞ ≤ 32 (icp.hip pack16_sorted)
@@ -682,7 +696,7 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st) {
   if (s->params.nn_method == M3D_NN_GRID) {
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->qorder, s->tgrid, off, s->state, s->keys,
-                          st);
+                          s->corr, s->tgt->xyz32, s->tgt->n, st);
   }
   hipError_t e = launch_icp_keyinit(s, off, st);
   if (e != hipSuccess) return e;

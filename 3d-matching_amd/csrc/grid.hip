@@ -30,6 +30,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "m3d_internal.h"
+#include "nnkey.h"
 
 namespace m3d {
 
@@ -113,10 +114,6 @@ __global__ __launch_bounds__(kGridBlock) void grid_gather_kernel(const float4* _
 }
 
 // ------------------------------------------------------------------------------- query
-__device__ __forceinline__ float gd2f(float qx, float qy, float qz, float tx, float ty, float tz) {
-  const float dx = qx - tx, dy = qy - ty, dz = qz - tz;  // == icp.hip d2f
-  return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-}
 
 // kGridLanes lanes cooperate on one query: the query's cell rows (contiguous runs of the sorted
 // array) are dealt round-robin to the lanes, each lane keeps its packed (bits(d²) << 32 | index)
@@ -131,7 +128,14 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __res
                                                              const int32_t* __restrict__ order,
                                                              GridDev g, int64_t off,
                                                              const IcpState* __restrict__ s,
-                                                             int64_t* __restrict__ keys) {
+                                                             int64_t* __restrict__ keys,
+                                                             const int32_t* __restrict__ prev,
+                                                             const float4* __restrict__ tgt32,
+                                                             int64_t nt_shard) {
+  // The query starts from seed_key (its previous correspondence re-evaluated, or a bound): the
+  // cell box then only has to cover d² ≤ the seed's d² instead of r2_hi (same lemma as above
+  // with r2_hi replaced by that bound), and the result is still the lexicographic minimum over
+  // all targets with d² ≤ r2_hi — the seed is one of them, or a bound on the winner's d².
   if (s->done) return;
   const int64_t t = ((int64_t)blockIdx.x * kGridBlock + threadIdx.x) / kGridLanes;
   const int sub = threadIdx.x & (kGridLanes - 1);
@@ -141,14 +145,13 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __res
   int64_t i = 0;
   if (t < ns) {
     i = order != nullptr ? (int64_t)order[t] : t;
-    const float* Rt = s->Rt32;
     const float4 p = src32[i];
-    // == icp.hip xform32
-    const float qx = fmaf(Rt[0], p.x, fmaf(Rt[1], p.y, fmaf(Rt[2], p.z, Rt[9])));
-    const float qy = fmaf(Rt[3], p.x, fmaf(Rt[4], p.y, fmaf(Rt[5], p.z, Rt[10])));
-    const float qz = fmaf(Rt[6], p.x, fmaf(Rt[7], p.y, fmaf(Rt[8], p.z, Rt[11])));
+    float qx, qy, qz;
+    xform32(s->Rt32, p, qx, qy, qz);
+    const int64_t seed = seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, keys);
+    if (seed != kKeyNone) key = (uint64_t)seed;
     if (g.ncells > 0) {
-      const float R = sqrtf(r2_hi) * 1.001f;
+      const float R = sqrtf(__uint_as_float((uint32_t)(key >> 32))) * 1.001f;
       const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
       const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
       const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __res
         const int32_t j0 = g.start[row + x0], j1 = g.start[row + x1 + 1];
         for (int32_t j = j0; j < j1; ++j) {
           const float4 v = g.pts[j];
-          const float d2 = gd2f(qx, qy, qz, v.x, v.y, v.z);
+          const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
           const uint64_t kc = ((uint64_t)__float_as_uint(d2) << 32) |
                               (uint64_t)(uint32_t)(off + __float_as_int(v.w));
           key = kc < key ? kc : key;
@@ -292,11 +295,12 @@ void grid_free(Grid* g) {
 }
 
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
-                          int64_t off, const IcpState* s, int64_t* keys, hipStream_t st) {
+                          int64_t off, const IcpState* s, int64_t* keys, const int32_t* prev,
+                          const float4* tgt32, int64_t nt_shard, hipStream_t st) {
   if (ns == 0) return hipSuccess;
   const int64_t threads = ns * kGridLanes;
   grid_nn_kernel<<<(unsigned)((threads + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
-      src32, ns, order, g->dev, off, s, keys);
+      src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
   return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@
 
 #include "linalg.h"
 #include "m3d_internal.h"
+#include "nnkey.h"
 
 namespace m3d {
 
@@ -35,28 +36,16 @@ constexpr int kNNTile = 16;   // screen sub-tile (one branch per sub-tile)
 constexpr int kNNLds = 512;   // targets per LDS tile (8 KB, double-buffered)
 constexpr int kNNBlock = 256;
 constexpr int kTermsBlock = 256;
+constexpr int kTermsPts = 4;  // sources per terms thread: 4× fewer block partials to reduce
 constexpr double kU = 5.9604644775390625e-08;
 
-__device__ __forceinline__ float d2f(float qx, float qy, float qz, float tx, float ty, float tz) {
-  const float dx = qx - tx, dy = qy - ty, dz = qz - tz;
-  return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-}
-
-__device__ __forceinline__ void xform32(const float* Rt, float4 p, float& x, float& y, float& z) {
-  x = fmaf(Rt[0], p.x, fmaf(Rt[1], p.y, fmaf(Rt[2], p.z, Rt[9])));
-  y = fmaf(Rt[3], p.x, fmaf(Rt[4], p.y, fmaf(Rt[5], p.z, Rt[10])));
-  z = fmaf(Rt[6], p.x, fmaf(Rt[7], p.y, fmaf(Rt[8], p.z, Rt[11])));
-}
-
-__device__ __forceinline__ uint64_t make_key(float d2, uint32_t j) {
-  return ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)j;
-}
 
 // ------------------------------------------------------------------------------- state
 struct FrameParams {
   double cs[3], ct[3];
   double pinf, qinf;
   double s16;  // the target cloud's fp16 operand scale (power of two)
+  int shared;  // the target's frame is shared by every shard (m3d_cloud_create_framed)
 };
 
 // Refresh the fp32 search transform and radius bound for the current T (device side).
@@ -123,6 +112,7 @@ __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, do
   s->evals = s->iters = s->done = s->converged = 0;
   s->ticket = 0;
   s->r2 = r2;
+  s->bound_ok = 0;
   refresh_rt32(s, f);
 }
 
@@ -135,6 +125,7 @@ __global__ void icp_set_T_kernel(IcpState* s, const double* __restrict__ T, doub
   s->evals = s->iters = s->done = s->converged = 0;
   s->ticket = 0;
   s->r2 = r2;
+  s->bound_ok = 0;  // keys/corr of another transform: no bound seeds until the next update
   refresh_rt32(s, f);
 }
 
@@ -145,20 +136,15 @@ __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__
                                                       const IcpState* __restrict__ s,
                                                       const int32_t* __restrict__ prev,
                                                       int64_t* __restrict__ keys) {
+  // keys ← seed_key (nnkey.h); on entry keys holds the previous evaluation's (reduced) keys
   if (s->done) return;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= ns) return;
   const float* Rt = s->Rt32;  // uniform → scalar loads (a local copy went to scratch)
-  int64_t key = kKeyNone;
-  const int64_t j = prev != nullptr ? (int64_t)prev[i] : -1;
-  if (j >= off && j < off + nt_shard) {
-    float x, y, z;
-    xform32(Rt, src32[i], x, y, z);
-    const float4 t = tgt32[j - off];
-    const float d2 = d2f(x, y, z, t.x, t.y, t.z);
-    if (d2 < s->r2_hi) key = (int64_t)make_key(d2, (uint32_t)j);
-  }
-  keys[i] = key;
+  const float4 p = src32[i];
+  float x, y, z;
+  xform32(Rt, p, x, y, z);
+  keys[i] = seed_key(s, i, p, x, y, z, tgt32, nt_shard, off, prev, keys);
 }
 
 // ------------------------------------------------------------------------------- NN scan
@@ -281,17 +267,20 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
 
 // ------------------------------------------------------------------------------- NN, MFMA screen
 // The screen key |t|² − 2q·t is a rank-4 contraction over (x, y, z, 1): here it runs on the
-// matrix cores.  One v_mfma_f32_32x32x16_f16 computes S²·key for 32 targets (A rows) × 32
-// queries (B columns) from fp16 hi/lo splits of the S-scaled operands, K = 16:
-//   A (target) = [xh, xh, xl, yh, yh, yl, zh, zh | zl, wh, wl, 0, 0, 0, 0, 0]
-//   B (query)  = [ah, al, ah, bh, bl, bh, ch, cl | ch, 1,  1,  0, 0, 0, 0, 0]   (a,b,c) = −2S·q
-// Products of fp16 are exact in fp32; the bound on the whole key error is screen_eps_m
-// (refresh_rt32).  A lane holds column c = lane & 31 (its query) and 16 of the 32 rows; the
-// lane pair (c, c + 32) covers all 32.  Per MFMA the lane takes the minimum of its 16 values
-// (v_min3) and tests it against its query's threshold; a sub-tile that hits anywhere in the
-// wave runs the fp32 exact path of nn_kernel (direct d², lexicographic (d², index)) over the
-// lane's 16 rows, and the pair merges its two states with one shuffle.  Result: the same key
-// as nn_kernel and the grid search, at ~1/16 of the fp32 VALU screen's issue cost per pair.
+// matrix cores.  One v_mfma_f32_32x32x16_f16 computes S²·(key − thr) for 32 targets (A rows) ×
+// 32 queries (B columns) from fp16 hi/lo splits of the S-scaled operands, K = 16:
+//   A (target) = [xh, xh, xl, yh, yh, yl, zh, zh | zl, wh, wl, 1,   1,   0, 0, 0]
+//   B (query)  = [ah, al, ah, bh, bl, bh, ch, cl | ch, 1,  1,  −Th, −Tl, 0, 0, 0]
+// (a,b,c) = −2S·q; Th + Tl = the query's threshold S²·thr split in fp16 (thr_split).  Products
+// of fp16 are exact in fp32; the bound on the key error is screen_eps_m (refresh_rt32) plus the
+// threshold terms' share of the accumulation and split error (thr_operand).  So a target can
+// only be a candidate if its value is negative, and the screen is a sign test: per MFMA a lane
+// ORs the bit patterns of its 16 values with v_bitop3_b32 — a full-rate 3-input op on gfx950,
+// where v_min3/v_minimum3/v_or3 issue at half rate (tools/ubench_ops.hip) — and tests bit 31.
+// A lane holds column c = lane & 31 (its query) and 16 of the 32 rows; the lane pair (c, c + 32)
+// covers all 32.  A sub-tile that hits anywhere in the wave runs the fp32 exact path of
+// nn_kernel (direct d², lexicographic (d², index)) over the lane's 16 rows, and the pair merges
+// its two states with one shuffle.  Result: the same key as nn_kernel and the grid search.
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -312,12 +301,41 @@ union H8 {
   half8 h;
 };
 
-__device__ __forceinline__ float vmin3(float a, float b, float c) {
-  return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+// Sign bits of 16 screen values ORed by a full-rate tree: 7 v_bitop3_b32 (a | b | c) + 1 v_or.
+__device__ __forceinline__ uint32_t or16(const floatx16& k) {
+  const auto b = [&](int i) { return __float_as_uint(k[i]); };
+  const uint32_t o0 = __builtin_amdgcn_bitop3_b32(b(0), b(1), b(2), 0xFE);
+  const uint32_t o1 = __builtin_amdgcn_bitop3_b32(b(3), b(4), b(5), 0xFE);
+  const uint32_t o2 = __builtin_amdgcn_bitop3_b32(b(6), b(7), b(8), 0xFE);
+  const uint32_t o3 = __builtin_amdgcn_bitop3_b32(b(9), b(10), b(11), 0xFE);
+  const uint32_t o4 = __builtin_amdgcn_bitop3_b32(b(12), b(13), b(14), 0xFE);
+  const uint32_t o5 = __builtin_amdgcn_bitop3_b32(o0, o1, o2, 0xFE);
+  const uint32_t o6 = __builtin_amdgcn_bitop3_b32(o3, o4, b(15), 0xFE);
+  return o5 | o6;
+}
+
+// The query's threshold as B operand elements 11-12 (lane half 1), in S² units.  thr0 =
+// ((best − |q|²) + eps)·S² carries the key's error bound; the threshold terms add their own
+// share of the MFMA's accumulation bound (32u·|thr|, as for the other products) and of the fp16
+// split (u16²|thr| + σ), with 5 % slack that also covers this sum's fp32 rounding, so that every
+// candidate's value is strictly negative.  |thr| is clamped to 32768 (fp16 range): clamping a
+// negative threshold up only adds false hits; a positive threshold that large (radius far
+// beyond the cloud's extent) sets `force`, and the group then runs the exact path everywhere.
+__device__ __forceinline__ void thr_operand(half8& b, float thr0, bool& force) {
+  const float extra = 1.05f * ((32.0f * 1.01f * 5.9604645e-08f + 2.3841858e-07f) * fabsf(thr0) +
+                               5.9604645e-08f);
+  float thr = thr0 + extra;
+  force = thr > 32768.0f;
+  thr = fminf(fmaxf(thr, -32768.0f), 32768.0f);
+  const _Float16 th = (_Float16)thr;
+  const _Float16 tl = (_Float16)(thr - (float)th);
+  b[3] = -th;
+  b[4] = -tl;
 }
 
 // MFMA screen operands of a cloud in its grid's cell order (A rows of nn_mfma_kernel):
-// mf16 = fp16 split, mf32 = (x, y, z, original index bits).  Pads: key 65504 (never hit),
+// mf16 = fp16 split (+ the two constant-1 threshold slots), mf32 = (x, y, z, original index
+// bits).  Pads: key 65504 (never hit),
 // far-away coordinates (never accepted by the exact path).
 __global__ __launch_bounds__(256) void pack16_sorted_kernel(const float4* __restrict__ sorted,
                                                             const float4* __restrict__ xyz32,
@@ -338,10 +356,12 @@ __global__ __launch_bounds__(256) void pack16_sorted_kernel(const float4* __rest
     split16(t.z * S, zh, zl);
     split16(t.w * (S * S), wh, wl);
     a.h = half8{xh, xh, xl, yh, yh, yl, zh, zh};
-    b.h = half8{zl, wh, wl, (_Float16)0, (_Float16)0, (_Float16)0, (_Float16)0, (_Float16)0};
+    b.h = half8{zl, wh, wl, (_Float16)1, (_Float16)1, (_Float16)0, (_Float16)0, (_Float16)0};
     mf32[k] = make_float4(t.x, t.y, t.z, __int_as_float(idx));
   } else {
-    b.h[1] = (_Float16)65504.0f;
+    b.h[1] = (_Float16)65504.0f;  // value ≥ 65504 − 32768 > 0: never a hit
+    b.h[3] = (_Float16)1;
+    b.h[4] = (_Float16)1;
     mf32[k] = make_float4(1.0e18f, 1.0e18f, 1.0e18f, __int_as_float(-1));
   }
   mf16[k] = a.u;  // two planes: elements 0-7 (lane half 0), elements 8-15 (lane half 1)
@@ -397,6 +417,25 @@ __device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
   }
 }
 
+// Exact fp32 pass of nn_mfma_kernel over one flagged sub-tile (32 targets from `rows`), of which
+// this lane takes its 16 MFMA rows: direct d² and the lexicographic (d², index) update of
+// nn_kernel.  Pads: far coordinates, d² ~ 1e36.
+__device__ __forceinline__ void nn_exact_rows(const float4* __restrict__ rows, int64_t off, int h,
+                                              float qx, float qy, float qz, float& best,
+                                              uint32_t& bidx) {
+  float4 t[16];  // all 16 loads in flight before the first use (one memory latency per sub-tile)
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) t[reg] = rows[(reg & 3) + 8 * (reg >> 2) + 4 * h];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const float d2 = d2f(qx, qy, qz, t[reg].x, t[reg].y, t[reg].z);
+    const uint32_t gj = (uint32_t)(off + __float_as_int(t[reg].w));
+    const bool take = (d2 < best) | ((d2 == best) & (gj < bidx));
+    best = take ? d2 : best;
+    bidx = take ? gj : bidx;
+  }
+}
+
 template <int kMG>
 __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restrict__ src32,
                                                           int64_t ns,
@@ -407,9 +446,11 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           int64_t off,
                                                           const IcpState* __restrict__ s,
                                                           int64_t* __restrict__ keys,
-                                                          uint32_t exp_mask) {
+                                                          uint32_t exp_mask,
+                                                          unsigned long long* __restrict__ stats) {
   // exp_mask: 0xFF always; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
-  // (profiling experiment only: the keys are then wrong)
+  // (profiling experiment only: the keys are then wrong).  stats (M3D_NN_STATS=1, diagnostics
+  // only, else null): [0] flagged (group, sub-tile) steps, [1] all steps.
   if (s->done) return;
   if (!s->mfma_ok) {
     const int64_t jb = (int64_t)blockIdx.y * slice_len;
@@ -421,7 +462,8 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   const float* Rt = s->Rt32;
   const float r2_hi = s->r2_hi, eps = s->screen_eps_m, S = s->mfma_scale;
   const float S2 = S * S;
-  float qx[kMG], qy[kMG], qz[kMG], qq[kMG], best[kMG], thr[kMG];
+  float qx[kMG], qy[kMG], qz[kMG], qq[kMG], best[kMG];
+  uint32_t force = 0;  // groups whose threshold exceeds the fp16 range: exact path everywhere
   uint32_t bidx[kMG], bidx0[kMG];
   int64_t qi[kMG];
   half8 bq[kMG];
@@ -447,13 +489,17 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
     }
     bidx0[g] = bidx[g];
     qq[g] = fmaf(qz[g], qz[g], fmaf(qy[g], qy[g], qx[g] * qx[g]));
-    thr[g] = ((best[g] - qq[g]) + eps) * S2;  // × power of two: exact
     _Float16 ah, al, bh, bl, ch, cl;
     split16(-2.0f * S * qx[g], ah, al);
     split16(-2.0f * S * qy[g], bh, bl);
     split16(-2.0f * S * qz[g], ch, cl);
     const _Float16 one = (_Float16)1.0f, zero = (_Float16)0.0f;
     bq[g] = h == 0 ? half8{ah, al, ah, bh, bl, bh, ch, cl} : half8{ch, one, one, zero, zero, zero, zero, zero};
+    bool fg;
+    half8 bt = bq[g];
+    thr_operand(bt, ((best[g] - qq[g]) + eps) * S2, fg);  // × power of two: exact
+    if (h == 1) bq[g] = bt;
+    if (__any(fg)) force |= 0xFFu << (g * 8);
   }
   const floatx16 zacc = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
                          0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -488,35 +534,33 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
       floatx16 kn;
       if (t + 1 < kSteps)
         kn = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[(t + 1) / kMG].h, bq[(t + 1) % kMG], zacc, 0, 0, 0);
-      // depth-3 tree of v_minimum3_f32 (IEEE minimum: no canonicalising v_max in front, as
-      // fminf needs; the keys are finite — fp16 operands — so NaN propagation never occurs)
-      const float m0 = vmin3(kc[0], kc[1], kc[2]), m1 = vmin3(kc[3], kc[4], kc[5]);
-      const float m2 = vmin3(kc[6], kc[7], kc[8]), m3 = vmin3(kc[9], kc[10], kc[11]);
-      const float m4 = vmin3(kc[12], kc[13], kc[14]);
-      const float m = __builtin_elementwise_minimum(vmin3(m0, m1, m2), vmin3(m3, m4, kc[15]));
+      // keep the pipeline the source states: without this fence the scheduler sinks each
+      // MFMA next to its consumer (same accumulator registers, the VALU then waits out the
+      // whole MFMA latency every step and the matrix pipe idles under the minimum tree)
+      __builtin_amdgcn_sched_barrier(0);
+      // a candidate's value is strictly negative: OR of the 16 bit patterns, test bit 31
       const int g = t % kMG, sub = t / kMG;
-      if (__any(m <= thr[g])) hm |= 1u << (g * 8 + sub);
+      if (__any((int32_t)or16(kc) < 0)) hm |= 1u << (g * 8 + sub);
+      __builtin_amdgcn_sched_barrier(0);
       if (t + 1 < kSteps) kc = kn;
     }
     // Exact path for the flagged (group, sub-tile) pairs, every lane (exact for any lane): direct
     // fp32 d² over the lane's 16 rows, then the lane pair (c, c + 32) merges its two states.
+    // (Deferring the flagged sub-tiles to a per-wave list evaluated after the sweep, off the
+    // barrier path, measured slower: 0.360 vs 0.328 ms per launch at cfg1.)
+    hm |= force;
+    if (stats != nullptr && lane == 0) {
+      atomicAdd(&stats[0], (unsigned long long)__builtin_popcount(hm & ((1u << (8 * kMG)) - 1u)));
+      atomicAdd(&stats[1], (unsigned long long)kSteps);
+    }
 #pragma unroll
     for (int g = 0; g < kMG; ++g) {
       uint32_t m8 = (hm >> (g * 8)) & 0xFFu & exp_mask;
+      if (m8 == 0) continue;
       while (m8 != 0) {
         const int sub = __builtin_ctz(m8);
         m8 &= m8 - 1;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int r = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-          const float4 t = tgt32[j0 + sub * 32 + r];
-          const float d2 = d2f(qx[g], qy[g], qz[g], t.x, t.y, t.z);
-          const uint32_t gj = (uint32_t)(off + __float_as_int(t.w));  // pads: d² ~ 1e36
-          if (d2 < best[g] || (d2 == best[g] && gj < bidx[g])) {
-            best[g] = d2;
-            bidx[g] = gj;
-          }
-        }
+        nn_exact_rows(tgt32 + j0 + sub * 32, off, h, qx[g], qy[g], qz[g], best[g], bidx[g]);
         const float ob = __shfl_xor(best[g], 32);
         const uint32_t oi = (uint32_t)__shfl_xor((int)bidx[g], 32);
         if (ob < best[g] || (ob == best[g] && oi < bidx[g])) {
@@ -524,7 +568,10 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
           bidx[g] = oi;
         }
       }
-      thr[g] = ((best[g] - qq[g]) + eps) * S2;
+      bool fg;
+      half8 bt = bq[g];
+      thr_operand(bt, ((best[g] - qq[g]) + eps) * S2, fg);
+      if (h == 1) bq[g] = bt;  // the threshold only ever tightens: force stays as it was
     }
     if (has_next) t16[buf ^ 1][sp][sk] = pre;
     __syncthreads();
@@ -589,11 +636,12 @@ __device__ __forceinline__ void terms_block(
     int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
     double* __restrict__ partials) {
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
-  const int64_t i = (int64_t)blockIdx.x * kTermsBlock + threadIdx.x;
   double acc[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) acc[k] = 0.0;
-  if (i < ns) {
+  for (int u = 0; u < kTermsPts; ++u) {
+    const int64_t i = ((int64_t)blockIdx.x * kTermsPts + u) * kTermsBlock + threadIdx.x;
+    if (i >= ns) break;
     const int64_t key = keys[i];
     int32_t out = -1;
     if (key != kKeyNone) {
@@ -610,8 +658,8 @@ __device__ __forceinline__ void terms_block(
         const double d2 = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
         if (d2 < s->r2) {
           out = (int32_t)gj;
-          acc[28] = 1.0;
-          acc[29] = d2;
+          acc[28] += 1.0;
+          acc[29] += d2;
           if (est == M3D_EST_POINT_TO_PLANE) {
             const double* n = nrm64 + 3 * (gj - off);
             const double r = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
@@ -624,19 +672,19 @@ __device__ __forceinline__ void terms_block(
 #pragma unroll
             for (int a = 0; a < 6; ++a)
 #pragma unroll
-              for (int b = a; b < 6; ++b) acc[k++] = J[a] * J[b];
+              for (int b = a; b < 6; ++b) acc[k++] += J[a] * J[b];
 #pragma unroll
-            for (int a = 0; a < 6; ++a) acc[21 + a] = J[a] * r;
-            acc[27] = r * r;
+            for (int a = 0; a < 6; ++a) acc[21 + a] += J[a] * r;
+            acc[27] += r * r;
           } else {
             const double pc[3] = {vs[0] - c0, vs[1] - c1, vs[2] - c2};
             const double qc[3] = {q[0] - c0, q[1] - c1, q[2] - c2};
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-              acc[a] = pc[a];
-              acc[3 + a] = qc[a];
+              acc[a] += pc[a];
+              acc[3 + a] += qc[a];
 #pragma unroll
-              for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] = pc[a] * qc[b];
+              for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] += pc[a] * qc[b];
             }
           }
         } else if (!sharded) {
@@ -751,6 +799,9 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   }
   double upd[16];
   for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  // the search transform of the evaluation just reduced: seed_key's bound for the next one
+  for (int k = 0; k < 12; ++k) s->Rt32_prev[k] = s->Rt32[k];
+  s->bound_ok = sp.f.shared;  // bounds compare keys across ranks: only in a shared frame
   if (count > 0.0) {
     if (sp.est == M3D_EST_POINT_TO_PLANE) {
       double A[36], b[6], x[6];
@@ -911,6 +962,7 @@ static FrameParams frame_of(const m3d_icp* s) {
   f.pinf = s->src->rmax;
   f.qinf = s->tgt->rmax;
   f.s16 = s->tgt->s16;
+  f.shared = s->tgt->center_given;
   return f;
 }
 
@@ -980,17 +1032,35 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
       const char* e = getenv("M3D_NN_EXP");
       return (e && atoi(e) == 1) ? 0u : 0xFFu;
     }();
+    // M3D_NN_STATS=1 (diagnostics): count flagged sub-tiles, print after every launch (syncs)
+    static unsigned long long* nn_stats = [] {
+      const char* e = getenv("M3D_NN_STATS");
+      unsigned long long* p = nullptr;
+      if (e && atoi(e) == 1 && hipMalloc(&p, 2 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
+      return p;
+    }();
+    if (nn_stats != nullptr) (void)hipMemsetAsync(nn_stats, 0, 2 * sizeof(unsigned long long), st);
     const int64_t mq = MG == 4 ? mqueries<4>() : (MG == 2 ? mqueries<2>() : mqueries<1>());
     const dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, kMTile, &slice);
     if (MG == 4)
       nn_mfma_kernel<4><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask);
+                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask,
+                                                nn_stats);
     else if (MG == 2)
       nn_mfma_kernel<2><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask);
+                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask,
+                                                nn_stats);
     else
       nn_mfma_kernel<1><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask);
+                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask,
+                                                nn_stats);
+    if (nn_stats != nullptr) {
+      unsigned long long h[2] = {0, 0};
+      if (hipMemcpyAsync(h, nn_stats, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
+          hipStreamSynchronize(st) == hipSuccess)
+        fprintf(stderr, "[m3d nn stats] flagged %llu of %llu steps (%.3f%%)\n", h[0], h[1],
+                h[1] ? 100.0 * (double)h[0] / (double)h[1] : 0.0);
+    }
     return hipGetLastError();
   }
   const dim3 grid = nn_grid((ns + kNNBlock * Q - 1) / (kNNBlock * Q), nt_pad, kNNLds, &slice);
@@ -1065,6 +1135,9 @@ hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipS
   return hipGetLastError();
 }
 
-int64_t terms_blocks(int64_t ns) { return ns > 0 ? (ns + kTermsBlock - 1) / kTermsBlock : 1; }
+int64_t terms_blocks(int64_t ns) {
+  const int64_t per = (int64_t)kTermsBlock * kTermsPts;
+  return ns > 0 ? (ns + per - 1) / per : 1;
+}
 
 }  // namespace m3d

@@ -69,6 +69,8 @@ struct IcpState {
   float mfma_scale;   // power-of-two scale of the fp16 operands (the target cloud's s16)
   int32_t mfma_ok;    // scaled query magnitudes fit fp16: the MFMA screen may run
   uint32_t ticket;    // fused terms→reduce→solve: blocks done this iteration (last one resets)
+  float Rt32_prev[12];  // Rt32 of the previous evaluation (nnkey.h seed_key bounds)
+  int32_t bound_ok;     // Rt32_prev, keys and corr belong to the previous evaluation
 };
 
 // Uniform grid over a cloud's centred fp32 points (grid.hip): kernel view + owner.
@@ -140,6 +142,7 @@ struct m3d_cloud {
   double center[3] = {0, 0, 0};
   double rmax = 0.0;  // max |x_c|∞ (guard-band bound)
   double s16 = 1.0;  // power-of-two scale of the fp16 MFMA screen operands (|s16·x|∞ ≤ 32)
+  int center_given = 0;  // centre supplied by the caller (a frame shared by target shards)
   mutable std::vector<m3d::Grid*> grids;  // uniform grids built on demand, one per cell size
 };
 
@@ -221,8 +224,10 @@ hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st);
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g);
 void grid_free(Grid* g);
+// prev/tgt32/nt_shard: seed each query with seed_key (nnkey.h); prev == nullptr: no seeds
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
-                          int64_t off, const IcpState* s, int64_t* keys, hipStream_t st);
+                          int64_t off, const IcpState* s, int64_t* keys, const int32_t* prev,
+                          const float4* tgt32, int64_t nt_shard, hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
 hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st);
 hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st);

@@ -487,6 +487,17 @@ __global__ __launch_bounds__(256) void hyp16_kernel(const double* __restrict__ T
   heps[j] = eps;
 }
 
+// acc − x·x as one scalar v_fma_f32 (single rounding, = fma(−x, x, acc)).  The empty asm makes
+// each operand an opaque scalar so that no pass pairs neighbours into v_pk_fma_f32: beside MFMAs
+// a packed fp32 op costs ≈ 22 cycles more than the two scalar FMAs it replaces
+// (MI355X_MICROARCH.md, filler prices; measured here 0.189 → 0.178 ms per 1e9 pairs).  The FMA
+// itself stays compiler-generated: an asm FMA reading an MFMA result would bypass the hazard
+// recogniser's wait states.
+__device__ __forceinline__ float fnmsq(float x, float acc) {
+  asm volatile("" : "+v"(x));
+  return __builtin_fmaf(-x, x, acc);
+}
+
 __device__ __forceinline__ float vmin3a(float a, float b, float c) {
   return __builtin_elementwise_minimum(__builtin_elementwise_minimum(fabsf(a), fabsf(b)), fabsf(c));
 }
@@ -527,7 +538,6 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   // costs 1.65x VALU issue time on gfx950: tools/ubench_valu.hip)
   float t2r;
   asm volatile("v_mov_b32 %0, %1" : "=v"(t2r) : "s"(T2));
-  const s_float2 t2v = {t2r, t2r};
   // [buffer][plane][correspondence]: plane 0 = p part (lane half 0 of every component),
   // planes 1-3 = the q_x / q_y / q_z parts (lane half 1).  Thread t stages two of the tile's
   // 4 × 256 16-B operands.
@@ -563,14 +573,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
         const s_floatx16 dz = __builtin_amdgcn_mfma_f32_32x32x16_f16(az.h, bz[g], zacc, 0, 0, 0);
         float v[16];
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const s_float2 x = {dx[r], dx[r + 1]}, y = {dy[r], dy[r + 1]}, z = {dz[r], dz[r + 1]};
-          s_float2 w = __builtin_elementwise_fma(-x, x, t2v);
-          w = __builtin_elementwise_fma(-y, y, w);
-          w = __builtin_elementwise_fma(-z, z, w);
-          v[r] = w[0];
-          v[r + 1] = w[1];
-        }
+        for (int r = 0; r < 16; ++r) v[r] = fnmsq(dz[r], fnmsq(dy[r], fnmsq(dx[r], t2r)));
         // v > 0 ⇔ inlier (outside the band): count sign bits (outliers) per lane
         uint32_t s = 0;
 #pragma unroll

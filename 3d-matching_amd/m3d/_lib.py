@@ -25,7 +25,7 @@ EST_POINT_TO_POINT, EST_POINT_TO_PLANE = 0, 1
 KERNEL_NN, KERNEL_SCORE, KERNEL_KABSCH, KERNEL_TERMS = 0, 1, 2, 3
 NN_BRUTE, NN_GRID = 0, 1
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -86,6 +86,7 @@ SIGNATURES = {
     "m3d_replay_triples": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(i32), i64, i64,
                                      C.POINTER(i32)]),
     "m3d_cloud_create": (C.c_int, [vp, vp, vp, i64, vp, C.POINTER(vp)]),
+    "m3d_cloud_create_framed": (C.c_int, [vp, vp, vp, i64, C.POINTER(C.c_double), vp, C.POINTER(vp)]),
     "m3d_cloud_destroy": (None, [vp]),
     "m3d_cloud_size": (i64, [vp]),
     "m3d_nn1": (C.c_int, [vp, vp, vp, C.POINTER(dbl), dbl, i32, vp, vp, vp]),

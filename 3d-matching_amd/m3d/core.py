@@ -228,9 +228,14 @@ def replay_triples(nc: int, H: int, state=None):
 
 # --------------------------------------------------------------------------------- ICP
 class Cloud:
-    """Packed point cloud on the device (fp64 AoS + centred fp32 float4, optional normals)."""
+    """Packed point cloud on the device (fp64 AoS + centred fp32 float4, optional normals).
 
-    def __init__(self, points, normals=None, ctx: Context | None = None):
+    center: the centring offset (3 floats) instead of the cloud's own mean.  Give every shard of
+    a target-sharded cloud the same centre (e.g. the whole cloud's mean): the shards then share
+    one fp32 frame and target-sharded ICP seeds non-owning ranks with a distance bound
+    (m3d_cloud_create_framed)."""
+
+    def __init__(self, points, normals=None, ctx: Context | None = None, center=None):
         self.ctx = ctx or context()
         p = to_device(points)
         nrm = None if normals is None else to_device(normals)
@@ -238,8 +243,14 @@ class Cloud:
             raise ValueError("normals must match points")
         self.n = p.shape[0]
         h = C.c_void_p()
-        self.ctx.check(self.ctx.lib.m3d_cloud_create(self.ctx.h, ptr(p), ptr(nrm), self.n,
-                                                     stream_handle(), C.byref(h)), "cloud_create")
+        if center is None:
+            rc = self.ctx.lib.m3d_cloud_create(self.ctx.h, ptr(p), ptr(nrm), self.n, stream_handle(),
+                                               C.byref(h))
+        else:
+            c3 = (C.c_double * 3)(*[float(x) for x in np.asarray(center, np.float64).reshape(3)])
+            rc = self.ctx.lib.m3d_cloud_create_framed(self.ctx.h, ptr(p), ptr(nrm), self.n, c3,
+                                                      stream_handle(), C.byref(h))
+        self.ctx.check(rc, "cloud_create")
         self.h = h
         self.has_normals = nrm is not None
 

@@ -135,7 +135,9 @@ def main():
     else:  # target-sharded: nt targets per rank, sources replicated
         src, tgt_all, nrm_all, T_true = synth.icp_pair(ns, nt * world, seed=0)
         off = rank * nt
-        tgt_c = Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt])
+        # one fp32 frame for every shard (the whole target's mean): keys compare bit for bit
+        # across ranks, and non-owning ranks start from a distance bound (m3d_cloud_create_framed)
+        tgt_c = Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0))
     src_c = Cloud(src)
     keys = torch.empty(ns, dtype=torch.int64, device=dev)
     sums = torch.empty(32, dtype=torch.float64, device=dev)

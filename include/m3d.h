@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 3
+#define M3D_ABI_VERSION 4
 
 /* return codes */
 #define M3D_OK 0
@@ -158,6 +158,13 @@ int m3d_replay_triples(uint32_t* mt_key, int32_t* mt_pos, int64_t nc, int64_t H,
  * KDTreeFlann::SetGeometry (Registration.cpp RegistrationICP). */
 int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
                      void* stream, m3d_cloud** out);
+/* The same with an explicit centring offset center [host] 3 f64 instead of the cloud's mean.
+ * Shards of one target cloud created with the same centre share one fp32 frame, so their NN
+ * keys are comparable bit for bit: target-sharded ICP (m3d_icp_shard_nn on each rank, MIN of
+ * the keys) then seeds the queries whose previous winner another rank owns with a distance
+ * bound instead of the radius (nnkey.h seed_key) — same result, far fewer screen hits. */
+int m3d_cloud_create_framed(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                            const double* center, void* stream, m3d_cloud** out);
 void m3d_cloud_destroy(m3d_cloud* c);
 int64_t m3d_cloud_size(const m3d_cloud* c);
 

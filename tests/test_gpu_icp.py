@@ -261,7 +261,8 @@ def test_target_sharded_loop_matches_single_device(nn):
     full = icp(s, Cloud(tgt, nrm), 0.12, np.eye(4), relative_fitness=-1, relative_rmse=-1,
                max_iteration=6, nn="brute")
     bounds = [0, 7000, 19001, 30000]
-    shards = [Cloud(tgt[a:b], nrm[a:b]) for a, b in zip(bounds[:-1], bounds[1:])]
+    c = tgt.mean(axis=0)  # one frame for all shards: seed bounds on non-owning shards
+    shards = [Cloud(tgt[a:b], nrm[a:b], center=c) for a, b in zip(bounds[:-1], bounds[1:])]
     loops = [IcpLoop(s, sh, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=6, nn=nn)
              for sh in shards]
     for lp in loops:
