@@ -121,8 +121,9 @@ __global__ __launch_bounds__(kGridBlock) void grid_gather_kernel(const float4* _
 // (d², index) compare of the brute-force scan (d² ≥ +0, so the float bits order as the values;
 // NaN bits order above every finite bound and are never selected).  16 lanes per query keep
 // ~16x more loads in flight than one lane per query: the scan is latency-bound, not bandwidth.
-constexpr int kGridLanes = 16;
+constexpr int kGridLanesDefault = 4;  // M3D_GRID_LANES = 1|2|4|8|16 overrides (tuning)
 
+template <int kGridLanes>
 __global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __restrict__ src32,
                                                              int64_t ns,
                                                              const int32_t* __restrict__ order,
@@ -298,9 +299,22 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order,
                           int64_t off, const IcpState* s, int64_t* keys, const int32_t* prev,
                           const float4* tgt32, int64_t nt_shard, hipStream_t st) {
   if (ns == 0) return hipSuccess;
-  const int64_t threads = ns * kGridLanes;
-  grid_nn_kernel<<<(unsigned)((threads + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
-      src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+  static const int L = [] {
+    const char* e = getenv("M3D_GRID_LANES");
+    const int v = e ? atoi(e) : kGridLanesDefault;
+    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : kGridLanesDefault;
+  }();
+  const unsigned blocks = (unsigned)((ns * L + kGridBlock - 1) / kGridBlock);
+  if (L == 1)
+    grid_nn_kernel<1><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+  else if (L == 2)
+    grid_nn_kernel<2><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+  else if (L == 4)
+    grid_nn_kernel<4><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+  else if (L == 8)
+    grid_nn_kernel<8><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+  else
+    grid_nn_kernel<16><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
   return hipGetLastError();
 }
 

@@ -36,7 +36,16 @@ constexpr int kNNTile = 16;   // screen sub-tile (one branch per sub-tile)
 constexpr int kNNLds = 512;   // targets per LDS tile (8 KB, double-buffered)
 constexpr int kNNBlock = 256;
 constexpr int kTermsBlock = 256;
-constexpr int kTermsPts = 4;  // sources per terms thread: 4× fewer block partials to reduce
+constexpr int kTermsPtsDefault = 2;  // sources per terms thread (M3D_TERMS_PTS = 1|2|4|8, tuning):
+                                     // 2× fewer block partials for the last block to reduce
+static int terms_pts() {
+  static const int v = [] {
+    const char* e = getenv("M3D_TERMS_PTS");
+    const int k = e ? atoi(e) : kTermsPtsDefault;
+    return (k == 1 || k == 2 || k == 4 || k == 8) ? k : kTermsPtsDefault;
+  }();
+  return v;
+}
 constexpr double kU = 5.9604644775390625e-08;
 
 
@@ -634,13 +643,13 @@ __device__ __forceinline__ void terms_block(
     const double* __restrict__ nrm64, int64_t nt_shard, int64_t off,
     const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
     int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
-    double* __restrict__ partials) {
+    double* __restrict__ partials, int pts) {
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
   double acc[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) acc[k] = 0.0;
-  for (int u = 0; u < kTermsPts; ++u) {
-    const int64_t i = ((int64_t)blockIdx.x * kTermsPts + u) * kTermsBlock + threadIdx.x;
+  for (int u = 0; u < pts; ++u) {
+    const int64_t i = ((int64_t)blockIdx.x * pts + u) * kTermsBlock + threadIdx.x;
     if (i >= ns) break;
     const int64_t key = keys[i];
     int32_t out = -1;
@@ -721,10 +730,10 @@ __global__ __launch_bounds__(kTermsBlock) void terms_kernel(
     const double* __restrict__ nrm64, int64_t nt_shard, int64_t off,
     const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
     int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
-    double* __restrict__ partials) {
+    double* __restrict__ partials, int pts) {
   if (s->done) return;
   terms_block<false>(src64, ns, tgt64, nrm64, nt_shard, off, s, keys, corr, est, c0, c1, c2,
-                     sharded, partials);
+                     sharded, partials, pts);
 }
 
 // ------------------------------------------------------------------------------- reduce
@@ -857,10 +866,10 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
     const double* __restrict__ nrm64, int64_t nt, IcpState* s, const int64_t* __restrict__ keys,
     int32_t* __restrict__ corr, double* partials, int64_t nblocks, double* __restrict__ sums,
-    SolveParams sp) {
+    SolveParams sp, int pts) {
   if (s->done) return;
   terms_block<true>(src64, ns, tgt64, nrm64, nt, 0, s, keys, corr, sp.est, sp.c[0], sp.c[1],
-                    sp.c[2], 0, partials);
+                    sp.c[2], 0, partials, pts);
   __shared__ double red[kReduceGroups][kTermSlots];
   __shared__ int last;
   // the partial went out write-through (sc1): drain it, then one lane takes the ticket
@@ -1081,7 +1090,7 @@ hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hip
   terms_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
       s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, off, s->state, s->keys, s->corr,
       s->params.estimation, s->src->center[0], s->src->center[1], s->src->center[2], sharded,
-      s->partials);
+      s->partials, terms_pts());
   return hipGetLastError();
 }
 
@@ -1116,7 +1125,7 @@ hipError_t launch_icp_terms_solve(const m3d_icp* s, hipStream_t st) {
   }
   terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
       s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
-      s->partials, s->nblocks, s->sums, solve_params(s));
+      s->partials, s->nblocks, s->sums, solve_params(s), terms_pts());
   return hipGetLastError();
 }
 
@@ -1136,7 +1145,7 @@ hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipS
 }
 
 int64_t terms_blocks(int64_t ns) {
-  const int64_t per = (int64_t)kTermsBlock * kTermsPts;
+  const int64_t per = (int64_t)kTermsBlock * terms_pts();
   return ns > 0 ? (ns + per - 1) / per : 1;
 }
 
