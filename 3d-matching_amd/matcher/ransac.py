@@ -53,6 +53,27 @@ def _corr_array(correspondences) -> np.ndarray:
     return c.reshape(-1, 2)
 
 
+def _check_gather(corr: np.ndarray, n_src: int, n_tgt: int) -> None:
+    """numpy fancy-indexing semantics of the reference's gathers (ransac.py:147-148, 226-227):
+    indices in [-n, n) are valid (negatives wrap — the device does the same), anything else
+    raises numpy's IndexError."""
+    for col, n in ((0, n_src), (1, n_tgt)):
+        v = corr[:, col]
+        bad = (v >= n) | (v < -n)
+        if bad.any():
+            raise IndexError(f"index {int(v[np.argmax(bad)])} is out of bounds for axis 0 with size {n}")
+
+
+def _only_in_range(corr: np.ndarray, n_src: int, n_tgt: int) -> np.ndarray:
+    """Rows the reference never reads may hold anything: out-of-range entries → 0 (a copy)."""
+    ok = (corr[:, 0] < n_src) & (corr[:, 0] >= -n_src) & (corr[:, 1] < n_tgt) & (corr[:, 1] >= -n_tgt)
+    if ok.all():
+        return corr
+    c = corr.copy()
+    c[~ok] = 0
+    return c
+
+
 def global_registration(src, tgt, voxel_size: float, iteration: int = 30) -> RegistrationResult:
     """ransac.py:20-59: feature-matching RANSAC (mutual filter, Point-to-Point, ransac_n=3,
     EdgeLength(0.9) + Distance(1.5·v) checkers, RANSACConvergenceCriteria(iteration, 0.999))."""
@@ -90,7 +111,9 @@ def compute_step_transformation(src, tgt, correspondences) -> RegistrationResult
     if n_corres < 3:
         return res
     idxs = np.random.choice(n_corres, 3, replace=False)       # same RNG stream as the reference
-    cs = _cache.corrset(_down_points(src), _down_points(tgt), corres_np)
+    s_pts, t_pts = _down_points(src), _down_points(tgt)
+    _check_gather(corres_np[idxs], len(s_pts), len(t_pts))     # only the sampled rows are read
+    cs = _cache.corrset(s_pts, t_pts, _only_in_range(corres_np, len(s_pts), len(t_pts)))
     T, status = cs.kabsch3(1, triples=np.asarray(idxs, np.int32).reshape(1, 3))
     if int(status[0].item()) == _lib.HYP_OK:
         res.transformation = T[0].cpu().numpy()
@@ -103,7 +126,9 @@ def evaluate_inlier_ratio(src, tgt, correspondences, transform, voxel_size) -> f
     corres = _corr_array(correspondences)
     if len(corres) == 0:
         return 0.0
-    cs = _cache.corrset(_down_points(src), _down_points(tgt), corres)
+    s_pts, t_pts = _down_points(src), _down_points(tgt)
+    _check_gather(corres, len(s_pts), len(t_pts))
+    cs = _cache.corrset(s_pts, t_pts, corres)
     cnt = cs.score(np.asarray(transform, np.float64).reshape(1, 4, 4), dist_thresh, _lib.SCORE_NORM)
     return np.int64(cnt[0].item()) / len(corres)
 
@@ -142,7 +167,9 @@ def run_ransac(src, tgt, correspondences, voxel_size: float = 0.3, max_iter: int
         thr, mode = dist_thresh, _lib.SCORE_NORM
     else:
         raise ValueError("score must be 'fast' or 'norm'")
-    cs = _cache.corrset(_down_points(src), _down_points(tgt), corres)
+    s_pts, t_pts = _down_points(src), _down_points(tgt)
+    _check_gather(corres, len(s_pts), len(t_pts))
+    cs = _cache.corrset(s_pts, t_pts, corres)
     params = RansacParams(max_iter=max_iter, thr=thr, mode=mode, early_stop=early_stop,
                           es_threshold=early_stop_threshold, es_confidence=early_stop_confidence)
     triples = None

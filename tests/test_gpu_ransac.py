@@ -192,8 +192,17 @@ def test_negative_and_out_of_range_indices():
     pts = np.random.default_rng(0).random((10, 3))
     c = np.array([[-1, -1], [0, 0], [1, 1]], dtype=np.int32)  # numpy wraps -1
     assert M.evaluate_inlier_ratio(pts, pts, c, np.eye(4), 0.3) == 1.0
-    with pytest.raises(ValueError):
+    with pytest.raises(IndexError):  # numpy's error, as the reference's gather raises it
         M.evaluate_inlier_ratio(pts, pts, np.array([[0, 10]], np.int32), np.eye(4), 0.3)
+    # compute_step_transformation reads only its 3 sampled rows (ransac.py:143-148): an
+    # out-of-range row elsewhere is harmless, a sampled one raises IndexError
+    bad = np.array([[0, 0], [1, 1], [2, 2], [3, 99]], np.int32)
+    np.random.seed(0)  # choice(4, 3) = [2, 3, 1]: row 3 is sampled
+    with pytest.raises(IndexError):
+        M.compute_step_transformation(pts, pts, bad)
+    np.random.seed(5)  # choice(4, 3) = [0, 1, 2]: row 3 is never read
+    r = M.compute_step_transformation(pts, pts, bad)
+    np.testing.assert_allclose(r.transformation, np.eye(4), atol=1e-9)
 
 
 @pytest.mark.parametrize("nc", [1, 2, 3, 5, 63, 2047, 2048, 2049, 10007])
