@@ -445,7 +445,7 @@ __device__ __forceinline__ void nn_exact_rows(const float4* __restrict__ rows, i
   }
 }
 
-template <int kMG>
+template <int kMG, bool kL32>
 __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restrict__ src32,
                                                           int64_t ns,
                                                           const int32_t* __restrict__ order,
@@ -456,7 +456,8 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           const IcpState* __restrict__ s,
                                                           int64_t* __restrict__ keys,
                                                           uint32_t exp_mask,
-                                                          unsigned long long* __restrict__ stats) {
+                                                          unsigned long long* __restrict__ stats,
+                                                          int strided) {
   // exp_mask: 0xFF always; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
   // (profiling experiment only: the keys are then wrong).  stats (M3D_NN_STATS=1, diagnostics
   // only, else null): [0] flagged (group, sub-tile) steps, [1] all steps.
@@ -518,16 +519,23 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   // the (rare) exact path only (staging them in LDS as well cost the sweep more than it saved).
   static_assert(kMBlock == 2 * kMTile, "one 16-B operand half per thread per tile");
   __shared__ uint4 t16[2][2][kMTile];
+  // kL32 (M3D_NN_LDS32=1): the tile's fp32 coordinates staged in LDS too, for the exact path
+  __shared__ float4 t32s[kL32 ? 2 : 1][kL32 ? kMTile : 1];
   const int sp = threadIdx.x / kMTile, sk = threadIdx.x % kMTile;
-  const int64_t jb = (int64_t)blockIdx.y * slice_len;
-  const int64_t je = min(nt_pad, jb + slice_len);
+  // contiguous slice of slice_len targets per grid.y, or (strided) every gridDim.y-th tile
+  const int64_t tstep = strided ? (int64_t)gridDim.y * kMTile : (int64_t)kMTile;
+  const int64_t jb = strided ? (int64_t)blockIdx.y * kMTile : (int64_t)blockIdx.y * slice_len;
+  const int64_t je = strided ? nt_pad : min(nt_pad, jb + slice_len);
   t16[0][sp][sk] = tgt16[sp * nt_pad + jb + sk];
+  if (kL32 && sp == 0) t32s[0][sk] = tgt32[jb + sk];
   __syncthreads();
   int buf = 0;
-  for (int64_t j0 = jb; j0 < je; j0 += kMTile) {
-    const bool has_next = j0 + kMTile < je;
+  for (int64_t j0 = jb; j0 < je; j0 += tstep) {
+    const bool has_next = j0 + tstep < je;
     uint4 pre;
-    if (has_next) pre = tgt16[sp * nt_pad + j0 + kMTile + sk];
+    if (has_next) pre = tgt16[sp * nt_pad + j0 + tstep + sk];
+    float4 pre32;
+    if (kL32 && has_next && sp == 0) pre32 = tgt32[j0 + tstep + sk];
     // Sweep: MFMA + minimum + threshold test for the tile's 8 sub-tiles, branch-free; a
     // sub-tile that hits anywhere in the wave sets a bit of the wave-uniform mask (SALU).
     // Software-pipelined: the MFMA of step t+1 is issued before the minimum of step t is taken,
@@ -559,7 +567,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
     // barrier path, measured slower: 0.360 vs 0.328 ms per launch at cfg1.)
     hm |= force;
     if (stats != nullptr && lane == 0) {
-      atomicAdd(&stats[0], (unsigned long long)__builtin_popcount(hm & ((1u << (8 * kMG)) - 1u)));
+      atomicAdd(&stats[0], (unsigned long long)__builtin_popcount(hm & (0xFFFFFFFFu >> (32 - 8 * kMG))));
       atomicAdd(&stats[1], (unsigned long long)kSteps);
     }
 #pragma unroll
@@ -569,7 +577,8 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
       while (m8 != 0) {
         const int sub = __builtin_ctz(m8);
         m8 &= m8 - 1;
-        nn_exact_rows(tgt32 + j0 + sub * 32, off, h, qx[g], qy[g], qz[g], best[g], bidx[g]);
+        nn_exact_rows(kL32 ? &t32s[buf][sub * 32] : tgt32 + j0 + sub * 32, off, h, qx[g], qy[g],
+                      qz[g], best[g], bidx[g]);
         const float ob = __shfl_xor(best[g], 32);
         const uint32_t oi = (uint32_t)__shfl_xor((int)bidx[g], 32);
         if (ob < best[g] || (ob == best[g] && oi < bidx[g])) {
@@ -583,6 +592,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
       if (h == 1) bq[g] = bt;  // the threshold only ever tightens: force stays as it was
     }
     if (has_next) t16[buf ^ 1][sp][sk] = pre;
+    if (kL32 && has_next && sp == 0) t32s[buf ^ 1][sk] = pre32;
     __syncthreads();
     buf ^= 1;
   }
@@ -1049,20 +1059,48 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
       return p;
     }();
     if (nn_stats != nullptr) (void)hipMemsetAsync(nn_stats, 0, 2 * sizeof(unsigned long long), st);
+    // grid.y blocks take every S-th target tile instead of a contiguous slice (M3D_NN_STRIDED=0:
+    // slices).  Targets are stored in cell order, so a query block's few candidate tiles are
+    // adjacent: in a contiguous slice they all land in ONE block, whose exact-path work then
+    // sets the kernel's tail; strided, they spread over S blocks (cfg1: 0.334 → 0.305 ms).
+    static const int strided = [] {
+      const char* e = getenv("M3D_NN_STRIDED");
+      return (e && atoi(e) == 0) ? 0 : 1;
+    }();
+    static const bool lds32 = [] {
+      const char* e = getenv("M3D_NN_LDS32");
+      return e && atoi(e) == 1;
+    }();
     const int64_t mq = MG == 4 ? mqueries<4>() : (MG == 2 ? mqueries<2>() : mqueries<1>());
     const dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, kMTile, &slice);
-    if (MG == 4)
-      nn_mfma_kernel<4><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask,
-                                                nn_stats);
-    else if (MG == 2)
-      nn_mfma_kernel<2><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask,
-                                                nn_stats);
-    else
-      nn_mfma_kernel<1><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16, tg->mf32,
-                                                tg->mf_npad, slice, off, s->state, s->keys, exp_mask,
-                                                nn_stats);
+    if (MG == 4) {
+      if (lds32)
+        nn_mfma_kernel<4, true><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
+                                                        tg->mf32, tg->mf_npad, slice, off, s->state,
+                                                        s->keys, exp_mask, nn_stats, strided);
+      else
+        nn_mfma_kernel<4, false><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
+                                                         tg->mf32, tg->mf_npad, slice, off, s->state,
+                                                         s->keys, exp_mask, nn_stats, strided);
+    } else if (MG == 2) {
+      if (lds32)
+        nn_mfma_kernel<2, true><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
+                                                        tg->mf32, tg->mf_npad, slice, off, s->state,
+                                                        s->keys, exp_mask, nn_stats, strided);
+      else
+        nn_mfma_kernel<2, false><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
+                                                         tg->mf32, tg->mf_npad, slice, off, s->state,
+                                                         s->keys, exp_mask, nn_stats, strided);
+    } else {
+      if (lds32)
+        nn_mfma_kernel<1, true><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
+                                                        tg->mf32, tg->mf_npad, slice, off, s->state,
+                                                        s->keys, exp_mask, nn_stats, strided);
+      else
+        nn_mfma_kernel<1, false><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
+                                                         tg->mf32, tg->mf_npad, slice, off, s->state,
+                                                         s->keys, exp_mask, nn_stats, strided);
+    }
     if (nn_stats != nullptr) {
       unsigned long long h[2] = {0, 0};
       if (hipMemcpyAsync(h, nn_stats, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
