@@ -441,8 +441,13 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   const int64_t max_iter = p->max_iter;
   int64_t B = p->batch;
   if (B <= 0) {
-    // ~1e9 pair evaluations per batch amortise the per-batch launches; early stop caps it
-    B = nc > 0 ? std::max<int64_t>(1024, (int64_t)1e9 / std::max<int64_t>(nc, 1)) : 1024;
+    // ~1e10 pair evaluations per batch (≤ 2^18 hypotheses, ~80 MB of scratch) amortise the
+    // per-batch kabsch3/select latency and give the scoring grid more blocks (cfg2, 1e5
+    // hypotheses: 10k per batch 2.15 ms, 25k 1.66 ms, 100k 1.55 ms — tools/ransac_batch.py);
+    // early stop caps it (the stop is decided per batch)
+    B = nc > 0 ? std::max<int64_t>(1024, std::min<int64_t>((int64_t)1 << 18,
+                                                           (int64_t)1e10 / std::max<int64_t>(nc, 1)))
+               : 1024;
     if (p->early_stop) B = std::min<int64_t>(B, 16384);
   }
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(max_iter, 1)));

@@ -23,6 +23,8 @@
 // The multi-GPU paths use the same pieces as separate launches (terms_kernel, reduce_kernel,
 // solve_kernel) with the RCCL MIN on keys / SUM on the 32 term slots between them.
 #include <float.h>
+
+#include <algorithm>
 #include <stdlib.h>
 
 #include "linalg.h"
@@ -1067,12 +1069,45 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
       const char* e = getenv("M3D_NN_STRIDED");
       return (e && atoi(e) == 0) ? 0 : 1;
     }();
+    static const bool fill = [] {
+      const char* e = getenv("M3D_NN_FILL");
+      return !(e && atoi(e) == 0);
+    }();
     static const bool lds32 = [] {
       const char* e = getenv("M3D_NN_LDS32");
       return e && atoi(e) == 1;
     }();
     const int64_t mq = MG == 4 ? mqueries<4>() : (MG == 2 ? mqueries<2>() : mqueries<1>());
-    const dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, kMTile, &slice);
+    dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, kMTile, &slice);
+    if (strided && fill) {
+      // Strided tiles decouple grid.y from slice boundaries: pick S in [S0, 2·S0] so that the
+      // block count fills the resident block slots in whole rounds (the last partial round of
+      // equal-length blocks idles the rest of the chip: 196 × 11 blocks on 512 slots = 4.2
+      // rounds ran as 5).
+      static const int64_t slots = [] {
+        int dev = 0, per = 0;
+        hipDeviceProp_t p;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, nn_mfma_kernel<kMGDefault, false>, kMBlock, 0) != hipSuccess)
+          return (int64_t)0;
+        return (int64_t)p.multiProcessorCount * (per > 0 ? per : 1);
+      }();
+      const int64_t bx = gm.x, ntiles = tg->mf_npad / kMTile;
+      if (slots > 0 && ntiles > 1) {
+        int64_t s0 = std::min<int64_t>(std::max<int64_t>((2048 + bx - 1) / bx, 1), ntiles);
+        int64_t best = s0;
+        double best_eff = 0.0;
+        for (int64_t S = s0; S <= std::min<int64_t>(2 * s0, ntiles); ++S) {
+          const int64_t blocks = bx * S, rounds = (blocks + slots - 1) / slots;
+          const double eff = (double)blocks / (double)(rounds * slots);
+          if (eff > best_eff + 1e-9) {
+            best_eff = eff;
+            best = S;
+          }
+        }
+        gm.y = (unsigned)best;
+      }
+    }
     if (MG == 4) {
       if (lds32)
         nn_mfma_kernel<4, true><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,

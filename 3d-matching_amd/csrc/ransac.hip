@@ -545,20 +545,25 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   __shared__ uint32_t qn;                 // guard-band queue: entries used
   __shared__ uint2 qbuf[kSQueue];         // (correspondence, hypothesis | screen sign << 31)
   if (threadIdx.x == 0) qn = 0;
-  const int64_t jb = (int64_t)blockIdx.y * slice_len;
-  const int64_t je = min(nc_pad, jb + slice_len);
+  // grid.y block y visits every gridDim.y-th correspondence tile (slice_len = 0) or a contiguous
+  // slice of slice_len rows
+  const int64_t tstep = slice_len == 0 ? (int64_t)gridDim.y * kSTile : (int64_t)kSTile;
+  const int64_t jb = slice_len == 0 ? (int64_t)blockIdx.y * kSTile : (int64_t)blockIdx.y * slice_len;
+  const int64_t je = slice_len == 0 ? nc_pad : min(nc_pad, jb + slice_len);
   const int p0 = threadIdx.x / kSTile, k0 = threadIdx.x % kSTile;  // planes p0 and p0 + 2
 #pragma unroll
   for (int u = 0; u < 2; ++u) a16[0][p0 + 2 * u][k0] = ca16[(p0 + 2 * u) * nc_pad + jb + k0];
   __syncthreads();
   int buf = 0;
   const int pa = h == 0 ? 0 : 1;  // planes read by this lane for x, y, z: pa·(1 + comp)
-  for (int64_t j0 = jb; j0 < je; j0 += kSTile) {
-    const bool has_next = j0 + kSTile < je;
+  uint32_t tiles_seen = 0;
+  for (int64_t j0 = jb; j0 < je; j0 += tstep) {
+    ++tiles_seen;
+    const bool has_next = j0 + tstep < je;
     uint4 pre[2];
     if (has_next) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) pre[u] = ca16[(p0 + 2 * u) * nc_pad + j0 + kSTile + k0];
+      for (int u = 0; u < 2; ++u) pre[u] = ca16[(p0 + 2 * u) * nc_pad + j0 + tstep + k0];
     }
 #pragma unroll 2
     for (int sub = 0; sub < kSTile / 32; ++sub) {
@@ -627,7 +632,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
     buf ^= 1;
   }
   // inliers of hypothesis column c over this slice: rows − outliers, the two lane halves summed
-  const uint32_t rows = (uint32_t)(je - jb) / 2;  // each lane half sees half of every 32-row block
+  const uint32_t rows = tiles_seen * (kSTile / 2);  // each lane half sees half of every 32-row block
 #pragma unroll
   for (int g = 0; g < kSMG; ++g) {
     const uint32_t in = 2 * rows - (outl[g] + (uint32_t)__shfl_xor((int)outl[g], 32));
@@ -888,13 +893,34 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
     }();
     const int64_t hp = score_mf_hpad(H);
     const int64_t bx = hp / (MG == 4 ? shyps<4>() : (MG == 2 ? shyps<2>() : shyps<1>()));
-    // correspondence slices over grid.y so that ≥ ~2048 blocks fill the chip
-    int64_t sy = (2048 + bx - 1) / bx;
+    // correspondence tiles over grid.y so that ≥ ~2048 blocks fill the chip: block y visits
+    // every sy-th tile (slice 0), sy chosen in [S0, 2·S0] to fill the resident block slots in
+    // whole rounds (20 × 98 contiguous slices = 3.8 rounds of 512 slots ran as 4)
     const int64_t tiles = cs->nc_pad / kSTile;
-    if (sy > tiles) sy = tiles;
-    if (sy < 1) sy = 1;
-    const int64_t slice = (tiles + sy - 1) / sy * kSTile;
-    sy = (cs->nc_pad + slice - 1) / slice;
+    int64_t sy = std::min<int64_t>(std::max<int64_t>((2048 + bx - 1) / bx, 1), tiles);
+    {
+      static const int64_t slots = [] {
+        int dev = 0, per = 0;
+        hipDeviceProp_t p;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, score_mfma_kernel<kSMGDefault>, kSBlock, 0) != hipSuccess)
+          return (int64_t)0;
+        return (int64_t)p.multiProcessorCount * (per > 0 ? per : 1);
+      }();
+      if (slots > 0) {
+        const int64_t s0 = sy;
+        double best_eff = 0.0;
+        for (int64_t S = s0; S <= std::min<int64_t>(2 * s0, tiles); ++S) {
+          const int64_t blocks = bx * S, rounds = (blocks + slots - 1) / slots;
+          const double eff = (double)blocks / (double)(rounds * slots);
+          if (eff > best_eff + 1e-9) {
+            best_eff = eff;
+            sy = S;
+          }
+        }
+      }
+    }
+    const int64_t slice = 0;  // strided tiles
     const float T2 = (float)(cs->s16 * cs->s16 * thr_sq);
     static const float band_on = [] {
       const char* e = getenv("M3D_SCORE_EXP");

@@ -176,6 +176,18 @@ class CorrSet:
         return RansacOutcome(np.array(res.T[:]).reshape(4, 4), res.fitness, res.best_index,
                              res.iterations, res.best_count, self.nc)
 
+    def run_async(self, params: "RansacParams", result, triples=None) -> None:
+        """a4 enqueued on the current stream, no host sync: the m3d_ransac_result lands in
+        `result` (a cuda int64 tensor of RESULT_WORDS elements; best_index = result[17],
+        best_count = result[19]).  Read it with RansacOutcome.from_device."""
+        p = params.to_c()
+        tri = None if triples is None else to_device(triples, "int32", (3,))
+        self.ctx.check(self.ctx.lib.m3d_ransac_run_async(self.ctx.h, self.h, C.byref(p), ptr(tri), None,
+                                                         ptr(result), stream_handle()), "ransac_run_async")
+
+
+RESULT_WORDS = C.sizeof(_lib.RansacResult) // 8  # m3d_ransac_result as int64 words
+
 
 @dataclass
 class RansacParams:
@@ -203,6 +215,14 @@ class RansacOutcome:
     iterations: int
     best_count: int
     n_correspondences: int
+
+    @staticmethod
+    def from_device(result, nc: int) -> "RansacOutcome":
+        """Decode the m3d_ransac_result written by CorrSet.run_async (synchronises)."""
+        raw = result.detach().cpu().numpy().astype(np.int64).tobytes()
+        r = _lib.RansacResult.from_buffer_copy(raw[:C.sizeof(_lib.RansacResult)])
+        return RansacOutcome(np.array(r.T[:]).reshape(4, 4), r.fitness, r.best_index, r.iterations,
+                             r.best_count, nc)
 
 
 def replay_triples(nc: int, H: int, state=None):

@@ -234,13 +234,16 @@ def main():
         params = RansacParams(max_iter=H, seed=42, thr=thr, mode=_lib.SCORE_NORM, early_stop=False,
                               hyp0=rank * H)
 
+        from m3d.core import RESULT_WORDS, RansacOutcome
+        res_buf = torch.zeros(RESULT_WORDS, dtype=torch.int64, device=dev)
+
         def ransac_run():
-            out = cs.run(params)
-            if world > 1:
-                key = torch.tensor([out.best_count * (1 << 32) + (0xFFFFFFFF - (rank * H + out.best_index))],
-                                   dtype=torch.int64, device=dev)
+            # enqueued without a host round trip (m3d_ransac_run_async): runs go back to back
+            cs.run_async(params, res_buf)
+            if world > 1:  # best over ranks: highest count, lowest global id (device-side key)
+                key = (res_buf[19:20] * (1 << 32) + (0xFFFFFFFF - (rank * H + res_buf[17:18])))
                 dist.all_reduce(key, op=dist.ReduceOp.MAX)
-            return out
+            return res_buf
 
         ransac_run()
         torch.cuda.synchronize()
@@ -260,7 +263,7 @@ def main():
             sc = ctx.profile_read(_lib.KERNEL_SCORE)
             kb = ctx.profile_read(_lib.KERNEL_KABSCH)
             ctx.profile(False)
-            return el, sc, kb, out
+            return el, sc, kb, RansacOutcome.from_device(out, nc)
 
         rel, _, _, out = ransac_timed(False)  # value: no events on the stream
         rel_ev, (sc_ms, sc_n), (kb_ms, kb_n), _ = ransac_timed(True)  # kernel durations

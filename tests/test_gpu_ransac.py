@@ -281,3 +281,24 @@ def test_score_edge_transforms_exact():
                       (_lib.SCORE_NORM, 50.0), (_lib.SCORE_SQUARED, 1e-12)):
         got = cs.score(Ts, thr, mode).cpu().numpy()
         np.testing.assert_array_equal(got, O.inlier_counts(p, q, Ts, thr, mode))
+
+
+@pytest.mark.parametrize("early_stop", [True, False])
+def test_run_async_matches_run(early_stop):
+    """m3d_ransac_run_async (no host round trip; bench.py enqueues runs back to back) gives the
+    synchronous run's outcome bit for bit, batches of 2^18 included."""
+    import torch
+
+    from m3d import synth
+    from m3d.core import RESULT_WORDS, RansacOutcome
+
+    src, tgt, corr, _ = synth.ransac_pair(20000, seed=3, noise_ratio=1.0)
+    cs = CorrSet(src, tgt, corr)
+    p = RansacParams(max_iter=3000, seed=7, thr=THR, mode=_lib.SCORE_NORM, early_stop=early_stop)
+    a = cs.run(p)
+    buf = torch.zeros(RESULT_WORDS, dtype=torch.int64, device="cuda")
+    cs.run_async(p, buf)
+    b = RansacOutcome.from_device(buf, cs.nc)
+    assert (a.best_index, a.iterations, a.best_count) == (b.best_index, b.iterations, b.best_count)
+    np.testing.assert_array_equal(a.transformation, b.transformation)
+    assert a.fitness == b.fitness
