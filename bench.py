@@ -101,8 +101,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # M3D_BENCH_SAME_DEVICE=1 + M3D_BENCH_BACKEND=gloo: every rank on cuda:0 over gloo — a
+        # functional rehearsal of the N > 1 path on a one-GPU box (tools/gpu_multi_rehearsal.sh);
+        # the real runs are one rank per GPU over RCCL ("nccl")
+        same = os.environ.get("M3D_BENCH_SAME_DEVICE") == "1"
+        backend = os.environ.get("M3D_BENCH_BACKEND", "nccl")
+        torch.cuda.set_device(0 if same else local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", 0 if same else local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
