@@ -685,6 +685,15 @@ __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict_
                                                       double es_conf,
                                                       const double* __restrict__ T_batch,
                                                       RansacState* __restrict__ rs) {
+  // The batch in chunks of 1024 × kSelPer counts, staged into LDS with coalesced loads (thread t
+  // owns the contiguous run [t·kSelPer, (t+1)·kSelPer) of the chunk): per-thread first-max,
+  // inclusive block scan with the first-max combine, the running best carried from chunk to
+  // chunk, and — early stop — each thread walks its run from its prefix and the first stopping
+  // iteration is a block min.  Same result as a sequential walk; per-thread contiguous segments
+  // of the whole batch read straight from memory were uncoalesced (81 µs at 1e5 counts).
+  constexpr int kSelPer = 8;
+  constexpr int kChunk = 1024 * kSelPer;
+  __shared__ int32_t cbuf[kChunk];
   __shared__ int64_t sc[1024], si[1024];
   __shared__ int64_t stop_s[1024];
   __shared__ int32_t done_s;
@@ -692,59 +701,65 @@ __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict_
   if (t == 0) done_s = rs->done;
   __syncthreads();
   if (done_s) return;
-  const int64_t seg = (n + 1023) / 1024;
-  const int64_t b = (int64_t)t * seg, e = min(n, b + seg);
-  BestPair loc{-1, -1};
-  for (int64_t i = b; i < e; ++i) loc = combine(loc, BestPair{counts[i], h_begin + i});
-  sc[t] = loc.c;
-  si[t] = loc.i;
-  __syncthreads();
-  // inclusive Hillis-Steele scan of (count, index) with the first-max combine
-  for (int off = 1; off < 1024; off <<= 1) {
-    BestPair v{sc[t], si[t]};
-    if (t >= off) v = combine(BestPair{sc[t - off], si[t - off]}, v);
+  BestPair carry{rs->best_count, rs->best_index};  // running best before the current chunk
+  int64_t first_stop = INT64_MAX;
+  BestPair fin = carry;
+  bool writer = false;
+  for (int64_t c0 = 0; c0 < n; c0 += kChunk) {
+    const int m = (int)min((int64_t)kChunk, n - c0);
+    for (int k = t; k < m; k += 1024) cbuf[k] = counts[c0 + k];
     __syncthreads();
-    sc[t] = v.c;
-    si[t] = v.i;
+    const int b = t * kSelPer, e = min(m, b + kSelPer);
+    BestPair loc{-1, -1};
+    for (int k = b; k < e; ++k) loc = combine(loc, BestPair{cbuf[k], h_begin + c0 + k});
+    sc[t] = loc.c;
+    si[t] = loc.i;
     __syncthreads();
-  }
-  BestPair carry{rs->best_count, rs->best_index};
-  if (t > 0) carry = combine(carry, BestPair{sc[t - 1], si[t - 1]});
-  // second pass: walk own segment with the running best, find first early-stop iteration
-  int64_t stop = INT64_MAX;
-  BestPair at_stop = carry;
-  BestPair cur = carry;
-  if (early) {
-    for (int64_t i = b; i < e; ++i) {
-      cur = combine(cur, BestPair{counts[i], h_begin + i});
-      const double fit = (double)cur.c / (double)nc;
-      if (fit > es_thr) {
-        const int64_t it = h_begin + i + 1;
-        if (it >= required_iters(fit, es_conf, max_iter)) {
-          stop = i;
-          at_stop = cur;
-          break;
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+      BestPair v{sc[t], si[t]};
+      if (t >= off) v = combine(BestPair{sc[t - off], si[t - off]}, v);
+      __syncthreads();
+      sc[t] = v.c;
+      si[t] = v.i;
+      __syncthreads();
+    }
+    if (early) {
+      BestPair cur = carry;
+      if (t > 0) cur = combine(carry, BestPair{sc[t - 1], si[t - 1]});
+      int64_t stop = INT64_MAX;
+      BestPair at_stop = cur;
+      for (int k = b; k < e; ++k) {
+        cur = combine(cur, BestPair{cbuf[k], h_begin + c0 + k});
+        const double fit = (double)cur.c / (double)nc;
+        if (fit > es_thr) {
+          const int64_t it = h_begin + c0 + k + 1;
+          if (it >= required_iters(fit, es_conf, max_iter)) {
+            stop = c0 + k;
+            at_stop = cur;
+            break;
+          }
         }
       }
+      stop_s[t] = stop;
+      __syncthreads();
+      for (int w = 512; w > 0; w >>= 1) {
+        if (t < w) stop_s[t] = min(stop_s[t], stop_s[t + w]);
+        __syncthreads();
+      }
+      first_stop = stop_s[0];
+      if (first_stop != INT64_MAX) {
+        writer = (stop == first_stop);
+        fin = at_stop;
+        break;  // uniform: every thread read the same stop_s[0]
+      }
     }
+    carry = combine(carry, BestPair{sc[1023], si[1023]});
+    __syncthreads();  // before the next chunk overwrites cbuf / sc / stop_s
   }
-  stop_s[t] = stop;
-  __syncthreads();
-  for (int w = 512; w > 0; w >>= 1) {
-    if (t < w) stop_s[t] = min(stop_s[t], stop_s[t + w]);
-    __syncthreads();
+  if (first_stop == INT64_MAX) {
+    writer = (t == 0);
+    fin = carry;
   }
-  const int64_t first_stop = stop_s[0];
-  BestPair fin;
-  bool writer;
-  if (first_stop != INT64_MAX) {
-    writer = (stop == first_stop);
-    fin = at_stop;
-  } else {
-    writer = (t == 1023);
-    fin = combine(BestPair{rs->best_count, rs->best_index}, BestPair{sc[1023], si[1023]});
-  }
-  __syncthreads();
   if (writer) {
     if (fin.i != rs->best_index && fin.i >= h_begin) {
       for (int k = 0; k < 16; ++k) rs->T_best[k] = T_batch[16 * (fin.i - h_begin) + k];
