@@ -701,6 +701,39 @@ __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict_
   if (t == 0) done_s = rs->done;
   __syncthreads();
   if (done_s) return;
+  if (!early) {
+    // no stop to find: the batch's best is an order-free reduction under (count desc, index
+    // asc) — the first strict improvement of the sequential walk — with coalesced strided loads
+    BestPair loc{-1, -1};
+    for (int64_t k = t; k < n; k += 1024) {
+      const BestPair v{counts[k], h_begin + k};
+      if (v.c > loc.c || (v.c == loc.c && v.i < loc.i)) loc = v;
+    }
+    sc[t] = loc.c;
+    si[t] = loc.i;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+      if (t < w) {
+        const BestPair a{sc[t], si[t]}, b{sc[t + w], si[t + w]};
+        if (b.c > a.c || (b.c == a.c && b.i < a.i && b.c >= 0)) {
+          sc[t] = b.c;
+          si[t] = b.i;
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      const BestPair fin = combine(BestPair{rs->best_count, rs->best_index}, BestPair{sc[0], si[0]});
+      if (fin.i != rs->best_index && fin.i >= h_begin) {
+        for (int k = 0; k < 16; ++k) rs->T_best[k] = T_batch[16 * (fin.i - h_begin) + k];
+      }
+      rs->best_count = fin.c;
+      rs->best_index = fin.i;
+      rs->iterations = h_begin + n;
+      if (rs->iterations >= max_iter) rs->done = 1;
+    }
+    return;
+  }
   BestPair carry{rs->best_count, rs->best_index};  // running best before the current chunk
   int64_t first_stop = INT64_MAX;
   BestPair fin = carry;
