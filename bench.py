@@ -6,9 +6,12 @@ BASELINE.json metric "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pt
 * step (the timed unit) = one full cfg1 ICP run: 100k source ↔ 100k target points per GPU,
   50 point-to-plane iterations (convergence disabled → exactly 50 updates, 51 NN evaluations),
   brute-force radius-bounded NN (r = 0.4·0.3), fp64 terms/solve, all device resident.
-  value = ICP iterations/s summed over ranks (each rank's 100k-target shard is one 100k×100k
-  block; N>1 shards the target over ranks with RCCL MIN on the packed NN keys and SUM on the
-  32 estimation terms per iteration → weak scaling).
+  value = ICP iterations/s summed over ranks (each rank does one 100k×100k block per
+  iteration; N>1 is weak scaling).  N>1 follows the north-star's rule: the TARGET is sharded
+  (100k targets per rank, sources replicated, RCCL MIN of the packed NN keys + SUM of the 32
+  estimation terms per iteration — the cfg3 protocol) only when the cloud would not fit one
+  GPU's HBM; otherwise the sources are sharded (100k per rank) against the replicated target
+  with one RCCL SUM of the terms per iteration.  `--shard target|source` forces either.
 * "ransac": cfg2 — benchmark_ransac.py's loop (a1 sample + Kabsch, a2 ‖d‖ < 1.5·v scoring) at
   Nc = 1e5, H = 1e5 hypotheses per GPU, counter sampler seed 42, no early stop; N>1 shards the
   hypothesis ids and all-reduces MAX of the packed (count, ~id) best key.  Its roofline prices
@@ -69,9 +72,11 @@ def parse():
     ap.add_argument("--ransac-steps", type=int, default=3)
     ap.add_argument("--no-ransac", action="store_true")
     ap.add_argument("--no-grid", action="store_true")
-    ap.add_argument("--shard", choices=["target", "source"], default="target",
-                    help="N>1 ICP sharding: target (north-star: RCCL MIN keys + SUM terms) or "
-                         "source (target replicated, SUM terms only)")
+    ap.add_argument("--shard", choices=["auto", "target", "source"], default="auto",
+                    help="N>1 ICP sharding: target (RCCL MIN of the NN keys + SUM of the terms), "
+                         "source (target replicated, SUM of the terms only), or auto: the "
+                         "north-star's rule -- shard the target only when it would not fit one "
+                         "GPU's HBM budget (M3D_TARGET_SHARD_BYTES, default 64 GiB), else source")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline leg")
     return ap.parse_args()
@@ -134,6 +139,12 @@ def main():
     # ------------------------------------------------------------------ cfg1: ICP
     ns, nt, iters = args.ns, args.nt, args.icp_iters
     r = 0.4 * 0.3
+    if args.shard == "auto":
+        # north_star: "shards the target cloud ... with an RCCL all-reduce of per-shard
+        # (min_dist, argmin) ... only for clouds large enough to saturate one GPU's HBM"; a
+        # replicated cloud costs 64 B per point
+        budget = float(os.environ.get("M3D_TARGET_SHARD_BYTES", 64 * 2**30))
+        args.shard = "target" if 64.0 * nt * world > budget else "source"
     source_shard = world > 1 and args.shard == "source"
     if source_shard:  # weak scaling: ns sources per rank against the whole (replicated) target
         src_all, tgt_all, nrm_all, T_true = synth.icp_pair(ns * world, nt, seed=0)
