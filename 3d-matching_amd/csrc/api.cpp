@@ -832,6 +832,15 @@ int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* keys, double* su
   hipStream_t st = S(stream);
   if (keys && keys != s->keys)
     HIPX(ctx, hipMemcpyAsync(s->keys, keys, sizeof(int64_t) * s->src->n, hipMemcpyDeviceToDevice, st));
+  static const bool fused = [] {
+    const char* e = getenv("M3D_ICP_FUSED");
+    return !(e && atoi(e) == 0);
+  }();
+  if (fused) {  // terms + fixed-order reduce in one launch (same bits as the two kernels)
+    KTimer kt(ctx, M3D_KERNEL_TERMS, st);
+    HIPX(ctx, launch_icp_terms_reduce(s, off, sums, st));
+    return M3D_OK;
+  }
   { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, off, 1, st)); }
   HIPX(ctx, launch_icp_reduce(s, sums, st));
   return M3D_OK;

@@ -878,10 +878,12 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
     const double* __restrict__ nrm64, int64_t nt, IcpState* s, const int64_t* __restrict__ keys,
     int32_t* __restrict__ corr, double* partials, int64_t nblocks, double* __restrict__ sums,
-    SolveParams sp, int pts) {
+    SolveParams sp, int pts, int64_t off, int sharded, int do_solve) {
+  // do_solve = 0: the sharded tail (m3d_icp_shard_terms) — terms + the fixed-order reduce into
+  // `sums` in one launch; the caller all-reduces them and runs m3d_icp_solve
   if (s->done) return;
-  terms_block<true>(src64, ns, tgt64, nrm64, nt, 0, s, keys, corr, sp.est, sp.c[0], sp.c[1],
-                    sp.c[2], 0, partials, pts);
+  terms_block<true>(src64, ns, tgt64, nrm64, nt, off, s, keys, corr, sp.est, sp.c[0], sp.c[1],
+                    sp.c[2], sharded, partials, pts);
   __shared__ double red[kReduceGroups][kTermSlots];
   __shared__ int last;
   // the partial went out write-through (sc1): drain it, then one lane takes the ticket
@@ -932,7 +934,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
   __syncthreads();
   if (threadIdx.x < kWave) {
     if (threadIdx.x == 0) s->ticket = 0;
-    solve_state(red[0], s, sp);
+    if (do_solve) solve_state(red[0], s, sp);
   }
 }
 
@@ -1184,6 +1186,19 @@ static SolveParams solve_params(const m3d_icp* s) {
   return sp;
 }
 
+// sharded tail: terms (sharded semantics, shard offset off) + reduce into sums, one launch
+hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, hipStream_t st) {
+  const int64_t ns = s->src->n;
+  if (ns == 0) {
+    hipError_t e = launch_icp_terms_mode(s, off, 1, st);
+    return e == hipSuccess ? launch_icp_reduce(s, sums, st) : e;
+  }
+  terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
+      s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
+      s->partials, s->nblocks, sums, solve_params(s), terms_pts(), off, 1, 0);
+  return hipGetLastError();
+}
+
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st) {
   solve_kernel<<<1, 64, 0, st>>>(sums, s->state, solve_params(s));
   return hipGetLastError();
@@ -1198,7 +1213,7 @@ hipError_t launch_icp_terms_solve(const m3d_icp* s, hipStream_t st) {
   }
   terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
       s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
-      s->partials, s->nblocks, s->sums, solve_params(s), terms_pts());
+      s->partials, s->nblocks, s->sums, solve_params(s), terms_pts(), (int64_t)0, 0, 1);
   return hipGetLastError();
 }
 

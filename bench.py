@@ -173,9 +173,9 @@ def main():
                 loop.steps(iters + 1)  # the library enqueues the 51 iterations natively
                 return
             for _ in range(iters + 1):
-                if source_shard:
-                    loop.shard_nn(0, keys)
-                    loop.shard_terms(0, keys, sums)
+                if source_shard:  # keys stay inside the loop object: no copies
+                    loop.shard_nn(0, None)
+                    loop.shard_terms(0, None, sums)
                     dist.all_reduce(sums, op=dist.ReduceOp.SUM)
                     loop.solve(sums)
                 else:
