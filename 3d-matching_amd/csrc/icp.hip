@@ -296,7 +296,9 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMGDefault = 2;  // 32-query groups per wave (M3D_NN_MG = 1|2|4 overrides, tuning)
-constexpr int kMTile = 256;   // targets per LDS tile: fp16 operands 8 KB + fp32 coordinates 4 KB
+constexpr int kMTile = 256;   // targets per half tile (8 sub-tiles of 32)
+constexpr int kTHDefault = 1; // half tiles per LDS tile (M3D_NN_TH = 1 | 2; 2 measured 0.312 vs 0.290 ms: spills)
+constexpr int kMTilePad = 512;  // MFMA operand arrays are padded to a multiple of every tile size
 constexpr int kMBlock = 512;  // 8 waves × kMG × 32 = 512 queries per block: every target tile
                               // staged in LDS serves 512 queries (L2→LDS traffic per pair halved)
 template <int kMG>
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(256) void pack16_sorted_kernel(const float4* __rest
 
 hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st) {
   const int64_t n = c->n;
-  const int64_t n_pad = std::max<int64_t>((n + kMTile - 1) / kMTile * kMTile, kMTile);
+  const int64_t n_pad = std::max<int64_t>((n + kMTilePad - 1) / kMTilePad * kMTilePad, kMTilePad);
   hipError_t e = hipMalloc(&g->mf16, sizeof(uint4) * 2 * n_pad);
   if (e == hipSuccess) e = hipMalloc(&g->mf32, sizeof(float4) * n_pad);
   if (e != hipSuccess) return e;
@@ -447,7 +449,7 @@ __device__ __forceinline__ void nn_exact_rows(const float4* __restrict__ rows, i
   }
 }
 
-template <int kMG, bool kL32>
+template <int kMG, int kTH>
 __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restrict__ src32,
                                                           int64_t ns,
                                                           const int32_t* __restrict__ order,
@@ -457,10 +459,10 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           int64_t off,
                                                           const IcpState* __restrict__ s,
                                                           int64_t* __restrict__ keys,
-                                                          uint32_t exp_mask,
+                                                          uint64_t exp_mask,
                                                           unsigned long long* __restrict__ stats,
                                                           int strided) {
-  // exp_mask: 0xFF always; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
+  // exp_mask: all ones; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
   // (profiling experiment only: the keys are then wrong).  stats (M3D_NN_STATS=1, diagnostics
   // only, else null): [0] flagged (group, sub-tile) steps, [1] all steps.
   if (s->done) return;
@@ -515,72 +517,86 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   }
   const floatx16 zacc = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
                          0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  // [buffer][lane half][target]: a half-wave's 32 ds_read_b128 hit 32 consecutive 16-B slots.
-  // Thread t stages element plane t / kMTile of target t % kMTile (mf16 is stored as two
-  // planes, so the loads are coalesced).  The fp32 coordinates are read from global memory by
-  // the (rare) exact path only (staging them in LDS as well cost the sweep more than it saved).
-  static_assert(kMBlock == 2 * kMTile, "one 16-B operand half per thread per tile");
-  __shared__ uint4 t16[2][2][kMTile];
-  // kL32 (M3D_NN_LDS32=1): the tile's fp32 coordinates staged in LDS too, for the exact path
-  __shared__ float4 t32s[kL32 ? 2 : 1][kL32 ? kMTile : 1];
-  const int sp = threadIdx.x / kMTile, sk = threadIdx.x % kMTile;
+  // Tiles of kTH × 256 targets, [buffer][lane half][target]: a half-wave's 32 ds_read_b128 hit
+  // 32 consecutive 16-B slots.  Thread t stages kTH elements (e = t + u·512: plane e / kTT, target
+  // e % kTT; mf16 is stored as two planes, so the loads are coalesced).  The sweep runs the tile
+  // in halves of 8 sub-tiles (8 A-operand registers live), one barrier per tile.  The fp32
+  // coordinates are read from global memory by the (rare) exact path only.
+  constexpr int kTT = kTH * kMTile;
+  constexpr int kSub = kTT / 32;                  // sub-tiles per tile
+  constexpr uint64_t kGMask = (kSub == 64) ? ~0ull : ((1ull << kSub) - 1ull);
+  static_assert(kMBlock == 2 * kMTile, "one 16-B operand half per thread per half tile");
+  static_assert(kSub * kMG <= 64, "hit mask holds every (group, sub-tile)");
+  __shared__ uint4 t16[2][2][kTT];
   // contiguous slice of slice_len targets per grid.y, or (strided) every gridDim.y-th tile
-  const int64_t tstep = strided ? (int64_t)gridDim.y * kMTile : (int64_t)kMTile;
-  const int64_t jb = strided ? (int64_t)blockIdx.y * kMTile : (int64_t)blockIdx.y * slice_len;
+  const int64_t tstep = strided ? (int64_t)gridDim.y * kTT : (int64_t)kTT;
+  const int64_t jb = strided ? (int64_t)blockIdx.y * kTT : (int64_t)blockIdx.y * slice_len;
   const int64_t je = strided ? nt_pad : min(nt_pad, jb + slice_len);
-  t16[0][sp][sk] = tgt16[sp * nt_pad + jb + sk];
-  if (kL32 && sp == 0) t32s[0][sk] = tgt32[jb + sk];
+#pragma unroll
+  for (int u = 0; u < kTH; ++u) {
+    const int e = threadIdx.x + u * kMBlock;
+    t16[0][e / kTT][e % kTT] = tgt16[(e / kTT) * nt_pad + jb + e % kTT];
+  }
+  uint64_t force64 = 0;
+#pragma unroll
+  for (int g = 0; g < kMG; ++g)
+    if ((force >> (g * 8)) & 1u) force64 |= kGMask << (g * kSub);
   __syncthreads();
   int buf = 0;
   for (int64_t j0 = jb; j0 < je; j0 += tstep) {
     const bool has_next = j0 + tstep < je;
-    uint4 pre;
-    if (has_next) pre = tgt16[sp * nt_pad + j0 + tstep + sk];
-    float4 pre32;
-    if (kL32 && has_next && sp == 0) pre32 = tgt32[j0 + tstep + sk];
-    // Sweep: MFMA + minimum + threshold test for the tile's 8 sub-tiles, branch-free; a
-    // sub-tile that hits anywhere in the wave sets a bit of the wave-uniform mask (SALU).
-    // Software-pipelined: the MFMA of step t+1 is issued before the minimum of step t is taken,
-    // so a wave never waits on its own MFMA result (two accumulator sets live).
-    uint32_t hm = 0;
-    constexpr int kSteps = (kMTile / 32) * kMG;  // (sub-tile, group) steps of this tile
-    H8 av[kMTile / 32];
+    uint4 pre[kTH];
+    if (has_next) {
 #pragma unroll
-    for (int sub = 0; sub < kMTile / 32; ++sub) av[sub].u = t16[buf][h][sub * 32 + c];
-    floatx16 kc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0].h, bq[0], zacc, 0, 0, 0);
+      for (int u = 0; u < kTH; ++u) {
+        const int e = threadIdx.x + u * kMBlock;
+        pre[u] = tgt16[(e / kTT) * nt_pad + j0 + tstep + e % kTT];
+      }
+    }
+    // Sweep: MFMA + sign-OR test for the tile's sub-tiles, branch-free; a sub-tile that hits
+    // anywhere in the wave sets a bit of the wave-uniform mask (SALU).  Software-pipelined: the
+    // MFMA of step t+1 is issued before step t's tree, so a wave never waits on its own MFMA.
+    uint64_t hm = 0;
+    constexpr int kSteps = 8 * kMG;  // (sub-tile, group) steps of one half tile
 #pragma unroll
-    for (int t = 0; t < kSteps; ++t) {
-      floatx16 kn;
-      if (t + 1 < kSteps)
-        kn = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[(t + 1) / kMG].h, bq[(t + 1) % kMG], zacc, 0, 0, 0);
-      // keep the pipeline the source states: without this fence the scheduler sinks each
-      // MFMA next to its consumer (same accumulator registers, the VALU then waits out the
-      // whole MFMA latency every step and the matrix pipe idles under the minimum tree)
-      __builtin_amdgcn_sched_barrier(0);
-      // a candidate's value is strictly negative: OR of the 16 bit patterns, test bit 31
-      const int g = t % kMG, sub = t / kMG;
-      if (__any((int32_t)or16(kc) < 0)) hm |= 1u << (g * 8 + sub);
-      __builtin_amdgcn_sched_barrier(0);
-      if (t + 1 < kSteps) kc = kn;
+    for (int half = 0; half < kTH; ++half) {
+      H8 av[8];
+#pragma unroll
+      for (int sub = 0; sub < 8; ++sub) av[sub].u = t16[buf][h][half * kMTile + sub * 32 + c];
+      floatx16 kc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0].h, bq[0], zacc, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < kSteps; ++t) {
+        floatx16 kn;
+        if (t + 1 < kSteps)
+          kn = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[(t + 1) / kMG].h, bq[(t + 1) % kMG], zacc, 0, 0, 0);
+        // keep the pipeline the source states: without this fence the scheduler sinks each
+        // MFMA next to its consumer (same accumulator registers, the VALU then waits out the
+        // whole MFMA latency every step and the matrix pipe idles under the tree)
+        __builtin_amdgcn_sched_barrier(0);
+        // a candidate's value is strictly negative: OR of the 16 bit patterns, test bit 31
+        const int g = t % kMG, sub = half * 8 + t / kMG;
+        if (__any((int32_t)or16(kc) < 0)) hm |= 1ull << (g * kSub + sub);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < kSteps) kc = kn;
+      }
     }
     // Exact path for the flagged (group, sub-tile) pairs, every lane (exact for any lane): direct
     // fp32 d² over the lane's 16 rows, then the lane pair (c, c + 32) merges its two states.
     // (Deferring the flagged sub-tiles to a per-wave list evaluated after the sweep, off the
     // barrier path, measured slower: 0.360 vs 0.328 ms per launch at cfg1.)
-    hm |= force;
+    hm |= force64;
     if (stats != nullptr && lane == 0) {
-      atomicAdd(&stats[0], (unsigned long long)__builtin_popcount(hm & (0xFFFFFFFFu >> (32 - 8 * kMG))));
-      atomicAdd(&stats[1], (unsigned long long)kSteps);
+      atomicAdd(&stats[0], (unsigned long long)__builtin_popcountll(hm));
+      atomicAdd(&stats[1], (unsigned long long)(kSub * kMG));
     }
 #pragma unroll
     for (int g = 0; g < kMG; ++g) {
-      uint32_t m8 = (hm >> (g * 8)) & 0xFFu & exp_mask;
-      if (m8 == 0) continue;
-      while (m8 != 0) {
-        const int sub = __builtin_ctz(m8);
-        m8 &= m8 - 1;
-        nn_exact_rows(kL32 ? &t32s[buf][sub * 32] : tgt32 + j0 + sub * 32, off, h, qx[g], qy[g],
-                      qz[g], best[g], bidx[g]);
+      uint64_t mg = (hm >> (g * kSub)) & kGMask & exp_mask;
+      if (mg == 0) continue;
+      while (mg != 0) {
+        const int sub = __builtin_ctzll(mg);
+        mg &= mg - 1;
+        nn_exact_rows(tgt32 + j0 + sub * 32, off, h, qx[g], qy[g], qz[g], best[g], bidx[g]);
         const float ob = __shfl_xor(best[g], 32);
         const uint32_t oi = (uint32_t)__shfl_xor((int)bidx[g], 32);
         if (ob < best[g] || (ob == best[g] && oi < bidx[g])) {
@@ -593,8 +609,13 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
       thr_operand(bt, ((best[g] - qq[g]) + eps) * S2, fg);
       if (h == 1) bq[g] = bt;  // the threshold only ever tightens: force stays as it was
     }
-    if (has_next) t16[buf ^ 1][sp][sk] = pre;
-    if (kL32 && has_next && sp == 0) t32s[buf ^ 1][sk] = pre32;
+    if (has_next) {
+#pragma unroll
+      for (int u = 0; u < kTH; ++u) {
+        const int e = threadIdx.x + u * kMBlock;
+        t16[buf ^ 1][e / kTT][e % kTT] = pre[u];
+      }
+    }
     __syncthreads();
     buf ^= 1;
   }
@@ -1051,9 +1072,9 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
       const int v = e ? atoi(e) : kMGDefault;
       return (v == 1 || v == 2 || v == 4) ? v : kMGDefault;
     }();
-    static const uint32_t exp_mask = [] {
+    static const uint64_t exp_mask = [] {
       const char* e = getenv("M3D_NN_EXP");
-      return (e && atoi(e) == 1) ? 0u : 0xFFu;
+      return (e && atoi(e) == 1) ? 0ull : ~0ull;
     }();
     // M3D_NN_STATS=1 (diagnostics): count flagged sub-tiles, print after every launch (syncs)
     static unsigned long long* nn_stats = [] {
@@ -1075,12 +1096,16 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
       const char* e = getenv("M3D_NN_FILL");
       return !(e && atoi(e) == 0);
     }();
-    static const bool lds32 = [] {
-      const char* e = getenv("M3D_NN_LDS32");
-      return e && atoi(e) == 1;
+    // target tile = TH × 256 (one barrier per tile; M3D_NN_TH = 1 | 2)
+    static const int TH = [] {
+      const char* e = getenv("M3D_NN_TH");
+      const int v = e ? atoi(e) : kTHDefault;
+      return (v == 1 || v == 2) ? v : kTHDefault;
     }();
+    const int64_t tt = (int64_t)TH * kMTile;
+    if (tg->mf_npad % tt != 0) return hipErrorInvalidValue;  // pack16 pads to kMTilePad
     const int64_t mq = MG == 4 ? mqueries<4>() : (MG == 2 ? mqueries<2>() : mqueries<1>());
-    dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, kMTile, &slice);
+    dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, tt, &slice);
     if (strided && fill) {
       // Strided tiles decouple grid.y from slice boundaries: pick S in [S0, 2·S0] so that the
       // block count fills the resident block slots in whole rounds (the last partial round of
@@ -1090,11 +1115,11 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
         int dev = 0, per = 0;
         hipDeviceProp_t p;
         if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, nn_mfma_kernel<kMGDefault, false>, kMBlock, 0) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, nn_mfma_kernel<kMGDefault, kTHDefault>, kMBlock, 0) != hipSuccess)
           return (int64_t)0;
         return (int64_t)p.multiProcessorCount * (per > 0 ? per : 1);
       }();
-      const int64_t bx = gm.x, ntiles = tg->mf_npad / kMTile;
+      const int64_t bx = gm.x, ntiles = tg->mf_npad / tt;
       if (slots > 0 && ntiles > 1) {
         int64_t s0 = std::min<int64_t>(std::max<int64_t>((2048 + bx - 1) / bx, 1), ntiles);
         int64_t best = s0;
@@ -1110,34 +1135,18 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
         gm.y = (unsigned)best;
       }
     }
+#define M3D_NN_LAUNCH(MGV, THV)                                                                  \
+  nn_mfma_kernel<MGV, THV><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,         \
+                                                   tg->mf32, tg->mf_npad, slice, off, s->state,    \
+                                                   s->keys, exp_mask, nn_stats, strided)
     if (MG == 4) {
-      if (lds32)
-        nn_mfma_kernel<4, true><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
-                                                        tg->mf32, tg->mf_npad, slice, off, s->state,
-                                                        s->keys, exp_mask, nn_stats, strided);
-      else
-        nn_mfma_kernel<4, false><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
-                                                         tg->mf32, tg->mf_npad, slice, off, s->state,
-                                                         s->keys, exp_mask, nn_stats, strided);
+      if (TH == 2) M3D_NN_LAUNCH(4, 2); else M3D_NN_LAUNCH(4, 1);
     } else if (MG == 2) {
-      if (lds32)
-        nn_mfma_kernel<2, true><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
-                                                        tg->mf32, tg->mf_npad, slice, off, s->state,
-                                                        s->keys, exp_mask, nn_stats, strided);
-      else
-        nn_mfma_kernel<2, false><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
-                                                         tg->mf32, tg->mf_npad, slice, off, s->state,
-                                                         s->keys, exp_mask, nn_stats, strided);
+      if (TH == 2) M3D_NN_LAUNCH(2, 2); else M3D_NN_LAUNCH(2, 1);
     } else {
-      if (lds32)
-        nn_mfma_kernel<1, true><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
-                                                        tg->mf32, tg->mf_npad, slice, off, s->state,
-                                                        s->keys, exp_mask, nn_stats, strided);
-      else
-        nn_mfma_kernel<1, false><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,
-                                                         tg->mf32, tg->mf_npad, slice, off, s->state,
-                                                         s->keys, exp_mask, nn_stats, strided);
+      if (TH == 2) M3D_NN_LAUNCH(1, 2); else M3D_NN_LAUNCH(1, 1);
     }
+#undef M3D_NN_LAUNCH
     if (nn_stats != nullptr) {
       unsigned long long h[2] = {0, 0};
       if (hipMemcpyAsync(h, nn_stats, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
