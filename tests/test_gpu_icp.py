@@ -218,6 +218,35 @@ def test_fused_tail_matches_separate_kernels(nn, estimation):
 
 
 @pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_icp_rank_deficient_plane_matches_oracle(nn):
+    """A planar target with exact (0, 0, 1) normals: the point-to-plane rows are
+    (p_y, −p_x, 0, 0, 0, 1), so the 6×6 system has exact zero rows and columns for rz, tx and ty —
+    the LDLT pivoting moves them last and zero pivots give zero components (Eigen::LDLT, as
+    linalg.h ldlt6_solve and the oracle restate).  In-plane motion stays unobserved."""
+    rng = np.random.default_rng(7)
+    n = 20000
+    tgt = np.zeros((n, 3))
+    tgt[:, :2] = rng.uniform(-1, 1, (n, 2))
+    nrm = np.tile([0.0, 0.0, 1.0], (n, 1))
+    c, s_ = np.cos(0.02), np.sin(0.02)
+    T = np.eye(4)
+    T[:3, :3] = [[1, 0, 0], [0, c, -s_], [0, s_, c]]
+    T[:3, 3] = [0.0, 0.0, 0.03]
+    src = synth.apply(np.linalg.inv(T), tgt[rng.permutation(n)[: n // 2]]) + rng.normal(0, 1e-3, (n // 2, 3))
+    ref = I.registration_icp(src, tgt, 0.1, init=np.eye(4), tgt_normals=nrm,
+                             estimation="point_to_plane", max_iteration=20)
+    out = icp(Cloud(src), Cloud(tgt, nrm), 0.1, np.eye(4), estimation=_lib.EST_POINT_TO_PLANE,
+              max_iteration=20, nn=nn)
+    assert np.all(np.isfinite(out.transformation))
+    np.testing.assert_allclose(out.transformation[:3, :3], ref["transformation"][:3, :3], atol=1e-6)
+    np.testing.assert_allclose(out.transformation[:3, 3], ref["transformation"][:3, 3], atol=1e-5)
+    assert abs(out.fitness - ref["fitness"]) < 2e-4
+    # the aligned source lies on the plane again
+    aligned = synth.apply(out.transformation, src)
+    assert np.abs(aligned[:, 2]).mean() < 5e-3
+
+
+@pytest.mark.parametrize("nn", ["brute", "grid"])
 def test_source_sharded_loop_matches_single_device(nn):
     """The source-sharded protocol (local NN + terms, SUM of the 32 term slots, global fitness
     denominator) emulated with three source shards on one device."""
