@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--hyps", type=int, default=100_000, help="RANSAC hypotheses per GPU per run")
     ap.add_argument("--ransac-steps", type=int, default=3)
     ap.add_argument("--no-ransac", action="store_true")
+    ap.add_argument("--ransac-warmup-s", type=float, default=0.5,
+                    help="untimed RANSAC runs for at least this long before the timed ones")
     ap.add_argument("--no-grid", action="store_true")
     ap.add_argument("--shard", choices=["auto", "target", "source"], default="auto",
                     help="N>1 ICP sharding: target (RCCL MIN of the NN keys + SUM of the terms), "
@@ -264,7 +266,17 @@ def main():
                 dist.all_reduce(key, op=dist.ReduceOp.MAX)
             return res_buf
 
+        # warm-up: the clocks drop while the host prepares the RANSAC data with the GPU idle, so
+        # run about --ransac-warmup-s seconds of untimed runs (the same count on every rank: the
+        # runs of N > 1 contain a collective)
         ransac_run()
+        torch.cuda.synchronize()
+        t_w = time.perf_counter()
+        ransac_run()
+        torch.cuda.synchronize()
+        t_one = max_over_ranks(time.perf_counter() - t_w)
+        for _ in range(max(0, int(args.ransac_warmup_s / max(t_one, 1e-6)) - 2)):
+            ransac_run()
         torch.cuda.synchronize()
 
         def ransac_timed(events: bool):
