@@ -15,7 +15,7 @@
 namespace m3d {
 hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st);
 hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hipStream_t st);
-hipError_t launch_icp_terms_solve(const m3d_icp* s, hipStream_t st);
+hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t st);
 hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStream_t st);
 int64_t terms_blocks(int64_t ns);
 }  // namespace m3d
@@ -695,18 +695,24 @@ int ensure_grid(m3d_ctx* ctx, const m3d_cloud* c, double cell, hipStream_t st, c
   return M3D_OK;
 }
 
-// NN evaluation for the current transform → s->keys (brute: keyinit + scan; grid: one kernel)
-hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st) {
+// NN evaluation for the current transform → s->keys (brute: keyinit + scan; grid: one kernel).
+// self_seed (m3d_icp_step's fused loop): when the previous fused tail left every key at
+// kKeyNone (s->keys_clean), the brute-force scan seeds itself and the keyinit launch is skipped.
+hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = false) {
   m3d_ctx* ctx = s->ctx;
+  const bool seeded = self_seed && s->keys_clean && off == 0;
+  s->keys_clean = false;
   if (s->params.nn_method == M3D_NN_GRID) {
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->qorder, s->tgrid, off, s->state, s->keys,
                           s->corr, s->tgt->xyz32, s->tgt->n, st);
   }
-  hipError_t e = launch_icp_keyinit(s, off, st);
-  if (e != hipSuccess) return e;
+  if (!seeded) {
+    hipError_t e = launch_icp_keyinit(s, off, st);
+    if (e != hipSuccess) return e;
+  }
   KTimer kt(ctx, M3D_KERNEL_NN, st);
-  return launch_icp_nn(s, off, st);
+  return launch_icp_nn(s, off, seeded, st);
 }
 }  // namespace
 
@@ -781,6 +787,7 @@ int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
   hipStream_t st = S(stream);
   HIPX(ctx, hipMemsetAsync(s->corr, 0xFF, sizeof(int32_t) * std::max<int64_t>(s->src->n, 1), st));
   HIPX(ctx, launch_icp_reset(s, T, st));
+  s->keys_clean = false;
   return M3D_OK;
 }
 
@@ -792,10 +799,13 @@ int m3d_icp_step(m3d_icp* s, void* stream) {
     const char* e = getenv("M3D_ICP_FUSED");
     return !(e && atoi(e) == 0);
   }();
-  HIPX(ctx, enqueue_nn(s, 0, st));
+  HIPX(ctx, enqueue_nn(s, 0, st, fused));
   if (fused) {
+    // brute force: the tail hands the keys back as kKeyNone, the next NN seeds itself
+    const bool reset = s->params.nn_method != M3D_NN_GRID && s->src->n > 0;
     KTimer kt(ctx, M3D_KERNEL_TERMS, st);
-    HIPX(ctx, launch_icp_terms_solve(s, st));
+    HIPX(ctx, launch_icp_terms_solve(s, reset, st));
+    s->keys_clean = reset;
     return M3D_OK;
   }
   { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, 0, 0, st)); }
@@ -830,6 +840,7 @@ int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* keys, double* su
   m3d_ctx* ctx = s->ctx;
   CHECK_ARG(ctx, sums != nullptr, "null sums");
   hipStream_t st = S(stream);
+  s->keys_clean = false;
   if (keys && keys != s->keys)
     HIPX(ctx, hipMemcpyAsync(s->keys, keys, sizeof(int64_t) * s->src->n, hipMemcpyDeviceToDevice, st));
   static const bool fused = [] {

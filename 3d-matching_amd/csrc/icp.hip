@@ -395,6 +395,28 @@ hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st) {
   return e;
 }
 
+// Self-seeding (single-device fused loop, m3d_icp_step): the fused tail of the previous
+// iteration left every key at kKeyNone, so instead of a keyinit launch every block computes
+// its queries' starting key itself (nnkey.h seed_key: the previous correspondence, exact — one
+// target load per query) and the blocks of grid.y == 0 also publish it; the MIN over the
+// blocks' atomics is the keyinit → scan result bit for bit.
+struct SeedArgs {
+  const int32_t* prev;  // corr of the previous evaluation
+  const float4* tgt;    // the target cloud's centred fp32 points, original order
+  int64_t nt;           // its size
+  int on;
+};
+
+__device__ __forceinline__ int64_t start_key(const SeedArgs& sa, const IcpState* __restrict__ s,
+                                             int64_t i, float4 p, float qx, float qy, float qz,
+                                             int64_t off, const int64_t* __restrict__ keys) {
+  return sa.on ? seed_key(s, i, p, qx, qy, qz, sa.tgt, sa.nt, off, sa.prev, nullptr) : keys[i];
+}
+
+__device__ __forceinline__ bool publish_key(const SeedArgs& sa, uint32_t bidx, uint32_t bidx0) {
+  return bidx != bidx0 || (sa.on && blockIdx.y == 0 && bidx != 0xFFFFFFFFu);
+}
+
 // Exact fallback of nn_mfma_kernel when the scaled operands do not fit fp16 (mfma_ok == 0, a
 // far-off transform): the same lexicographic (fp32 d², index) minimum over the block's slice by
 // a plain scan, one thread per query.  Keeps the fp32 VALU kernel off the launch path.
@@ -402,7 +424,7 @@ template <int kMG>
 __device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
                               const int32_t* __restrict__ order, const float4* __restrict__ tgt32,
                               int64_t jb, int64_t je, int64_t off, const IcpState* __restrict__ s,
-                              int64_t* __restrict__ keys) {
+                              int64_t* __restrict__ keys, const SeedArgs& sa) {
   const float* Rt = s->Rt32;
   const float r2_hi = s->r2_hi;
   for (int qs = threadIdx.x; qs < mqueries<kMG>(); qs += kMBlock) {
@@ -410,8 +432,9 @@ __device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
     if (slot >= ns) return;
     const int64_t i = order != nullptr ? (int64_t)order[slot] : slot;
     float qx, qy, qz;
-    xform32(Rt, src32[i], qx, qy, qz);
-    const int64_t key = keys[i];  // keyinit_kernel's starting key
+    const float4 p = src32[i];
+    xform32(Rt, p, qx, qy, qz);
+    const int64_t key = start_key(sa, s, i, p, qx, qy, qz, off, keys);  // keyinit's starting key
     float best = key == kKeyNone ? r2_hi : __uint_as_float((uint32_t)((uint64_t)key >> 32));
     uint32_t bidx = key == kKeyNone ? 0xFFFFFFFFu : (uint32_t)key;
     const uint32_t bidx0 = bidx;
@@ -425,7 +448,7 @@ __device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
         bidx = gj;
       }
     }
-    if (bidx != bidx0)
+    if (publish_key(sa, bidx, bidx0))
       atomicMin((unsigned long long*)&keys[i], (unsigned long long)make_key(best, bidx));
   }
 }
@@ -461,14 +484,14 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           int64_t* __restrict__ keys,
                                                           uint64_t exp_mask,
                                                           unsigned long long* __restrict__ stats,
-                                                          int strided) {
+                                                          int strided, SeedArgs sa) {
   // exp_mask: all ones; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
   // (profiling experiment only: the keys are then wrong).  stats (M3D_NN_STATS=1, diagnostics
   // only, else null): [0] flagged (group, sub-tile) steps, [1] all steps.
   if (s->done) return;
   if (!s->mfma_ok) {
     const int64_t jb = (int64_t)blockIdx.y * slice_len;
-    nn_slice_scan<kMG>(src32, ns, order, tgt32, jb, min(nt_pad, jb + slice_len), off, s, keys);
+    nn_slice_scan<kMG>(src32, ns, order, tgt32, jb, min(nt_pad, jb + slice_len), off, s, keys, sa);
     return;
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -487,8 +510,9 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
     const int64_t i = slot < ns ? (order != nullptr ? (int64_t)order[slot] : slot) : ns;
     qi[g] = i;
     if (i < ns) {
-      xform32(Rt, src32[i], qx[g], qy[g], qz[g]);
-      const int64_t key = keys[i];
+      const float4 p = src32[i];
+      xform32(Rt, p, qx[g], qy[g], qz[g]);
+      const int64_t key = start_key(sa, s, i, p, qx[g], qy[g], qz[g], off, keys);
       if (key == kKeyNone) {
         best[g] = r2_hi;
         bidx[g] = 0xFFFFFFFFu;
@@ -621,7 +645,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   }
 #pragma unroll
   for (int g = 0; g < kMG; ++g)
-    if (h == 0 && qi[g] < ns && bidx[g] != bidx0[g])
+    if (h == 0 && qi[g] < ns && publish_key(sa, bidx[g], bidx0[g]))
       atomicMin((unsigned long long*)&keys[qi[g]], (unsigned long long)make_key(best[g], bidx[g]));
 }
 
@@ -676,7 +700,9 @@ __device__ __forceinline__ void terms_block(
     const double* __restrict__ nrm64, int64_t nt_shard, int64_t off,
     const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
     int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
-    double* __restrict__ partials, int pts) {
+    double* __restrict__ partials, int pts, int64_t* __restrict__ reset_keys = nullptr) {
+  // reset_keys (= keys, fused single-device loop): each key is consumed here and set back to
+  // kKeyNone for the next evaluation's self-seeding NN (SeedArgs)
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
   double acc[30];
 #pragma unroll
@@ -685,6 +711,7 @@ __device__ __forceinline__ void terms_block(
     const int64_t i = ((int64_t)blockIdx.x * pts + u) * kTermsBlock + threadIdx.x;
     if (i >= ns) break;
     const int64_t key = keys[i];
+    if (reset_keys != nullptr) reset_keys[i] = kKeyNone;
     int32_t out = -1;
     if (key != kKeyNone) {
       const int64_t gj = (int64_t)(uint32_t)key;
@@ -899,12 +926,12 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
     const double* __restrict__ nrm64, int64_t nt, IcpState* s, const int64_t* __restrict__ keys,
     int32_t* __restrict__ corr, double* partials, int64_t nblocks, double* __restrict__ sums,
-    SolveParams sp, int pts, int64_t off, int sharded, int do_solve) {
+    SolveParams sp, int pts, int64_t off, int sharded, int do_solve, int64_t* reset_keys) {
   // do_solve = 0: the sharded tail (m3d_icp_shard_terms) — terms + the fixed-order reduce into
   // `sums` in one launch; the caller all-reduces them and runs m3d_icp_solve
   if (s->done) return;
   terms_block<true>(src64, ns, tgt64, nrm64, nt, off, s, keys, corr, sp.est, sp.c[0], sp.c[1],
-                    sp.c[2], sharded, partials, pts);
+                    sp.c[2], sharded, partials, pts, reset_keys);
   __shared__ double red[kReduceGroups][kTermSlots];
   __shared__ int last;
   // the partial went out write-through (sc1): drain it, then one lane takes the ticket
@@ -1052,10 +1079,10 @@ static bool icp_nn_uses_mfma(const m3d_icp* s) {
   return mfma_env && s->tgrid != nullptr && s->tgrid->mf16 != nullptr;
 }
 
-// Brute-force NN into s->keys (after launch_icp_keyinit).  MFMA tiles present: nn_mfma_kernel
-// alone (its exact in-kernel scan covers transforms whose operands do not fit fp16); otherwise
-// the fp32 VALU nn_kernel.
-hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
+// Brute-force NN into s->keys (after launch_icp_keyinit, or self_seed: keys all kKeyNone, see
+// SeedArgs).  MFMA tiles present: nn_mfma_kernel alone (its exact in-kernel scan covers
+// transforms whose operands do not fit fp16); otherwise the fp32 VALU nn_kernel.
+hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStream_t st) {
   const int64_t ns = s->src->n;
   const int64_t nt_pad = s->tgt->n_pad;
   if (ns == 0 || s->tgt->n == 0) return hipSuccess;
@@ -1135,10 +1162,11 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
         gm.y = (unsigned)best;
       }
     }
+    const SeedArgs sa{s->corr, s->tgt->xyz32, s->tgt->n, self_seed ? 1 : 0};
 #define M3D_NN_LAUNCH(MGV, THV)                                                                  \
   nn_mfma_kernel<MGV, THV><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,         \
                                                    tg->mf32, tg->mf_npad, slice, off, s->state,    \
-                                                   s->keys, exp_mask, nn_stats, strided)
+                                                   s->keys, exp_mask, nn_stats, strided, sa)
     if (MG == 4) {
       if (TH == 2) M3D_NN_LAUNCH(4, 2); else M3D_NN_LAUNCH(4, 1);
     } else if (MG == 2) {
@@ -1155,6 +1183,10 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, hipStream_t st) {
                 h[1] ? 100.0 * (double)h[0] / (double)h[1] : 0.0);
     }
     return hipGetLastError();
+  }
+  if (self_seed) {  // the fp32 VALU kernel reads its starting keys
+    const hipError_t e = launch_icp_keyinit(s, off, st);
+    if (e != hipSuccess) return e;
   }
   const dim3 grid = nn_grid((ns + kNNBlock * Q - 1) / (kNNBlock * Q), nt_pad, kNNLds, &slice);
   const float4* tp = s->tgt->xyz32;
@@ -1204,7 +1236,7 @@ hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, 
   }
   terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
       s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
-      s->partials, s->nblocks, sums, solve_params(s), terms_pts(), off, 1, 0);
+      s->partials, s->nblocks, sums, solve_params(s), terms_pts(), off, 1, 0, nullptr);
   return hipGetLastError();
 }
 
@@ -1213,7 +1245,7 @@ hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st
   return hipGetLastError();
 }
 
-hipError_t launch_icp_terms_solve(const m3d_icp* s, hipStream_t st) {
+hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t st) {
   const int64_t ns = s->src->n;
   if (ns == 0) {  // no blocks to take tickets: the unfused tail handles the empty source
     hipError_t e = launch_icp_terms_mode(s, 0, 0, st);
@@ -1222,7 +1254,8 @@ hipError_t launch_icp_terms_solve(const m3d_icp* s, hipStream_t st) {
   }
   terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
       s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
-      s->partials, s->nblocks, s->sums, solve_params(s), terms_pts(), (int64_t)0, 0, 1);
+      s->partials, s->nblocks, s->sums, solve_params(s), terms_pts(), (int64_t)0, 0, 1,
+      reset_keys ? s->keys : nullptr);
   return hipGetLastError();
 }
 

@@ -154,6 +154,7 @@ struct m3d_icp {
   double max_dist = 0.0;
   m3d::IcpState* state = nullptr;  // device
   int64_t* keys = nullptr;         // ns packed NN keys
+  bool keys_clean = false;         // host view: every key is kKeyNone (fused tail reset them)
   int32_t* corr = nullptr;         // ns current correspondence (-1 none)
   double* partials = nullptr;      // nblocks × kTermSlots
   double* sums = nullptr;          // kTermSlots
@@ -219,7 +220,7 @@ hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* 
 
 // ICP
 hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_t st);
-hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, hipStream_t st);
+hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, bool self_seed, hipStream_t st);
 hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st);
 hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, hipStream_t st);
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);

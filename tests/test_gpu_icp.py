@@ -218,6 +218,43 @@ def test_fused_tail_matches_separate_kernels(nn, estimation):
 
 
 @pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_mixed_fused_and_separate_steps(nn):
+    """The fused m3d_icp_step hands the keys back as kKeyNone and its next brute-force scan seeds
+    itself; separate shard_nn / shard_terms / solve calls (keyinit path) interleaved with fused
+    steps on the same loop must give the bits of the all-separate loop."""
+    import torch
+
+    src, tgt, nrm, _ = synth.icp_pair(60000, 50000, seed=31)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=9,
+              estimation=_lib.EST_POINT_TO_PLANE, nn=nn)
+    k = torch.empty(len(src), dtype=torch.int64, device="cuda")
+    sm = torch.empty(32, dtype=torch.float64, device="cuda")
+
+    def separate(lp, n):
+        for _ in range(n):
+            lp.shard_nn(0, k)
+            lp.shard_terms(0, k, sm)
+            lp.solve(sm)
+
+    ref = IcpLoop(s, t, 0.12, **kw)
+    ref.reset(np.eye(4))
+    separate(ref, 10)
+    r_ref = ref.result()
+    mix = IcpLoop(s, t, 0.12, **kw)
+    for _ in range(2):  # the second pass starts from keys a finished fused run left behind
+        mix.reset(np.eye(4))
+        mix.steps(3)
+        separate(mix, 2)
+        mix.steps(3)
+        separate(mix, 1)
+        mix.steps(1)
+        r = mix.result()
+        np.testing.assert_array_equal(r.transformation, r_ref.transformation)
+        assert (r.fitness, r.inlier_rmse, r.iterations) == (r_ref.fitness, r_ref.inlier_rmse, 9)
+
+
+@pytest.mark.parametrize("nn", ["brute", "grid"])
 def test_icp_rank_deficient_plane_matches_oracle(nn):
     """A planar target with exact (0, 0, 1) normals: the point-to-plane rows are
     (p_y, −p_x, 0, 0, 0, 1), so the 6×6 system has exact zero rows and columns for rz, tx and ty —
