@@ -829,7 +829,9 @@ int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* keys, void* stream) {
   m3d_ctx* ctx = s->ctx;
   CHECK_ARG(ctx, off >= 0, "negative shard offset");
   hipStream_t st = S(stream);
-  HIPX(ctx, enqueue_nn(s, off, st));
+  // keys kept inside (source-sharded protocol: no MIN exchange) → the keyinit-free scan may run
+  const bool own = off == 0 && (keys == nullptr || keys == s->keys);
+  HIPX(ctx, enqueue_nn(s, off, st, own));
   if (keys && keys != s->keys)
     HIPX(ctx, hipMemcpyAsync(keys, s->keys, sizeof(int64_t) * s->src->n, hipMemcpyDeviceToDevice, st));
   return M3D_OK;
@@ -848,8 +850,12 @@ int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* keys, double* su
     return !(e && atoi(e) == 0);
   }();
   if (fused) {  // terms + fixed-order reduce in one launch (same bits as the two kernels)
+    // keys kept inside (see m3d_icp_shard_nn): hand them back as kKeyNone like m3d_icp_step
+    const bool reset = off == 0 && (keys == nullptr || keys == s->keys) && s->src->n > 0 &&
+                       s->params.nn_method != M3D_NN_GRID;
     KTimer kt(ctx, M3D_KERNEL_TERMS, st);
-    HIPX(ctx, launch_icp_terms_reduce(s, off, sums, st));
+    HIPX(ctx, launch_icp_terms_reduce(s, off, sums, reset, st));
+    s->keys_clean = reset;
     return M3D_OK;
   }
   { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, off, 1, st)); }

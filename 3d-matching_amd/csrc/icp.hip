@@ -1228,7 +1228,8 @@ static SolveParams solve_params(const m3d_icp* s) {
 }
 
 // sharded tail: terms (sharded semantics, shard offset off) + reduce into sums, one launch
-hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, hipStream_t st) {
+hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, bool reset_keys,
+                                   hipStream_t st) {
   const int64_t ns = s->src->n;
   if (ns == 0) {
     hipError_t e = launch_icp_terms_mode(s, off, 1, st);
@@ -1236,7 +1237,8 @@ hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, 
   }
   terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
       s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
-      s->partials, s->nblocks, sums, solve_params(s), terms_pts(), off, 1, 0, nullptr);
+      s->partials, s->nblocks, sums, solve_params(s), terms_pts(), off, 1, 0,
+      reset_keys ? s->keys : nullptr);
   return hipGetLastError();
 }
 

@@ -222,7 +222,8 @@ hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* 
 hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_t st);
 hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, bool self_seed, hipStream_t st);
 hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st);
-hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, hipStream_t st);
+hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, bool reset_keys,
+                                   hipStream_t st);
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g);
 void grid_free(Grid* g);

@@ -283,10 +283,13 @@ def test_icp_rank_deficient_plane_matches_oracle(nn):
     assert np.abs(aligned[:, 2]).mean() < 5e-3
 
 
+@pytest.mark.parametrize("keys_inside", [False, True])
 @pytest.mark.parametrize("nn", ["brute", "grid"])
-def test_source_sharded_loop_matches_single_device(nn):
+def test_source_sharded_loop_matches_single_device(nn, keys_inside):
     """The source-sharded protocol (local NN + terms, SUM of the 32 term slots, global fitness
-    denominator) emulated with three source shards on one device."""
+    denominator) emulated with three source shards on one device.  keys_inside: no key buffer
+    passed (bench.py's form) — the keys stay in the loop, the terms hand them back as kKeyNone
+    and the next brute-force scan seeds itself."""
     import torch
 
     src, tgt, nrm, _ = synth.icp_pair(30001, 20000, seed=14)
@@ -304,8 +307,8 @@ def test_source_sharded_loop_matches_single_device(nn):
         for lp in loops:
             k = torch.empty(lp.src.n, dtype=torch.int64, device="cuda")
             sm = torch.empty(32, dtype=torch.float64, device="cuda")
-            lp.shard_nn(0, k)
-            lp.shard_terms(0, k, sm)
+            lp.shard_nn(0, None if keys_inside else k)
+            lp.shard_terms(0, None if keys_inside else k, sm)
             sums.append(sm)
         tot = torch.stack(sums).sum(dim=0)
         for lp in loops:
