@@ -461,16 +461,7 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   ScoreScratch s = score_bind(a, o);
   double* Tb = a.at<double>(o_T);
   int32_t* cb = a.at<int32_t>(o_c);
-  RansacState init;
-  memset(&init, 0, sizeof(init));
-  for (int k = 0; k < 16; ++k) init.T_best[k] = (k % 5 == 0) ? 1.0 : 0.0;
-  init.best_count = -1;
-  init.best_index = -1;
-  init.iterations = 0;
-  init.done = (max_iter == 0) ? 1 : 0;
-  HIPX(ctx, hipMemcpyAsync(ctx->rstate, &init, sizeof(init), hipMemcpyHostToDevice, st));
-  HIPX(ctx, hipMemcpyAsync(&ctx->rstate->rechecked, ctx->stats, sizeof(int64_t),
-                           hipMemcpyDeviceToDevice, st));
+  HIPX(ctx, launch_ransac_init(ctx->rstate, ctx->stats, max_iter == 0 ? 1 : 0, st));
   const int32_t* done = &ctx->rstate->done;
   const double thr_sq = thr_sq_of(p->thr, p->mode);
   for (int64_t b0 = 0; b0 < max_iter; b0 += B) {

@@ -49,6 +49,7 @@ struct RansacState {
   int64_t rechecked;
   int32_t done;
   int32_t pad[3];
+  uint64_t batch_key;  // select_best_kernel → select_kernel (no-early-stop batches)
 };
 
 // ICP loop state (device resident), Open3D RegistrationICP semantics.
@@ -215,6 +216,7 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
 hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int64_t nc,
                          int64_t max_iter, int early_stop, double es_thr, double es_conf,
                          const double* T_batch, RansacState* rs, hipStream_t st);
+hipError_t launch_ransac_init(RansacState* rs, const int64_t* stats, int done, hipStream_t st);
 hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* stats,
                               m3d_ransac_result* out_dev, hipStream_t st);
 

@@ -679,6 +679,35 @@ __device__ __forceinline__ int64_t required_iters(double ratio, double conf, int
   return (int64_t)v;  // int() truncation (v >= 0 here)
 }
 
+// Batch best for the no-early-stop select: key = (count << 32) | (2³² − 1 − k), k the batch
+// position, so the MAX is the highest count at the lowest position; one 64-bit atomicMax per
+// wave into rs->batch_key (0 = empty: below every real key).  Many blocks — a single-block
+// reduction of 1e5 counts was latency-bound at 20–40 µs.
+constexpr int kSelBestBlock = 256, kSelBestPer = 8;
+__global__ __launch_bounds__(kSelBestBlock) void select_best_kernel(const int32_t* __restrict__ counts,
+                                                                    int64_t n, RansacState* __restrict__ rs) {
+  if (rs->done) return;
+  uint64_t best = 0;
+  const int64_t base = (int64_t)blockIdx.x * kSelBestBlock * kSelBestPer + threadIdx.x;
+  int32_t v[kSelBestPer];
+#pragma unroll
+  for (int u = 0; u < kSelBestPer; ++u) v[u] = counts[min(base + u * kSelBestBlock, n - 1)];
+#pragma unroll
+  for (int u = 0; u < kSelBestPer; ++u) {
+    const int64_t k = base + u * kSelBestBlock;
+    const uint64_t key = ((uint64_t)(uint32_t)v[u] << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)k);
+    if (k < n && key > best) best = key;
+  }
+#pragma unroll
+  for (int w = 32; w > 0; w >>= 1) {
+    const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(best >> 32), w) << 32) |
+                       (uint32_t)__shfl_xor((int)(uint32_t)best, w);
+    best = o > best ? o : best;
+  }
+  if ((threadIdx.x & 63) == 0 && best != 0)
+    atomicMax((unsigned long long*)&rs->batch_key, (unsigned long long)best);
+}
+
 __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict__ counts,
                                                       int64_t h_begin, int64_t n, int64_t nc,
                                                       int64_t max_iter, int early, double es_thr,
@@ -702,41 +731,13 @@ __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict_
   __syncthreads();
   if (done_s) return;
   if (!early) {
-    // no stop to find: the batch's best is an order-free reduction under (count desc, index
-    // asc) — the first strict improvement of the sequential walk — with coalesced strided loads
-    // kSelLoads independent loads in flight per thread: one dependent load per iteration left
-    // the single block latency-bound (38 µs at 1e5 counts)
-    constexpr int kSelLoads = 16;
-    BestPair loc{-1, -1};
-    for (int64_t k0 = 0; k0 < n; k0 += 1024 * kSelLoads) {
-      int32_t v[kSelLoads];
-#pragma unroll
-      for (int u = 0; u < kSelLoads; ++u) {
-        const int64_t k = k0 + u * 1024 + t;
-        const int32_t raw = counts[min(k, n - 1)];  // unconditional: the loads batch
-        v[u] = k < n ? raw : -1;
-      }
-#pragma unroll
-      for (int u = 0; u < kSelLoads; ++u) {
-        const BestPair b{v[u], h_begin + k0 + u * 1024 + t};
-        if (b.c > loc.c || (b.c == loc.c && b.i < loc.i)) loc = b;
-      }
-    }
-    sc[t] = loc.c;
-    si[t] = loc.i;
-    __syncthreads();
-    for (int w = 512; w > 0; w >>= 1) {
-      if (t < w) {
-        const BestPair a{sc[t], si[t]}, b{sc[t + w], si[t + w]};
-        if (b.c > a.c || (b.c == a.c && b.i < a.i && b.c >= 0)) {
-          sc[t] = b.c;
-          si[t] = b.i;
-        }
-      }
-      __syncthreads();
-    }
+    // no stop to find: the batch's best (count desc, index asc — the first strict improvement
+    // of the sequential walk) is order-free; select_best_kernel left it as one packed key
     if (t == 0) {
-      const BestPair fin = combine(BestPair{rs->best_count, rs->best_index}, BestPair{sc[0], si[0]});
+      const uint64_t key = rs->batch_key;
+      rs->batch_key = 0;  // for the next batch
+      const BestPair bb{(int64_t)(key >> 32), h_begin + (int64_t)(0xFFFFFFFFu - (uint32_t)key)};
+      const BestPair fin = combine(BestPair{rs->best_count, rs->best_index}, bb);
       if (fin.i != rs->best_index && fin.i >= h_begin) {
         for (int k = 0; k < 16; ++k) rs->T_best[k] = T_batch[16 * (fin.i - h_begin) + k];
       }
@@ -1022,8 +1023,31 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
 hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int64_t nc,
                          int64_t max_iter, int early_stop, double es_thr, double es_conf,
                          const double* T_batch, RansacState* rs, hipStream_t st) {
+  if (!early_stop && n > 0) {
+    const int64_t per = (int64_t)kSelBestBlock * kSelBestPer;
+    select_best_kernel<<<(unsigned)((n + per - 1) / per), kSelBestBlock, 0, st>>>(counts, n, rs);
+  }
   select_kernel<<<1, 1024, 0, st>>>(counts, h_begin, n, nc, max_iter, early_stop, es_thr, es_conf,
                                     T_batch, rs);
+  return hipGetLastError();
+}
+
+// state of a fresh a4 run (one launch instead of a pageable H2D copy + a D2D copy: ~10 µs)
+__global__ void ransac_init_kernel(RansacState* __restrict__ rs, const int64_t* __restrict__ stats,
+                                   int done) {
+  if (threadIdx.x != 0) return;
+  for (int k = 0; k < 16; ++k) rs->T_best[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  rs->best_count = -1;
+  rs->best_index = -1;
+  rs->iterations = 0;
+  rs->rechecked = stats != nullptr ? stats[0] : 0;  // copy_result reports the difference
+  rs->done = done;
+  for (int k = 0; k < 3; ++k) rs->pad[k] = 0;
+  rs->batch_key = 0;
+}
+
+hipError_t launch_ransac_init(RansacState* rs, const int64_t* stats, int done, hipStream_t st) {
+  ransac_init_kernel<<<1, 64, 0, st>>>(rs, stats, done);
   return hipGetLastError();
 }
 
