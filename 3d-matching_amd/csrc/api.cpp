@@ -394,8 +394,9 @@ double thr_sq_of(double thr, int mode) { return mode == M3D_SCORE_SQUARED ? thr 
 // zeroed by the kernel that produced them
 hipError_t score_enqueue(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64_t H,
                          double thr, int mode, int32_t* counts, const ScoreScratch& s,
-                         const int32_t* done, hipStream_t st) {
-  hipError_t e = launch_score_prep(cs, T, H, thr, mode, s.mf, st);
+                         const int32_t* done, hipStream_t st, bool prepared = false) {
+  // prepared: kabsch3 already wrote the MFMA operands (ScoreFuse)
+  hipError_t e = prepared ? hipSuccess : launch_score_prep(cs, T, H, thr, mode, s.mf, st);
   if (e != hipSuccess) return e;
   KTimer kt(ctx, M3D_KERNEL_SCORE, st);
   return launch_score(cs, s.hypf, H, counts, T, thr, mode, ctx->stats, done, s.mf, st);
@@ -464,6 +465,10 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   HIPX(ctx, launch_ransac_init(ctx->rstate, ctx->stats, max_iter == 0 ? 1 : 0, st));
   const int32_t* done = &ctx->rstate->done;
   const double thr_sq = thr_sq_of(p->thr, p->mode);
+  static const bool fuse_on = [] {  // M3D_RANSAC_FUSE=0: separate hyp16 launch (A/B)
+    const char* e = getenv("M3D_RANSAC_FUSE");
+    return !(e && atoi(e) == 0);
+  }();
   for (int64_t b0 = 0; b0 < max_iter; b0 += B) {
     const int64_t n = std::min(B, max_iter - b0);
     const int32_t* tri = triples ? triples + 3 * b0 : nullptr;
@@ -471,12 +476,13 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
     hipError_t e;
     {
       KTimer kt(ctx, M3D_KERNEL_KABSCH, st);
+      const ScoreFuse fz{&s.mf, p->thr, p->mode};
       e = launch_kabsch3(cs, tri, p->seed, p->hyp0 + b0, n, thr_sq, Tb, nullptr, s.hypf, done,
-                         ZeroArgs{cnt}, st);
+                         ZeroArgs{cnt}, st, (nc > 0 && fuse_on) ? &fz : nullptr);
     }
     if (e == hipSuccess) {
       if (nc > 0)
-        e = score_enqueue(ctx, cs, Tb, n, p->thr, p->mode, cnt, s, done, st);
+        e = score_enqueue(ctx, cs, Tb, n, p->thr, p->mode, cnt, s, done, st, fuse_on);
       else
         e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * n, st);
     }

@@ -194,9 +194,18 @@ hipError_t launch_sum3(const double* a, int64_t n, double* partial /*[blocks*3]*
 hipError_t launch_center_pack(const double* a, int64_t n, int64_t n_pad, const double c[3],
                               float4* out, float pad_value, float* maxnorm_partial, int blocks,
                               int maxinf, hipStream_t st);
+struct ScoreMf;
+// a4 batches: kabsch3_kernel also writes the MFMA screen's per-hypothesis operands (hyp16) for
+// the score launch that follows (thr/mode of that launch; no effect when it will not use them)
+struct ScoreFuse {
+  const ScoreMf* mf;
+  double thr;
+  int mode;
+};
 hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_t seed,
                           int64_t hyp0, int64_t H, double thr_sq, double* T_out, uint8_t* status,
-                          HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st);
+                          HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st,
+                          const ScoreFuse* fuse = nullptr);
 hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
                               HypF32* hypf, ZeroArgs z, hipStream_t st);
 // MFMA scoring (score_mfma_kernel): per-batch hypothesis operands built from the fp64

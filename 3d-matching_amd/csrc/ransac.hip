@@ -172,6 +172,23 @@ __device__ __forceinline__ void zero_scoring_state(const ZeroArgs& z, int64_t h,
   if (h < H && z.counts) z.counts[h] = 0;
 }
 
+struct Mf16Params {
+  double cs[3], ct[3];
+  double S, pinf, qinf, thr_sq;
+};
+
+// hyp16_kernel's per-hypothesis body folded into kabsch3_kernel (the transform is already in
+// registers there): one launch less per RANSAC batch when the MFMA screen scores it
+struct Hyp16Fuse {
+  Mf16Params m;
+  uint4* hb16;
+  float* heps;
+  int64_t h_pad;
+  int on;
+};
+__device__ void hyp16_one(const double* T, bool valid, int64_t j, int64_t h_pad,
+                          const Mf16Params& m, uint4* __restrict__ hb16, float* __restrict__ heps);
+
 __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__ p64,
                                                       const double* __restrict__ q64, int64_t nc,
                                                       const int32_t* __restrict__ triples,
@@ -180,11 +197,14 @@ __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__
                                                       uint8_t* __restrict__ status,
                                                       HypF32* __restrict__ hypf,
                                                       const int32_t* __restrict__ done,
-                                                      ZeroArgs z) {
+                                                      ZeroArgs z, Hyp16Fuse hf) {
   if (done != nullptr && *done) return;
   const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   zero_scoring_state(z, h, H);
-  if (h >= H) return;
+  if (h >= H) {  // padding hypotheses of the MFMA operands
+    if (hf.on && h < hf.h_pad) hyp16_one(nullptr, false, h, hf.h_pad, hf.m, hf.hb16, hf.heps);
+    return;
+  }
   double T[16];
   int st = M3D_HYP_OK;
   if (nc < 3) {  // ransac.py:139-140
@@ -211,6 +231,7 @@ __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__
   for (int k = 0; k < 16; ++k) T_out[16 * h + k] = T[k];
   if (status != nullptr) status[h] = (uint8_t)st;
   hypf[h] = make_hypf(T, g);
+  if (hf.on) hyp16_one(T, true, h, hf.h_pad, hf.m, hf.hb16, hf.heps);
 }
 
 __global__ __launch_bounds__(256) void hypf_from_T_kernel(const double* __restrict__ T, int64_t H,
@@ -407,24 +428,17 @@ __global__ __launch_bounds__(256) void corr16_kernel(const double* __restrict__ 
   for (int c = 0; c < 3; ++c) ca16[(1 + c) * nc_pad + i] = Q[c].u;
 }
 
-struct Mf16Params {
-  double cs[3], ct[3];
-  double S, pinf, qinf, thr_sq;
-};
-
 // B operands + guard band of hypotheses [0, h_pad) of a batch (fp64 transforms T64).
-__global__ __launch_bounds__(256) void hyp16_kernel(const double* __restrict__ T64, int64_t H,
-                                                    int64_t h_pad, Mf16Params m,
-                                                    uint4* __restrict__ hb16,
-                                                    float* __restrict__ heps) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= h_pad) return;
+// hypothesis j's B operands + guard band from its fp64 transform T (valid: j < H; the padding
+// hypotheses get far operands)
+__device__ __forceinline__ void hyp16_one(const double* T, bool valid, int64_t j, int64_t h_pad,
+                                          const Mf16Params& m, uint4* __restrict__ hb16,
+                                          float* __restrict__ heps) {
   const _Float16 zero = (_Float16)0.0f, mone = (_Float16)-1.0f;
   SH8 B0[3], B1[3];
   float eps = -1.0f;  // no guard band: v is never inside (−1, 1)·ε
   bool far = true, general = false;
-  if (j < H) {
-    const double* T = T64 + 16 * j;
+  if (valid) {
     double tp[3], rowl1 = 0.0, tinf = 0.0;
     bool finite = true;
     for (int c = 0; c < 3; ++c) {
@@ -485,6 +499,15 @@ __global__ __launch_bounds__(256) void hyp16_kernel(const double* __restrict__ T
     hb16[(3 + c) * h_pad + j] = B1[c].u;
   }
   heps[j] = eps;
+}
+
+__global__ __launch_bounds__(256) void hyp16_kernel(const double* __restrict__ T64, int64_t H,
+                                                    int64_t h_pad, Mf16Params m,
+                                                    uint4* __restrict__ hb16,
+                                                    float* __restrict__ heps) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= h_pad) return;
+  hyp16_one(j < H ? T64 + 16 * j : nullptr, j < H, j, h_pad, m, hb16, heps);
 }
 
 // acc − x·x as one scalar v_fma_f32 (single rounding, = fma(−x, x, acc)).  The empty asm makes
@@ -880,13 +903,25 @@ static GuardParams guard_of(const m3d_corrset* cs, double thr_sq) {
   return g;
 }
 
+static bool score_prep_params(const m3d_corrset* cs, int64_t H, double thr, int mode,
+                              const ScoreMf& mf, Mf16Params* m, int64_t* hp);
+
 hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_t seed,
                           int64_t hyp0, int64_t H, double thr_sq, double* T_out, uint8_t* status,
-                          HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st) {
+                          HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st,
+                          const ScoreFuse* fuse) {
   if (H == 0) return hipSuccess;
-  kabsch3_kernel<<<blocks_for(H, 256), 256, 0, st>>>(cs->p64, cs->q64, cs->nc, triples, seed,
+  Hyp16Fuse hf{};
+  hf.on = 0;
+  if (fuse != nullptr && score_prep_params(cs, H, fuse->thr, fuse->mode, *fuse->mf, &hf.m, &hf.h_pad)) {
+    hf.hb16 = fuse->mf->hb16;
+    hf.heps = fuse->mf->heps;
+    hf.on = 1;
+  }
+  const int64_t n = hf.on ? hf.h_pad : H;
+  kabsch3_kernel<<<blocks_for(n, 256), 256, 0, st>>>(cs->p64, cs->q64, cs->nc, triples, seed,
                                                      hyp0, H, guard_of(cs, thr_sq), T_out, status,
-                                                     hypf, done, z);
+                                                     hypf, done, z, hf);
   return hipGetLastError();
 }
 
@@ -931,20 +966,28 @@ static bool use_mfma_score(const m3d_corrset* cs, const ScoreMf& mf, double thr_
 
 static double thr_sq_mode(double thr, int mode) { return mode == M3D_SCORE_SQUARED ? thr : thr * thr; }
 
+// the MFMA screen's per-batch parameters; false: the batch is not scored by the MFMA screen
+static bool score_prep_params(const m3d_corrset* cs, int64_t H, double thr, int mode,
+                              const ScoreMf& mf, Mf16Params* m, int64_t* hp) {
+  const double thr_sq = thr_sq_mode(thr, mode);
+  if (H == 0 || cs->nc == 0 || !use_mfma_score(cs, mf, thr_sq)) return false;
+  for (int k = 0; k < 3; ++k) {
+    m->cs[k] = cs->cs[k];
+    m->ct[k] = cs->ct[k];
+  }
+  m->S = cs->s16;
+  m->pinf = cs->pmax2;
+  m->qinf = cs->qmaxinf;
+  m->thr_sq = thr_sq;
+  *hp = score_mf_hpad(H);
+  return true;
+}
+
 hipError_t launch_score_prep(const m3d_corrset* cs, const double* T64, int64_t H, double thr,
                              int mode, const ScoreMf& mf, hipStream_t st) {
-  const double thr_sq = thr_sq_mode(thr, mode);
-  if (H == 0 || cs->nc == 0 || !use_mfma_score(cs, mf, thr_sq)) return hipSuccess;
   Mf16Params m;
-  for (int k = 0; k < 3; ++k) {
-    m.cs[k] = cs->cs[k];
-    m.ct[k] = cs->ct[k];
-  }
-  m.S = cs->s16;
-  m.pinf = cs->pmax2;
-  m.qinf = cs->qmaxinf;
-  m.thr_sq = thr_sq;
-  const int64_t hp = score_mf_hpad(H);
+  int64_t hp = 0;
+  if (!score_prep_params(cs, H, thr, mode, mf, &m, &hp)) return hipSuccess;
   hyp16_kernel<<<blocks_for(hp, 256), 256, 0, st>>>(T64, H, hp, m, mf.hb16, mf.heps);
   return hipGetLastError();
 }
