@@ -14,7 +14,6 @@
 
 namespace m3d {
 hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st);
-hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hipStream_t st);
 hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t st);
 hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStream_t st);
 int64_t terms_blocks(int64_t ns);
@@ -702,7 +701,7 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = 
   if (s->params.nn_method == M3D_NN_GRID) {
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->qorder, s->tgrid, off, s->state, s->keys,
-                          s->corr, s->tgt->xyz32, s->tgt->n, st);
+                          s->near2, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st);
   }
   if (!seeded) {
     hipError_t e = launch_icp_keyinit(s, off, st);
@@ -754,6 +753,10 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   s->qorder = sg->order;
   int rc = dev_alloc(ctx, &s->state, 1);
   if (!rc) rc = dev_alloc(ctx, &s->keys, std::max<int64_t>(src->n, 1));
+  if (!rc) rc = dev_alloc(ctx, &s->near2, std::max<int64_t>(src->n, 1));
+  if (!rc) rc = dev_alloc(ctx, &s->dprev, std::max<int64_t>(src->n, 1));
+  if (!rc) rc = dev_alloc(ctx, &s->ld64, std::max<int64_t>(src->n, 1));
+  if (!rc) rc = dev_alloc(ctx, &s->lidx, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->corr, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->partials, s->nblocks * kTermSlots);
   if (!rc) rc = dev_alloc(ctx, &s->sums, kTermSlots);
@@ -769,6 +772,10 @@ void m3d_icp_destroy(m3d_icp* s) {
   if (!s) return;
   hipFree(s->state);
   hipFree(s->keys);
+  hipFree(s->near2);
+  hipFree(s->dprev);
+  hipFree(s->ld64);
+  hipFree(s->lidx);
   hipFree(s->corr);
   hipFree(s->partials);
   hipFree(s->sums);
@@ -783,6 +790,8 @@ int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
   HIPX(ctx, hipMemsetAsync(s->corr, 0xFF, sizeof(int32_t) * std::max<int64_t>(s->src->n, 1), st));
+  // all-ones bits = a NaN distance: no bound seed until a target-shard exchange wrote dprev
+  HIPX(ctx, hipMemsetAsync(s->dprev, 0xFF, sizeof(int64_t) * std::max<int64_t>(s->src->n, 1), st));
   HIPX(ctx, launch_icp_reset(s, T, st));
   s->keys_clean = false;
   return M3D_OK;
@@ -805,7 +814,7 @@ int m3d_icp_step(m3d_icp* s, void* stream) {
     s->keys_clean = reset;
     return M3D_OK;
   }
-  { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, 0, 0, st)); }
+  { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, 0, nullptr, nullptr, st)); }
   HIPX(ctx, launch_icp_reduce(s, s->sums, st));
   HIPX(ctx, launch_icp_solve(s, s->sums, st));
   return M3D_OK;
@@ -821,41 +830,48 @@ int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream) {
   return M3D_OK;
 }
 
-int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* keys, void* stream) {
+int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* dkeys, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;
   CHECK_ARG(ctx, off >= 0, "negative shard offset");
+  CHECK_ARG(ctx, dkeys != nullptr || off == 0, "a target shard (offset > 0) needs the dkeys exchange buffer");
   hipStream_t st = S(stream);
-  // keys kept inside (source-sharded protocol: no MIN exchange) → the keyinit-free scan may run
-  const bool own = off == 0 && (keys == nullptr || keys == s->keys);
-  HIPX(ctx, enqueue_nn(s, off, st, own));
-  if (keys && keys != s->keys)
-    HIPX(ctx, hipMemcpyAsync(keys, s->keys, sizeof(int64_t) * s->src->n, hipMemcpyDeviceToDevice, st));
+  // dkeys == NULL: source-sharded protocol, the keys stay inside and the keyinit-free scan may
+  // run; else target shard: this shard's fp64 winners → the MIN exchange buffer
+  HIPX(ctx, enqueue_nn(s, off, st, dkeys == nullptr));
+  if (dkeys != nullptr) HIPX(ctx, launch_shard_winner(s, off, dkeys, st));
   return M3D_OK;
 }
 
-int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* keys, double* sums, void* stream) {
+int m3d_icp_shard_claim(m3d_icp* s, const int64_t* dmin, int32_t* claim, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  CHECK_ARG(s->ctx, dmin != nullptr && claim != nullptr, "null exchange buffer");
+  HIPX(s->ctx, launch_shard_claim(s, dmin, claim, S(stream)));
+  return M3D_OK;
+}
+
+int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* dmin, const int32_t* claim,
+                        double* sums, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;
   CHECK_ARG(ctx, sums != nullptr, "null sums");
+  CHECK_ARG(ctx, (dmin == nullptr) == (claim == nullptr), "dmin and claim go together");
+  CHECK_ARG(ctx, claim != nullptr || off == 0, "a target shard (offset > 0) needs dmin and claim");
   hipStream_t st = S(stream);
   s->keys_clean = false;
-  if (keys && keys != s->keys)
-    HIPX(ctx, hipMemcpyAsync(s->keys, keys, sizeof(int64_t) * s->src->n, hipMemcpyDeviceToDevice, st));
   static const bool fused = [] {
     const char* e = getenv("M3D_ICP_FUSED");
     return !(e && atoi(e) == 0);
   }();
   if (fused) {  // terms + fixed-order reduce in one launch (same bits as the two kernels)
-    // keys kept inside (see m3d_icp_shard_nn): hand them back as kKeyNone like m3d_icp_step
-    const bool reset = off == 0 && (keys == nullptr || keys == s->keys) && s->src->n > 0 &&
-                       s->params.nn_method != M3D_NN_GRID;
+    // keys kept inside (source shard): hand them back as kKeyNone like m3d_icp_step
+    const bool reset = claim == nullptr && s->src->n > 0 && s->params.nn_method != M3D_NN_GRID;
     KTimer kt(ctx, M3D_KERNEL_TERMS, st);
-    HIPX(ctx, launch_icp_terms_reduce(s, off, sums, reset, st));
+    HIPX(ctx, launch_icp_terms_reduce(s, off, claim, dmin, sums, reset, st));
     s->keys_clean = reset;
     return M3D_OK;
   }
-  { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, off, 1, st)); }
+  { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, off, claim, dmin, st)); }
   HIPX(ctx, launch_icp_reduce(s, sums, st));
   return M3D_OK;
 }
@@ -1095,7 +1111,7 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
     if (!hpass[h]) continue;
     e = launch_icp_set_T(s, T.p + 16 * h, st);
     if (e == hipSuccess) e = enqueue_nn(s, 0, st);
-    if (e == hipSuccess) e = launch_icp_terms_mode(s, 0, 0, st);
+    if (e == hipSuccess) e = launch_icp_terms_mode(s, 0, nullptr, nullptr, st);
     if (e == hipSuccess) e = launch_icp_reduce(s, sums.p + kTermSlots * h, st);
   }
   std::vector<double> hs((size_t)kTermSlots * H);
@@ -1132,7 +1148,7 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
     if (e == hipSuccess && corr_set_out) {
       e = launch_icp_set_T(s, T.p + 16 * best, st);
       if (e == hipSuccess) e = enqueue_nn(s, 0, st);
-      if (e == hipSuccess) e = launch_icp_terms_mode(s, 0, 0, st);
+      if (e == hipSuccess) e = launch_icp_terms_mode(s, 0, nullptr, nullptr, st);
       if (e == hipSuccess)
         e = hipMemcpyAsync(corr_set_out, s->corr, 4 * ns, hipMemcpyDeviceToDevice, st);
     }

@@ -37,12 +37,6 @@ namespace m3d {
 constexpr int kGridBlock = 256;
 constexpr int64_t kMaxCells = (int64_t)1 << 25;
 
-__device__ __forceinline__ int grid_coord(float x, float o, float inv_h, int n) {
-  float f = (x - o) * inv_h;
-  f = fminf(fmaxf(f, 0.0f), (float)(n - 1));
-  return (int)f;
-}
-
 __global__ __launch_bounds__(kGridBlock) void minmax3_kernel(const float4* __restrict__ p, int64_t n,
                                                              float* __restrict__ part) {
   __shared__ float s[6][kGridBlock];
@@ -117,10 +111,11 @@ __global__ __launch_bounds__(kGridBlock) void grid_gather_kernel(const float4* _
 
 // kGridLanes lanes cooperate on one query: the query's cell rows (contiguous runs of the sorted
 // array) are dealt round-robin to the lanes, each lane keeps its packed (bits(d²) << 32 | index)
-// minimum, and the lanes combine with shuffles.  A key compare is exactly the lexicographic
-// (d², index) compare of the brute-force scan (d² ≥ +0, so the float bits order as the values;
-// NaN bits order above every finite bound and are never selected).  16 lanes per query keep
-// ~16x more loads in flight than one lane per query: the scan is latency-bound, not bandwidth.
+// minimum and the runner-up distance near2 (nnkey.h near_push), and the lanes combine with
+// shuffles.  A key compare is exactly the lexicographic (d², index) compare of the brute-force
+// scan (d² ≥ +0, so the float bits order as the values; NaN bits order above every finite bound
+// and are never selected).  Several lanes per query keep more loads in flight than one lane
+// per query: the scan is latency-bound, not bandwidth.
 constexpr int kGridLanesDefault = 4;  // M3D_GRID_LANES = 1|2|4|8|16 overrides (tuning)
 
 template <int kGridLanes>
@@ -130,29 +125,34 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __res
                                                              GridDev g, int64_t off,
                                                              const IcpState* __restrict__ s,
                                                              int64_t* __restrict__ keys,
+                                                             uint32_t* __restrict__ near2,
                                                              const int32_t* __restrict__ prev,
+                                                             const int64_t* __restrict__ dprev,
                                                              const float4* __restrict__ tgt32,
                                                              int64_t nt_shard) {
   // The query starts from seed_key (its previous correspondence re-evaluated, or a bound): the
-  // cell box then only has to cover d² ≤ the seed's d² instead of r2_hi (same lemma as above
-  // with r2_hi replaced by that bound), and the result is still the lexicographic minimum over
-  // all targets with d² ≤ r2_hi — the seed is one of them, or a bound on the winner's d².
+  // cell box then only has to cover the seed's search bound (search_bound: the fp64 band around
+  // it, capped at r2_hi) instead of r2_hi (same lemma as above with r2_hi replaced by that
+  // bound); k1 is still the lexicographic minimum over all targets with d² ≤ r2_hi, and near2
+  // covers every other target within the band of k1 (nnkey.h header).
   if (s->done) return;
   const int64_t t = ((int64_t)blockIdx.x * kGridBlock + threadIdx.x) / kGridLanes;
   const int sub = threadIdx.x & (kGridLanes - 1);
-  const float r2_hi = s->r2_hi;
+  const float r2_hi = s->r2_hi, be = s->band_e;
   const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
-  uint64_t key = key0;
+  uint64_t k1 = key0;
+  float k1d = kInf, n2 = kInf;
   int64_t i = 0;
   if (t < ns) {
     i = order != nullptr ? (int64_t)order[t] : t;
     const float4 p = src32[i];
     float qx, qy, qz;
     xform32(s->Rt32, p, qx, qy, qz);
-    const int64_t seed = seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, keys);
-    if (seed != kKeyNone) key = (uint64_t)seed;
+    const int64_t seed = seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
+    if (seed != kKeyNone) k1 = (uint64_t)seed;
+    k1d = key_real_d2(k1);
     if (g.ncells > 0) {
-      const float R = sqrtf(__uint_as_float((uint32_t)(key >> 32))) * 1.001f;
+      const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
       const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
       const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
       const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
@@ -168,21 +168,23 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __res
         for (int32_t j = j0; j < j1; ++j) {
           const float4 v = g.pts[j];
           const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
-          const uint64_t kc = ((uint64_t)__float_as_uint(d2) << 32) |
-                              (uint64_t)(uint32_t)(off + __float_as_int(v.w));
-          key = kc < key ? kc : key;
+          if (d2 <= r2_hi)
+            near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(v.w))), d2);
         }
       }
     }
   }
 #pragma unroll
   for (int o = kGridLanes / 2; o > 0; o >>= 1) {
-    const uint32_t hi = __shfl_xor((uint32_t)(key >> 32), o, kGridLanes);
-    const uint32_t lo = __shfl_xor((uint32_t)key, o, kGridLanes);
-    const uint64_t other = ((uint64_t)hi << 32) | lo;
-    key = other < key ? other : key;
+    const uint64_t b1 = ((uint64_t)(uint32_t)__shfl_xor((int)(k1 >> 32), o, kGridLanes) << 32) |
+                        (uint32_t)__shfl_xor((int)(uint32_t)k1, o, kGridLanes);
+    const float bn2 = __shfl_xor(n2, o, kGridLanes);
+    near_merge(k1, k1d, n2, b1, bn2);
   }
-  if (t < ns && sub == 0) keys[i] = key == key0 ? kKeyNone : (int64_t)key;
+  if (t < ns && sub == 0) {
+    keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
+    near2[i] = __float_as_uint(n2);
+  }
 }
 
 // ------------------------------------------------------------------------------- host side
@@ -296,8 +298,9 @@ void grid_free(Grid* g) {
 }
 
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
-                          int64_t off, const IcpState* s, int64_t* keys, const int32_t* prev,
-                          const float4* tgt32, int64_t nt_shard, hipStream_t st) {
+                          int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
+                          const int32_t* prev, const int64_t* dprev, const float4* tgt32,
+                          int64_t nt_shard, hipStream_t st) {
   if (ns == 0) return hipSuccess;
   static const int L = [] {
     const char* e = getenv("M3D_GRID_LANES");
@@ -306,15 +309,15 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order,
   }();
   const unsigned blocks = (unsigned)((ns * L + kGridBlock - 1) / kGridBlock);
   if (L == 1)
-    grid_nn_kernel<1><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+    grid_nn_kernel<1><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
   else if (L == 2)
-    grid_nn_kernel<2><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+    grid_nn_kernel<2><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
   else if (L == 4)
-    grid_nn_kernel<4><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+    grid_nn_kernel<4><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
   else if (L == 8)
-    grid_nn_kernel<8><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+    grid_nn_kernel<8><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
   else
-    grid_nn_kernel<16><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, prev, tgt32, nt_shard);
+    grid_nn_kernel<16><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
   return hipGetLastError();
 }
 

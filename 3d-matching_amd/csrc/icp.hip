@@ -49,6 +49,7 @@ static int terms_pts() {
   return v;
 }
 constexpr double kU = 5.9604644775390625e-08;
+constexpr double kU64 = 1.1102230246251565e-16;
 
 
 // ------------------------------------------------------------------------------- state
@@ -73,7 +74,23 @@ __device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
     rowl1 = fmax(rowl1, fabs(r[0]) + fabs(r[1]) + fabs(r[2]));
     tinf = fmax(tinf, fabs(tp));
   }
-  const double E = 8.0 * kU * (rowl1 * pinf + tinf + qinf);
+  // E: per-coordinate bound on |fp32 query − fp64 query| + |fp32 target − fp64 target| in the
+  // centred frame: the fp32 roundings of p_c, R, t' and the three fmas (≤ 5u·Σ|r||p| + 4u|t'|),
+  // the target's u|t_c|, and the fp64 evaluation of the contract's query Q (nnkey.h q64_of) in
+  // absolute coordinates (≤ 4 roundings of 2⁻⁵³ of the magnitudes involved)
+  double tabs = 0.0, csinf = 0.0, ctinf = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    tabs = fmax(tabs, fabs(s->T[4 * i + 3]));
+    csinf = fmax(csinf, fabs(cs[i]));
+    ctinf = fmax(ctinf, fabs(ct[i]));
+  }
+  const double E = 8.0 * kU * (rowl1 * pinf + tinf + qinf) +
+                   8.0 * kU64 * (rowl1 * (csinf + pinf) + tabs + ctinf + qinf);
+  // nnkey.h: |√d2f − |Q − t|| ≤ e_q + 3u√d2f with e_q = √3·E; band_of's absolute term 2·e_q
+  const double eq = 1.7320508075688772 * E * 1.01;
+  const float eqf = __double2float_ru(eq), bef = __double2float_ru(2.0 * eq * 1.01);
+  s->eq = isfinite(eqf) ? eqf : FLT_MAX;
+  s->band_e = isfinite(bef) ? bef : FLT_MAX;
   const double r = sqrt(s->r2);
   const double e = 2.0 * (3.0 * kU * (r + 1.7320508075688772 * E) * (r + 1.7320508075688772 * E) +
                           2.0 * 1.7320508075688772 * E * r + 3.0 * E * E);
@@ -125,6 +142,7 @@ __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, do
   s->r2 = r2;
   s->bound_ok = 0;
   refresh_rt32(s, f);
+  s->eq_prev = s->eq;
 }
 
 // state for evaluating transform T (device, row-major 4×4): feature-RANSAC validation (a6)
@@ -138,6 +156,7 @@ __global__ void icp_set_T_kernel(IcpState* s, const double* __restrict__ T, doub
   s->r2 = r2;
   s->bound_ok = 0;  // keys/corr of another transform: no bound seeds until the next update
   refresh_rt32(s, f);
+  s->eq_prev = s->eq;
 }
 
 // ------------------------------------------------------------------------------- keyinit
@@ -146,8 +165,10 @@ __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__
                                                       int64_t nt_shard, int64_t off,
                                                       const IcpState* __restrict__ s,
                                                       const int32_t* __restrict__ prev,
-                                                      int64_t* __restrict__ keys) {
-  // keys ← seed_key (nnkey.h); on entry keys holds the previous evaluation's (reduced) keys
+                                                      const int64_t* __restrict__ dprev,
+                                                      int64_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ near2) {
+  // keys ← seed_key (nnkey.h), near2 ← none
   if (s->done) return;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= ns) return;
@@ -155,54 +176,53 @@ __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__
   const float4 p = src32[i];
   float x, y, z;
   xform32(Rt, p, x, y, z);
-  keys[i] = seed_key(s, i, p, x, y, z, tgt32, nt_shard, off, prev, keys);
+  keys[i] = seed_key(s, i, p, x, y, z, tgt32, nt_shard, off, prev, dprev);
+  near2[i] = kNearNone;
 }
 
 // ------------------------------------------------------------------------------- NN scan
+// fp32 VALU form of the brute-force scan (fallback: no MFMA tiles, M3D_NN_MFMA=0).  Per query
+// the scan state (k1, near2) of nnkey.h; the screen bound is search_bound(k1).
 template <int kNNQ>
 __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__ src32, int64_t ns,
                                                       const float4* __restrict__ tgt,
                                                       int64_t nt_pad, int64_t slice_len,
                                                       int64_t off, const IcpState* __restrict__ s,
-                                                      int64_t* __restrict__ keys) {
+                                                      int64_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ near2) {
   if (s->done) return;
   const float* Rt = s->Rt32;  // uniform → scalar loads (a local copy went to scratch)
-  const float r2_hi = s->r2_hi;
+  const float r2_hi = s->r2_hi, be = s->band_e;
   const float eps = s->screen_eps;
-  // per query: q (exact-path coordinates), a = −2q (screen), qq = |q|², bound `best` (+ index)
-  // and the screen threshold thr = best − qq + eps.
-  float qx[kNNQ], qy[kNNQ], qz[kNNQ], ax[kNNQ], ay[kNNQ], az[kNNQ], qq[kNNQ], best[kNNQ],
-      thr[kNNQ];
-  uint32_t bidx[kNNQ];
+  // per query: q (exact-path coordinates), a = −2q (screen), qq = |q|², scan state (k1, k1d,
+  // n2) and the screen threshold thr = search_bound(k1) − qq + eps (inactive: never fires)
+  float qx[kNNQ], qy[kNNQ], qz[kNNQ], ax[kNNQ], ay[kNNQ], az[kNNQ], qq[kNNQ], thr[kNNQ];
+  float k1d[kNNQ], n2[kNNQ];
+  uint64_t k1[kNNQ], k10[kNNQ];
   int64_t qi[kNNQ];
 #pragma unroll
   for (int q = 0; q < kNNQ; ++q) {
     const int64_t i = (int64_t)blockIdx.x * (kNNBlock * kNNQ) + q * kNNBlock + threadIdx.x;
     qi[q] = i;
+    n2[q] = kInf;
+    float X = -1.0f;
     if (i < ns) {
       xform32(Rt, src32[i], qx[q], qy[q], qz[q]);
       const int64_t key = keys[i];
-      if (key == kKeyNone) {
-        best[q] = r2_hi;
-        bidx[q] = 0xFFFFFFFFu;
-      } else {
-        best[q] = __uint_as_float((uint32_t)((uint64_t)key >> 32));
-        bidx[q] = (uint32_t)key;
-      }
+      k1[q] = key == kKeyNone ? make_key(r2_hi, 0xFFFFFFFFu) : (uint64_t)key;
+      X = search_bound(key_d2(k1[q]), be, r2_hi);
     } else {
-      qx[q] = qy[q] = qz[q] = 0.0f;  // inactive lane: negative bound, the screen never fires
-      best[q] = -1.0f;
-      bidx[q] = 0xFFFFFFFFu;
+      qx[q] = qy[q] = qz[q] = 0.0f;
+      k1[q] = (uint64_t)kKeyNone;
     }
+    k10[q] = k1[q];
+    k1d[q] = key_real_d2(k1[q]);
     ax[q] = -2.0f * qx[q];
     ay[q] = -2.0f * qy[q];
     az[q] = -2.0f * qz[q];
     qq[q] = fmaf(qz[q], qz[q], fmaf(qy[q], qy[q], qx[q] * qx[q]));
-    thr[q] = (best[q] - qq[q]) + eps;
+    thr[q] = X < 0.0f ? -FLT_MAX : (X - qq[q]) + eps;
   }
-  uint32_t bidx0[kNNQ];
-#pragma unroll
-  for (int q = 0; q < kNNQ; ++q) bidx0[q] = bidx[q];
   // Targets are staged through LDS (double-buffered tiles of kNNLds points): every wave reads
   // each target with one broadcast ds_read_b128 into VGPRs, so the FMAs have no SGPR operand
   // (an SGPR source costs 1.65x issue time on gfx950, tools/ubench_valu.hip).
@@ -225,7 +245,7 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
     const float4* tl = tile[buf];
     for (int sb = 0; sb < kNNLds; sb += kNNTile) {
       // Screen: key = |t|² − 2 q·t (3 FMA per pair, |t|² precomputed in t.w) differs from
-      // d² − |q|² by at most eps, so any target whose exact d² could reach `best` has
+      // d² − |q|² by at most eps, so any target whose exact d² could reach the search bound has
       // key ≤ thr.  Sub-tiles whose screen minimum stays above thr are skipped exactly.
       float m[kNNQ];
 #pragma unroll
@@ -245,18 +265,15 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
 #pragma unroll
       for (int q = 0; q < kNNQ; ++q) {
         if (__any(m[q] <= thr[q])) {
-          // exact path: direct fp32 d², lexicographic (d², index) update
+          // exact path: direct fp32 d², scan-state update
 #pragma unroll
           for (int k = 0; k < kNNTile; ++k) {
             const float4 t = tl[sb + k];
             const float d2 = d2f(qx[q], qy[q], qz[q], t.x, t.y, t.z);
-            const uint32_t gj = (uint32_t)(off + j0 + sb + k);
-            if (d2 < best[q] || (d2 == best[q] && gj < bidx[q])) {
-              best[q] = d2;
-              bidx[q] = gj;
-            }
+            if (d2 <= r2_hi)
+              near_push(k1[q], k1d[q], n2[q], make_key(d2, (uint32_t)(off + j0 + sb + k)), d2);
           }
-          thr[q] = (best[q] - qq[q]) + eps;
+          if (qi[q] < ns) thr[q] = (search_bound(key_d2(k1[q]), be, r2_hi) - qq[q]) + eps;
         }
       }
     }
@@ -268,12 +285,9 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
     buf ^= 1;
   }
 #pragma unroll
-  for (int q = 0; q < kNNQ; ++q) {
-    // every improvement changes the index (strict d² or strictly lower index on a tie)
-    if (qi[q] < ns && bidx[q] != bidx0[q]) {
-      atomicMin((unsigned long long*)&keys[qi[q]], (unsigned long long)make_key(best[q], bidx[q]));
-    }
-  }
+  for (int q = 0; q < kNNQ; ++q)
+    if (qi[q] < ns && (k1[q] != k10[q] || n2[q] < kInf))
+      near_publish((unsigned long long*)&keys[qi[q]], &near2[qi[q]], k1[q], n2[q], k1[q] != k10[q]);
 }
 
 // ------------------------------------------------------------------------------- NN, MFMA screen
@@ -413,18 +427,21 @@ __device__ __forceinline__ int64_t start_key(const SeedArgs& sa, const IcpState*
   return sa.on ? seed_key(s, i, p, qx, qy, qz, sa.tgt, sa.nt, off, sa.prev, nullptr) : keys[i];
 }
 
-__device__ __forceinline__ bool publish_key(const SeedArgs& sa, uint32_t bidx, uint32_t bidx0) {
-  return bidx != bidx0 || (sa.on && blockIdx.y == 0 && bidx != 0xFFFFFFFFu);
+// whether a block publishes its k1: it changed, or (self-seeding) the grid.y = 0 blocks publish
+// the seed every block started from
+__device__ __forceinline__ bool publish_k1(const SeedArgs& sa, uint64_t k1, uint64_t k10) {
+  return k1 != k10 || (sa.on && blockIdx.y == 0 && key_real(k1));
 }
 
 // Exact fallback of nn_mfma_kernel when the scaled operands do not fit fp16 (mfma_ok == 0, a
-// far-off transform): the same lexicographic (fp32 d², index) minimum over the block's slice by
-// a plain scan, one thread per query.  Keeps the fp32 VALU kernel off the launch path.
+// far-off transform): the same scan state over the block's slice by a plain scan, one thread
+// per query.  Keeps the fp32 VALU kernel off the launch path.
 template <int kMG>
 __device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
                               const int32_t* __restrict__ order, const float4* __restrict__ tgt32,
                               int64_t jb, int64_t je, int64_t off, const IcpState* __restrict__ s,
-                              int64_t* __restrict__ keys, const SeedArgs& sa) {
+                              int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
+                              const SeedArgs& sa) {
   const float* Rt = s->Rt32;
   const float r2_hi = s->r2_hi;
   for (int qs = threadIdx.x; qs < mqueries<kMG>(); qs += kMBlock) {
@@ -435,41 +452,41 @@ __device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
     const float4 p = src32[i];
     xform32(Rt, p, qx, qy, qz);
     const int64_t key = start_key(sa, s, i, p, qx, qy, qz, off, keys);  // keyinit's starting key
-    float best = key == kKeyNone ? r2_hi : __uint_as_float((uint32_t)((uint64_t)key >> 32));
-    uint32_t bidx = key == kKeyNone ? 0xFFFFFFFFu : (uint32_t)key;
-    const uint32_t bidx0 = bidx;
+    uint64_t k1 = key == kKeyNone ? make_key(r2_hi, 0xFFFFFFFFu) : (uint64_t)key;
+    float k1d = key_real_d2(k1), n2 = kInf;
+    const uint64_t k10 = k1;
     for (int64_t j = jb; j < je; ++j) {
       const float4 t = tgt32[j];
       if (__float_as_int(t.w) < 0) continue;  // pad
       const float d2 = d2f(qx, qy, qz, t.x, t.y, t.z);
-      const uint32_t gj = (uint32_t)(off + __float_as_int(t.w));
-      if (d2 < best || (d2 == best && gj < bidx)) {
-        best = d2;
-        bidx = gj;
-      }
+      if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(t.w))), d2);
     }
-    if (publish_key(sa, bidx, bidx0))
-      atomicMin((unsigned long long*)&keys[i], (unsigned long long)make_key(best, bidx));
+    const bool pk = publish_k1(sa, k1, k10);
+    if (pk || n2 < kInf) near_publish((unsigned long long*)&keys[i], &near2[i], k1, n2, pk);
   }
 }
 
 // Exact fp32 pass of nn_mfma_kernel over one flagged sub-tile (32 targets from `rows`), of which
-// this lane takes its 16 MFMA rows: direct d² and the lexicographic (d², index) update of
-// nn_kernel.  Pads: far coordinates, d² ~ 1e36.
+// this lane takes its 16 MFMA rows: direct d² pushed into the lane's scan state.  Pads: far
+// coordinates, d² ~ 1e36 > r2_hi.
 __device__ __forceinline__ void nn_exact_rows(const float4* __restrict__ rows, int64_t off, int h,
-                                              float qx, float qy, float qz, float& best,
-                                              uint32_t& bidx) {
+                                              float qx, float qy, float qz, float r2_hi,
+                                              uint64_t& k1, float& k1d, float& n2) {
   float4 t[16];  // all 16 loads in flight before the first use (one memory latency per sub-tile)
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) t[reg] = rows[(reg & 3) + 8 * (reg >> 2) + 4 * h];
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) {
     const float d2 = d2f(qx, qy, qz, t[reg].x, t[reg].y, t[reg].z);
-    const uint32_t gj = (uint32_t)(off + __float_as_int(t[reg].w));
-    const bool take = (d2 < best) | ((d2 == best) & (gj < bidx));
-    best = take ? d2 : best;
-    bidx = take ? gj : bidx;
+    const uint64_t kc = make_key(d2, (uint32_t)(off + __float_as_int(t[reg].w)));
+    if (d2 <= r2_hi) near_push(k1, k1d, n2, kc, d2);
   }
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 template <int kMG, int kTH>
@@ -482,6 +499,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           int64_t off,
                                                           const IcpState* __restrict__ s,
                                                           int64_t* __restrict__ keys,
+                                                          uint32_t* __restrict__ near2,
                                                           uint64_t exp_mask,
                                                           unsigned long long* __restrict__ stats,
                                                           int strided, SeedArgs sa) {
@@ -491,17 +509,20 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   if (s->done) return;
   if (!s->mfma_ok) {
     const int64_t jb = (int64_t)blockIdx.y * slice_len;
-    nn_slice_scan<kMG>(src32, ns, order, tgt32, jb, min(nt_pad, jb + slice_len), off, s, keys, sa);
+    nn_slice_scan<kMG>(src32, ns, order, tgt32, jb, min(nt_pad, jb + slice_len), off, s, keys,
+                       near2, sa);
     return;
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const float* Rt = s->Rt32;
-  const float r2_hi = s->r2_hi, eps = s->screen_eps_m, S = s->mfma_scale;
+  const float r2_hi = s->r2_hi, eps = s->screen_eps_m, S = s->mfma_scale, be = s->band_e;
   const float S2 = S * S;
-  float qx[kMG], qy[kMG], qz[kMG], qq[kMG], best[kMG];
+  float qx[kMG], qy[kMG], qz[kMG], qq[kMG];
   uint32_t force = 0;  // groups whose threshold exceeds the fp16 range: exact path everywhere
-  uint32_t bidx[kMG], bidx0[kMG];
+  uint32_t act = 0;    // groups whose query (column c) exists
+  uint64_t k1[kMG], k10[kMG];
+  float k1d[kMG], n2[kMG];
   int64_t qi[kMG];
   half8 bq[kMG];
 #pragma unroll
@@ -509,23 +530,21 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
     const int64_t slot = (int64_t)blockIdx.x * mqueries<kMG>() + (wave * kMG + g) * 32 + c;
     const int64_t i = slot < ns ? (order != nullptr ? (int64_t)order[slot] : slot) : ns;
     qi[g] = i;
+    n2[g] = kInf;
+    float X = -1.0f;  // inactive: negative threshold, never hits
     if (i < ns) {
       const float4 p = src32[i];
       xform32(Rt, p, qx[g], qy[g], qz[g]);
       const int64_t key = start_key(sa, s, i, p, qx[g], qy[g], qz[g], off, keys);
-      if (key == kKeyNone) {
-        best[g] = r2_hi;
-        bidx[g] = 0xFFFFFFFFu;
-      } else {
-        best[g] = __uint_as_float((uint32_t)((uint64_t)key >> 32));
-        bidx[g] = (uint32_t)key;
-      }
+      k1[g] = key == kKeyNone ? make_key(r2_hi, 0xFFFFFFFFu) : (uint64_t)key;
+      X = search_bound(key_d2(k1[g]), be, r2_hi);
+      act |= 1u << g;
     } else {
-      qx[g] = qy[g] = qz[g] = 0.0f;  // inactive: negative threshold, never hits
-      best[g] = -1.0f;
-      bidx[g] = 0xFFFFFFFFu;
+      qx[g] = qy[g] = qz[g] = 0.0f;
+      k1[g] = (uint64_t)kKeyNone;
     }
-    bidx0[g] = bidx[g];
+    k10[g] = k1[g];
+    k1d[g] = key_real_d2(k1[g]);
     qq[g] = fmaf(qz[g], qz[g], fmaf(qy[g], qy[g], qx[g] * qx[g]));
     _Float16 ah, al, bh, bl, ch, cl;
     split16(-2.0f * S * qx[g], ah, al);
@@ -535,7 +554,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
     bq[g] = h == 0 ? half8{ah, al, ah, bh, bl, bh, ch, cl} : half8{ch, one, one, zero, zero, zero, zero, zero};
     bool fg;
     half8 bt = bq[g];
-    thr_operand(bt, ((best[g] - qq[g]) + eps) * S2, fg);  // × power of two: exact
+    thr_operand(bt, X < 0.0f ? -1.0f : ((X - qq[g]) + eps) * S2, fg);  // × power of two: exact
     if (h == 1) bq[g] = bt;
     if (__any(fg)) force |= 0xFFu << (g * 8);
   }
@@ -620,17 +639,15 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
       while (mg != 0) {
         const int sub = __builtin_ctzll(mg);
         mg &= mg - 1;
-        nn_exact_rows(tgt32 + j0 + sub * 32, off, h, qx[g], qy[g], qz[g], best[g], bidx[g]);
-        const float ob = __shfl_xor(best[g], 32);
-        const uint32_t oi = (uint32_t)__shfl_xor((int)bidx[g], 32);
-        if (ob < best[g] || (ob == best[g] && oi < bidx[g])) {
-          best[g] = ob;
-          bidx[g] = oi;
-        }
+        nn_exact_rows(tgt32 + j0 + sub * 32, off, h, qx[g], qy[g], qz[g], r2_hi, k1[g], k1d[g], n2[g]);
+        const uint64_t o1 = shfl_xor64(k1[g], 32);
+        const float on2 = __shfl_xor(n2[g], 32);
+        near_merge(k1[g], k1d[g], n2[g], o1, on2);
       }
       bool fg;
       half8 bt = bq[g];
-      thr_operand(bt, ((best[g] - qq[g]) + eps) * S2, fg);
+      const float X = (act >> g) & 1u ? search_bound(key_d2(k1[g]), be, r2_hi) : -1.0f;
+      thr_operand(bt, X < 0.0f ? -1.0f : ((X - qq[g]) + eps) * S2, fg);
       if (h == 1) bq[g] = bt;  // the threshold only ever tightens: force stays as it was
     }
     if (has_next) {
@@ -644,9 +661,12 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
     buf ^= 1;
   }
 #pragma unroll
-  for (int g = 0; g < kMG; ++g)
-    if (h == 0 && qi[g] < ns && publish_key(sa, bidx[g], bidx0[g]))
-      atomicMin((unsigned long long*)&keys[qi[g]], (unsigned long long)make_key(best[g], bidx[g]));
+  for (int g = 0; g < kMG; ++g) {
+    if (h != 0 || qi[g] >= ns) continue;
+    const bool pk = publish_k1(sa, k1[g], k10[g]);
+    if (pk || n2[g] < kInf)
+      near_publish((unsigned long long*)&keys[qi[g]], &near2[qi[g]], k1[g], n2[g], pk);
+  }
 }
 
 // ------------------------------------------------------------------------------- terms
@@ -690,78 +710,103 @@ __device__ __forceinline__ double wave_transpose_sum32(const double (&v)[32], in
   return w1 + __shfl_xor(w1, 1, kWave);  // slot lane >> 1
 }
 
+// Inputs of the terms pass.  Winner of source i:
+//  * claim == nullptr (one device, or a source shard against the whole target): the fp64 winner
+//    decided from the scan keys (nnkey.h winner_fp64; ambiguous queries resolved over the
+//    target grid g);
+//  * claim != nullptr (target shard, after the two MIN exchanges of m3d_icp_shard_*): claim[i],
+//    the global winner (INT32_MAX none), whose fp64 d² every rank knows from dmin; the rank
+//    owning the target adds its terms.  dmin is kept in dprev for the next bound seeds.
+struct TermsArgs {
+  const double* src64;
+  const float4* src32;
+  int64_t ns;
+  const double* tgt64;
+  const double* nrm64;
+  int64_t nt_shard, off;
+  const int64_t* keys;
+  uint32_t* near2;
+  GridDev g;
+  const int32_t* claim;
+  const int64_t* dmin;
+  int64_t* dprev;
+  int32_t* corr;
+  int est;
+  double c[3];
+  int64_t* reset_keys;   // fused single-device loop: hand the keys back as kKeyNone
+};
+
 // est: M3D_EST_POINT_TO_PLANE → slots 0..20 JTJ (upper, row-major), 21..26 JTr, 27 Σr²
 //      M3D_EST_POINT_TO_POINT → slots 0..2 Σp_c, 3..5 Σq_c, 6..14 Σ p_c q_cᵀ (row-major)
 // both: 28 count, 29 Σd²  (c = source centre: identical on every shard)
 // kWT: write the block partial through to memory (sc1 store) for the fused last-block reduce
 template <bool kWT>
-__device__ __forceinline__ void terms_block(
-    const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
-    const double* __restrict__ nrm64, int64_t nt_shard, int64_t off,
-    const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
-    int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
-    double* __restrict__ partials, int pts, int64_t* __restrict__ reset_keys = nullptr) {
-  // reset_keys (= keys, fused single-device loop): each key is consumed here and set back to
-  // kKeyNone for the next evaluation's self-seeding NN (SeedArgs)
+__device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* __restrict__ s,
+                                            double* __restrict__ partials, int pts) {
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
   double acc[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) acc[k] = 0.0;
   for (int u = 0; u < pts; ++u) {
+    // every lane stays in the loop (resolve_wave is a whole-wave operation)
     const int64_t i = ((int64_t)blockIdx.x * pts + u) * kTermsBlock + threadIdx.x;
-    if (i >= ns) break;
-    const int64_t key = keys[i];
-    if (reset_keys != nullptr) reset_keys[i] = kKeyNone;
-    int32_t out = -1;
-    if (key != kKeyNone) {
-      const int64_t gj = (int64_t)(uint32_t)key;
-      if (sharded) out = (int32_t)gj;  // tentative hint; the owner decides validity
-      if (gj >= off && gj < off + nt_shard) {
-        const double* T = s->T;
-        const double* p = src64 + 3 * i;
-        const double vs[3] = {fma(T[2], p[2], fma(T[1], p[1], T[0] * p[0])) + T[3],
-                              fma(T[6], p[2], fma(T[5], p[1], T[4] * p[0])) + T[7],
-                              fma(T[10], p[2], fma(T[9], p[1], T[8] * p[0])) + T[11]};
-        const double* q = tgt64 + 3 * (gj - off);
-        const double d[3] = {vs[0] - q[0], vs[1] - q[1], vs[2] - q[2]};
-        const double d2 = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
-        if (d2 < s->r2) {
-          out = (int32_t)gj;
-          acc[28] += 1.0;
-          acc[29] += d2;
-          if (est == M3D_EST_POINT_TO_PLANE) {
-            const double* n = nrm64 + 3 * (gj - off);
-            const double r = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
-            double J[6];
-            cross3(vs, n, J);
-            J[3] = n[0];
-            J[4] = n[1];
-            J[5] = n[2];
-            int k = 0;
+    const bool valid = i < a.ns;
+    const int64_t ii = valid ? i : 0;
+    const double* p = a.src64 + 3 * ii;
+    double vs[3];
+    q64_of(s->T, p, vs);
+    int64_t gj = -1;
+    double d2 = 0.0;
+    if (a.claim == nullptr) {
+      const uint64_t k1 = valid ? (uint64_t)a.keys[ii] : (uint64_t)kKeyNone;
+      const float n2 = valid ? __uint_as_float(a.near2[ii]) : kInf;
+      if (valid && a.reset_keys != nullptr) {
+        a.reset_keys[ii] = kKeyNone;
+        a.near2[ii] = kNearNone;
+      }
+      winner_fp64(valid, k1, n2, s, a.g, a.tgt64, a.off, a.nt_shard, a.src32[ii], vs, gj, d2);
+    } else if (valid) {
+      const int32_t cj = a.claim[ii];
+      if (cj != 0x7FFFFFFF) {
+        gj = cj;
+        d2 = __longlong_as_double(a.dmin[ii]);
+      }
+      if (a.dprev != nullptr) a.dprev[ii] = a.dmin[ii];
+    }
+    if (!valid) continue;
+    if (a.corr != nullptr) a.corr[i] = (int32_t)gj;
+    if (gj < a.off || gj >= a.off + a.nt_shard) continue;  // none, or another shard's target
+    const double* q = a.tgt64 + 3 * (gj - a.off);
+    const double d[3] = {vs[0] - q[0], vs[1] - q[1], vs[2] - q[2]};
+    acc[28] += 1.0;
+    acc[29] += d2;
+    if (a.est == M3D_EST_POINT_TO_PLANE) {
+      const double* n = a.nrm64 + 3 * (gj - a.off);
+      const double r = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
+      double J[6];
+      cross3(vs, n, J);
+      J[3] = n[0];
+      J[4] = n[1];
+      J[5] = n[2];
+      int k = 0;
 #pragma unroll
-            for (int a = 0; a < 6; ++a)
+      for (int x = 0; x < 6; ++x)
 #pragma unroll
-              for (int b = a; b < 6; ++b) acc[k++] += J[a] * J[b];
+        for (int y = x; y < 6; ++y) acc[k++] += J[x] * J[y];
 #pragma unroll
-            for (int a = 0; a < 6; ++a) acc[21 + a] += J[a] * r;
-            acc[27] += r * r;
-          } else {
-            const double pc[3] = {vs[0] - c0, vs[1] - c1, vs[2] - c2};
-            const double qc[3] = {q[0] - c0, q[1] - c1, q[2] - c2};
+      for (int x = 0; x < 6; ++x) acc[21 + x] += J[x] * r;
+      acc[27] += r * r;
+    } else {
+      const double pc[3] = {vs[0] - a.c[0], vs[1] - a.c[1], vs[2] - a.c[2]};
+      const double qc[3] = {q[0] - a.c[0], q[1] - a.c[1], q[2] - a.c[2]};
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-              acc[a] += pc[a];
-              acc[3 + a] += qc[a];
+      for (int x = 0; x < 3; ++x) {
+        acc[x] += pc[x];
+        acc[3 + x] += qc[x];
 #pragma unroll
-              for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] += pc[a] * qc[b];
-            }
-          }
-        } else if (!sharded) {
-          out = -1;
-        }
+        for (int y = 0; y < 3; ++y) acc[6 + 3 * x + y] += pc[x] * qc[y];
       }
     }
-    if (corr != nullptr && (!sharded || out >= 0 || key == kKeyNone)) corr[i] = out;
   }
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   {
@@ -785,15 +830,50 @@ __device__ __forceinline__ void terms_block(
   }
 }
 
-__global__ __launch_bounds__(kTermsBlock) void terms_kernel(
-    const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
-    const double* __restrict__ nrm64, int64_t nt_shard, int64_t off,
-    const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
-    int32_t* __restrict__ corr, int est, double c0, double c1, double c2, int sharded,
-    double* __restrict__ partials, int pts) {
+__global__ __launch_bounds__(kTermsBlock) void terms_kernel(TermsArgs a, const IcpState* __restrict__ s,
+                                                            double* __restrict__ partials, int pts) {
   if (s->done) return;
-  terms_block<false>(src64, ns, tgt64, nrm64, nt_shard, off, s, keys, corr, est, c0, c1, c2,
-                     sharded, partials, pts);
+  terms_block<false>(a, s, partials, pts);
+}
+
+// Target-sharded evaluation, step 1 (m3d_icp_shard_nn): this shard's fp64 winner of every query
+// (winner_fp64 over the shard's targets) → lidx / ld64 and the exchange key dkey = bits(d64)
+// (INT64_MAX none; d64 ≥ +0, so the integer MIN over ranks is the fp64 minimum).
+__global__ __launch_bounds__(256) void shard_winner_kernel(
+    const double* __restrict__ src64, const float4* __restrict__ src32, int64_t ns,
+    const double* __restrict__ tgt64, int64_t nt_shard, int64_t off, GridDev g,
+    const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
+    const uint32_t* __restrict__ near2, int32_t* __restrict__ lidx, int64_t* __restrict__ ld64,
+    int64_t* __restrict__ dkey) {
+  if (s->done) return;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = i0 < ns;
+  const int64_t i = valid ? i0 : 0;
+  double Q[3];
+  q64_of(s->T, src64 + 3 * i, Q);
+  int64_t gj;
+  double d;
+  winner_fp64(valid, valid ? (uint64_t)keys[i] : (uint64_t)kKeyNone,
+              valid ? __uint_as_float(near2[i]) : kInf, s, g, tgt64, off, nt_shard, src32[i], Q, gj, d);
+  if (!valid) return;
+  const int64_t k = gj >= 0 ? __double_as_longlong(d) : kKeyNone;
+  lidx[i] = (int32_t)gj;
+  ld64[i] = k;
+  dkey[i] = k;
+}
+
+// Step 2 (m3d_icp_shard_claim): after MIN(dkey) over ranks, the ranks whose own winner has the
+// global minimum d64 claim it with their target index; MIN(claim) over ranks then breaks exact
+// fp64 ties between shards by the lowest index (the lexicographic (d64, index) minimum).
+__global__ __launch_bounds__(256) void shard_claim_kernel(int64_t ns, const IcpState* __restrict__ s,
+                                                          const int32_t* __restrict__ lidx,
+                                                          const int64_t* __restrict__ ld64,
+                                                          const int64_t* __restrict__ dmin,
+                                                          int32_t* __restrict__ claim) {
+  if (s->done) return;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= ns) return;
+  claim[i] = (lidx[i] >= 0 && ld64[i] == dmin[i]) ? lidx[i] : 0x7FFFFFFF;
 }
 
 // ------------------------------------------------------------------------------- reduce
@@ -870,6 +950,7 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
   // the search transform of the evaluation just reduced: seed_key's bound for the next one
   for (int k = 0; k < 12; ++k) s->Rt32_prev[k] = s->Rt32[k];
+  s->eq_prev = s->eq;
   s->bound_ok = sp.f.shared;  // bounds compare keys across ranks: only in a shared frame
   if (count > 0.0) {
     if (sp.est == M3D_EST_POINT_TO_PLANE) {
@@ -923,15 +1004,12 @@ __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restri
 // block whose add returned nblocks − 1 reads every partial with sc1 loads.  No L2 write-back or
 // invalidate fences are needed.
 __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
-    const double* __restrict__ src64, int64_t ns, const double* __restrict__ tgt64,
-    const double* __restrict__ nrm64, int64_t nt, IcpState* s, const int64_t* __restrict__ keys,
-    int32_t* __restrict__ corr, double* partials, int64_t nblocks, double* __restrict__ sums,
-    SolveParams sp, int pts, int64_t off, int sharded, int do_solve, int64_t* reset_keys) {
+    TermsArgs a, IcpState* s, double* partials, int64_t nblocks, double* __restrict__ sums,
+    SolveParams sp, int pts, int do_solve) {
   // do_solve = 0: the sharded tail (m3d_icp_shard_terms) — terms + the fixed-order reduce into
   // `sums` in one launch; the caller all-reduces them and runs m3d_icp_solve
   if (s->done) return;
-  terms_block<true>(src64, ns, tgt64, nrm64, nt, off, s, keys, corr, sp.est, sp.c[0], sp.c[1],
-                    sp.c[2], sharded, partials, pts, reset_keys);
+  terms_block<true>(a, s, partials, pts);
   __shared__ double red[kReduceGroups][kTermSlots];
   __shared__ int last;
   // the partial went out write-through (sc1): drain it, then one lane takes the ticket
@@ -986,35 +1064,29 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
   }
 }
 
-// finalize standalone NN (m3d_nn1): exact radius test in fp64
+// finalize standalone NN (m3d_nn1): the fp64 winner (nnkey.h winner_fp64) and its d64
 __global__ __launch_bounds__(256) void nn_finalize_kernel(const double* __restrict__ src64,
+                                                          const float4* __restrict__ src32,
                                                           int64_t ns,
                                                           const double* __restrict__ tgt64,
+                                                          int64_t nt, GridDev g,
                                                           const IcpState* __restrict__ s,
                                                           const int64_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ near2,
                                                           int32_t* __restrict__ idx,
                                                           double* __restrict__ d2out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= ns) return;
-  const int64_t key = keys[i];
-  int32_t o = -1;
-  double dd = INFINITY;
-  if (key != kKeyNone) {
-    const int64_t j = (int64_t)(uint32_t)key;
-    const double* T = s->T;
-    const double* p = src64 + 3 * i;
-    const double* q = tgt64 + 3 * j;
-    const double dx = fma(T[2], p[2], fma(T[1], p[1], T[0] * p[0])) + T[3] - q[0];
-    const double dy = fma(T[6], p[2], fma(T[5], p[1], T[4] * p[0])) + T[7] - q[1];
-    const double dz = fma(T[10], p[2], fma(T[9], p[1], T[8] * p[0])) + T[11] - q[2];
-    const double d2 = (dx * dx + dy * dy) + dz * dz;
-    if (d2 < s->r2) {
-      o = (int32_t)j;
-      dd = d2;
-    }
-  }
-  idx[i] = o;
-  if (d2out != nullptr) d2out[i] = dd;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = i0 < ns;
+  const int64_t i = valid ? i0 : 0;
+  double Q[3];
+  q64_of(s->T, src64 + 3 * i, Q);
+  int64_t gj;
+  double d;
+  winner_fp64(valid, valid ? (uint64_t)keys[i] : (uint64_t)kKeyNone,
+              valid ? __uint_as_float(near2[i]) : kInf, s, g, tgt64, 0, nt, src32[i], Q, gj, d);
+  if (!valid) return;
+  idx[i] = (int32_t)gj;
+  if (d2out != nullptr) d2out[i] = gj >= 0 ? d : INFINITY;
 }
 
 __global__ void keys_to_idx_kernel(const int64_t* __restrict__ keys, int64_t n,
@@ -1053,7 +1125,8 @@ hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t off, hipStream_t st) {
   const int64_t ns = s->src->n;
   if (ns == 0) return hipSuccess;
   keyinit_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(
-      s->src->xyz32, ns, s->tgt->xyz32, s->tgt->n, off, s->state, s->corr, s->keys);
+      s->src->xyz32, ns, s->tgt->xyz32, s->tgt->n, off, s->state, s->corr, s->dprev, s->keys,
+      s->near2);
   return hipGetLastError();
 }
 
@@ -1166,7 +1239,7 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
 #define M3D_NN_LAUNCH(MGV, THV)                                                                  \
   nn_mfma_kernel<MGV, THV><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,         \
                                                    tg->mf32, tg->mf_npad, slice, off, s->state,    \
-                                                   s->keys, exp_mask, nn_stats, strided, sa)
+                                                   s->keys, s->near2, exp_mask, nn_stats, strided, sa)
     if (MG == 4) {
       if (TH == 2) M3D_NN_LAUNCH(4, 2); else M3D_NN_LAUNCH(4, 1);
     } else if (MG == 2) {
@@ -1191,22 +1264,44 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
   const dim3 grid = nn_grid((ns + kNNBlock * Q - 1) / (kNNBlock * Q), nt_pad, kNNLds, &slice);
   const float4* tp = s->tgt->xyz32;
   if (Q == 4)
-    nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
+    nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, s->near2);
   else if (Q == 2)
-    nn_kernel<2><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
+    nn_kernel<2><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, s->near2);
   else
-    nn_kernel<1><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys);
+    nn_kernel<1><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, s->near2);
   return hipGetLastError();
 }
 
 
-hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, int sharded, hipStream_t st) {
+static TermsArgs terms_args(const m3d_icp* s, int64_t off, const int32_t* claim,
+                            const int64_t* dmin, bool reset_keys) {
+  TermsArgs a;
+  a.src64 = s->src->xyz64;
+  a.src32 = s->src->xyz32;
+  a.ns = s->src->n;
+  a.tgt64 = s->tgt->xyz64;
+  a.nrm64 = s->tgt->nrm64;
+  a.nt_shard = s->tgt->n;
+  a.off = off;
+  a.keys = s->keys;
+  a.near2 = s->near2;
+  a.g = s->tgrid->dev;
+  a.claim = claim;
+  a.dmin = dmin;
+  a.dprev = claim != nullptr ? s->dprev : nullptr;
+  a.corr = s->corr;
+  a.est = s->params.estimation;
+  for (int k = 0; k < 3; ++k) a.c[k] = s->src->center[k];
+  a.reset_keys = reset_keys ? s->keys : nullptr;
+  return a;
+}
+
+hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* claim,
+                                 const int64_t* dmin, hipStream_t st) {
   const int64_t ns = s->src->n;
   if (ns == 0) return hipMemsetAsync(s->partials, 0, sizeof(double) * kTermSlots, st);
-  terms_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
-      s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, off, s->state, s->keys, s->corr,
-      s->params.estimation, s->src->center[0], s->src->center[1], s->src->center[2], sharded,
-      s->partials, terms_pts());
+  terms_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(terms_args(s, off, claim, dmin, false),
+                                                             s->state, s->partials, terms_pts());
   return hipGetLastError();
 }
 
@@ -1227,18 +1322,19 @@ static SolveParams solve_params(const m3d_icp* s) {
   return sp;
 }
 
-// sharded tail: terms (sharded semantics, shard offset off) + reduce into sums, one launch
-hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, bool reset_keys,
+// sharded tail: terms (shard offset off; claim/dmin: the target-shard exchange results, or null
+// for a source shard) + reduce into sums, one launch
+hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, const int32_t* claim,
+                                   const int64_t* dmin, double* sums, bool reset_keys,
                                    hipStream_t st) {
   const int64_t ns = s->src->n;
   if (ns == 0) {
-    hipError_t e = launch_icp_terms_mode(s, off, 1, st);
+    hipError_t e = launch_icp_terms_mode(s, off, claim, dmin, st);
     return e == hipSuccess ? launch_icp_reduce(s, sums, st) : e;
   }
   terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
-      s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
-      s->partials, s->nblocks, sums, solve_params(s), terms_pts(), off, 1, 0,
-      reset_keys ? s->keys : nullptr);
+      terms_args(s, off, claim, dmin, reset_keys), s->state, s->partials, s->nblocks, sums,
+      solve_params(s), terms_pts(), 0);
   return hipGetLastError();
 }
 
@@ -1250,23 +1346,39 @@ hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st
 hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t st) {
   const int64_t ns = s->src->n;
   if (ns == 0) {  // no blocks to take tickets: the unfused tail handles the empty source
-    hipError_t e = launch_icp_terms_mode(s, 0, 0, st);
+    hipError_t e = launch_icp_terms_mode(s, 0, nullptr, nullptr, st);
     if (e == hipSuccess) e = launch_icp_reduce(s, s->sums, st);
     return e == hipSuccess ? launch_icp_solve(s, s->sums, st) : e;
   }
   terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
-      s->src->xyz64, ns, s->tgt->xyz64, s->tgt->nrm64, s->tgt->n, s->state, s->keys, s->corr,
-      s->partials, s->nblocks, s->sums, solve_params(s), terms_pts(), (int64_t)0, 0, 1,
-      reset_keys ? s->keys : nullptr);
+      terms_args(s, 0, nullptr, nullptr, reset_keys), s->state, s->partials, s->nblocks, s->sums,
+      solve_params(s), terms_pts(), 1);
   return hipGetLastError();
 }
 
 hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStream_t st) {
   const int64_t ns = s->src->n;
   if (ns == 0) return hipSuccess;
-  nn_finalize_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(s->src->xyz64, ns,
-                                                                   s->tgt->xyz64, s->state,
-                                                                   s->keys, idx, d2);
+  nn_finalize_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(
+      s->src->xyz64, s->src->xyz32, ns, s->tgt->xyz64, s->tgt->n, s->tgrid->dev, s->state, s->keys,
+      s->near2, idx, d2);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hipStream_t st) {
+  const int64_t ns = s->src->n;
+  if (ns == 0) return hipSuccess;
+  shard_winner_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(
+      s->src->xyz64, s->src->xyz32, ns, s->tgt->xyz64, s->tgt->n, off, s->tgrid->dev, s->state,
+      s->keys, s->near2, s->lidx, s->ld64, dkey);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_claim(const m3d_icp* s, const int64_t* dmin, int32_t* claim, hipStream_t st) {
+  const int64_t ns = s->src->n;
+  if (ns == 0) return hipSuccess;
+  shard_claim_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(ns, s->state, s->lidx, s->ld64,
+                                                                   dmin, claim);
   return hipGetLastError();
 }
 

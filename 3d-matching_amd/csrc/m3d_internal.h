@@ -72,6 +72,9 @@ struct IcpState {
   uint32_t ticket;    // fused terms→reduce→solve: blocks done this iteration (last one resets)
   float Rt32_prev[12];  // Rt32 of the previous evaluation (nnkey.h seed_key bounds)
   int32_t bound_ok;     // Rt32_prev, keys and corr belong to the previous evaluation
+  float band_e;         // 2·e_q·1.01: absolute term of nnkey.h band_of (fp32 → fp64 ambiguity)
+  float eq;             // e_q: bound on |fp32 distance − fp64 distance| for the current T
+  float eq_prev;        // e_q of the previous evaluation (seed_key bounds)
 };
 
 // Uniform grid over a cloud's centred fp32 points (grid.hip): kernel view + owner.
@@ -154,7 +157,11 @@ struct m3d_icp {
   m3d_icp_params params{};
   double max_dist = 0.0;
   m3d::IcpState* state = nullptr;  // device
-  int64_t* keys = nullptr;         // ns packed NN keys
+  int64_t* keys = nullptr;         // ns packed NN keys: k1 = (d2f, index) minimum of the scan
+  uint32_t* near2 = nullptr;       // ns: bits of the smallest d2f of any other target evaluated
+  int64_t* dprev = nullptr;        // ns: target-sharded loops, bits of the global winner's d64
+  int64_t* ld64 = nullptr;         // ns: target-sharded loops, bits of this shard's winner's d64
+  int32_t* lidx = nullptr;         // ns: target-sharded loops, this shard's fp64 winner (-1 none)
   bool keys_clean = false;         // host view: every key is kKeyNone (fused tail reset them)
   int32_t* corr = nullptr;         // ns current correspondence (-1 none)
   double* partials = nullptr;      // nblocks × kTermSlots
@@ -233,15 +240,22 @@ hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* 
 hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_t st);
 hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, bool self_seed, hipStream_t st);
 hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st);
-hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, double* sums, bool reset_keys,
+// claim/dmin: target-shard exchange results (m3d_icp_shard_claim), or null
+hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* claim,
+                                 const int64_t* dmin, hipStream_t st);
+hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, const int32_t* claim,
+                                   const int64_t* dmin, double* sums, bool reset_keys,
                                    hipStream_t st);
+hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hipStream_t st);
+hipError_t launch_shard_claim(const m3d_icp* s, const int64_t* dmin, int32_t* claim, hipStream_t st);
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g);
 void grid_free(Grid* g);
-// prev/tgt32/nt_shard: seed each query with seed_key (nnkey.h); prev == nullptr: no seeds
+// prev/dprev/tgt32/nt_shard: seed each query with seed_key (nnkey.h); prev == nullptr: no seeds
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
-                          int64_t off, const IcpState* s, int64_t* keys, const int32_t* prev,
-                          const float4* tgt32, int64_t nt_shard, hipStream_t st);
+                          int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
+                          const int32_t* prev, const int64_t* dprev, const float4* tgt32,
+                          int64_t nt_shard, hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
 hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st);
 hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st);

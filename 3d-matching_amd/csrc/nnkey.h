@@ -1,6 +1,22 @@
-// nnkey.h — the fp32 query/distance expressions and packed keys shared by every NN kernel
-// (icp.hip nn_kernel / nn_mfma_kernel / keyinit, grid.hip grid_nn_kernel), so that all of them
-// compute bit-identical (d², index) keys.
+// nnkey.h — the fp32 query/distance expressions, packed keys and the fp64 resolution shared by
+// every NN kernel (icp.hip nn_mfma_kernel / nn_kernel / keyinit / terms, grid.hip grid_nn_kernel).
+//
+// Result contract (Open3D KDTreeFlann::SearchHybrid(p, r, 1) in fp64): for each
+// source point the lexicographic (d64, index) minimum over the targets with d64 < r², where
+//   Q   = T·p in fp64 in Eigen's (non-FMA) order: ((T00·px + T01·py) + T02·pz) + T03  (q64_of)
+//   d64 = ((dx·dx + dy·dy) + dz·dz), d = Q − t in fp64                                 (d2_64)
+// (oracle/icp_oracle.py uses the same expressions in numpy).  The kernels search in fp32 on
+// centred coordinates: d2f = the fp32 d² of the fp32 query and target.  Two values per query
+// come out of the scan: the key k1 = the lexicographic (d2f, index) minimum, and near2 = the
+// smallest d2f of any OTHER target the scan evaluated (+inf none).  The fp64 winner can differ
+// from k1 only if some other target lies inside the error band of k1 (band_of), which the scan
+// always evaluates, so
+//   near2 ≤ band_of(d2f(k1))  ⇔  "ambiguous": re-evaluate in fp64 (resolve_wave)
+//   otherwise                     the winner is k1's target (if its d64 < r²).
+// Error bound (refresh_rt32): |√d2f − |Q − t|| ≤ e_q + 3u·√d2f, e_q = √3·E with E a
+// per-coordinate bound on the fp32 query/target rounding plus the fp64 evaluation of Q.  If
+// d64(c) ≤ d64(w) then √d2f(c) ≤ (√d2f(w)(1 + 3u) + e_q)(1 + 5ε) + e_q)(1 + 3u), which
+// band_of(d2f(w)) over-covers (×(1 + 4e-6) on the root and on the square, 2·e_q·1.01 absolute).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -22,46 +38,209 @@ __device__ __forceinline__ void xform32(const float* Rt, float4 p, float& x, flo
   z = fmaf(Rt[6], p.x, fmaf(Rt[7], p.y, fmaf(Rt[8], p.z, Rt[11])));
 }
 
+// the fp64 query of the contract (Open3D PointCloud::Transform, Eigen non-FMA order; the
+// library is built with -ffp-contract=off, so these products and sums are not fused)
+__device__ __forceinline__ void q64_of(const double* __restrict__ T, const double* __restrict__ p,
+                                       double q[3]) {
+  q[0] = ((T[0] * p[0] + T[1] * p[1]) + T[2] * p[2]) + T[3];
+  q[1] = ((T[4] * p[0] + T[5] * p[1]) + T[6] * p[2]) + T[7];
+  q[2] = ((T[8] * p[0] + T[9] * p[1]) + T[10] * p[2]) + T[11];
+}
+
+__device__ __forceinline__ double d2_64(const double q[3], const double* __restrict__ t) {
+  const double dx = q[0] - t[0], dy = q[1] - t[1], dz = q[2] - t[2];
+  return (dx * dx + dy * dy) + dz * dz;
+}
+
 // (bits(d²) << 32) | index: for d² ≥ +0 the integer order is the lexicographic (d², index) order
 __device__ __forceinline__ uint64_t make_key(float d2, uint32_t j) {
   return ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)j;
 }
+__device__ __forceinline__ float key_d2(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
+// a key naming a target (not kKeyNone, not a radius or distance-bound pseudo key)
+__device__ __forceinline__ bool key_real(uint64_t k) { return (uint32_t)k != 0xFFFFFFFFu; }
 
-// Starting key of query i (source point p, current fp32 query q) for the lexicographic
-// (fp32 d², index) minimum over the targets with d² ≤ r2_hi that every NN kernel computes.
-// prev[i] = j is the previous correspondence (the winner of the last evaluation; −1 none):
-//  * j in this shard: the candidate (d2f(q, t_j), j) itself — exact, it is one of the targets,
-//    so the search only has to look for something smaller;
+// The fp32 band around a best d2f inside which another target may still win in fp64.
+__device__ __forceinline__ float band_of(float d2, float be) {
+  const float s = fmaf(sqrtf(d2), 1.000004f, be);
+  return s * s * 1.000004f;
+}
+// the fp32 search bound a query with current best `d2` screens against
+__device__ __forceinline__ float search_bound(float d2, float be, float r2_hi) {
+  return d2 < 0.0f ? d2 : fminf(band_of(d2, be), r2_hi);
+}
+
+constexpr float kInf = __builtin_huge_valf();
+constexpr uint32_t kNearNone = 0x7F800000u;  // bits of +inf: "no other target evaluated"
+
+// d2f of a key that names a target, +inf for kKeyNone and pseudo keys
+__device__ __forceinline__ float key_real_d2(uint64_t k) { return key_real(k) ? key_d2(k) : kInf; }
+
+// Scan state of one query: k1 (lexicographic (d2f, index) minimum), k1d = key_real_d2(k1), and
+// near2 = min d2f over the evaluated targets other than k1's.  Push a candidate target key kc
+// with d2f d2c (a real target; kc == k1 only when the seed's target is met again).  Branch-free.
+__device__ __forceinline__ void near_push(uint64_t& k1, float& k1d, float& near2, uint64_t kc,
+                                          float d2c) {
+  const bool lt = kc < k1;
+  const float dd = lt ? k1d : (kc == k1 ? kInf : d2c);  // the value not kept as k1
+  k1 = lt ? kc : k1;
+  k1d = lt ? d2c : k1d;
+  near2 = fminf(near2, dd);
+}
+// merge another state (b1, bn2) of the same query into (k1, k1d, near2)
+__device__ __forceinline__ void near_merge(uint64_t& k1, float& k1d, float& near2, uint64_t b1,
+                                           float bn2) {
+  near_push(k1, k1d, near2, b1, key_real_d2(b1));
+  near2 = fminf(near2, bn2);
+}
+// Publish a block's (k1, near2) into the global (keys, near2g) such that, after every block has
+// published, keys = the minimum of all published keys and near2g = the minimum d2f of the
+// published real keys other than it and of the published near2: the key an atomicMin on keys
+// rejects or displaces goes to near2g.  publish_k1 = false: k1 is already in keys (an unchanged
+// seed).  near2g holds float bits (d2f ≥ +0: the unsigned order is the float order).
+__device__ __forceinline__ void near_publish(unsigned long long* keys, unsigned int* near2g,
+                                             uint64_t k1, float near2, bool publish_k1) {
+  float n2 = near2;
+  if (publish_k1) {
+    const uint64_t old = atomicMin(keys, (unsigned long long)k1);
+    if (old != k1) n2 = fminf(n2, key_real_d2(old > k1 ? old : k1));
+  }
+  if (n2 < kInf) atomicMin(near2g, __float_as_uint(n2));
+}
+
+__device__ __forceinline__ int grid_coord(float x, float o, float inv_h, int n) {
+  float f = (x - o) * inv_h;
+  f = fminf(fmaxf(f, 0.0f), (float)(n - 1));
+  return (int)f;
+}
+
+// Exact fp64 decision for the ambiguous queries of a wave (every lane of the wave calls it, with
+// amb set on the lanes whose query needs it).  For each such query the whole wave scans the
+// cell box of q ± 1.001·√X (grid.hip header lemma: it holds every target with d2f ≤ X), lanes
+// split over the box's (y, z) rows and the points of a row; every target with d2f(q, t) ≤ X is
+// re-evaluated with the contract's fp64 d² from its fp64 coordinates, and a butterfly takes the
+// lexicographic (d64, global index) minimum among d64 < r2 (bj = −1: none).
+__device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
+                                             const double* __restrict__ tgt64, int64_t off,
+                                             float qx, float qy, float qz, float X,
+                                             const double Q[3], double r2, int64_t& bj,
+                                             double& bd) {
+  const int lane = threadIdx.x & (kWave - 1);
+  uint64_t m = __ballot(amb);
+  while (m != 0) {
+    const int L = __builtin_ctzll(m);
+    m &= m - 1;
+    const float lx = __shfl(qx, L), ly = __shfl(qy, L), lz = __shfl(qz, L), lX = __shfl(X, L);
+    const double Q0 = __shfl(Q[0], L), Q1 = __shfl(Q[1], L), Q2 = __shfl(Q[2], L);
+    double dl = kInf;
+    int64_t jl = INT64_MAX;
+    if (g.ncells > 0 && lX >= 0.0f) {
+      const float R = sqrtf(lX) * 1.001f;
+      const int x0 = grid_coord(lx - R, g.o[0], g.inv_h, g.n[0]);
+      const int x1 = grid_coord(lx + R, g.o[0], g.inv_h, g.n[0]);
+      const int y0 = grid_coord(ly - R, g.o[1], g.inv_h, g.n[1]);
+      const int y1 = grid_coord(ly + R, g.o[1], g.inv_h, g.n[1]);
+      const int z0 = grid_coord(lz - R, g.o[2], g.inv_h, g.n[2]);
+      const int z1 = grid_coord(lz + R, g.o[2], g.inv_h, g.n[2]);
+      const int ny = y1 - y0 + 1;
+      const int rows = ny * (z1 - z0 + 1);
+      const int lpr = rows >= kWave ? 1 : kWave / rows;  // lanes per row
+      const int rstep = kWave / lpr;
+      for (int r = lane / lpr; r < rows; r += rstep) {
+        const int cz = z0 + r / ny, cy = y0 + r % ny;
+        const int64_t row = ((int64_t)cz * g.n[1] + cy) * g.n[0];
+        const int32_t j1 = g.start[row + x1 + 1];
+        for (int32_t j = g.start[row + x0] + lane % lpr; j < j1; j += lpr) {
+          const float4 v = g.pts[j];
+          if (!(d2f(lx, ly, lz, v.x, v.y, v.z) <= lX)) continue;
+          const int64_t lj = (int64_t)__float_as_int(v.w);
+          const double* t = tgt64 + 3 * lj;
+          const double dx = Q0 - t[0], dy = Q1 - t[1], dz = Q2 - t[2];
+          const double d = (dx * dx + dy * dy) + dz * dz;
+          const int64_t gj = off + lj;
+          if (d < r2 && (d < dl || (d == dl && gj < jl))) {
+            dl = d;
+            jl = gj;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const double od = __shfl_xor(dl, o);
+      const int64_t oj = __shfl_xor(jl, o);
+      if (od < dl || (od == dl && oj < jl)) {
+        dl = od;
+        jl = oj;
+      }
+    }
+    if (lane == L) {
+      bj = jl == INT64_MAX ? -1 : jl;
+      bd = dl;
+    }
+  }
+}
+
+// The fp64 winner of query i from its scan results (k1, near2) — see the header.  Q = its fp64
+// query, p32 its centred fp32 source point.  Called by every lane of the wave (valid = the lane
+// has a query).
+__device__ __forceinline__ void winner_fp64(bool valid, uint64_t k1, float near2,
+                                            const IcpState* __restrict__ s, const GridDev& g,
+                                            const double* __restrict__ tgt64, int64_t off,
+                                            int64_t nt_shard, const float4& p32, const double Q[3],
+                                            int64_t& bj, double& bd) {
+  bj = -1;
+  bd = 0.0;
+  const float X = valid && k1 != (uint64_t)kKeyNone ? search_bound(key_d2(k1), s->band_e, s->r2_hi)
+                                                    : -1.0f;
+  const bool amb = X >= 0.0f && near2 <= X;
+  float qx = 0.0f, qy = 0.0f, qz = 0.0f;
+  if (amb) xform32(s->Rt32, p32, qx, qy, qz);
+  resolve_wave(amb, g, tgt64, off, qx, qy, qz, X, Q, s->r2, bj, bd);
+  if (amb || !valid || !key_real(k1)) return;
+  const int64_t gj = (int64_t)(uint32_t)k1;
+  if (gj < off || gj >= off + nt_shard) return;
+  const double d = d2_64(Q, tgt64 + 3 * (gj - off));
+  if (d < s->r2) {
+    bj = gj;
+    bd = d;
+  }
+}
+
+// Starting key of query i (source point p, current fp32 query q) for the scan.
+// prev[i] = j is the previous correspondence (the fp64 winner of the last evaluation; −1 none):
+//  * j in this shard: the candidate (d2f(q, t_j), j) itself — one of the targets, so the search
+//    only has to look for something smaller (or inside its band);
 //  * j in another shard (target-sharded loops, after an update: bound_ok): a bound only, the
-//    key (B, 0xFFFFFFFF) with B ≥ d2f(q, t_j).  By the triangle inequality
-//    |q − t_j| ≤ |q − q_old| + |q_old − t_j|, q_old = the previous query (Rt32_prev), and
-//    keys_prev[i] holds the previous reduced key (d2f(q_old, t_j), j); each fp32 evaluation is
-//    within ~5u of its exact value and the 1e-5 factors cover that 20× over.  Every real target
-//    beats the pseudo index, so the rank owning t_j still finds it (or better) and the MIN over
-//    ranks is unchanged; a rank whose shard holds nothing within B keeps the bound, whose index
-//    no shard owns (the terms kernels skip it).  Without the bound those ranks searched with
-//    r2_hi: on N ranks, N − 1 of every N queries.
+//    pseudo key (B, 0xFFFFFFFF) with B ≥ d2f(q, t_j).  dprev[i] holds the bits of the previous
+//    global fp64 winner's d64 = |Q_old − t_j|² (±ε); the fp32 distance of the old fp32 query is
+//    ≤ √d64 + e_q_prev, and by the triangle inequality |q − t_j| ≤ |q − q_old| + |q_old − t_j|
+//    (q_old from Rt32_prev).  A local target c that could beat t_j in fp64 has d2f(c) ≤
+//    band_of(B), which is the bound the scan screens with (search_bound), so the rank owning
+//    the new winner still finds it, and the MIN over ranks is unchanged.  Without the bound those
+//    ranks searched with r2_hi: on N ranks, N − 1 of every N queries.
 __device__ __forceinline__ int64_t seed_key(const IcpState* __restrict__ s, int64_t i, float4 p,
                                             float qx, float qy, float qz,
                                             const float4* __restrict__ tgt32, int64_t nt_shard,
                                             int64_t off, const int32_t* __restrict__ prev,
-                                            const int64_t* __restrict__ keys_prev) {
+                                            const int64_t* __restrict__ dprev) {
   if (prev == nullptr) return kKeyNone;
   const int64_t j = (int64_t)prev[i];
   if (j < 0) return kKeyNone;
   if (j >= off && j < off + nt_shard) {
     const float4 t = tgt32[j - off];
     const float d2 = d2f(qx, qy, qz, t.x, t.y, t.z);
-    return d2 < s->r2_hi ? (int64_t)make_key(d2, (uint32_t)j) : kKeyNone;
+    return d2 <= s->r2_hi ? (int64_t)make_key(d2, (uint32_t)j) : kKeyNone;
   }
-  if (!s->bound_ok || keys_prev == nullptr) return kKeyNone;
-  const int64_t kp = keys_prev[i];
-  if (kp == kKeyNone || (uint32_t)kp != (uint32_t)j) return kKeyNone;
-  const float d2o = __uint_as_float((uint32_t)((uint64_t)kp >> 32));
+  if (!s->bound_ok || dprev == nullptr) return kKeyNone;
+  const int64_t dp = dprev[i];
+  if (dp == kKeyNone) return kKeyNone;
+  const float d64o = __double2float_ru(__longlong_as_double(dp));
   float ox, oy, oz;
   xform32(s->Rt32_prev, p, ox, oy, oz);
   const float mx = qx - ox, my = qy - oy, mz = qz - oz;
-  const float b = (sqrtf(d2o) + sqrtf(fmaf(mz, mz, fmaf(my, my, mx * mx)))) * 1.00001f;
+  const float b = (sqrtf(d64o) * 1.000001f + s->eq_prev + sqrtf(fmaf(mz, mz, fmaf(my, my, mx * mx))) * 1.000001f) *
+                  1.00001f;
   const float B = b * b * 1.00001f;
   return B < s->r2_hi ? (int64_t)make_key(B, 0xFFFFFFFFu) : kKeyNone;
 }

@@ -25,7 +25,7 @@ EST_POINT_TO_POINT, EST_POINT_TO_PLANE = 0, 1
 KERNEL_NN, KERNEL_SCORE, KERNEL_KABSCH, KERNEL_TERMS = 0, 1, 2, 3
 NN_BRUTE, NN_GRID = 0, 1
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -98,7 +98,8 @@ SIGNATURES = {
     "m3d_icp_step": (C.c_int, [vp, vp]),
     "m3d_icp_steps": (C.c_int, [vp, C.c_int32, vp]),
     "m3d_icp_shard_nn": (C.c_int, [vp, i64, vp, vp]),
-    "m3d_icp_shard_terms": (C.c_int, [vp, i64, vp, vp, vp]),
+    "m3d_icp_shard_claim": (C.c_int, [vp, vp, vp, vp]),
+    "m3d_icp_shard_terms": (C.c_int, [vp, i64, vp, vp, vp, vp]),
     "m3d_icp_solve": (C.c_int, [vp, vp, vp]),
     "m3d_icp_result_get": (C.c_int, [vp, C.POINTER(IcpResult), vp]),
     "m3d_icp_set_source_total": (C.c_int, [vp, i64]),

@@ -115,6 +115,7 @@ class CorrSet:
     def __init__(self, src_points=None, tgt_points=None, corr=None, *, p_src=None, p_tgt=None,
                  ctx: Context | None = None):
         self.ctx = ctx or context()
+        self.device = _torch().device("cuda", self.ctx.device)
         lib = self.ctx.lib
         h = C.c_void_p()
         st = stream_handle()
@@ -368,13 +369,24 @@ class IcpLoop:
         """n iterations enqueued by the library in one call (m3d_icp_steps)."""
         self.ctx.check(self.ctx.lib.m3d_icp_steps(self.h, int(n), stream_handle()), "icp_steps")
 
-    def shard_nn(self, offset: int, keys):
-        self.ctx.check(self.ctx.lib.m3d_icp_shard_nn(self.h, int(offset), ptr(keys), stream_handle()),
+    def shard_nn(self, offset: int, dkeys):
+        """This shard's NN.  dkeys (cuda int64, ns) → target shard: bits of the shard's fp64
+        winner d² per source (INT64_MAX none), to be MIN-reduced over ranks; None → source
+        shard (the keys stay inside the loop object)."""
+        self.ctx.check(self.ctx.lib.m3d_icp_shard_nn(self.h, int(offset), ptr(dkeys), stream_handle()),
                        "icp_shard_nn")
 
-    def shard_terms(self, offset: int, keys, sums):
-        self.ctx.check(self.ctx.lib.m3d_icp_shard_terms(self.h, int(offset), ptr(keys), ptr(sums),
-                                                        stream_handle()), "icp_shard_terms")
+    def shard_claim(self, dmin, claim):
+        """Target shard, after MIN(dkeys): claim (cuda int32, ns) = own winner's index where it
+        has the global d², else INT32_MAX; MIN-reduce it over ranks."""
+        self.ctx.check(self.ctx.lib.m3d_icp_shard_claim(self.h, ptr(dmin), ptr(claim), stream_handle()),
+                       "icp_shard_claim")
+
+    def shard_terms(self, offset: int, dmin, claim, sums):
+        """Estimation terms of the owned winners → sums (cuda f64, 32), to be SUM-reduced.
+        Source shard: dmin = claim = None."""
+        self.ctx.check(self.ctx.lib.m3d_icp_shard_terms(self.h, int(offset), ptr(dmin), ptr(claim),
+                                                        ptr(sums), stream_handle()), "icp_shard_terms")
 
     def solve(self, sums):
         self.ctx.check(self.ctx.lib.m3d_icp_solve(self.h, ptr(sums), stream_handle()), "icp_solve")

@@ -1,27 +1,33 @@
-"""Multi-GPU protocols over torch.distributed (backend "nccl" = RCCL over xGMI; "gloo" in tests).
+"""Multi-GPU protocols: one process per GPU.
 
-One process per GPU.  Hot-path shardings; the source-sharded ICP variant
-(``SourceShardedIcp``: sources split, target replicated, one 256-B SUM per iteration) is the
-cheaper exchange whenever the target fits one GPU; the target-sharded one is the north-star's:
+The collectives go through a communicator object with three in-place all-reduces (min_, sum_,
+max_).  ``TorchComm`` uses torch.distributed (backend "nccl" = RCCL over xGMI, "gloo" in the CPU
+tests); ``m3d.comm.LibComm`` issues RCCL from inside libm3d.so on the library's stream
+(m3d_comm_*), with torch.distributed used only for the rendezvous.
 
-* ICP, target-sharded (cfg3).  Rank r owns target points [off_r, off_r + n_r) (points + normals)
-  and a replica of the source.  Per iteration:
-    1. local NN over the shard → packed key per source: (bits(d²_f32) << 32) | global_idx
-       (d² ≥ 0 so float bits order like the values; the low word breaks exact ties towards the
-       lowest index; KEY_NONE = INT64_MAX = "no target inside the radius");
-    2. all_reduce(keys, MIN)               — Ns × 8 B (0.8 MB at 100k, 8 MB at 1M);
-    3. each rank accumulates the fp64 estimation terms of the sources whose winner it owns
-       (it holds that target's point and normal) → 32 doubles;
-    4. all_reduce(sums, SUM)               — 256 B;
-    5. every rank runs the identical solve/update → identical T everywhere (no broadcast).
+* ICP, target-sharded (cfg3; the north-star variant).  Rank r owns target points
+  [off_r, off_r + n_r) (points + normals, one shared fp32 frame) and a replica of the source.
+  Per iteration (include/m3d.h "Multi-GPU pieces"):
+    1. shard NN → each source's fp64 winner on this shard; exchange key = bits(d64) (d64 ≥ +0 so
+       the integer order is the fp64 order; KEY_NONE = INT64_MAX = none within the radius);
+    2. MIN(dkeys)            — Ns × 8 B (8 MB at 1M);
+    3. claim = own winner's global index where its d64 is the global minimum, else INT32_MAX;
+    4. MIN(claim)            — Ns × 4 B: exact fp64 ties across shards go to the lowest index, so
+       the result is the lexicographic (d64, index) minimum — the single-device answer;
+    5. the rank owning each winner accumulates its fp64 estimation terms → 32 doubles;
+    6. SUM(sums)             — 256 B;
+    7. every rank runs the identical solve/update → identical T everywhere (no broadcast).
+* ICP, source-sharded (SURVEY §8(e) "ICP alternative"): rank r owns sources and the whole target;
+  per iteration local NN + local terms → SUM(sums) → identical solve (global fitness
+  denominator).  The cheaper exchange whenever the target fits one GPU.
 * RANSAC, hypothesis-sharded (cfg2 at N>1).  Rank r evaluates hypothesis ids
   [hyp0_r, hyp0_r + H_r) with the counter-based sampler (ids are global, so the union equals the
-  single-GPU run); the winner is all_reduce(MAX) of (count << 32) | (0xFFFFFFFF − id) — highest
-  count, lowest id on ties (the reference's first strict improvement) — and every rank
-  recomputes the winner's transform from its id (the sampler is a pure function of the id).
+  single-GPU run); the winner is MAX of (count << 32) | (0xFFFFFFFF − id) — highest count, lowest
+  id on ties (the reference's first strict improvement) — and every rank recomputes the winner's
+  transform from its id (the sampler is a pure function of the id).
 
-The driver below is backend-agnostic: the GPU backend is ``m3d.core.IcpLoop``; the CPU tests
-plug in an oracle-backed backend and run the identical protocol over gloo.
+The drivers are backend-agnostic: the GPU backend is ``m3d.core.IcpLoop``; the CPU tests plug in
+an oracle-backed backend and run the identical protocol over gloo.
 """
 
 from __future__ import annotations
@@ -29,7 +35,35 @@ from __future__ import annotations
 import numpy as np
 
 KEY_NONE = 0x7FFFFFFFFFFFFFFF
+CLAIM_NONE = 0x7FFFFFFF
 _LOW = 0xFFFFFFFF
+
+
+class TorchComm:
+    """All-reduces through torch.distributed (the default process group, or `group`)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def _ar(self, t, op):
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=op, group=self.group)
+
+    def min_(self, t):
+        import torch.distributed as dist
+
+        self._ar(t, dist.ReduceOp.MIN)
+
+    def sum_(self, t):
+        import torch.distributed as dist
+
+        self._ar(t, dist.ReduceOp.SUM)
+
+    def max_(self, t):
+        import torch.distributed as dist
+
+        self._ar(t, dist.ReduceOp.MAX)
 
 
 def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
@@ -40,7 +74,7 @@ def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
 
 
 def pack_nn_key(d2_f32, idx):
-    """numpy: (float32 bits << 32) | idx as int64; KEY_NONE where idx < 0."""
+    """numpy: (float32 bits << 32) | idx as int64; KEY_NONE where idx < 0 (the scan's key)."""
     d2 = np.asarray(d2_f32, np.float32)
     idx = np.asarray(idx, np.int64)
     k = (d2.view(np.uint32).astype(np.int64) << 32) | (idx & _LOW)
@@ -55,6 +89,17 @@ def unpack_nn_key(keys):
     return np.where(none, np.float32(np.inf), d2), np.where(none, -1, idx)
 
 
+def pack_d64(d2, valid):
+    """numpy: the target-shard exchange key, bits of the fp64 d² (KEY_NONE where not valid)."""
+    d = np.ascontiguousarray(np.asarray(d2, np.float64))
+    return np.where(np.asarray(valid, bool), d.view(np.int64), np.int64(KEY_NONE))
+
+
+def unpack_d64(keys):
+    k = np.ascontiguousarray(np.asarray(keys, np.int64))
+    return np.where(k == KEY_NONE, np.inf, k.view(np.float64))
+
+
 def best_key(count: int, hyp_id: int) -> int:
     return (int(count) << 32) | (_LOW - int(hyp_id))
 
@@ -64,24 +109,26 @@ def unpack_best_key(key: int) -> tuple[int, int]:
 
 
 class ShardedIcp:
-    """Target-sharded ICP driver: backend has shard_nn / shard_terms / solve / reset."""
+    """Target-sharded ICP driver: backend has shard_nn / shard_claim / shard_terms / solve /
+    reset / result."""
 
-    def __init__(self, backend, offset: int, ns: int, device, group=None):
+    def __init__(self, backend, offset: int, ns: int, device, comm=None):
         import torch
 
         self.b = backend
         self.off = int(offset)
-        self.group = group
-        self.keys = torch.empty(ns, dtype=torch.int64, device=device)
+        self.comm = comm or TorchComm()
+        self.dkeys = torch.empty(ns, dtype=torch.int64, device=device)
+        self.claim = torch.empty(ns, dtype=torch.int32, device=device)
         self.sums = torch.empty(32, dtype=torch.float64, device=device)
 
     def iteration(self):
-        import torch.distributed as dist
-
-        self.b.shard_nn(self.off, self.keys)
-        dist.all_reduce(self.keys, op=dist.ReduceOp.MIN, group=self.group)
-        self.b.shard_terms(self.off, self.keys, self.sums)
-        dist.all_reduce(self.sums, op=dist.ReduceOp.SUM, group=self.group)
+        self.b.shard_nn(self.off, self.dkeys)
+        self.comm.min_(self.dkeys)
+        self.b.shard_claim(self.dkeys, self.claim)
+        self.comm.min_(self.claim)
+        self.b.shard_terms(self.off, self.dkeys, self.claim, self.sums)
+        self.comm.sum_(self.sums)
         self.b.solve(self.sums)
 
     def run(self, init, max_iteration: int):
@@ -95,24 +142,21 @@ class ShardedIcp:
 class SourceShardedIcp:
     """Source-sharded ICP driver (SURVEY §8(e) "ICP alternative"): rank r owns sources
     [off_r, off_r + n_r) and the whole target.  Per iteration: local NN + local terms →
-    all_reduce(sums, SUM) (256 B, the only exchange) → identical solve on every rank, whose
-    fitness denominator is the global source count (backend.set_source_total)."""
+    SUM(sums) (256 B, the only exchange) → identical solve on every rank, whose fitness
+    denominator is the global source count (backend.set_source_total)."""
 
-    def __init__(self, backend, ns_local: int, ns_total: int, device, group=None):
+    def __init__(self, backend, ns_local: int, ns_total: int, device, comm=None):
         import torch
 
         self.b = backend
-        self.group = group
+        self.comm = comm or TorchComm()
         self.b.set_source_total(ns_total)
-        self.keys = torch.empty(ns_local, dtype=torch.int64, device=device)
         self.sums = torch.empty(32, dtype=torch.float64, device=device)
 
     def iteration(self):
-        import torch.distributed as dist
-
-        self.b.shard_nn(0, self.keys)
-        self.b.shard_terms(0, self.keys, self.sums)
-        dist.all_reduce(self.sums, op=dist.ReduceOp.SUM, group=self.group)
+        self.b.shard_nn(0, None)
+        self.b.shard_terms(0, None, None, self.sums)
+        self.comm.sum_(self.sums)
         self.b.solve(self.sums)
 
     def run(self, init, max_iteration: int):
@@ -122,18 +166,21 @@ class SourceShardedIcp:
         return self.b.result()
 
 
-def ransac_sharded(cs, params, group=None):
+def ransac_sharded(cs, params, comm=None):
     """Hypothesis-sharded a4 without early stop: returns (best_count, best_id, T) on every rank.
 
-    ``params.hyp0`` / ``params.max_iter`` must already describe this rank's id range."""
+    ``params.hyp0`` / ``params.max_iter`` must already describe this rank's id range.  The
+    shards are scored without early stop (each rank would otherwise stop on its own id range and
+    the MAX over ranks would not be the single-device loop's best)."""
     import torch
-    import torch.distributed as dist
 
+    if params.early_stop:
+        raise ValueError("ransac_sharded runs without early stop: set params.early_stop = False")
+    comm = comm or TorchComm()
     out = cs.run(params)
     gid = params.hyp0 + out.best_index
-    key = torch.tensor([best_key(out.best_count, gid)], dtype=torch.int64,
-                       device="cuda" if torch.cuda.is_available() else "cpu")
-    dist.all_reduce(key, op=dist.ReduceOp.MAX, group=group)
+    key = torch.tensor([best_key(out.best_count, gid)], dtype=torch.int64, device=cs.device)
+    comm.max_(key)
     count, wid = unpack_best_key(int(key.item()))
     T, _ = cs.kabsch3(1, seed=params.seed, hyp0=wid)
     return count, wid, T[0].cpu().numpy()

@@ -161,6 +161,7 @@ def main():
         tgt_c = Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0))
     src_c = Cloud(src)
     keys = torch.empty(ns, dtype=torch.int64, device=dev)
+    claim = torch.empty(ns, dtype=torch.int32, device=dev)
     sums = torch.empty(32, dtype=torch.float64, device=dev)
 
     def time_icp(nn: str):
@@ -177,13 +178,15 @@ def main():
             for _ in range(iters + 1):
                 if source_shard:  # keys stay inside the loop object: no copies
                     loop.shard_nn(0, None)
-                    loop.shard_terms(0, None, sums)
+                    loop.shard_terms(0, None, None, sums)
                     dist.all_reduce(sums, op=dist.ReduceOp.SUM)
                     loop.solve(sums)
                 else:
                     loop.shard_nn(off, keys)
                     dist.all_reduce(keys, op=dist.ReduceOp.MIN)
-                    loop.shard_terms(off, keys, sums)
+                    loop.shard_claim(keys, claim)
+                    dist.all_reduce(claim, op=dist.ReduceOp.MIN)
+                    loop.shard_terms(off, keys, claim, sums)
                     dist.all_reduce(sums, op=dist.ReduceOp.SUM)
                     loop.solve(sums)
 

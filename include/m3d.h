@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 4
+#define M3D_ABI_VERSION 5
 
 /* return codes */
 #define M3D_OK 0
@@ -215,18 +215,31 @@ int m3d_icp_step(m3d_icp* s, void* stream);
 /* n iterations (n × m3d_icp_step, enqueued from native code: no per-iteration host binding
  * overhead).  Iterations after convergence / max_iteration are device no-ops. */
 int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream);
-/* Target-sharded pieces (cfg3): `tgt` of m3d_icp_create is this rank's shard whose first
- * point has global index shard_offset.  keys [device] ns int64: packed (bits(d²)<<32 | idx),
- * INT64_MAX = none; reduce with MIN across ranks.  sums [device] 32 f64; reduce with SUM. */
-int m3d_icp_shard_nn(m3d_icp* s, int64_t shard_offset, int64_t* keys, void* stream);
-int m3d_icp_shard_terms(m3d_icp* s, int64_t shard_offset, const int64_t* keys, double* sums,
-                        void* stream);
+/* Multi-GPU pieces (icp.py:42-48 with the correspondence search split over ranks).
+ * Result contract of every NN (nnkey.h): for each source point the lexicographic (d64, index)
+ * minimum over the targets with d64 < r², d64 the fp64 d² of the fp64 transformed point —
+ * identical on one device and over any number of target shards.
+ *
+ * Target shard (cfg3): `tgt` of m3d_icp_create is this rank's shard whose first point has global
+ * index shard_offset (create every shard with the same centre, m3d_cloud_create_framed).  Per
+ * iteration, with the exchanges done by the caller (or m3d_comm_*):
+ *   m3d_icp_shard_nn(s, off, dkeys)      this shard's fp64 winners; dkeys [device] ns int64 =
+ *                                        bits(d64) (INT64_MAX none)          → all-reduce MIN
+ *   m3d_icp_shard_claim(s, dmin, claim)  claim [device] ns int32 = own target index where the own
+ *                                        winner has the global d64, else INT32_MAX → all-reduce MIN
+ *                                        (exact fp64 ties across shards → lowest index)
+ *   m3d_icp_shard_terms(s, off, dmin, claim, sums)  terms of the owned winners; sums [device]
+ *                                        32 f64                               → all-reduce SUM
+ *   m3d_icp_solve(s, sums)               identical update on every rank.
+ * Source shard (SURVEY §8(e) "ICP alternative"): `src` is this rank's source shard, `tgt` the
+ * whole target: m3d_icp_shard_nn(s, 0, NULL) + m3d_icp_shard_terms(s, 0, NULL, NULL, sums),
+ * SUM of the sums, m3d_icp_solve; the fitness denominator is m3d_icp_set_source_total's. */
+int m3d_icp_shard_nn(m3d_icp* s, int64_t shard_offset, int64_t* dkeys, void* stream);
+int m3d_icp_shard_claim(m3d_icp* s, const int64_t* dmin, int32_t* claim, void* stream);
+int m3d_icp_shard_terms(m3d_icp* s, int64_t shard_offset, const int64_t* dmin, const int32_t* claim,
+                        double* sums, void* stream);
 int m3d_icp_solve(m3d_icp* s, const double* sums, void* stream);
-/* Source-sharded pieces (SURVEY §8(e) "ICP alternative"): `src` of m3d_icp_create is this
- * rank's source shard, `tgt` the whole target; per iteration m3d_icp_shard_nn(s, 0, ...) +
- * m3d_icp_shard_terms(s, 0, ...) on the shard, SUM of the 32 term slots across ranks, then
- * m3d_icp_solve.  The fitness denominator is the source count over all ranks, set here
- * (0 = this shard's own count). */
+/* Source-sharded runs: the source count over all ranks (0 = this shard's own count). */
 int m3d_icp_set_source_total(m3d_icp* s, int64_t ns_total);
 /* Read the loop state (synchronises the stream). */
 int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream);

@@ -24,7 +24,15 @@ published algorithm (Open3D 0.19 ``pipelines/registration/Registration.cpp``,
 PARITY UNPINNED against Open3D itself (no Open3D in this container, and the reference's tests
 pin no ICP output).  It is pinned instead by known-R|t recovery on synthetic pairs
 (``tests/test_oracle_icp.py``) and the GPU path is checked against it within stated tolerances.
-Nearest neighbours use scipy's exact ``cKDTree``; exact ties resolve to the lowest target index.
+
+Arithmetic contract (shared with the device, 3d-matching_amd/csrc/nnkey.h):
+* ``transform_points`` is Open3D's PointCloud::Transform (Eigen 4×4 · (x, y, z, 1)) in Eigen's
+  non-FMA order, ((r0·x + r1·y) + r2·z) + t, written elementwise so that no BLAS kernel (whose
+  FMA order depends on the host CPU) decides the rounding;
+* d² = ((dx·dx + dy·dy) + dz·dz) in fp64;
+* the nearest neighbour is the exact lexicographic (d², index) minimum over the targets with
+  d² < r² (nanoflann's radius result set keeps d² < r²; exact ties → lowest index).  scipy's
+  ``cKDTree`` proposes candidates; the decision is taken on the d² above (``nn_exact``).
 """
 
 from __future__ import annotations
@@ -34,7 +42,64 @@ from scipy.spatial import cKDTree
 
 
 def transform_points(T: np.ndarray, pts: np.ndarray) -> np.ndarray:
-    return pts @ T[:3, :3].T + T[:3, 3]
+    """Open3D PointCloud::Transform: ((r0·x + r1·y) + r2·z) + t per row, fp64, no FMA."""
+    T = np.asarray(T, np.float64)
+    p = np.asarray(pts, np.float64).reshape(-1, 3)
+    x, y, z = p[:, 0], p[:, 1], p[:, 2]
+    out = np.empty_like(p)
+    for k in range(3):
+        out[:, k] = ((T[k, 0] * x + T[k, 1] * y) + T[k, 2] * z) + T[k, 3]
+    return out
+
+
+def sq_dist(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """((dx·dx + dy·dy) + dz·dz) row-wise, fp64."""
+    d = a - b
+    return (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+
+
+def nn_exact(tree: cKDTree, tgt: np.ndarray, q: np.ndarray, max_dist: float, k: int = 8):
+    """Radius-bounded exact 1-NN: for every query the lexicographic (d², index) minimum over the
+    targets with d² < max_dist² (d² = ``sq_dist``).  Returns (idx int64, -1 = none; d² with inf).
+
+    The kd-tree's own distances may round differently from ``sq_dist``, so k candidates are
+    decided on ``sq_dist``; a query whose k-th candidate is not clearly farther than its best (a
+    cluster of near-duplicates) is redone with every target inside a slightly larger ball."""
+    nq = len(q)
+    idx = np.full(nq, -1, np.int64)
+    d2 = np.full(nq, np.inf)
+    if nq == 0 or len(tgt) == 0 or max_dist <= 0:
+        return idx, d2
+    r2 = max_dist * max_dist
+    k = min(k, len(tgt))
+    dd, jj = tree.query(q, k=k, distance_upper_bound=max_dist * (1 + 1e-9), workers=-1)
+    dd = dd.reshape(nq, k)
+    jj = jj.reshape(nq, k).astype(np.int64)
+    valid = jj < len(tgt)
+    jc = np.where(valid, jj, 0)
+    cand = np.full((nq, k), np.inf)
+    for c in range(k):
+        cand[:, c] = np.where(valid[:, c], sq_dist(q, tgt[jc[:, c]]), np.inf)
+    cand = np.where(cand < r2, cand, np.inf)
+    # lexicographic (d², index) minimum over the k candidates
+    bd = cand.min(axis=1)
+    tie = (cand == bd[:, None]) & np.isfinite(bd)[:, None]
+    bj = np.where(tie, jc, np.iinfo(np.int64).max).min(axis=1)
+    ok = np.isfinite(bd)
+    idx[ok] = bj[ok]
+    d2[ok] = bd[ok]
+    # near-duplicate clusters: the k-th kd-tree candidate within 1e-9 of the best
+    if k < len(tgt):
+        dk = dd[:, k - 1]
+        crowd = np.nonzero(ok & np.isfinite(dk) & (dk <= np.sqrt(bd) * (1 + 1e-9) + 1e-300))[0]
+        for i in crowd:
+            js = np.asarray(tree.query_ball_point(q[i], np.sqrt(bd[i]) * (1 + 1e-9) + 1e-300), np.int64)
+            dj = sq_dist(np.repeat(q[i:i + 1], len(js), 0), tgt[js])
+            m = dj < r2
+            js, dj = js[m], dj[m]
+            o = np.lexsort((js, dj))[0]
+            idx[i], d2[i] = js[o], dj[o]
+    return idx, d2
 
 
 def registration_result(src_t: np.ndarray, tgt: np.ndarray, max_dist: float, tree=None):
@@ -43,13 +108,8 @@ def registration_result(src_t: np.ndarray, tgt: np.ndarray, max_dist: float, tre
     ns = len(src_t)
     if ns == 0 or max_dist <= 0:
         return 0.0, 0.0, np.zeros((0, 2), dtype=np.int64), np.full(ns, np.inf)
-    d, j = tree.query(src_t, k=1, workers=-1)
-    j = np.asarray(j, dtype=np.int64)
-    diff = src_t - tgt[np.minimum(j, len(tgt) - 1)]
-    d2 = (diff[:, 0] * diff[:, 0] + diff[:, 1] * diff[:, 1]) + diff[:, 2] * diff[:, 2]
-    ok = d2 < max_dist * max_dist
-    d2 = np.where(ok, d2, np.inf)
-    idx = np.nonzero(ok)[0]
+    j, d2 = nn_exact(tree, tgt, src_t, max_dist)
+    idx = np.nonzero(j >= 0)[0]
     corr = np.stack([idx, j[idx]], axis=1)
     if len(idx) == 0:
         return 0.0, 0.0, corr, d2

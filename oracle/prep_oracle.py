@@ -411,15 +411,13 @@ def check_distance(ps, pt, T, thr):
 
 
 def evaluate(src, tgt, T, max_corr, tree=None):
-    """GetRegistrationResultAndCorrespondences: fitness, rmse of 1-NN within max_corr."""
-    tree = tree or cKDTree(tgt)
-    x = src @ T[:3, :3].T + T[:3, 3]
-    d, j = tree.query(x, k=1)
-    ok = d * d < max_corr * max_corr
-    n = int(ok.sum())
-    if n == 0:
-        return 0.0, 0.0
-    return n / len(src), math.sqrt(float(np.sum(d[ok] ** 2)) / n)
+    """GetRegistrationResultAndCorrespondences: fitness, rmse of 1-NN within max_corr (the exact
+    fp64 contract of icp_oracle.registration_result)."""
+    import icp_oracle
+
+    fit, rmse, _, _ = icp_oracle.registration_result(icp_oracle.transform_points(T, src), tgt,
+                                                     max_corr, tree or cKDTree(tgt))
+    return fit, rmse
 
 
 def ransac_feature(src, tgt, corres, max_corr, rows_fn, max_iteration=30, confidence=0.999,

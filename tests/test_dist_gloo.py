@@ -1,9 +1,9 @@
 """Multi-process (world_size 2, gloo, CPU) tests of the N>1 protocols in m3d/dist.py.
 
 The driver (ShardedIcp) is the code bench.py runs over RCCL; here its backend is an oracle-backed
-CPU implementation of the same three calls (shard_nn / shard_terms / solve), so the protocol —
-key packing, MIN/SUM reductions, ownership of terms, identical solve on every rank — is checked
-against the single-process oracle.  The GPU kernels behind the same calls are covered by
+CPU implementation of the same calls (shard_nn / shard_claim / shard_terms / solve), so the
+protocol — d64 exchange keys, MIN on keys and claims, SUM on terms, ownership of terms,
+identical solve on every rank — is checked against the single-process oracle.  The GPU kernels behind the same calls are covered by
 tests/test_gpu_icp.py::test_target_sharded_loop_matches_single_device.
 """
 import os
@@ -28,7 +28,8 @@ def free_port():
 
 
 class OracleShard:
-    """CPU stand-in for IcpLoop on one target shard (fp64 NN, fp32 keys, fp64 terms)."""
+    """CPU stand-in for IcpLoop on one shard: the exact fp64 NN of the oracle, the d64 exchange
+    keys and claims of the target-shard protocol, fp64 terms."""
 
     def __init__(self, src, tgt, nrm, r, max_iteration):
         self.src, self.tgt, self.nrm, self.r = src, tgt, nrm, r
@@ -46,20 +47,31 @@ class OracleShard:
         self.done = False
         self.fitness = self.rmse = 0.0
 
-    def shard_nn(self, off, keys):
-        if self.done:
-            return
-        pcd = I.transform_points(self.T, self.src)
-        d, j = self.tree.query(pcd, k=1)
-        d2 = d * d
-        ok = d2 < self.r * self.r
-        k = D.pack_nn_key(d2.astype(np.float32), np.where(ok, j + off, -1))
-        keys.copy_(torch.from_numpy(k))
+    def _local(self, off):
+        j, d2 = I.nn_exact(self.tree, self.tgt, I.transform_points(self.T, self.src), self.r)
+        return np.where(j >= 0, j + off, -1), d2
 
-    def shard_terms(self, off, keys, sums):
+    def shard_nn(self, off, dkeys):
         if self.done:
             return
-        _, idx = D.unpack_nn_key(keys.numpy())
+        self.lj, self.ld = self._local(off)
+        if dkeys is not None:
+            dkeys.copy_(torch.from_numpy(D.pack_d64(self.ld, self.lj >= 0)))
+
+    def shard_claim(self, dmin, claim):
+        if self.done:
+            return
+        own = (self.lj >= 0) & (D.pack_d64(self.ld, self.lj >= 0) == dmin.numpy())
+        claim.copy_(torch.from_numpy(np.where(own, self.lj, D.CLAIM_NONE).astype(np.int32)))
+
+    def shard_terms(self, off, dmin, claim, sums):
+        if self.done:
+            return
+        if claim is None:  # source shard: the local winners are the global ones
+            idx = self.lj
+        else:
+            idx = claim.numpy().astype(np.int64)
+            idx[idx == D.CLAIM_NONE] = -1
         mine = (idx >= off) & (idx < off + len(self.tgt))
         i = np.nonzero(mine)[0]
         j = idx[mine] - off
@@ -70,9 +82,8 @@ class OracleShard:
             out[:21] = JTJ[np.triu_indices(6)]
             out[21:27] = JTr
             out[27] = r2
-            dd = pcd[i] - self.tgt[j]
             out[28] = len(i)
-            out[29] = np.sum(dd * dd)
+            out[29] = np.sum(I.sq_dist(pcd[i], self.tgt[j]))
         sums.copy_(torch.from_numpy(out))
 
     def solve(self, sums):
