@@ -77,10 +77,25 @@ int dev_alloc(m3d_ctx* ctx, T** p, int64_t count) {
 }
 
 // Bump allocator over the context scratch arena.  Growing synchronises the device.
+// The scratch arena and the RANSAC loop state (ctx->rstate) are shared by every call on the
+// context, and each call only enqueues work on its caller's stream: a call on a different stream
+// than the previous scratch user first waits (device-side) for that user's work, and records its
+// own completion event when it is done enqueueing — calls on several streams are serialised on
+// the device, never racing on the scratch.
 struct Arena {
   m3d_ctx* ctx;
+  hipStream_t st;
   size_t off = 0;
-  explicit Arena(m3d_ctx* c) : ctx(c) {}
+  Arena(m3d_ctx* c, hipStream_t s) : ctx(c), st(s) {
+    if (ctx->scratch_ev != nullptr && ctx->scratch_used && ctx->scratch_stream != st)
+      (void)hipStreamWaitEvent(st, ctx->scratch_ev, 0);
+  }
+  ~Arena() {
+    if (ctx->scratch_ev != nullptr && hipEventRecord(ctx->scratch_ev, st) == hipSuccess) {
+      ctx->scratch_used = true;
+      ctx->scratch_stream = st;
+    }
+  }
   size_t take(size_t bytes) {
     size_t o = (off + 255) & ~size_t(255);
     off = o + bytes;
@@ -181,6 +196,7 @@ int m3d_create(int device, m3d_ctx** out) {
   ctx->device = device;
   if (hipMalloc(&ctx->stats, 8 * sizeof(int64_t)) != hipSuccess ||
       hipMalloc(&ctx->rstate, sizeof(RansacState)) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess ||
       hipMemset(ctx->stats, 0, 8 * sizeof(int64_t)) != hipSuccess) {
     m3d_destroy(ctx);
     return M3D_ERR_OOM;
@@ -196,6 +212,7 @@ void m3d_destroy(m3d_ctx* ctx) {
   if (ctx->scratch) hipFree(ctx->scratch);
   if (ctx->stats) hipFree(ctx->stats);
   if (ctx->rstate) hipFree(ctx->rstate);
+  if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
   for (auto& v : ctx->ev)
     for (auto& pr : v) {
       hipEventDestroy(pr.first);
@@ -352,7 +369,7 @@ int m3d_kabsch3_batch(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triple
   CHECK_ARG(ctx, cs != nullptr && H >= 0 && (H == 0 || T_out), "invalid arguments");
   CHECK_ARG(ctx, triples != nullptr || cs->nc >= 3 || cs->nc < 3, "");
   hipSetDevice(ctx->device);
-  Arena a(ctx);
+  Arena a(ctx, S(stream));
   size_t o_h = a.take(sizeof(HypF32) * (size_t)std::max<int64_t>(H, 1));
   int rc = a.commit();
   if (rc) return rc;
@@ -415,7 +432,7 @@ int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64
     HIPX(ctx, hipMemsetAsync(counts, 0, sizeof(int32_t) * H, st));
     return M3D_OK;
   }
-  Arena a(ctx);
+  Arena a(ctx, S(stream));
   size_t o[kScoreSlots];
   score_layout(a, H, o);
   int rc = a.commit();
@@ -451,7 +468,7 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
     if (p->early_stop) B = std::min<int64_t>(B, 16384);
   }
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(max_iter, 1)));
-  Arena a(ctx);
+  Arena a(ctx, S(stream));
   size_t o[kScoreSlots];
   score_layout(a, B, o);
   size_t o_T = a.take(sizeof(double) * 16 * B);
@@ -461,6 +478,9 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   ScoreScratch s = score_bind(a, o);
   double* Tb = a.at<double>(o_T);
   int32_t* cb = a.at<int32_t>(o_c);
+  // counts of the hypotheses after an early stop are never scored: they read 0
+  if (counts_out != nullptr && max_iter > 0)
+    HIPX(ctx, hipMemsetAsync(counts_out, 0, sizeof(int32_t) * max_iter, st));
   HIPX(ctx, launch_ransac_init(ctx->rstate, ctx->stats, max_iter == 0 ? 1 : 0, st));
   const int32_t* done = &ctx->rstate->done;
   const double thr_sq = thr_sq_of(p->thr, p->mode);
@@ -776,6 +796,9 @@ void m3d_icp_destroy(m3d_icp* s) {
   hipFree(s->dprev);
   hipFree(s->ld64);
   hipFree(s->lidx);
+  hipFree(s->xdk);
+  hipFree(s->xcl);
+  hipFree(s->xsums);
   hipFree(s->corr);
   hipFree(s->partials);
   hipFree(s->sums);

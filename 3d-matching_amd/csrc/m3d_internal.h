@@ -119,6 +119,10 @@ struct m3d_ctx {
   size_t scratch_bytes = 0;
   int64_t* stats = nullptr;  // [8] device counters
   m3d::RansacState* rstate = nullptr;
+  // cross-stream ordering of the scratch/rstate users (api.cpp Arena)
+  hipEvent_t scratch_ev = nullptr;
+  hipStream_t scratch_stream = nullptr;
+  bool scratch_used = false;
 };
 
 struct m3d_corrset {
@@ -170,6 +174,10 @@ struct m3d_icp {
   const int32_t* qorder = nullptr;  // grid NN: source visit order (source cell order)
   const m3d::Grid* tgrid = nullptr;  // grid NN: the target's grid (owned by the target cloud)
   int64_t ns_total = 0;  // source-sharded multi-GPU: sources over all ranks (fitness denominator)
+  // exchange buffers of the library-driven multi-GPU loops (m3d_icp_*shard_steps), lazily
+  int64_t* xdk = nullptr;   // ns: d64 keys, MIN-reduced
+  int32_t* xcl = nullptr;   // ns: claims, MIN-reduced
+  double* xsums = nullptr;  // kTermSlots, SUM-reduced
 };
 
 // error plumbing ------------------------------------------------------------------------
@@ -235,6 +243,8 @@ hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int6
 hipError_t launch_ransac_init(RansacState* rs, const int64_t* stats, int done, hipStream_t st);
 hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* stats,
                               m3d_ransac_result* out_dev, hipStream_t st);
+hipError_t launch_ransac_pack_key(const m3d_ransac_result* r, int64_t hyp0, int64_t* key,
+                                  hipStream_t st);
 
 // ICP
 hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_t st);

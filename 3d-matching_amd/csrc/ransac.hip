@@ -186,8 +186,10 @@ struct Hyp16Fuse {
   int64_t h_pad;
   int on;
 };
-__device__ void hyp16_one(const double* T, bool valid, int64_t j, int64_t h_pad,
-                          const Mf16Params& m, uint4* __restrict__ hb16, float* __restrict__ heps);
+// (defined with the MFMA screen below; declared inline here as it is there)
+__device__ __forceinline__ void hyp16_one(const double* T, bool valid, int64_t j, int64_t h_pad,
+                                          const Mf16Params& m, uint4* __restrict__ hb16,
+                                          float* __restrict__ heps);
 
 __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__ p64,
                                                       const double* __restrict__ q64, int64_t nc,
@@ -1097,6 +1099,21 @@ hipError_t launch_ransac_init(RansacState* rs, const int64_t* stats, int done, h
 hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* stats,
                               m3d_ransac_result* out_dev, hipStream_t st) {
   copy_result_kernel<<<1, 64, 0, st>>>(rs, nc, stats, out_dev);
+  return hipGetLastError();
+}
+
+// hypothesis-sharded a4: this rank's best as the MAX-reducible key (count << 32) | (2³²−1 − id)
+__global__ void ransac_pack_key_kernel(const m3d_ransac_result* __restrict__ r, int64_t hyp0,
+                                       int64_t* __restrict__ key) {
+  if (threadIdx.x != 0) return;
+  const int64_t c = r->best_count, bi = r->best_index;
+  key[0] = (c < 0 || bi < 0) ? 0
+                             : (int64_t)(((uint64_t)c << 32) | (0xFFFFFFFFull - (uint64_t)(hyp0 + bi)));
+}
+
+hipError_t launch_ransac_pack_key(const m3d_ransac_result* r, int64_t hyp0, int64_t* key,
+                                  hipStream_t st) {
+  ransac_pack_key_kernel<<<1, 64, 0, st>>>(r, hyp0, key);
   return hipGetLastError();
 }
 

@@ -24,6 +24,9 @@ SCORE_SQUARED, SCORE_NORM = 0, 1
 EST_POINT_TO_POINT, EST_POINT_TO_PLANE = 0, 1
 KERNEL_NN, KERNEL_SCORE, KERNEL_KABSCH, KERNEL_TERMS = 0, 1, 2, 3
 NN_BRUTE, NN_GRID = 0, 1
+COMM_ID_BYTES = 128
+DT_I32, DT_I64, DT_F64 = 0, 1, 2
+OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
 ABI_VERSION = 5
 
@@ -113,6 +116,14 @@ SIGNATURES = {
                                               C.POINTER(i64), vp]),
     "m3d_ransac_on_correspondences": (C.c_int, [vp, vp, vp, vp, i64, C.POINTER(FeatureRansacParams),
                                                 C.POINTER(FeatureRansacResult), vp, vp]),
+    "m3d_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "m3d_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int, C.POINTER(vp)]),
+    "m3d_comm_destroy": (None, [vp]),
+    "m3d_comm_allreduce": (C.c_int, [vp, vp, i64, C.c_int, C.c_int, vp]),
+    "m3d_icp_shard_steps": (C.c_int, [vp, vp, i64, i32, vp]),
+    "m3d_icp_source_shard_steps": (C.c_int, [vp, vp, i32, vp]),
+    "m3d_ransac_best_allreduce": (C.c_int, [vp, vp, i64, vp, vp]),
+    "m3d_ransac_run_sharded": (C.c_int, [vp, vp, vp, C.POINTER(RansacParams), C.POINTER(RansacResult), vp]),
     "m3d_debug_kabsch3_host":(C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
     "m3d_debug_ldlt6_host": (C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }

@@ -187,6 +187,25 @@ class CorrSet:
                                                          ptr(result), stream_handle()), "ransac_run_async")
 
 
+    def run_sharded(self, comm, params: "RansacParams") -> "RansacOutcome":
+        """Hypothesis-sharded a4 over comm's ranks (m3d_ransac_run_sharded): params.hyp0 /
+        max_iter = this rank's id range, no early stop; returns the global winner on every rank
+        (best_index = its global id)."""
+        p = params.to_c()
+        res = _lib.RansacResult()
+        self.ctx.check(self.ctx.lib.m3d_ransac_run_sharded(self.ctx.h, comm.h, self.h, C.byref(p),
+                                                           C.byref(res), stream_handle()),
+                       "ransac_run_sharded")
+        return RansacOutcome(np.array(res.T[:]).reshape(4, 4), res.fitness, res.best_index,
+                             res.iterations, res.best_count, self.nc)
+
+    def best_allreduce(self, comm, result, hyp0: int, key):
+        """MAX over ranks of this rank's packed best (count << 32 | ~global id) into key (cuda
+        int64 (1,)), enqueued after run_async on the same stream (m3d_ransac_best_allreduce)."""
+        self.ctx.check(self.ctx.lib.m3d_ransac_best_allreduce(comm.h, ptr(result), int(hyp0), ptr(key),
+                                                              stream_handle()), "ransac_best_allreduce")
+
+
 RESULT_WORDS = C.sizeof(_lib.RansacResult) // 8  # m3d_ransac_result as int64 words
 
 
@@ -390,6 +409,17 @@ class IcpLoop:
 
     def solve(self, sums):
         self.ctx.check(self.ctx.lib.m3d_icp_solve(self.h, ptr(sums), stream_handle()), "icp_solve")
+
+    def shard_steps(self, comm, offset: int, n: int):
+        """n target-sharded iterations with the MIN / MIN / SUM all-reduces issued by libm3d
+        (m3d_icp_shard_steps; comm = m3d.comm.LibComm)."""
+        self.ctx.check(self.ctx.lib.m3d_icp_shard_steps(self.h, comm.h, int(offset), int(n), stream_handle()),
+                       "icp_shard_steps")
+
+    def source_shard_steps(self, comm, n: int):
+        """n source-sharded iterations (one SUM all-reduce each) issued by libm3d."""
+        self.ctx.check(self.ctx.lib.m3d_icp_source_shard_steps(self.h, comm.h, int(n), stream_handle()),
+                       "icp_source_shard_steps")
 
     def set_source_total(self, ns_total: int):
         """Source-sharded runs: fitness denominator = sources over all ranks."""

@@ -20,7 +20,10 @@
  *     Numerical failure of a hypothesis is NOT an error: as in the reference
  *     (ransac.py:134-140,184-192) it yields the identity transform and a per-hypothesis status.
  *   - One context per (host thread, device).  A context owns its scratch memory; the library
- *     never frees caller memory.
+ *     never frees caller memory.  Calls on one context that use its scratch (the RANSAC entry
+ *     points) may pass different streams: a call on another stream than the previous one first
+ *     waits on the device for the previous call's work (no host synchronisation), so such calls
+ *     are ordered, not concurrent.
  */
 #ifndef M3D_H_
 #define M3D_H_
@@ -138,7 +141,8 @@ typedef struct {
 int m3d_ransac_run(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_params* params,
                    const int32_t* triples, m3d_ransac_result* out, void* stream);
 /* Asynchronous form: per-hypothesis counts of the whole run land in counts_out [device]
- * (max_iter int32, may be NULL) and the result struct in result_dev [device]. */
+ * (max_iter int32, may be NULL; hypotheses after an early stop are not scored and read 0) and
+ * the result struct in result_dev [device]. */
 int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_params* params,
                          const int32_t* triples, int32_t* counts_out, m3d_ransac_result* result_dev,
                          void* stream);
@@ -241,6 +245,42 @@ int m3d_icp_shard_terms(m3d_icp* s, int64_t shard_offset, const int64_t* dmin, c
 int m3d_icp_solve(m3d_icp* s, const double* sums, void* stream);
 /* Source-sharded runs: the source count over all ranks (0 = this shard's own count). */
 int m3d_icp_set_source_total(m3d_icp* s, int64_t ns_total);
+/* ------------------------------------------------------------------ RCCL inside the library
+ * (SURVEY §8(b)/(e)): one communicator per (context, rank) over RCCL/xGMI; the caller only
+ * carries the 128-byte unique id from rank 0 to the others (e.g. torch.distributed's
+ * broadcast_object_list) — the collectives of the multi-GPU loops are issued by libm3d on the
+ * caller's stream, with no host round trip. */
+typedef struct m3d_comm m3d_comm;
+#define M3D_COMM_ID_BYTES 128
+#define M3D_DT_I32 0
+#define M3D_DT_I64 1
+#define M3D_DT_F64 2
+#define M3D_OP_SUM 0
+#define M3D_OP_MIN 1
+#define M3D_OP_MAX 2
+/* id_out [host] M3D_COMM_ID_BYTES bytes (ncclGetUniqueId), called on rank 0. */
+int m3d_comm_unique_id(uint8_t* id_out);
+/* Collective over the world's ranks (every rank calls it with the same id).  Synchronous. */
+int m3d_comm_init(m3d_ctx* ctx, const uint8_t* id, int rank, int world, m3d_comm** out);
+void m3d_comm_destroy(m3d_comm* c);
+/* In-place all-reduce of buf [device] count elements of dtype M3D_DT_* with op M3D_OP_*. */
+int m3d_comm_allreduce(m3d_comm* c, void* buf, int64_t count, int dtype, int op, void* stream);
+/* n iterations of target-sharded ICP (the protocol of "Multi-GPU pieces" above) with the MIN /
+ * MIN / SUM all-reduces issued inside; every rank calls it with its shard offset. */
+int m3d_icp_shard_steps(m3d_icp* s, m3d_comm* c, int64_t shard_offset, int32_t n, void* stream);
+/* n iterations of source-sharded ICP (one SUM of the 32 term slots per iteration). */
+int m3d_icp_source_shard_steps(m3d_icp* s, m3d_comm* c, int32_t n, void* stream);
+/* Hypothesis-sharded a4 without early stop (cfg2 at N > 1): after m3d_ransac_run_async on each
+ * rank's id range [hyp0, hyp0 + max_iter), key_dev [device] 1 int64 ← MAX over ranks of
+ * (best_count << 32) | (2³² − 1 − (hyp0 + best_index)): highest count, lowest global id. */
+int m3d_ransac_best_allreduce(m3d_comm* c, const m3d_ransac_result* result_dev, int64_t hyp0,
+                              int64_t* key_dev, void* stream);
+/* The whole hypothesis-sharded run, synchronous: out holds the global winner (T recomputed
+ * from its id by the native sampler; best_index = global id; iterations and rechecked summed
+ * over ranks).  params->early_stop must be 0 and the native sampler is used. */
+int m3d_ransac_run_sharded(m3d_ctx* ctx, m3d_comm* c, const m3d_corrset* cs,
+                           const m3d_ransac_params* params, m3d_ransac_result* out, void* stream);
+
 /* Read the loop state (synchronises the stream). */
 int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream);
 /* Device pointer to the current correspondence index array (ns int32, -1 = none). */

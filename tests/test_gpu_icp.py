@@ -16,6 +16,7 @@ from scipy.spatial import cKDTree
 import icp_oracle as I
 from m3d import _lib, synth
 from m3d.core import Cloud, IcpLoop, icp, nn1
+from shard_emulation import run_target_shards, shard_step
 
 pytestmark = pytest.mark.gpu
 
@@ -25,18 +26,6 @@ def check_nn(src, tgt, T, r, idx, d2):
     ref_j, ref_d2 = I.nn_exact(cKDTree(tgt), tgt, I.transform_points(T, src), r)
     np.testing.assert_array_equal(idx, ref_j)
     np.testing.assert_array_equal(d2, ref_d2)
-
-
-def shard_step(lp, off, ns, sums):
-    """One iteration of the target-shard protocol on a single shard (no exchange needed)."""
-    import torch
-
-    dk = torch.empty(ns, dtype=torch.int64, device="cuda")
-    cl = torch.empty(ns, dtype=torch.int32, device="cuda")
-    lp.shard_nn(off, dk)
-    lp.shard_claim(dk, cl)
-    lp.shard_terms(off, dk, cl, sums)
-    lp.solve(sums)
 
 
 @pytest.mark.parametrize("nn", ["brute", "grid"])
@@ -321,39 +310,6 @@ def test_source_sharded_loop_matches_single_device(nn, keys_inside):
     assert abs(r.fitness - full.fitness) < 1e-12
     for lp in loops[1:]:
         np.testing.assert_array_equal(lp.result().transformation, r.transformation)
-
-
-def run_target_shards(src, tgt, nrm, bounds, iters, nn, r=0.12, check_keys=None):
-    """The multi-GPU target-shard protocol (MIN on the d64 keys, MIN on the claims, SUM on the
-    terms) emulated with one IcpLoop per shard on one device.  Returns the loops."""
-    import torch
-
-    s = Cloud(src)
-    c = tgt.mean(axis=0)  # one frame for all shards: seed bounds on non-owning shards
-    shards = [Cloud(tgt[a:b], nrm[a:b], center=c) for a, b in zip(bounds[:-1], bounds[1:])]
-    loops = [IcpLoop(s, sh, r, relative_fitness=-1, relative_rmse=-1, max_iteration=iters, nn=nn)
-             for sh in shards]
-    for lp in loops:
-        lp.reset(np.eye(4))
-    ns = len(src)
-    for it in range(iters + 1):
-        keys = [torch.empty(ns, dtype=torch.int64, device="cuda") for _ in loops]
-        for lp, off, k in zip(loops, bounds, keys):
-            lp.shard_nn(off, k)
-        kmin = torch.stack(keys).min(dim=0).values
-        claims = [torch.empty(ns, dtype=torch.int32, device="cuda") for _ in loops]
-        for lp, cl in zip(loops, claims):
-            lp.shard_claim(kmin, cl)
-        cmin = torch.stack(claims).min(dim=0).values
-        if check_keys is not None:
-            check_keys(it, loops[0], kmin, cmin)
-        sums = [torch.empty(32, dtype=torch.float64, device="cuda") for _ in loops]
-        for lp, off, sm in zip(loops, bounds, sums):
-            lp.shard_terms(off, kmin, cmin, sm)
-        tot = torch.stack(sums).sum(dim=0)
-        for lp in loops:
-            lp.solve(tot)
-    return loops
 
 
 @pytest.mark.parametrize("nn", ["brute", "grid"])
