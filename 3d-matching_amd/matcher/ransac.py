@@ -50,7 +50,12 @@ def _corr_array(correspondences) -> np.ndarray:
     c = np.asarray(correspondences)
     if c.size == 0:
         return np.zeros((0, 2), np.int32)
-    return c.reshape(-1, 2)
+    c = c.reshape(-1, 2)
+    if c.dtype != np.int32:  # the device takes int32 rows: wider values must not wrap silently
+        big = (c > np.iinfo(np.int32).max) | (c < np.iinfo(np.int32).min)
+        if big.any():
+            raise IndexError(f"index {int(c[big][0])} is out of bounds for axis 0")
+    return c
 
 
 def _check_gather(corr: np.ndarray, n_src: int, n_tgt: int) -> None:
@@ -64,14 +69,29 @@ def _check_gather(corr: np.ndarray, n_src: int, n_tgt: int) -> None:
             raise IndexError(f"index {int(v[np.argmax(bad)])} is out of bounds for axis 0 with size {n}")
 
 
-def _only_in_range(corr: np.ndarray, n_src: int, n_tgt: int) -> np.ndarray:
-    """Rows the reference never reads may hold anything: out-of-range entries → 0 (a copy)."""
-    ok = (corr[:, 0] < n_src) & (corr[:, 0] >= -n_src) & (corr[:, 1] < n_tgt) & (corr[:, 1] >= -n_tgt)
-    if ok.all():
-        return corr
-    c = corr.copy()
-    c[~ok] = 0
-    return c
+def _in_range(corr: np.ndarray, n_src: int, n_tgt: int) -> np.ndarray:
+    return (corr[:, 0] < n_src) & (corr[:, 0] >= -n_src) & (corr[:, 1] < n_tgt) & (corr[:, 1] >= -n_tgt)
+
+
+def _packed(s_pts: np.ndarray, t_pts: np.ndarray, corr: np.ndarray, need_all: bool):
+    """The cached device correspondence set for (s_pts, t_pts, corr).
+
+    need_all (evaluate_inlier_ratio / run_ransac read every row, ransac.py:226-227): an
+    out-of-range index raises numpy's IndexError.  Otherwise (compute_step_transformation reads
+    only its 3 sampled rows, checked by the caller) rows the reference never reads may hold
+    anything: out-of-range entries are packed as 0.  Whether every index is in range is decided
+    once per cached content (m3d.cache.memo)."""
+    key = _cache.corr_key(s_pts, t_pts, corr)
+    ok = _cache.memo(("in_range",) + key, lambda: bool(_in_range(corr, len(s_pts), len(t_pts)).all()))
+    if ok:
+        return _cache.get(key, lambda: CorrSet(s_pts, t_pts, corr))
+    if need_all:
+        _check_gather(corr, len(s_pts), len(t_pts))
+    def make():
+        c = corr.copy()
+        c[~_in_range(corr, len(s_pts), len(t_pts))] = 0
+        return CorrSet(s_pts, t_pts, c)
+    return _cache.get(("clean",) + key, make)
 
 
 def global_registration(src, tgt, voxel_size: float, iteration: int = 30) -> RegistrationResult:
@@ -113,7 +133,7 @@ def compute_step_transformation(src, tgt, correspondences) -> RegistrationResult
     idxs = np.random.choice(n_corres, 3, replace=False)       # same RNG stream as the reference
     s_pts, t_pts = _down_points(src), _down_points(tgt)
     _check_gather(corres_np[idxs], len(s_pts), len(t_pts))     # only the sampled rows are read
-    cs = _cache.corrset(s_pts, t_pts, _only_in_range(corres_np, len(s_pts), len(t_pts)))
+    cs = _packed(s_pts, t_pts, np.asarray(corres_np, np.int32), need_all=False)
     T, status = cs.kabsch3(1, triples=np.asarray(idxs, np.int32).reshape(1, 3))
     if int(status[0].item()) == _lib.HYP_OK:
         res.transformation = T[0].cpu().numpy()
@@ -127,8 +147,7 @@ def evaluate_inlier_ratio(src, tgt, correspondences, transform, voxel_size) -> f
     if len(corres) == 0:
         return 0.0
     s_pts, t_pts = _down_points(src), _down_points(tgt)
-    _check_gather(corres, len(s_pts), len(t_pts))
-    cs = _cache.corrset(s_pts, t_pts, corres)
+    cs = _packed(s_pts, t_pts, np.asarray(corres, np.int32), need_all=True)
     cnt = cs.score(np.asarray(transform, np.float64).reshape(1, 4, 4), dist_thresh, _lib.SCORE_NORM)
     return np.int64(cnt[0].item()) / len(corres)
 
@@ -168,8 +187,7 @@ def run_ransac(src, tgt, correspondences, voxel_size: float = 0.3, max_iter: int
     else:
         raise ValueError("score must be 'fast' or 'norm'")
     s_pts, t_pts = _down_points(src), _down_points(tgt)
-    _check_gather(corres, len(s_pts), len(t_pts))
-    cs = _cache.corrset(s_pts, t_pts, corres)
+    cs = _packed(s_pts, t_pts, np.asarray(corres, np.int32), need_all=True)
     params = RansacParams(max_iter=max_iter, thr=thr, mode=mode, early_stop=early_stop,
                           es_threshold=early_stop_threshold, es_confidence=early_stop_confidence)
     triples = None

@@ -1,40 +1,39 @@
 #!/usr/bin/env python3
-"""Benchmark: ICP iterations/s (cfg1) + RANSAC hypotheses/s (cfg2) on synthetic 100k↔100k pairs.
+"""Benchmark: ICP iterations/s (cfg1, cfg3) + RANSAC hypotheses/s (cfg2) on synthetic pairs.
 
 BASELINE.json metric "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pts, 1/2/4/8 GPU".
 
-* step (the timed unit) = one full cfg1 ICP run: 100k source ↔ 100k target points per GPU,
-  50 point-to-plane iterations (convergence disabled → exactly 50 updates, 51 NN evaluations),
-  brute-force radius-bounded NN (r = 0.4·0.3), fp64 terms/solve, all device resident.
-  value = ICP iterations/s summed over ranks (each rank does one 100k×100k block per
-  iteration; N>1 is weak scaling).  N>1 follows the north-star's rule: the TARGET is sharded
-  (100k targets per rank, sources replicated, RCCL MIN of the packed NN keys + SUM of the 32
-  estimation terms per iteration — the cfg3 protocol) only when the cloud would not fit one
-  GPU's HBM; otherwise the sources are sharded (100k per rank) against the replicated target
-  with one RCCL SUM of the terms per iteration.  `--shard target|source` forces either.
+* step (the timed unit of the headline) = one full cfg1 ICP run: 100k source ↔ 100k target
+  points per GPU, 50 point-to-plane iterations (convergence disabled → exactly 50 updates, 51 NN
+  evaluations), brute-force radius-bounded NN (r = 0.4·0.3), exact fp64 correspondences
+  (nnkey.h), fp64 terms/solve, all device resident.  value = ICP iterations/s summed over ranks;
+  N > 1 is weak scaling (one cfg1 block per GPU): the north-star's rule shards the TARGET only
+  when the cloud would not fit one GPU's HBM (M3D_TARGET_SHARD_BYTES), else the sources
+  (`--shard target|source` forces either).  The collectives run inside libm3d over RCCL
+  (m3d_comm_*, `"comm": "libm3d-rccl"`); torch.distributed only carries the RCCL unique id.
+* "cfg3": BASELINE cfg3 — the 1M ↔ 1M pair, target sharded over the N GPUs (1M/N targets per
+  rank, one shared fp32 frame, sources replicated), MIN of the fp64 NN keys + MIN of the
+  claims + SUM of the 32 terms per iteration: STRONG scaling of one fixed problem, value = ICP
+  iterations/s of that problem.  Brute-force NN (north_star) and, beside it, the uniform grid.
+  `--config cfg3` makes it the headline line.
 * "ransac": cfg2 — benchmark_ransac.py's loop (a1 sample + Kabsch, a2 ‖d‖ < 1.5·v scoring) at
-  Nc = 1e5, H = 1e5 hypotheses per GPU, counter sampler seed 42, no early stop; N>1 shards the
-  hypothesis ids and all-reduces MAX of the packed (count, ~id) best key.  Its roofline prices
-  score_mfma_kernel (three v_mfma_f32_32x32x16_f16 per 32×32 (correspondence, hypothesis)
-  block = 96 flop per pair) against the FP16 MFMA peak; the 27-flop algorithmic figure is given
-  beside it against the FP32 vector roof.
-* roofline: dominant kernel = the ICP NN scan (nn_mfma_kernel), timed with HIP events recorded
-  by the library on the launch stream around every NN launch during a second timed pass of the
-  same K steps (an event record costs ~4 us between dependent kernels — tools/loop_overhead.py —
-  so `value` comes from the pass without them; both step times are in the line).  Its
-  screen key |t|² − 2q·t is a rank-4 contraction run on the matrix cores as one
-  v_mfma_f32_32x32x16_f16 per 32×32 (target, query) block: 16 fp16 MACs = 32 flop per pair
-  (K = 16 fp16 hi/lo split terms, 11 non-zero), so bound = "mfma" against the
-  dense FP16 MFMA peak 2.5 PFLOP/s, achieved = 32 flop × Ns × Nt / launch time.  The SURVEY's
-  8-flop-per-pair algorithmic figure is reported beside it against the FP32 vector roof
-  (157.3 TFLOP/s) that a VALU implementation is bounded by.  traffic = HBM bytes per launch
-  from the committed rocprofv3 PMC summary (profiles/), or null.
-* "icp_grid": the same cfg1 workload with the radius-bounded uniform-grid NN (SURVEY §8(f)
-  rank 1; identical correspondences, tests/test_gpu_icp.py) — HBM/latency-bound, so its
-  roofline is priced in GB/s on 28·Ns + 16·Nt algorithmic bytes per launch (query float4 +
-  visit order + key write, each target read once).
-* cpu_baseline (rank 0, N = 1): the oracle restatement (oracle/icp_oracle.py: scipy cKDTree on
-  16 threads + numpy point-to-plane) timed on a bounded sample of the same workload.
+  Nc = 1e5, H = 1e5 hypotheses per GPU, counter sampler seed 42, no early stop; N > 1 shards the
+  hypothesis ids and all-reduces MAX of the packed (count, ~id) key (m3d_ransac_best_allreduce).
+* "ransac_api": the reference harness's own calling pattern through the drop-in
+  (matcher.ransac.compute_step_transformation + evaluate_inlier_ratio per hypothesis,
+  benchmark_ransac.py:87-125) at Nc = 5k and 1e5: ms per call next to BASELINE.md's numbers.
+* roofline (every section): the kernel's ALGORITHMIC work ÷ its average launch time, measured
+  with HIP events recorded by the library on the launch stream around every launch (a second
+  timed pass of the same steps; `value` comes from the pass without events), ÷ the peak of the
+  pipe the kernel runs on.  The NN screen and the RANSAC residuals run on the FP16 matrix pipe
+  (DESIGN.md §3.2a/§3.5 — a deviation from north_star's "MFMA not used" that beats the FP32
+  vector roof), so `frac` = SURVEY §8(d)'s 8 flop per (source, target) pair resp. 27 flop per
+  (hypothesis, correspondence) pair ÷ the dense FP16 MFMA peak (2.5 PFLOP/s); `mfma_issue_frac`
+  gives the issued fp16 MACs (32 resp. 96 flop per pair) against the same peak.  The grid NN is
+  priced in GB/s on 28·Ns + 16·Nt algorithmic bytes per launch.  traffic = HBM bytes per launch
+  from the committed rocprofv3 PMC summary (profiles/pmc_*.json), or null.
+* cpu_baseline (rank 0, N = 1): the oracle restatement (scipy cKDTree + numpy point-to-plane;
+  numpy a1+a2) timed on the host cores this process may use (affinity ∩ cgroup quota).
 """
 
 from __future__ import annotations
@@ -52,11 +51,12 @@ sys.path.insert(0, str(ROOT / "3d-matching_amd"))
 VALU_FP32_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector)
 HBM_PEAK_GBS = 8000.0
 MFMA_F16_PEAK_TF = 2500.0   # MI355X_MICROARCH.md: Peak BF16/FP16 MFMA, dense
-NN_FLOP_PER_PAIR = 8        # 3 sub + 1 mul + 2 FMA (SURVEY §8(d), fp32 VALU formulation)
+NN_FLOP_PER_PAIR = 8        # 3 sub + 1 mul + 2 FMA: the algorithmic basis
 NN_MFMA_FLOP_PER_PAIR = 32  # 16 fp16 MACs per (target, query) pair in v_mfma_f32_32x32x16_f16
 SCORE_FLOP_PER_PAIR = 27    # 9 FMA transform + 3 sub + (1 mul + 2 FMA) + 1 cmp
 SCORE_MFMA_FLOP_PER_PAIR = 96  # 3 x v_mfma_f32_32x32x16_f16 (16 fp16 MACs each) per pair
-CPU_THREADS = 16            # the GPU box's CPU share per GPU
+NN_NOTE = ("north_star expected VALU; the |t|^2-2q.t screen runs on the FP16 matrix pipe "
+           "(DESIGN.md 3.5): frac = the 8-flop/pair algorithmic rate / the dense FP16 MFMA peak of that pipe")
 
 
 def parse():
@@ -64,21 +64,30 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", choices=["cfg1", "cfg3"], default="cfg1",
+                    help="headline: cfg1 (100k<->100k per GPU, weak) or cfg3 (1M<->1M, strong)")
     ap.add_argument("--ns", type=int, default=100_000)
-    ap.add_argument("--nt", type=int, default=100_000, help="target points per GPU")
+    ap.add_argument("--nt", type=int, default=100_000, help="target points per GPU (cfg1)")
     ap.add_argument("--icp-iters", type=int, default=50)
+    ap.add_argument("--cfg3-n", type=int, default=1_000_000)
+    ap.add_argument("--cfg3-iters", type=int, default=10)
+    ap.add_argument("--cfg3-steps", type=int, default=2)
+    ap.add_argument("--no-cfg3", action="store_true")
     ap.add_argument("--nc", type=int, default=100_000)
     ap.add_argument("--hyps", type=int, default=100_000, help="RANSAC hypotheses per GPU per run")
     ap.add_argument("--ransac-steps", type=int, default=3)
     ap.add_argument("--no-ransac", action="store_true")
     ap.add_argument("--ransac-warmup-s", type=float, default=0.5,
                     help="untimed RANSAC runs for at least this long before the timed ones")
+    ap.add_argument("--no-ransac-api", action="store_true")
     ap.add_argument("--no-grid", action="store_true")
     ap.add_argument("--shard", choices=["auto", "target", "source"], default="auto",
-                    help="N>1 ICP sharding: target (RCCL MIN of the NN keys + SUM of the terms), "
+                    help="N>1 cfg1 sharding: target (MIN of the NN keys + claims, SUM of the terms), "
                          "source (target replicated, SUM of the terms only), or auto: the "
                          "north-star's rule -- shard the target only when it would not fit one "
                          "GPU's HBM budget (M3D_TARGET_SHARD_BYTES, default 64 GiB), else source")
+    ap.add_argument("--comm", choices=["lib", "torch"], default="lib",
+                    help="N>1 collectives: libm3d's RCCL communicator, or torch.distributed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline leg")
     return ap.parse_args()
@@ -98,6 +107,34 @@ def pmc_traffic(kernel_substr: str):
     return None, None
 
 
+def host_cores():
+    """CPU threads this process may use: sched affinity ∩ the cgroup CPU quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except Exception:
+        pass
+    used = min(aff, quota) if quota else aff
+    env = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    return used, {"affinity": aff, "cgroup_quota": quota, **env}
+
+
+def nn_roofline(ns, nt, avg_ms, launches, terms_ms):
+    algo = NN_FLOP_PER_PAIR * ns * nt / (avg_ms * 1e-3) / 1e12
+    issued = NN_MFMA_FLOP_PER_PAIR * ns * nt / (avg_ms * 1e-3) / 1e12
+    traffic, src = pmc_traffic("nn_mfma_kernel")
+    return {"bound": "mfma", "kernel": "nn_mfma_kernel", "achieved": algo, "peak": MFMA_F16_PEAK_TF,
+            "unit": "TFLOP/s", "frac": algo / MFMA_F16_PEAK_TF, "traffic": traffic,
+            "traffic_source": src, "avg_launch_ms": avg_ms, "launches": launches,
+            "flop_per_pair": NN_FLOP_PER_PAIR, "pairs_per_launch": ns * nt,
+            "mfma_issued_tflops": issued, "mfma_issue_frac": issued / MFMA_F16_PEAK_TF,
+            "vs_fp32_valu_roof": algo / VALU_FP32_PEAK_TF, "terms_avg_launch_ms": terms_ms,
+            "note": NN_NOTE}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -109,8 +146,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         # M3D_BENCH_SAME_DEVICE=1 + M3D_BENCH_BACKEND=gloo: every rank on cuda:0 over gloo — a
-        # functional rehearsal of the N > 1 path on a one-GPU box (tools/gpu_multi_rehearsal.sh);
-        # the real runs are one rank per GPU over RCCL ("nccl")
+        # functional rehearsal of the N > 1 path on a one-GPU box (RCCL refuses two ranks on one
+        # GPU, so that rehearsal uses --comm torch); the real runs are one rank per GPU
         same = os.environ.get("M3D_BENCH_SAME_DEVICE") == "1"
         backend = os.environ.get("M3D_BENCH_BACKEND", "nccl")
         torch.cuda.set_device(0 if same else local)
@@ -123,13 +160,27 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from m3d import _lib, synth
-    from m3d.core import Cloud, CorrSet, IcpLoop, RansacParams, context
+    from m3d import dist as D
+    from m3d.core import RESULT_WORDS, Cloud, CorrSet, IcpLoop, RansacOutcome, RansacParams, context
 
     ctx = context()
+    comm, comm_name = None, "none"
+    if world > 1:
+        if args.comm == "lib":
+            try:
+                from m3d.comm import LibComm
+
+                comm, comm_name = LibComm(rank, world), "libm3d-rccl"
+            except Exception as e:  # reported, never silent
+                print(f"[bench] libm3d RCCL communicator unavailable ({e}); using torch.distributed",
+                      file=sys.stderr)
+        if comm is None:
+            comm, comm_name = D.TorchComm(), f"torch.distributed-{dist.get_backend()}"
 
     def barrier():
         if world > 1:
             dist.barrier()
+            torch.cuda.synchronize()
 
     def max_over_ranks(x: float) -> float:
         if world == 1:
@@ -138,101 +189,110 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def timed(fn, steps, kernels):
+        """(elapsed s of `steps` × fn without events, elapsed with events, {kernel: (ms, n)})."""
+        out = []
+        prof = {}
+        for events in (False, True):
+            ctx.profile(events)
+            for k in kernels:
+                ctx.profile_read(k)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                fn()
+            torch.cuda.synchronize()
+            barrier()
+            out.append(max_over_ranks(time.perf_counter() - t0))
+            if events:
+                prof = {k: ctx.profile_read(k) for k in kernels}
+            ctx.profile(False)
+        return out[0], out[1], prof
+
+    # ------------------------------------------------------------------ ICP loop runner
+    def icp_runner(loop, iters, mode, off=0, ns_total=0):
+        """One ICP run of `iters` updates (iters + 1 evaluations) on this rank."""
+        drv = None
+        if mode == "source" and comm_name != "libm3d-rccl":
+            drv = D.SourceShardedIcp(loop, loop.src.n, ns_total, dev, comm=comm)
+        elif mode == "target" and comm_name != "libm3d-rccl":
+            drv = D.ShardedIcp(loop, off, loop.src.n, dev, comm=comm)
+
+        def run():
+            loop.reset(np.eye(4))
+            if mode == "single":
+                loop.steps(iters + 1)  # the library enqueues the iterations natively
+            elif drv is None:  # libm3d issues the RCCL collectives between its own kernels
+                if mode == "source":
+                    loop.source_shard_steps(comm, iters + 1)
+                else:
+                    loop.shard_steps(comm, off, iters + 1)
+            else:
+                for _ in range(iters + 1):
+                    drv.iteration()
+        return run
+
     # ------------------------------------------------------------------ cfg1: ICP
     ns, nt, iters = args.ns, args.nt, args.icp_iters
     r = 0.4 * 0.3
-    if args.shard == "auto":
+    shard = args.shard
+    if shard == "auto":
         # north_star: "shards the target cloud ... with an RCCL all-reduce of per-shard
         # (min_dist, argmin) ... only for clouds large enough to saturate one GPU's HBM"; a
         # replicated cloud costs 64 B per point (DESIGN.md §3.1)
         budget = float(os.environ.get("M3D_TARGET_SHARD_BYTES", 64 * 2**30))
-        args.shard = "target" if 64.0 * nt * world > budget else "source"
-    source_shard = world > 1 and args.shard == "source"
-    if source_shard:  # weak scaling: ns sources per rank against the whole (replicated) target
+        shard = "target" if 64.0 * nt * world > budget else "source"
+    mode1 = "single" if world == 1 else shard
+    if mode1 == "source":  # weak scaling: ns sources per rank against the whole (replicated) target
         src_all, tgt_all, nrm_all, T_true = synth.icp_pair(ns * world, nt, seed=0)
         src = src_all[rank * ns:(rank + 1) * ns]
         off = 0
         tgt_c = Cloud(tgt_all, nrm_all)
-    else:  # target-sharded: nt targets per rank, sources replicated
+    else:  # single device, or target-sharded: nt targets per rank, sources replicated
         src, tgt_all, nrm_all, T_true = synth.icp_pair(ns, nt * world, seed=0)
         off = rank * nt
-        # one fp32 frame for every shard (the whole target's mean): keys compare bit for bit
-        # across ranks, and non-owning ranks start from a distance bound (m3d_cloud_create_framed)
-        tgt_c = Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0))
+        tgt_c = (Cloud(tgt_all, nrm_all) if world == 1 else
+                 Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0)))
     src_c = Cloud(src)
-    keys = torch.empty(ns, dtype=torch.int64, device=dev)
-    claim = torch.empty(ns, dtype=torch.int32, device=dev)
-    sums = torch.empty(32, dtype=torch.float64, device=dev)
+    K_NN, K_TERMS = _lib.KERNEL_NN, _lib.KERNEL_TERMS
 
-    def time_icp(nn: str):
-        loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters,
-                       nn=nn)
-        if source_shard:
+    def bench_icp(nn):
+        loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters, nn=nn)
+        if mode1 == "source":
             loop.set_source_total(ns * world)
-
-        def icp_run():
-            loop.reset(np.eye(4))
-            if world == 1:
-                loop.steps(iters + 1)  # the library enqueues the 51 iterations natively
-                return
-            for _ in range(iters + 1):
-                if source_shard:  # keys stay inside the loop object: no copies
-                    loop.shard_nn(0, None)
-                    loop.shard_terms(0, None, None, sums)
-                    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-                    loop.solve(sums)
-                else:
-                    loop.shard_nn(off, keys)
-                    dist.all_reduce(keys, op=dist.ReduceOp.MIN)
-                    loop.shard_claim(keys, claim)
-                    dist.all_reduce(claim, op=dist.ReduceOp.MIN)
-                    loop.shard_terms(off, keys, claim, sums)
-                    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-                    loop.solve(sums)
-
-        def timed(events: bool):
-            ctx.profile(events)
-            ctx.profile_read(_lib.KERNEL_NN)
-            ctx.profile_read(_lib.KERNEL_TERMS)
-            barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                icp_run()
-            torch.cuda.synchronize()
-            barrier()
-            el = max_over_ranks(time.perf_counter() - t0)
-            nn_ms, nn_n = ctx.profile_read(_lib.KERNEL_NN)
-            terms_ms, terms_n = ctx.profile_read(_lib.KERNEL_TERMS)
-            ctx.profile(False)
-            return el, nn_ms, nn_n, terms_ms, terms_n
-
+        run = icp_runner(loop, iters, mode1, off, ns * world)
         for _ in range(args.warmup):
-            icp_run()
+            run()
         torch.cuda.synchronize()
-        # value: the K steps with nothing else on the stream.  Kernel durations: the same K steps
-        # again with the library's HIP events around every NN and terms launch (each event record
-        # costs ~4 us of stream time between dependent kernels: tools/loop_overhead.py).
-        el, _, _, _, _ = timed(False)
-        el_ev, nn_ms, nn_n, terms_ms, terms_n = timed(True)
-        return (el, max_over_ranks(nn_ms / max(nn_n, 1)), nn_n, terms_ms / max(terms_n, 1),
-                loop.result(), el_ev)
+        el, el_ev, prof = timed(run, args.steps, (K_NN, K_TERMS))
+        (nn_ms, nn_n), (t_ms, t_n) = prof[K_NN], prof[K_TERMS]
+        return el, el_ev, max_over_ranks(nn_ms / max(nn_n, 1)), nn_n, t_ms / max(t_n, 1), loop.result()
 
-    el, nn_avg_ms, nn_n, terms_avg_ms, res, el_ev = time_icp("brute")
+    el, el_ev, nn_avg_ms, nn_n, terms_avg_ms, res = bench_icp("brute")
     icp_value = world * iters * args.steps / el
-    nn_flop = NN_MFMA_FLOP_PER_PAIR * ns * nt
-    achieved_tf = nn_flop / (nn_avg_ms * 1e-3) / 1e12
-    algo_tf = NN_FLOP_PER_PAIR * ns * nt / (nn_avg_ms * 1e-3) / 1e12
     err = float(np.abs(res.transformation - T_true).max())
+    cfg1 = {
+        "value": icp_value, "ms_per_step": el / args.steps * 1e3,
+        "ms_per_step_with_kernel_events": el_ev / args.steps * 1e3,
+        "workload": (f"cfg1: {ns}<->{nt} synthetic pair per GPU, {iters} point-to-plane ICP "
+                     f"iterations, brute-force NN (r={r:g}), "
+                     + ("1 GPU" if world == 1 else
+                        (f"sources sharded over {world} GPUs ({ns} per GPU), target replicated (SUM terms)"
+                         if mode1 == "source" else
+                         f"target sharded over {world} GPUs ({nt} per GPU), sources replicated "
+                         "(MIN keys + MIN claims + SUM terms)"))),
+        "roofline": nn_roofline(ns, nt, nn_avg_ms, nn_n, terms_avg_ms),
+        "check": {"icp_fitness": res.fitness, "icp_rmse": res.inlier_rmse, "max_abs_err_vs_T_true": err},
+    }
 
-    # ------------------------------------------------------------------ cfg1 with the grid NN
     icp_grid = None
     if not args.no_grid:
         tg0 = time.perf_counter()
         IcpLoop(src_c, tgt_c, r, max_iteration=0, nn="grid")  # builds both clouds' grids once
         torch.cuda.synchronize()
         build_ms = (time.perf_counter() - tg0) * 1e3
-        gel, g_ms, g_n, g_terms_ms, gres, gel_ev = time_icp("grid")
+        gel, gel_ev, g_ms, g_n, g_terms_ms, gres = bench_icp("grid")
         g_bytes = 28 * ns + 16 * nt
         g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
         icp_grid = {
@@ -248,6 +308,48 @@ def main():
                          "terms_avg_launch_ms": g_terms_ms},
         }
 
+    # ------------------------------------------------------------------ cfg3: 1M <-> 1M, strong
+    cfg3 = None
+    if not args.no_cfg3 or args.config == "cfg3":
+        n3, it3 = args.cfg3_n, args.cfg3_iters
+        s3, t3, nr3, T3 = synth.icp_pair(n3, n3, seed=0)
+        o3, c3 = D.shard_bounds(n3, world, rank)
+        s3c = Cloud(s3)
+        t3c = Cloud(t3, nr3) if world == 1 else Cloud(t3[o3:o3 + c3], nr3[o3:o3 + c3], center=t3.mean(axis=0))
+        mode3 = "single" if world == 1 else "target"
+        cfg3 = {"metric": "ICP iterations/sec (cfg3: 1M<->1M pair, target sharded over the GPUs, strong scaling)",
+                "unit": "ICP iter/s (whole 1M x 1M problem)", "scaling": "strong",
+                "workload": f"cfg3: {n3}<->{n3} synthetic pair, {it3} point-to-plane iterations per step, "
+                            f"target sharded over {world} GPU(s) ({c3} targets on rank {rank}), sources "
+                            "replicated, MIN fp64 keys + MIN claims + SUM terms per iteration",
+                "steps": args.cfg3_steps, "icp_iterations_per_step": it3}
+        for nn in ("brute", "grid"):
+            lp = IcpLoop(s3c, t3c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=it3, nn=nn)
+            run = icp_runner(lp, it3, mode3, o3)
+            run()
+            torch.cuda.synchronize()
+            e3, e3_ev, prof = timed(run, args.cfg3_steps, (K_NN, K_TERMS))
+            (m, n), (tm, tn) = prof[K_NN], prof[K_TERMS]
+            avg = max_over_ranks(m / max(n, 1))
+            r3 = lp.result()
+            sec = {"value": it3 * args.cfg3_steps / e3, "ms_per_iteration": e3 / (it3 * args.cfg3_steps) * 1e3,
+                   "ms_per_iteration_with_kernel_events": e3_ev / (it3 * args.cfg3_steps) * 1e3,
+                   "nn_avg_launch_ms": avg, "terms_avg_launch_ms": tm / max(tn, 1),
+                   "fitness": r3.fitness, "max_abs_err_vs_T_true": float(np.abs(r3.transformation - T3).max())}
+            if nn == "brute":
+                sec["roofline"] = nn_roofline(n3, c3, avg, n, tm / max(tn, 1))
+                sec["roofline"]["note"] = "per rank: " + NN_NOTE
+                cfg3.update(sec)
+            else:
+                g_bytes = 28 * n3 + 16 * c3
+                sec["roofline"] = {"bound": "hbm", "kernel": "grid_nn_kernel",
+                                   "achieved": g_bytes / (avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": g_bytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                   "bytes_per_launch": g_bytes}
+                cfg3["grid"] = sec
+            del lp
+        del s3c, t3c
+
     # ------------------------------------------------------------------ cfg2: RANSAC
     ransac = None
     if not args.no_ransac:
@@ -257,17 +359,18 @@ def main():
         thr = 0.3 * 1.5
         params = RansacParams(max_iter=H, seed=42, thr=thr, mode=_lib.SCORE_NORM, early_stop=False,
                               hyp0=rank * H)
-
-        from m3d.core import RESULT_WORDS, RansacOutcome
         res_buf = torch.zeros(RESULT_WORDS, dtype=torch.int64, device=dev)
+        key = torch.zeros(1, dtype=torch.int64, device=dev)
 
         def ransac_run():
             # enqueued without a host round trip (m3d_ransac_run_async): runs go back to back
             cs.run_async(params, res_buf)
             if world > 1:  # best over ranks: highest count, lowest global id (device-side key)
-                key = (res_buf[19:20] * (1 << 32) + (0xFFFFFFFF - (rank * H + res_buf[17:18])))
-                dist.all_reduce(key, op=dist.ReduceOp.MAX)
-            return res_buf
+                if comm_name == "libm3d-rccl":
+                    cs.best_allreduce(comm, res_buf, rank * H, key)
+                else:
+                    key.copy_(res_buf[19:20] * (1 << 32) + (0xFFFFFFFF - (rank * H + res_buf[17:18])))
+                    comm.max_(key)
 
         # warm-up: the clocks drop while the host prepares the RANSAC data with the GPU idle, so
         # run about --ransac-warmup-s seconds of untimed runs (the same count on every rank: the
@@ -281,90 +384,132 @@ def main():
         for _ in range(max(0, int(args.ransac_warmup_s / max(t_one, 1e-6)) - 2)):
             ransac_run()
         torch.cuda.synchronize()
-
-        def ransac_timed(events: bool):
-            ctx.profile(events)
-            ctx.profile_read(_lib.KERNEL_SCORE)
-            ctx.profile_read(_lib.KERNEL_KABSCH)
-            barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.ransac_steps):
-                out = ransac_run()
-            torch.cuda.synchronize()
-            barrier()
-            el = max_over_ranks(time.perf_counter() - t0)
-            sc = ctx.profile_read(_lib.KERNEL_SCORE)
-            kb = ctx.profile_read(_lib.KERNEL_KABSCH)
-            ctx.profile(False)
-            return el, sc, kb, RansacOutcome.from_device(out, nc)
-
-        rel, _, _, out = ransac_timed(False)  # value: no events on the stream
-        rel_ev, (sc_ms, sc_n), (kb_ms, kb_n), _ = ransac_timed(True)  # kernel durations
+        K_SC, K_KB = _lib.KERNEL_SCORE, _lib.KERNEL_KABSCH
+        rel, rel_ev, prof = timed(ransac_run, args.ransac_steps, (K_SC, K_KB))
+        out = RansacOutcome.from_device(res_buf, nc)
+        (sc_ms, sc_n), (kb_ms, kb_n) = prof[K_SC], prof[K_KB]
         sc_avg = max_over_ranks(sc_ms / max(sc_n, 1))
         hyps_per_launch = H / max(sc_n // args.ransac_steps, 1)
-        sc_tf = SCORE_MFMA_FLOP_PER_PAIR * nc * hyps_per_launch / (sc_avg * 1e-3) / 1e12
-        sc_algo_tf = SCORE_FLOP_PER_PAIR * nc * hyps_per_launch / (sc_avg * 1e-3) / 1e12
+        pairs = nc * hyps_per_launch
+        sc_algo = SCORE_FLOP_PER_PAIR * pairs / (sc_avg * 1e-3) / 1e12
+        sc_issued = SCORE_MFMA_FLOP_PER_PAIR * pairs / (sc_avg * 1e-3) / 1e12
         ransac = {
             "metric": "RANSAC hypotheses/sec (cfg2: Nc=1e5, a1+a2, no early stop)",
             "value": world * H * args.ransac_steps / rel, "unit": "hyp/s",
             "ms_per_run": rel / args.ransac_steps * 1e3,
             "ms_per_run_with_kernel_events": rel_ev / args.ransac_steps * 1e3,
-            "hyps_per_gpu": H, "nc": nc,
-            "best_fitness": out.fitness,
-            "roofline": {"bound": "mfma", "kernel": "score_mfma_kernel", "achieved": sc_tf,
-                         "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s", "frac": sc_tf / MFMA_F16_PEAK_TF,
-                         "avg_launch_ms": sc_avg, "launches": sc_n,
-                         "flop_per_pair": SCORE_MFMA_FLOP_PER_PAIR,
-                         "algorithmic_27flop_per_pair_tflops": sc_algo_tf,
-                         "vs_fp32_valu_roof": sc_algo_tf / VALU_FP32_PEAK_TF},
+            "hyps_per_gpu": H, "nc": nc, "best_fitness": out.fitness,
+            "roofline": {"bound": "mfma", "kernel": "score_mfma_kernel", "achieved": sc_algo,
+                         "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s", "frac": sc_algo / MFMA_F16_PEAK_TF,
+                         "traffic": pmc_traffic("score_mfma_kernel")[0],
+                         "avg_launch_ms": sc_avg, "launches": sc_n, "flop_per_pair": SCORE_FLOP_PER_PAIR,
+                         "pairs_per_launch": pairs, "mfma_issued_tflops": sc_issued,
+                         "mfma_issue_frac": sc_issued / MFMA_F16_PEAK_TF,
+                         "vs_fp32_valu_roof": sc_algo / VALU_FP32_PEAK_TF,
+                         "note": "27-flop/pair algorithmic rate / dense FP16 MFMA peak (the residuals "
+                                 "run on the matrix pipe, DESIGN.md 3.2a)"},
             "kabsch_avg_launch_ms": kb_ms / max(kb_n, 1),
         }
+
+    # ------------------------------------------------------------------ drop-in per-call path
+    ransac_api = None
+    if rank == 0 and world == 1 and not args.no_ransac_api:
+        ransac_api = bench_ransac_api(args)
 
     # ------------------------------------------------------------------ CPU baseline
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(src, tgt_all[:nt], nrm_all[:nt], r, args, ransac is not None)
 
-    traffic, traffic_src = pmc_traffic("nn_mfma_kernel")
+    if args.config == "cfg3":
+        head = dict(metric="ICP iterations/sec (cfg3: 1M<->1M, target shard over N GPUs)",
+                    value=cfg3["value"], unit=cfg3["unit"], scaling="strong", steps=args.cfg3_steps,
+                    ms_per_step=cfg3["ms_per_iteration"] * args.cfg3_iters,
+                    workload=cfg3["workload"], roofline=cfg3["roofline"])
+    else:
+        head = dict(metric="ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pts, 1/2/4/8 GPU",
+                    value=cfg1["value"], unit="ICP iter/s (100k src x 100k tgt per GPU)", scaling="weak",
+                    steps=args.steps, ms_per_step=cfg1["ms_per_step"], workload=cfg1["workload"],
+                    roofline=cfg1["roofline"])
     line = {
-        "metric": "ICP iterations/sec + RANSAC hypotheses/sec, 100k↔100k pts, 1/2/4/8 GPU",
-        "value": icp_value,
-        "unit": "ICP iter/s (100k src x 100k tgt per GPU)",
+        "metric": head["metric"],
+        "value": head["value"],
+        "unit": head["unit"],
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": head["steps"],
         "warmup": args.warmup,
-        "ms_per_step": el / args.steps * 1e3,
-        "ms_per_step_with_kernel_events": el_ev / args.steps * 1e3,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": head["scaling"],
         "vs_baseline": None,
-        "dtype": "f16-split MFMA NN screen (exact f32 NN result) + f64 terms/solve",
+        "dtype": "fp16-split MFMA NN screen + fp32 scan, exact fp64 NN decision, fp64 terms/solve",
         "data": "synthetic (m3d.synth: asymmetric closed surface, extent ~10, analytic normals)",
-        "config": {"workload": "cfg1: 100k<->100k synthetic pair, 50 point-to-plane ICP iterations, "
-                               "brute-force NN (r=0.12), 1 GPU" if world == 1 else
-                               (f"cfg1 per GPU, sources sharded over {world} GPUs, target replicated (RCCL SUM terms)"
-                                if source_shard else
-                                f"cfg1 per GPU, target sharded over {world} GPUs (RCCL MIN keys + SUM terms)"),
-                   "ns": ns, "nt_per_gpu": nt, "icp_iterations_per_step": iters, "max_corr": r,
-                   "parallelism": "single" if world == 1 else f"{args.shard}-shard x{world}"},
-        "roofline": {"bound": "mfma", "kernel": "nn_mfma_kernel", "achieved": achieved_tf,
-                     "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / MFMA_F16_PEAK_TF,
-                     "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": nn_avg_ms,
-                     "launches": nn_n, "flop_per_launch": nn_flop,
-                     "flop_per_pair": NN_MFMA_FLOP_PER_PAIR,
-                     "algorithmic_8flop_per_pair_tflops": algo_tf,
-                     "vs_fp32_valu_roof": algo_tf / VALU_FP32_PEAK_TF,
-                     "terms_avg_launch_ms": terms_avg_ms},
+        "config": {"workload": head["workload"], "ns": ns, "nt_per_gpu": nt, "icp_iterations_per_step": iters,
+                   "max_corr": r, "parallelism": "single" if world == 1 else f"{mode1}-shard x{world}",
+                   "comm": comm_name},
+        "roofline": head["roofline"],
+        "ms_per_step_with_kernel_events": cfg1["ms_per_step_with_kernel_events"],
+        "cfg1": {k: v for k, v in cfg1.items() if k != "roofline"} if args.config == "cfg3" else None,
         "icp_grid": icp_grid,
+        "cfg3": (cfg3 if args.config != "cfg3" or cfg3 is None
+                 else {k: v for k, v in cfg3.items() if k != "roofline"}),
         "ransac": ransac,
+        "ransac_api": ransac_api,
         "cpu_baseline": cpu,
-        "check": {"icp_fitness": res.fitness, "icp_rmse": res.inlier_rmse, "max_abs_err_vs_T_true": err},
+        "check": cfg1["check"],
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
+    del comm
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_ransac_api(args, budget_s=1.5):
+    """benchmark_ransac.py:87-125 through the drop-in: per hypothesis one
+    compute_step_transformation + one evaluate_inlier_ratio on Ply-likes (cfg0's 5k and cfg2's
+    1e5 correspondences; legacy global RNG seeded 42).  Both cache key policies (m3d.cache)."""
+    import numpy as np
+    import torch
+
+    from m3d import cache, synth
+    from matcher import ransac as M
+    from ply import Ply
+
+    out = {"harness": "benchmark_ransac.py:87-125 (compute_step_transformation + evaluate_inlier_ratio "
+                      "per hypothesis) through matcher.ransac",
+           "reference_ms_survey_container_8_cores": {
+               "5000": {"compute_step_transformation": 0.125, "evaluate_inlier_ratio": 0.423},
+               "100000": {"compute_step_transformation": 1.43, "evaluate_inlier_ratio": 9.28}}}
+    for nc in (5000, args.nc):
+        s, t, corr, _ = synth.ransac_pair(nc, seed=42)
+        src, tgt = Ply.from_arrays(s), Ply.from_arrays(t)
+        for pol in ("content", "identity"):
+            cache.set_policy(pol)
+            cache.clear()
+            np.random.seed(42)
+            for _ in range(3):  # pack + first calls
+                res = M.compute_step_transformation(src, tgt, corr)
+                M.evaluate_inlier_ratio(src, tgt, corr, res.transformation, 0.3)
+            torch.cuda.synchronize()
+            a = b = 0.0
+            n = 0
+            t_end = time.perf_counter() + budget_s
+            while time.perf_counter() < t_end or n < 20:
+                t0 = time.perf_counter()
+                res = M.compute_step_transformation(src, tgt, corr)
+                t1 = time.perf_counter()
+                M.evaluate_inlier_ratio(src, tgt, corr, res.transformation, 0.3)
+                t2 = time.perf_counter()
+                a += t1 - t0
+                b += t2 - t1
+                n += 1
+            out[f"{nc}_{pol}"] = {"compute_step_transformation_ms": a / n * 1e3,
+                                  "evaluate_inlier_ratio_ms": b / n * 1e3,
+                                  "hyps_per_s": n / (a + b), "hypotheses": n}
+    cache.set_policy("content")
+    cache.clear()
+    return out
 
 
 def cpu_baseline(src, tgt, nrm, r, args, with_ransac):
@@ -377,6 +522,7 @@ def cpu_baseline(src, tgt, nrm, r, args, with_ransac):
     import ransac_oracle as O
     from m3d import synth
 
+    cores, detail = host_cores()
     # ICP: Open3D-semantics iterations (KD-tree built once, like RegistrationICP)
     tree = cKDTree(tgt)
     T = np.eye(4)
@@ -384,16 +530,16 @@ def cpu_baseline(src, tgt, nrm, r, args, with_ransac):
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < args.cpu_budget and n_it < 200:
         pcd = I.transform_points(T, src)
-        d, j = tree.query(pcd, k=1, workers=CPU_THREADS)
+        d, j = tree.query(pcd, k=1, workers=cores)
         ok = d * d < r * r
         corr = np.stack([np.nonzero(ok)[0], j[ok]], axis=1)
         T = I.point_to_plane_update(pcd, tgt, nrm, corr) @ T
         n_it += 1
     icp_el = time.perf_counter() - t0
-    out = {"value": n_it / icp_el, "unit": "ICP iter/s (100k src x 100k tgt)", "cores": CPU_THREADS,
-           "kind": "port",
+    out = {"value": n_it / icp_el, "unit": "ICP iter/s (100k src x 100k tgt)", "cores": cores,
+           "cores_detail": detail, "kind": "port",
            "sample": f"{n_it} Open3D-semantics point-to-plane iterations on the cfg1 pair "
-                     f"(oracle/icp_oracle.py: scipy cKDTree workers={CPU_THREADS}, numpy fp64; "
+                     f"(oracle/icp_oracle.py: scipy cKDTree workers={cores}, numpy fp64; "
                      "KD-tree build excluded)"}
     if with_ransac:
         src_r, tgt_r, corr_r, _ = synth.ransac_pair(args.nc, seed=42)
