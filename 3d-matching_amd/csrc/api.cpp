@@ -720,8 +720,8 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = 
   s->keys_clean = false;
   if (s->params.nn_method == M3D_NN_GRID) {
     KTimer kt(ctx, M3D_KERNEL_NN, st);
-    return launch_grid_nn(s->src->xyz32, s->src->n, s->qorder, s->tgrid, off, s->state, s->keys,
-                          s->near2, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st);
+    return launch_grid_nn(s->src->xyz32, s->src->n, s->sgrid, s->tgrid, off, s->state, s->keys,
+                          s->near2, s->sq, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st);
   }
   if (!seeded) {
     hipError_t e = launch_icp_keyinit(s, off, st);
@@ -753,9 +753,18 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
     // same grids only ORDER the points (targets and queries in cell order make the MFMA
     // screen's 32-target sub-tiles and 64-query waves spatially compact); every pair is still
     // screened.
-    const double cell = max_dist * 1.001;
+    static const double cell_div = [] {  // M3D_GRID_CELL_DIV (experiment): cell = radius / div
+      const char* e = getenv("M3D_GRID_CELL_DIV");
+      const double v = e ? atof(e) : 1.0;
+      return v >= 1.0 ? v : 1.0;
+    }();
+    const double cell = max_dist * 1.001 / cell_div;
     int grc = ensure_grid(ctx, tgt, cell, nullptr, &tg);
     if (!grc) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
+    if (!grc && params->nn_method == M3D_NN_GRID && sg->mpts == nullptr) {
+      hipError_t e = grid_morton(const_cast<Grid*>(sg), nullptr);
+      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("morton order: ") + hipGetErrorString(e));
+    }
     if (!grc && params->nn_method == M3D_NN_BRUTE && tg->mf16 == nullptr) {
       hipError_t e = build_mfma_tiles(tgt, const_cast<Grid*>(tg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("mfma tiles: ") + hipGetErrorString(e));
@@ -771,12 +780,22 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   s->nblocks = terms_blocks(src->n);
   s->tgrid = tg;
   s->qorder = sg->order;
+  s->sgrid = sg;
   int rc = dev_alloc(ctx, &s->state, 1);
   if (!rc) rc = dev_alloc(ctx, &s->keys, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->near2, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->dprev, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->ld64, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->lidx, std::max<int64_t>(src->n, 1));
+  // seed records (M3D_GRID_SEEDREC=1): measured slower while the clouds keep the caller's point
+  // order — the terms pass's writes to Morton positions scatter (cfg1 grid iteration 38.8 →
+  // 41.5 µs, 1M × 125k 137 → 152 µs)
+  static const bool seedrec = [] {
+    const char* e = getenv("M3D_GRID_SEEDREC");
+    return e && atoi(e) == 1;
+  }();
+  if (!rc && seedrec && params->nn_method == M3D_NN_GRID && sg->minv != nullptr)
+    rc = dev_alloc(ctx, &s->sq, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->corr, std::max<int64_t>(src->n, 1));
   if (!rc) rc = dev_alloc(ctx, &s->partials, s->nblocks * kTermSlots);
   if (!rc) rc = dev_alloc(ctx, &s->sums, kTermSlots);
@@ -796,6 +815,7 @@ void m3d_icp_destroy(m3d_icp* s) {
   hipFree(s->dprev);
   hipFree(s->ld64);
   hipFree(s->lidx);
+  hipFree(s->sq);
   hipFree(s->xdk);
   hipFree(s->xcl);
   hipFree(s->xsums);
@@ -815,6 +835,8 @@ int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
   HIPX(ctx, hipMemsetAsync(s->corr, 0xFF, sizeof(int32_t) * std::max<int64_t>(s->src->n, 1), st));
   // all-ones bits = a NaN distance: no bound seed until a target-shard exchange wrote dprev
   HIPX(ctx, hipMemsetAsync(s->dprev, 0xFF, sizeof(int64_t) * std::max<int64_t>(s->src->n, 1), st));
+  if (s->sq != nullptr)  // all-ones index: no seed (nnkey.h seed_rec)
+    HIPX(ctx, hipMemsetAsync(s->sq, 0xFF, sizeof(float4) * std::max<int64_t>(s->src->n, 1), st));
   HIPX(ctx, launch_icp_reset(s, T, st));
   s->keys_clean = false;
   return M3D_OK;

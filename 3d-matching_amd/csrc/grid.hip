@@ -187,6 +187,149 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __res
   }
 }
 
+// ------------------------------------------------------------------------------- batched
+// Per-query form over the Morton query order: kL lanes per query, the queries straight from the
+// Morton-sorted points (no order[] indirection).  Every lane of a query sees every cell row of
+// its box and takes the row's points sub, sub + kL, …: the start offsets of kR rows are loaded
+// together, then kR × kB point loads per lane go out at once, so a typical seeded query (≤ kR
+// rows of ≤ kL·kB points) costs one round of start loads and one round of point loads instead of
+// one dependent load per point.  Blocks are remapped XCD-contiguously (blocks b and b + 8 share
+// an XCD's L2: each XCD gets one contiguous slice of the Morton order, so its L2 holds one
+// region's targets and cell starts instead of every region's).
+template <int kL, int kR, int kB>
+__global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
+    const float4* __restrict__ qpts, int64_t ns, GridDev g, int64_t off,
+    const IcpState* __restrict__ s, int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
+    const float4* __restrict__ sq, const int32_t* __restrict__ prev,
+    const int64_t* __restrict__ dprev, const float4* __restrict__ tgt32, int64_t nt_shard,
+    int64_t nblocks, unsigned long long* __restrict__ stats) {
+  // stats (M3D_GRID_STATS=1, diagnostics only, else null): [0] queries, [1] cell rows,
+  // [2] candidate points, [3] queries with a seed
+  if (s->done) return;
+  const int64_t per = (nblocks + 7) / 8;
+  const int64_t blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (blk >= nblocks) return;
+  const int64_t t = (blk * kGridBlock + threadIdx.x) / kL;
+  const int sub = threadIdx.x & (kL - 1);
+  const float r2_hi = s->r2_hi, be = s->band_e;
+  const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
+  uint64_t k1 = key0;
+  float k1d = kInf, n2 = kInf;
+  int64_t i = -1;
+  if (t < ns) {
+    const float4 p = qpts[t];
+    i = (int64_t)__float_as_int(p.w);
+    float qx, qy, qz;
+    xform32(s->Rt32, p, qx, qy, qz);
+    // seed: the record the terms pass left in query order (no prev[] → target gather), or
+    // the correspondence array when no record buffer is kept
+    const int64_t seed = sq != nullptr ? seed_from_rec(s, sq[t], p, qx, qy, qz)
+                                       : seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
+    if (seed != kKeyNone) k1 = (uint64_t)seed;
+    k1d = key_real_d2(k1);
+    if (g.ncells > 0) {
+      const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
+      const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
+      const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
+      const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
+      const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
+      const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
+      const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
+      const int ny = y1 - y0 + 1;
+      const int rows = ny * (z1 - z0 + 1);
+      if (stats != nullptr && sub == 0) {
+        atomicAdd(&stats[0], 1ull);
+        atomicAdd(&stats[1], (unsigned long long)rows);
+        if (seed != kKeyNone) atomicAdd(&stats[3], 1ull);
+      }
+      for (int r0 = 0; r0 < rows; r0 += kR) {
+        int32_t a[kR], b[kR];
+        int32_t len = 0;
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          const int r = r0 + k;
+          a[k] = b[k] = 0;
+          if (r < rows) {
+            const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
+            a[k] = g.start[row + x0];
+            b[k] = g.start[row + x1 + 1];
+          }
+          len = max(len, b[k] - a[k]);
+          if (stats != nullptr && sub == 0) atomicAdd(&stats[2], (unsigned long long)(b[k] - a[k]));
+        }
+        for (int32_t base = sub; base < len; base += kL * kB) {
+          float4 v[kR][kB];
+#pragma unroll
+          for (int k = 0; k < kR; ++k)
+#pragma unroll
+            for (int m = 0; m < kB; ++m) {
+              const int32_t j = a[k] + base + m * kL;
+              if (j < b[k]) v[k][m] = g.pts[j];
+            }
+#pragma unroll
+          for (int k = 0; k < kR; ++k)
+#pragma unroll
+            for (int m = 0; m < kB; ++m) {
+              const int32_t j = a[k] + base + m * kL;
+              if (j < b[k]) {
+                const float d2 = d2f(qx, qy, qz, v[k][m].x, v[k][m].y, v[k][m].z);
+                if (d2 <= r2_hi)
+                  near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(v[k][m].w))), d2);
+              }
+            }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = kL / 2; o > 0; o >>= 1) {
+    const uint64_t b1 = ((uint64_t)(uint32_t)__shfl_xor((int)(k1 >> 32), o, kL) << 32) |
+                        (uint32_t)__shfl_xor((int)(uint32_t)k1, o, kL);
+    const float bn2 = __shfl_xor(n2, o, kL);
+    near_merge(k1, k1d, n2, b1, bn2);
+  }
+  if (i >= 0 && sub == 0) {
+    keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
+    near2[i] = __float_as_uint(n2);
+  }
+}
+
+// Morton (Z-curve) order of a cloud's points by their cells (10 bits per axis; finer grids are
+// coarsened — only locality matters, any order gives the same keys).
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {
+  v &= 0x3FF;
+  v = (v | (v << 16)) & 0x030000FF;
+  v = (v | (v << 8)) & 0x0300F00F;
+  v = (v | (v << 4)) & 0x030C30C3;
+  v = (v | (v << 2)) & 0x09249249;
+  return v;
+}
+
+__global__ __launch_bounds__(kGridBlock) void morton_key_kernel(const float4* __restrict__ pts, int64_t n,
+                                                                GridDev g, int sx, int sy, int sz,
+                                                                uint32_t* __restrict__ key,
+                                                                int32_t* __restrict__ val) {
+  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (k >= n) return;
+  const float4 v = pts[k];
+  const uint32_t cx = (uint32_t)grid_coord(v.x, g.o[0], g.inv_h, g.n[0]) >> sx;
+  const uint32_t cy = (uint32_t)grid_coord(v.y, g.o[1], g.inv_h, g.n[1]) >> sy;
+  const uint32_t cz = (uint32_t)grid_coord(v.z, g.o[2], g.inv_h, g.n[2]) >> sz;
+  key[k] = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
+  val[k] = (int32_t)k;
+}
+
+__global__ __launch_bounds__(kGridBlock) void morton_gather_kernel(const float4* __restrict__ pts,
+                                                                   const int32_t* __restrict__ perm,
+                                                                   int64_t n, float4* __restrict__ out,
+                                                                   int32_t* __restrict__ minv) {
+  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (k >= n) return;
+  const float4 v = pts[perm[k]];
+  out[k] = v;
+  minv[__float_as_int(v.w)] = (int32_t)k;
+}
+
 // ------------------------------------------------------------------------------- host side
 static hipError_t grid_fail(hipError_t e, void* a, void* b, void* c, void* d, void* tmp) {
   hipFree(a);
@@ -287,6 +430,10 @@ void grid_free(Grid* g) {
   hipFree(g->start);
   hipFree(g->pts);
   hipFree(g->order);
+  hipFree(g->mpts);
+  hipFree(g->minv);
+  g->mpts = nullptr;
+  g->minv = nullptr;
   hipFree(g->mf16);
   hipFree(g->mf32);
   g->start = nullptr;
@@ -297,16 +444,90 @@ void grid_free(Grid* g) {
   g->mf_npad = 0;
 }
 
-hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
+hipError_t grid_morton(Grid* g, hipStream_t st) {
+  if (g->mpts != nullptr || g->n_pts == 0) return hipSuccess;
+  const int64_t n = g->n_pts;
+  int sh[3];
+  for (int k = 0; k < 3; ++k) {
+    sh[k] = 0;
+    while ((g->dev.n[k] >> sh[k]) > 1024) ++sh[k];
+  }
+  uint32_t *kin = nullptr, *kout = nullptr;
+  int32_t *vin = nullptr, *vout = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  hipError_t e;
+  if ((e = hipMalloc(&kin, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&kout, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&vin, sizeof(int32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&vout, sizeof(int32_t) * n)) != hipSuccess)
+    return grid_fail(e, kin, kout, vin, vout, tmp);
+  const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
+  morton_key_kernel<<<blocks, kGridBlock, 0, st>>>(g->pts, n, g->dev, sh[0], sh[1], sh[2], kin, vin);
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
+  if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 1));
+  if (e == hipSuccess)
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
+  if (e == hipSuccess) e = hipMalloc(&g->mpts, sizeof(float4) * n);
+  if (e == hipSuccess) e = hipMalloc(&g->minv, sizeof(int32_t) * n);
+  if (e == hipSuccess) {
+    morton_gather_kernel<<<blocks, kGridBlock, 0, st>>>(g->pts, vout, n, g->mpts, g->minv);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    hipFree(g->mpts);
+    hipFree(g->minv);
+    g->mpts = nullptr;
+    g->minv = nullptr;
+  }
+  return grid_fail(e, kin, kout, vin, vout, tmp);
+}
+
+hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, const Grid* g,
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
-                          const int32_t* prev, const int64_t* dprev, const float4* tgt32,
-                          int64_t nt_shard, hipStream_t st) {
+                          const float4* sq, const int32_t* prev, const int64_t* dprev,
+                          const float4* tgt32, int64_t nt_shard, hipStream_t st) {
   if (ns == 0) return hipSuccess;
+  static const bool batched = [] {  // M3D_GRID_BATCHED=0: the per-query kernel above (A/B)
+    const char* e = getenv("M3D_GRID_BATCHED");
+    return !(e && atoi(e) == 0);
+  }();
   static const int L = [] {
     const char* e = getenv("M3D_GRID_LANES");
     const int v = e ? atoi(e) : kGridLanesDefault;
     return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : kGridLanesDefault;
   }();
+  static const int RB = [] {  // M3D_GRID_RB = kR·10 + kB (tuning): 22, 41, 42, 24
+    const char* e = getenv("M3D_GRID_RB");
+    const int v = e ? atoi(e) : 22;
+    return (v == 42 || v == 41 || v == 22 || v == 24) ? v : 22;
+  }();
+  if (batched && qgrid != nullptr && qgrid->mpts != nullptr) {
+    static unsigned long long* gstats = [] {
+      const char* e = getenv("M3D_GRID_STATS");
+      unsigned long long* p = nullptr;
+      if (e && atoi(e) == 1 && hipMalloc(&p, 4 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
+      return p;
+    }();
+    if (gstats != nullptr) (void)hipMemsetAsync(gstats, 0, 4 * sizeof(unsigned long long), st);
+    const int64_t nb = (ns * L + kGridBlock - 1) / kGridBlock;
+    const unsigned launch = (unsigned)((nb + 7) / 8 * 8);
+#define M3D_GB(LV, RV, BV) grid_nn_batched_kernel<LV, RV, BV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats)
+#define M3D_GBL(RV, BV) if (L == 1) M3D_GB(1, RV, BV); else if (L == 2) M3D_GB(2, RV, BV); else if (L == 4) M3D_GB(4, RV, BV); else if (L == 8) M3D_GB(8, RV, BV); else M3D_GB(16, RV, BV)
+    if (RB == 22) { M3D_GBL(2, 2); } else if (RB == 41) { M3D_GBL(4, 1); } else if (RB == 42) { M3D_GBL(4, 2); } else { M3D_GBL(2, 4); }
+#undef M3D_GBL
+#undef M3D_GB
+    if (gstats != nullptr) {
+      unsigned long long h[4] = {0, 0, 0, 0};
+      if (hipMemcpyAsync(h, gstats, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
+          hipStreamSynchronize(st) == hipSuccess && h[0] > 0)
+        fprintf(stderr, "[m3d grid stats] %llu queries (%.1f%% seeded): %.2f cell rows, %.1f candidates per query\n",
+                h[0], 100.0 * h[3] / h[0], (double)h[1] / h[0], (double)h[2] / h[0]);
+    }
+    return hipGetLastError();
+  }
+  const int32_t* order = qgrid != nullptr ? qgrid->order : nullptr;
   const unsigned blocks = (unsigned)((ns * L + kGridBlock - 1) / kGridBlock);
   if (L == 1)
     grid_nn_kernel<1><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);

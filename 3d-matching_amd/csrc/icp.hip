@@ -731,6 +731,9 @@ struct TermsArgs {
   const int64_t* dmin;
   int64_t* dprev;
   int32_t* corr;
+  float4* sq;             // grid NN seed records (nnkey.h seed_rec) in the source's Morton order
+  const int32_t* minv;    //   at position minv[i]
+  const float4* tgt32;    //   from the shard's centred fp32 targets
   int est;
   double c[3];
   int64_t* reset_keys;   // fused single-device loop: hand the keys back as kKeyNone
@@ -775,6 +778,10 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
     }
     if (!valid) continue;
     if (a.corr != nullptr) a.corr[i] = (int32_t)gj;
+    if (a.sq != nullptr) {
+      const bool local = gj >= a.off && gj < a.off + a.nt_shard;
+      a.sq[a.minv[i]] = seed_rec(gj, local, a.tgt32 + (local ? gj - a.off : 0), d2);
+    }
     if (gj < a.off || gj >= a.off + a.nt_shard) continue;  // none, or another shard's target
     const double* q = a.tgt64 + 3 * (gj - a.off);
     const double d[3] = {vs[0] - q[0], vs[1] - q[1], vs[2] - q[2]};
@@ -1290,6 +1297,10 @@ static TermsArgs terms_args(const m3d_icp* s, int64_t off, const int32_t* claim,
   a.dmin = dmin;
   a.dprev = claim != nullptr ? s->dprev : nullptr;
   a.corr = s->corr;
+  a.sq = s->sq;
+  a.minv = s->sgrid != nullptr ? s->sgrid->minv : nullptr;
+  a.tgt32 = s->tgt->xyz32;
+  if (a.minv == nullptr) a.sq = nullptr;
   a.est = s->params.estimation;
   for (int k = 0; k < 3; ++k) a.c[k] = s->src->center[k];
   a.reset_keys = reset_keys ? s->keys : nullptr;

@@ -92,6 +92,10 @@ struct Grid {
   int32_t* start = nullptr;
   float4* pts = nullptr;
   int32_t* order = nullptr;  // point indices in cell order
+  // the points in Morton (Z-curve) order of their cells (w = index bits) and each point's position
+  // in that order: the query order of the grid NN (grid.hip grid_morton); built on first use
+  float4* mpts = nullptr;
+  int32_t* minv = nullptr;
   int64_t n_pts = 0;
   double cell = 0.0;      // cell size used
   double cell_req = 0.0;  // cell size requested
@@ -166,12 +170,16 @@ struct m3d_icp {
   int64_t* dprev = nullptr;        // ns: target-sharded loops, bits of the global winner's d64
   int64_t* ld64 = nullptr;         // ns: target-sharded loops, bits of this shard's winner's d64
   int32_t* lidx = nullptr;         // ns: target-sharded loops, this shard's fp64 winner (-1 none)
+  // grid NN: each source's seed record in the source's Morton order (nnkey.h SeedRec), written by
+  // the terms pass with the correspondence, read by the grid scan beside the query point
+  float4* sq = nullptr;
   bool keys_clean = false;         // host view: every key is kKeyNone (fused tail reset them)
   int32_t* corr = nullptr;         // ns current correspondence (-1 none)
   double* partials = nullptr;      // nblocks × kTermSlots
   double* sums = nullptr;          // kTermSlots
   int64_t nblocks = 0;
   const int32_t* qorder = nullptr;  // grid NN: source visit order (source cell order)
+  const m3d::Grid* sgrid = nullptr;  // the source's grid (Morton query order of the grid NN)
   const m3d::Grid* tgrid = nullptr;  // grid NN: the target's grid (owned by the target cloud)
   int64_t ns_total = 0;  // source-sharded multi-GPU: sources over all ranks (fitness denominator)
   // exchange buffers of the library-driven multi-GPU loops (m3d_icp_*shard_steps), lazily
@@ -262,10 +270,13 @@ hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g);
 void grid_free(Grid* g);
 // prev/dprev/tgt32/nt_shard: seed each query with seed_key (nnkey.h); prev == nullptr: no seeds
-hipError_t launch_grid_nn(const float4* src32, int64_t ns, const int32_t* order, const Grid* g,
+// qgrid: the query cloud's grid (its Morton-ordered points, grid_morton) — the cooperative kernel
+// sq: seed records in qgrid's Morton order (nnkey.h SeedRec) or null (seeds from prev/dprev)
+hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, const Grid* g,
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
-                          const int32_t* prev, const int64_t* dprev, const float4* tgt32,
-                          int64_t nt_shard, hipStream_t st);
+                          const float4* sq, const int32_t* prev, const int64_t* dprev,
+                          const float4* tgt32, int64_t nt_shard, hipStream_t st);
+hipError_t grid_morton(Grid* g, hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
 hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st);
 hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st);

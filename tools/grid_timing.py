@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Grid-NN ICP timing at cfg1 (100k x 100k) and cfg3's per-rank geometry (1M sources x one 125k
+target shard) and 1M x 1M: per-launch averages of the NN and terms kernels (library HIP events).
+Usage: python tools/grid_timing.py [iters]"""
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "3d-matching_amd"))
+import numpy as np
+import torch
+
+from m3d import _lib, synth
+from m3d.core import Cloud, IcpLoop, context
+
+it = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+only = sys.argv[2] if len(sys.argv) > 2 else None
+torch.cuda.set_device(0)
+ctx = context()
+for name, ns, nt_all, shard in (("cfg1 100k x 100k", 100_000, 100_000, 1), ("1M x 125k shard", 1_000_000, 1_000_000, 8),
+                                ("1M x 1M", 1_000_000, 1_000_000, 1)):
+    if only and only not in name:
+        continue
+    src, tgt, nrm, _ = synth.icp_pair(ns, nt_all, seed=0)
+    nt = nt_all // shard
+    tc = Cloud(tgt[:nt], nrm[:nt], center=tgt.mean(axis=0)) if shard > 1 else Cloud(tgt, nrm)
+    lp = IcpLoop(Cloud(src), tc, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=it, nn="grid")
+    lp.reset(np.eye(4))
+    lp.steps(it + 1)
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_read(_lib.KERNEL_NN), ctx.profile_read(_lib.KERNEL_TERMS)
+    lp.reset(np.eye(4))
+    lp.steps(it + 1)
+    nn_ms, n = ctx.profile_read(_lib.KERNEL_NN)
+    t_ms, tn = ctx.profile_read(_lib.KERNEL_TERMS)
+    ctx.profile(False)
+    nn = nn_ms / n
+    b = 28 * ns + 16 * nt
+    print(f"{name}: grid_nn {nn * 1e3:.1f} us ({b / (nn * 1e-3) / 1e9:.0f} GB/s algorithmic, "
+          f"{b / (nn * 1e-3) / 8e12 * 100:.1f}% of 8 TB/s), terms {t_ms / tn * 1e3:.1f} us, fitness {lp.result().fitness:.4f}",
+          flush=True)
