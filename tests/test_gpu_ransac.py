@@ -302,3 +302,117 @@ def test_run_async_matches_run(early_stop):
     assert (a.best_index, a.iterations, a.best_count) == (b.best_index, b.iterations, b.best_count)
     np.testing.assert_array_equal(a.transformation, b.transformation)
     assert a.fitness == b.fitness
+
+
+# ---------------------------------------------------------------- cfg2 scale (Nc = 1e5)
+@pytest.fixture(scope="module")
+def cfg2(golden):
+    from golden_pairs import cfg2_pair
+
+    g, src, tgt, corr, noise = cfg2_pair(golden)
+    return g, src, tgt, corr, noise, CorrSet(src, tgt, corr), CorrSet(src, tgt, noise)
+
+
+@pytest.mark.parametrize("key", ("s42", "s7", "noise"))
+def test_cfg2_reference_calls_exact(cfg2, key):
+    """benchmark_ransac.py:105-113 at Nc = 1e5 (3e5 with noise): the reference's own sampled rows
+    replayed through a1 (transforms within 1e-9 of LAPACK) and its counts for both comparators
+    bit-exact; the replay-mode loop picks the reference's best of those calls."""
+    g, src, tgt, corr, noise, cs, csn = cfg2
+    c, s = (noise, csn) if key == "noise" else (corr, cs)
+    tri = g[f"{key}_triples"]
+    T, st = s.kabsch3(len(tri), triples=tri)
+    T = T.cpu().numpy()
+    p, q = src[c[:, 0]], tgt[c[:, 1]]
+    for h in range(len(tri)):
+        if not rank_deficient(p[tri[h]], q[tri[h]]):
+            np.testing.assert_allclose(T[h], g[f"{key}_T"][h], rtol=0, atol=1e-9, err_msg=f"hyp {h}")
+    Tg = g[f"{key}_T"]
+    np.testing.assert_array_equal(s.score(Tg, THR, _lib.SCORE_NORM).cpu().numpy(), g[f"{key}_count_slow"])
+    np.testing.assert_array_equal(s.score(Tg, THR * THR, _lib.SCORE_SQUARED).cpu().numpy(),
+                                  g[f"{key}_count_fast"])
+    out = s.run(RansacParams(max_iter=len(tri), thr=THR, mode=_lib.SCORE_NORM, early_stop=False),
+                triples=tri)
+    ref_best = int(np.argmax(g[f"{key}_count_slow"]))  # first strict improvement = first max
+    assert (out.best_index, out.best_count) == (ref_best, int(g[f"{key}_count_slow"][ref_best]))
+
+
+def test_cfg2_bench_batch_exact(cfg2):
+    """The exact batch bench.py times (H = 1e5 native hypotheses, seed 42, one batch, no early
+    stop, ‖d‖ < 0.45): the per-hypothesis counts of the run equal the oracle's for the top 64
+    hypotheses and a stratified sample of 500, and the run's best is the first maximum."""
+    import torch
+
+    g, src, tgt, corr, noise, cs, _ = cfg2
+    H = 100_000
+    from m3d.core import RESULT_WORDS, RansacOutcome
+
+    counts = torch.zeros(H, dtype=torch.int32, device="cuda")
+    buf = torch.zeros(RESULT_WORDS, dtype=torch.int64, device="cuda")
+    p = RansacParams(max_iter=H, seed=42, thr=THR, mode=_lib.SCORE_NORM, early_stop=False)
+    from m3d.core import ptr, stream_handle
+
+    cs.ctx.check(cs.ctx.lib.m3d_ransac_run_async(cs.ctx.h, cs.h, __import__("ctypes").byref(p.to_c()), None,
+                                                 ptr(counts), ptr(buf), stream_handle()), "run_async")
+    out = RansacOutcome.from_device(buf, cs.nc)
+    c = counts.cpu().numpy()
+    assert out.iterations == H
+    assert out.best_index == int(np.argmax(c)) and out.best_count == c.max()
+    T, _ = cs.kabsch3(H, seed=42)
+    Tn = T.cpu().numpy()
+    top = np.argsort(-c, kind="stable")[:64]
+    strat = np.arange(0, H, H // 500)
+    pick = np.unique(np.concatenate([top, strat]))
+    pp, qq = src[corr[:, 0]], tgt[corr[:, 1]]
+    np.testing.assert_array_equal(c[pick], O.inlier_counts(pp, qq, Tn[pick], THR, 1))
+    np.testing.assert_array_equal(out.transformation, Tn[out.best_index])
+
+
+def test_fused_hyp16_equals_separate_launch():
+    """kabsch3 writes the MFMA screen's per-hypothesis operands itself for a4 batches
+    (M3D_RANSAC_FUSE, latched per process): a subprocess with FUSE=0 (separate hyp16 launch) and one
+    with FUSE=1 give identical counts, at a ragged H whose padding hypotheses are exercised."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    code = r'''
+import json, sys
+import numpy as np
+sys.path[:0] = [sys.argv[1]]
+import torch
+import ctypes
+from m3d import _lib, synth
+from m3d.core import CorrSet, RansacParams, ptr, stream_handle
+src, tgt, corr, _ = synth.ransac_pair(30011, seed=12, noise_ratio=1.5)
+cs = CorrSet(src, tgt, corr)
+H = 2049 + 30
+counts = torch.zeros(H, dtype=torch.int32, device="cuda")
+buf = torch.zeros(64, dtype=torch.int64, device="cuda")
+out = {}
+for mode, thr in ((_lib.SCORE_NORM, 0.45), (_lib.SCORE_SQUARED, 0.45 * 0.45)):
+    p = RansacParams(max_iter=H, seed=5, thr=thr, mode=mode, early_stop=False, batch=1000)
+    cs.ctx.check(cs.ctx.lib.m3d_ransac_run_async(cs.ctx.h, cs.h, ctypes.byref(p.to_c()), None, ptr(counts), ptr(buf),
+                                                 stream_handle()), "run")
+    out[str(mode)] = counts.cpu().numpy().tolist()
+print(json.dumps(out))
+'''
+    pkg = str(Path(__file__).resolve().parents[1] / "3d-matching_amd")
+    res = {}
+    for fuse in ("0", "1"):
+        env = dict(os.environ, M3D_RANSAC_FUSE=fuse)
+        r = subprocess.run([sys.executable, "-c", code, pkg], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[fuse] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["0"] == res["1"]
+    from m3d import synth
+
+    src, tgt, corr, _ = synth.ransac_pair(30011, seed=12, noise_ratio=1.5)
+    T, _ = CorrSet(src, tgt, corr).kabsch3(2079, seed=5)
+    pick = np.arange(0, 2079, 97)
+    pp, qq = src[corr[:, 0]], tgt[corr[:, 1]]
+    np.testing.assert_array_equal(np.array(res["1"][str(_lib.SCORE_NORM)])[pick],
+                                  O.inlier_counts(pp, qq, T.cpu().numpy()[pick], 0.45, 1))

@@ -119,3 +119,22 @@ def test_native_sampler_properties():
     big = O.native_triples(1, 0, 20000, 10)
     cnt = np.bincount(big.ravel(), minlength=10)
     assert cnt.min() > 0.9 * cnt.mean()
+
+
+# ---------------------------------------------------------------- cfg2 scale (Nc = 1e5)
+from golden_pairs import cfg2_pair  # noqa: E402
+
+
+def test_cfg2_golden_pins_oracle(golden):
+    """The oracle restatement reproduces the reference's own cfg2-scale calls: sampled rows
+    (legacy RNG), transforms and both comparators' counts (first 25 of each set)."""
+    g, src, tgt, corr, noise = cfg2_pair(golden)
+    for key, c, seed in (("s42", corr, 42), ("s7", corr, 7), ("noise", noise, 42)):
+        rng = np.random.RandomState(seed)
+        p, q = src[c[:, 0]], tgt[c[:, 1]]
+        for h in range(25):
+            T, _, idx = O.compute_step_transformation(src, tgt, c, rng=rng)
+            np.testing.assert_array_equal(idx, g[f"{key}_triples"][h])
+            np.testing.assert_allclose(T, g[f"{key}_T"][h], rtol=0, atol=1e-12)
+            assert O.inlier_count(p, q, g[f"{key}_T"][h], 0.45, 1) == g[f"{key}_count_slow"][h]
+            assert O.inlier_count(p, q, g[f"{key}_T"][h], 0.45 * 0.45, 0) == g[f"{key}_count_fast"][h]

@@ -15,8 +15,14 @@ absent open3d wheel and records what the reference computes:
   outputs (minimal/collinear/coplanar/duplicate/zero-correspondence/large-transform).
 * tests/golden/loop_trajectory.npz — the step-RANSAC loop of _visualize_matcher.py:394-450
   driven by the reference's a1 + a3 (best index, best fitness, stop iteration, fitness stream).
+* tests/golden/ransac_cfg2.npz — cfg2 scale (benchmark_ransac.py:105-113 at Nc = 1e5): bench.py's
+  pair (m3d.synth.ransac_pair(1e5, seed=42), pinned by a SHA-256 of its arrays) and the
+  reference's noise_ratio 2.0 set on it (Nc = 3e5); for np.random.seed 42 and 7, 200 successive
+  compute_step_transformation calls (rows, 4×4) with their evaluate_inlier_ratio and
+  evaluate_inlier_ratio_fast counts (100 calls on the noisy set).  Only the rows, transforms and
+  counts are stored (the pair is regenerated from its seed).
 
-Run:  python tools/gen_golden.py      (skips cleanly when /root/reference is absent)
+Run:  python tools/gen_golden.py [--only cfg2]   (skips cleanly when /root/reference is absent)
 """
 
 from __future__ import annotations
@@ -58,6 +64,9 @@ def main() -> int:
     from m3d import synth
 
     OUT.mkdir(parents=True, exist_ok=True)
+    gen_cfg2(ref, stubreg, synth)
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "cfg2":
+        return 0
 
     # ---------------- G1: 5k pair ----------------
     n = 5000
@@ -179,6 +188,60 @@ def main() -> int:
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)
     return 0
+
+
+def pair_digest(*arrays) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for a in arrays:
+        a = np.ascontiguousarray(a)
+        h.update(str((a.dtype.str, a.shape)).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def replay_calls(ref, S, Tg, corr, seed, H, voxel):
+    """H successive reference a1 calls after np.random.seed(seed): rows, 4×4, a2 and a3 counts."""
+    src, tgt = S.pcd_down.points, Tg.pcd_down.points
+    p_src, p_tgt = src[corr[:, 0]], tgt[corr[:, 1]]
+    thr_sq = (voxel * 1.5) * (voxel * 1.5)
+    np.random.seed(seed)
+    tri = np.empty((H, 3), dtype=np.int32)
+    Ts = np.empty((H, 4, 4))
+    slow = np.empty(H, dtype=np.int64)
+    fast = np.empty(H, dtype=np.int64)
+    for h in range(H):
+        st = np.random.get_state()
+        res = ref.compute_step_transformation(S, Tg, corr)
+        after = np.random.get_state()
+        np.random.set_state(st)
+        tri[h] = np.random.choice(len(corr), 3, replace=False)
+        chk = np.random.get_state()
+        assert chk[2] == after[2] and np.array_equal(chk[1], after[1])
+        Ts[h] = res.transformation
+        slow[h] = int(np.rint(ref.evaluate_inlier_ratio(S, Tg, corr, res.transformation, voxel) * len(corr)))
+        fast[h] = int(np.rint(ref.evaluate_inlier_ratio_fast(p_src, p_tgt, res.transformation, thr_sq) * len(corr)))
+    return tri, Ts, slow, fast
+
+
+def gen_cfg2(ref, stubreg, synth):
+    n = 100_000
+    src, tgt, corr, _ = synth.ransac_pair(n, seed=42)
+    S, Tg = MockPly(src), MockPly(tgt)
+    stubreg.set_feature_correspondences(corr)
+    np.random.seed(3)
+    corr_noise = np.asarray(ref.compute_feature_correspondences(S, Tg, noise_ratio=2.0), dtype=np.int32)
+    rec = dict(n=n, pair_seed=42, voxel=0.3, digest=pair_digest(src, tgt, corr),
+               noise_seed=3, noise_digest=pair_digest(corr_noise))
+    for seed in (42, 7):
+        tri, Ts, slow, fast = replay_calls(ref, S, Tg, corr, seed, 200, 0.3)
+        rec.update({f"s{seed}_triples": tri, f"s{seed}_T": Ts, f"s{seed}_count_slow": slow,
+                    f"s{seed}_count_fast": fast})
+    tri, Ts, slow, fast = replay_calls(ref, S, Tg, corr_noise, 42, 100, 0.3)
+    rec.update(noise_triples=tri, noise_T=Ts, noise_count_slow=slow, noise_count_fast=fast)
+    np.savez_compressed(OUT / "ransac_cfg2.npz", **rec)
+    print("ransac_cfg2.npz", (OUT / "ransac_cfg2.npz").stat().st_size)
 
 
 if __name__ == "__main__":
