@@ -301,9 +301,9 @@ def main():
             "ms_per_step": gel / args.steps * 1e3, "grid_build_ms": build_ms,
             "ms_per_step_with_kernel_events": gel_ev / args.steps * 1e3,
             "same_result_as_brute": bool(np.array_equal(gres.transformation, res.transformation)),
-            "roofline": {"bound": "hbm", "kernel": "grid_nn_kernel", "achieved": g_gbs,
+            "roofline": {"bound": "hbm", "kernel": "grid_nn_batched_kernel", "achieved": g_gbs,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic("grid_nn_kernel")[0], "avg_launch_ms": g_ms,
+                         "traffic": pmc_traffic("grid_nn")[0], "avg_launch_ms": g_ms,
                          "launches": g_n, "bytes_per_launch": g_bytes,
                          "terms_avg_launch_ms": g_terms_ms},
         }
