@@ -1134,11 +1134,10 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
   }
   CHECK_ARG(ctx, corr != nullptr, "null correspondence pointer");
   const int64_t H = p->max_iteration;
-  DevTmp<double> T, sums;
+  DevTmp<double> T;
   DevTmp<int32_t> pass;
   int rc = dev_alloc(ctx, &T.p, 16 * H);
   if (!rc) rc = dev_alloc(ctx, &pass.p, H);
-  if (!rc) rc = dev_alloc(ctx, &sums.p, kTermSlots * H);
   if (rc) return rc;
   HIPX(ctx, launch_feat_hyp(src->xyz64, tgt->xyz64, corr, nc, p->seed, H, p->edge_length,
                             p->distance, T.p, pass.p, st));
@@ -1149,41 +1148,71 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
   m3d_icp* s = nullptr;
   rc = m3d_icp_create(ctx, src, tgt, p->max_correspondence_distance, &ip, &s);
   if (rc) return rc;
-  // validation of every hypothesis that passed the checkers (≤ max_iteration); the sequential
-  // early-exit selection below decides which of them Open3D would have validated
-  hipError_t e = hipSuccess;
-  for (int64_t h = 0; h < H && e == hipSuccess; ++h) {
-    if (!hpass[h]) continue;
-    e = launch_icp_set_T(s, T.p + 16 * h, st);
-    if (e == hipSuccess) e = enqueue_nn(s, 0, st);
-    if (e == hipSuccess) e = launch_icp_terms_mode(s, 0, nullptr, nullptr, st);
-    if (e == hipSuccess) e = launch_icp_reduce(s, sums.p + kTermSlots * h, st);
+  // Validation of the checker-passing hypotheses in batches (grid.hip validate_kernel: one launch
+  // evaluates a whole batch), each batch followed by Open3D's sequential selection over it:
+  // IsBetterRANSACThan and the early exit at est_k (a hypothesis at or past est_k is never
+  // validated).  Batches grow from 64 so the reference's iteration = 30 costs one small launch;
+  // a batch that straddles est_k only computes results the selection then ignores.
+  std::vector<int32_t> list;
+  for (int64_t h = 0; h < H; ++h)
+    if (hpass[h]) list.push_back((int32_t)h);
+  const int64_t npass = (int64_t)list.size();
+  const int64_t cap = std::min<int64_t>(
+      npass, std::max<int64_t>(64, std::min<int64_t>(8192, ((int64_t)1 << 23) / std::max<int64_t>(ns, 1))));
+  const int64_t nbq = validate_blocks(ns);
+  DevTmp<int32_t> dlist;
+  DevTmp<IcpState> vst;
+  DevTmp<double> vpart, vres;
+  if (npass > 0) {
+    rc = dev_alloc(ctx, &dlist.p, npass);
+    if (!rc) rc = dev_alloc(ctx, &vst.p, cap);
+    if (!rc) rc = dev_alloc(ctx, &vpart.p, cap * nbq * 2);
+    if (!rc) rc = dev_alloc(ctx, &vres.p, cap * 2);
+    if (rc) {
+      m3d_icp_destroy(s);
+      return rc;
+    }
   }
-  std::vector<double> hs((size_t)kTermSlots * H);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(hs.data(), sums.p, sizeof(double) * kTermSlots * H, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipError_t e = hipSuccess;
+  if (npass > 0)
+    e = hipMemcpyAsync(dlist.p, list.data(), 4 * npass, hipMemcpyHostToDevice, st);
+  int64_t est_k = H, best = -1;
+  double best_fit = 0.0, best_rmse = 0.0;
+  std::vector<double> hs;
+  for (int64_t c0 = 0, bsz = std::min<int64_t>(64, cap); c0 < npass && e == hipSuccess;
+       c0 += bsz, bsz = std::min<int64_t>(cap, 2 * bsz)) {
+    if (list[c0] >= est_k) break;
+    const int64_t n = std::min<int64_t>(bsz, npass - c0);
+    e = launch_val_states(s, T.p, dlist.p + c0, n, vst.p, st);
+    if (e == hipSuccess)
+      e = launch_validate(s->sgrid, ns, src->xyz64, s->tgrid, tgt->xyz64, tgt->n, vst.p, n, vpart.p,
+                          vres.p, st);
+    hs.resize(2 * (size_t)n);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(hs.data(), vres.p, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) break;
+    for (int64_t k = 0; k < n; ++k) {
+      const int64_t h = list[c0 + k];
+      if (h >= est_k) break;
+      out->validations += 1;
+      const double cnt = hs[2 * k], se = hs[2 * k + 1];
+      const double fit = cnt > 0.0 ? cnt / (double)ns : 0.0;
+      const double rmse = cnt > 0.0 ? std::sqrt(se / cnt) : 0.0;
+      if (fit > best_fit || (fit == best_fit && rmse < best_rmse)) {  // IsBetterRANSACThan
+        best = h;
+        best_fit = fit;
+        best_rmse = rmse;
+        const double kk = fit < 1.0 ? std::ceil(std::log(1.0 - p->confidence) /
+                                                std::log(1.0 - std::pow(fit, (double)p->ransac_n)))
+                                    : 0.0;
+        if (kk < (double)est_k) est_k = (int64_t)kk;
+      }
+    }
+  }
   if (e != hipSuccess) {
     m3d_icp_destroy(s);
     return m3d_fail(ctx, M3D_ERR_HIP, std::string("feature RANSAC: ") + hipGetErrorString(e));
-  }
-  int64_t est_k = H, best = -1;
-  double best_fit = 0.0, best_rmse = 0.0;
-  for (int64_t h = 0; h < H && h < est_k; ++h) {
-    if (!hpass[h]) continue;
-    out->validations += 1;
-    const double cnt = hs[kTermSlots * h + 28], se = hs[kTermSlots * h + 29];
-    const double fit = cnt > 0.0 ? cnt / (double)ns : 0.0;
-    const double rmse = cnt > 0.0 ? std::sqrt(se / cnt) : 0.0;
-    if (fit > best_fit || (fit == best_fit && rmse < best_rmse)) {  // IsBetterRANSACThan
-      best = h;
-      best_fit = fit;
-      best_rmse = rmse;
-      const double k = fit < 1.0 ? std::ceil(std::log(1.0 - p->confidence) /
-                                             std::log(1.0 - std::pow(fit, (double)p->ransac_n)))
-                                 : 0.0;
-      if (k < (double)est_k) est_k = (int64_t)k;
-    }
   }
   if (best >= 0) {
     e = hipMemcpyAsync(out->T, T.p + 16 * best, sizeof(double) * 16, hipMemcpyDeviceToHost, st);

@@ -294,6 +294,131 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------- a6 validation
+// Feature-RANSAC validation of many hypotheses in one launch (Open3D
+// RegistrationRANSACBasedOnCorrespondence evaluates every checker-passing hypothesis with
+// GetRegistrationResultAndCorrespondences — 1-NN within the distance threshold, fitness =
+// count / Ns, rmse = √(Σd² / count)).  blockIdx.y = hypothesis k of the batch (its evaluation
+// state states[k], icp.hip val_states_kernel); kL lanes per source point, the source in its
+// Morton order.  Per point: the unseeded scan of the grid NN (r2_hi box, packed-key minimum and
+// runner-up), then nnkey.h winner_fp64 — the same fp64 decision as the single-hypothesis chain
+// (set_T → grid NN → terms) it replaces, so the (count, Σd²) pairs are the same up to the
+// summation order.  Block partials (count, Σd²) go out in a fixed tree order; val_reduce_kernel
+// adds them per hypothesis in block order: deterministic.
+template <int kL>
+__global__ __launch_bounds__(kGridBlock) void validate_kernel(const float4* __restrict__ qpts,
+                                                              int64_t ns,
+                                                              const double* __restrict__ src64,
+                                                              GridDev g,
+                                                              const double* __restrict__ tgt64,
+                                                              int64_t nt,
+                                                              const IcpState* __restrict__ states,
+                                                              double* __restrict__ part) {
+  __shared__ double red[2][kGridBlock / kWave];
+  const IcpState* s = states + blockIdx.y;
+  const int64_t t = ((int64_t)blockIdx.x * kGridBlock + threadIdx.x) / kL;
+  const int sub = threadIdx.x & (kL - 1);
+  const float r2_hi = s->r2_hi;
+  const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
+  uint64_t k1 = key0;
+  float k1d = kInf, n2 = kInf;
+  int64_t i = -1;
+  float4 p = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (t < ns) {
+    p = qpts[t];
+    i = (int64_t)__float_as_int(p.w);
+    float qx, qy, qz;
+    xform32(s->Rt32, p, qx, qy, qz);
+    if (g.ncells > 0) {
+      const float R = sqrtf(r2_hi) * 1.001f;
+      const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
+      const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
+      const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
+      const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
+      const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
+      const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
+      const int ny = y1 - y0 + 1;
+      const int rows = ny * (z1 - z0 + 1);
+      for (int r = sub; r < rows; r += kL) {
+        const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
+        const int32_t j1 = g.start[row + x1 + 1];
+        for (int32_t j = g.start[row + x0]; j < j1; ++j) {
+          const float4 v = g.pts[j];
+          const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
+          if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)__float_as_int(v.w)), d2);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = kL / 2; o > 0; o >>= 1) {
+    const uint64_t b1 = ((uint64_t)(uint32_t)__shfl_xor((int)(k1 >> 32), o, kL) << 32) |
+                        (uint32_t)__shfl_xor((int)(uint32_t)k1, o, kL);
+    const float bn2 = __shfl_xor(n2, o, kL);
+    near_merge(k1, k1d, n2, b1, bn2);
+  }
+  const bool valid = i >= 0 && sub == 0;
+  double Q[3] = {0.0, 0.0, 0.0};
+  if (valid) q64_of(s->T, src64 + 3 * i, Q);
+  int64_t bj = -1;
+  double bd = 0.0;
+  winner_fp64(valid, k1 == key0 ? (uint64_t)kKeyNone : k1, n2, s, g, tgt64, 0, nt, p, Q, bj, bd);
+  double c = valid && bj >= 0 ? 1.0 : 0.0;
+  double e = valid && bj >= 0 ? bd : 0.0;
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    e += __shfl_xor(e, o);
+  }
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  if (lane == 0) {
+    red[0][wave] = c;
+    red[1][wave] = e;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double v = 0.0;
+    for (int w = 0; w < kGridBlock / kWave; ++w) v += red[threadIdx.x][w];
+    part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 + threadIdx.x] = v;
+  }
+}
+
+// out[2k] = count, out[2k + 1] = Σd² of hypothesis k: its nb block partials in block order
+__global__ __launch_bounds__(kWave) void val_reduce_kernel(const double* __restrict__ part, int64_t nb,
+                                                          double* __restrict__ out) {
+  const double* p = part + (int64_t)blockIdx.x * nb * 2;
+  double c = 0.0, e = 0.0;
+  for (int64_t b = threadIdx.x; b < nb; b += kWave) {
+    c += p[2 * b];
+    e += p[2 * b + 1];
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    e += __shfl_xor(e, o);
+  }
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = c;
+    out[2 * blockIdx.x + 1] = e;
+  }
+}
+
+int64_t validate_blocks(int64_t ns) { return (ns * 4 + kGridBlock - 1) / kGridBlock; }
+
+hipError_t launch_validate(const Grid* qgrid, int64_t ns, const double* src64, const Grid* g,
+                           const double* tgt64, int64_t nt, const IcpState* states, int64_t nhyp,
+                           double* part, double* out, hipStream_t st) {
+  if (nhyp == 0) return hipSuccess;
+  if (ns == 0) return hipMemsetAsync(out, 0, sizeof(double) * 2 * nhyp, st);
+  if (qgrid == nullptr || qgrid->mpts == nullptr) return hipErrorInvalidValue;
+  const int64_t nb = validate_blocks(ns);
+  if (nb > INT32_MAX || nhyp > 65535) return hipErrorInvalidValue;
+  validate_kernel<4><<<dim3((unsigned)nb, (unsigned)nhyp), kGridBlock, 0, st>>>(
+      qgrid->mpts, ns, src64, g->dev, tgt64, nt, states, part);
+  val_reduce_kernel<<<(unsigned)nhyp, kWave, 0, st>>>(part, nb, out);
+  return hipGetLastError();
+}
+
 // Morton (Z-curve) order of a cloud's points by their cells (10 bits per axis; finer grids are
 // coarsened — only locality matters, any order gives the same keys).
 __device__ __forceinline__ uint32_t spread3(uint32_t v) {

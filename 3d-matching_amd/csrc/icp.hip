@@ -159,6 +159,27 @@ __global__ void icp_set_T_kernel(IcpState* s, const double* __restrict__ T, doub
   s->eq_prev = s->eq;
 }
 
+// a6 batched validation (grid.hip validate_kernel): one evaluation state per hypothesis, with
+// icp_set_T's semantics, for the hypotheses list[0..n) of the transform array T
+__global__ __launch_bounds__(64) void val_states_kernel(IcpState* __restrict__ states,
+                                                        const double* __restrict__ T,
+                                                        const int32_t* __restrict__ list, int64_t n,
+                                                        double r2, FrameParams f) {
+  const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (k >= n) return;
+  IcpState* s = states + k;
+  const double* Th = T + 16 * (int64_t)list[k];
+  for (int j = 0; j < 16; ++j) s->T[j] = Th[j];
+  s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
+  s->count = 0;
+  s->evals = s->iters = s->done = s->converged = 0;
+  s->ticket = 0;
+  s->r2 = r2;
+  s->bound_ok = 0;
+  refresh_rt32(s, f);
+  s->eq_prev = s->eq;
+}
+
 // ------------------------------------------------------------------------------- keyinit
 __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__ src32, int64_t ns,
                                                       const float4* __restrict__ tgt32,
@@ -1125,6 +1146,14 @@ hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st) {
 
 hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st) {
   icp_set_T_kernel<<<1, 64, 0, st>>>(s->state, T_dev, s->max_dist * s->max_dist, frame_of(s));
+  return hipGetLastError();
+}
+
+hipError_t launch_val_states(const m3d_icp* s, const double* T_dev, const int32_t* list, int64_t n,
+                             IcpState* states, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  val_states_kernel<<<(unsigned)((n + 63) / 64), 64, 0, st>>>(states, T_dev, list, n,
+                                                              s->max_dist * s->max_dist, frame_of(s));
   return hipGetLastError();
 }
 

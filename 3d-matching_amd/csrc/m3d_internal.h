@@ -279,6 +279,15 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
 hipError_t grid_morton(Grid* g, hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
 hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st);
+// a6 batched validation: states[k] ← evaluation state of T[list[k]] (icp_set_T semantics), then
+// out[2k], out[2k + 1] = (correspondence count, Σd²) of hypothesis k (grid.hip validate_kernel);
+// part: validate_blocks(ns) × 2 doubles per hypothesis of scratch
+hipError_t launch_val_states(const m3d_icp* s, const double* T_dev, const int32_t* list, int64_t n,
+                             IcpState* states, hipStream_t st);
+int64_t validate_blocks(int64_t ns);
+hipError_t launch_validate(const Grid* qgrid, int64_t ns, const double* src64, const Grid* g,
+                           const double* tgt64, int64_t nt, const IcpState* states, int64_t nhyp,
+                           double* part, double* out, hipStream_t st);
 hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st);
 
 // preprocessing (prep.hip) and feature matching (feat.hip)

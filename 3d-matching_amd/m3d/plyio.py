@@ -181,12 +181,16 @@ def read_stl(path):
         if len(v) % 3:
             raise ValueError(f"{path}: ASCII STL vertex count is not a multiple of 3")
         tri = v.reshape(-1, 3, 3)
-    flat = tri.reshape(-1, 3)
-    _, first, inverse = np.unique(flat, axis=0, return_index=True, return_inverse=True)
+    flat = np.ascontiguousarray(tri.reshape(-1, 3))
+    # exact-equality merge on the raw bytes of each (x, y, z) (one 1-D sort of 24-byte keys);
+    # +0.0 and -0.0 differ in bytes, so canonicalise them first
+    flat = flat + 0.0
+    key = flat.view(np.dtype((np.void, 24))).ravel()
+    _, first, inverse = np.unique(key, return_index=True, return_inverse=True)
     order = np.argsort(first, kind="stable")     # unique vertices in first-occurrence order
     rank = np.empty_like(order)
     rank[order] = np.arange(len(order))
-    verts = flat[np.sort(first)]
+    verts = flat[first[order]]
     faces = rank[inverse.reshape(-1)].reshape(-1, 3)
     return verts, faces
 
@@ -196,3 +200,31 @@ def convert_stl_to_ply(stl_path, ply_path):
     verts, _ = read_stl(stl_path)
     write_ply(ply_path, verts, binary=False, dtype="double")
     return len(verts)
+
+
+def write_stl(path, vertices, faces, binary: bool = True):
+    """Write a triangle mesh as STL (binary little-endian or ASCII), facet normals from the
+    vertex winding.  Test/benchmark fixtures only: the reference reads STL, never writes it."""
+    v = np.asarray(vertices, np.float64).reshape(-1, 3)
+    f = np.asarray(faces, np.int64).reshape(-1, 3)
+    tri = v[f].astype(np.float32).astype(np.float64)  # STL stores float32 coordinates
+    n = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+    ln = np.linalg.norm(n, axis=1, keepdims=True)
+    n = np.divide(n, ln, out=np.zeros_like(n), where=ln > 0)
+    if binary:
+        rec = np.zeros(len(f), np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]))
+        rec["n"] = n
+        rec["v"] = tri
+        with open(path, "wb") as fh:
+            fh.write(b"m3d synthetic mesh".ljust(80, b" "))
+            fh.write(np.array([len(f)], "<u4").tobytes())
+            fh.write(rec.tobytes())
+        return
+    with open(path, "w") as fh:
+        fh.write("solid m3d\n")
+        for k in range(len(f)):
+            fh.write(f"facet normal {n[k, 0]:.9g} {n[k, 1]:.9g} {n[k, 2]:.9g}\n outer loop\n")
+            for j in range(3):
+                fh.write(f"  vertex {tri[k, j, 0]:.9g} {tri[k, j, 1]:.9g} {tri[k, j, 2]:.9g}\n")
+            fh.write(" endloop\nendfacet\n")
+        fh.write("endsolid m3d\n")

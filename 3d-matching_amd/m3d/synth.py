@@ -116,3 +116,48 @@ def icp_pair(ns: int, nt: int | None = None, seed: int = 0):
     Tinv = np.linalg.inv(T)
     src = apply(Tinv, src_world)
     return src, tgt, tgt_n, T
+
+
+_CUSPS = (((0.3, 0.8, 0.5), 0.2, 0.05), ((-0.7, 0.2, 0.6), 0.12, 0.03),
+          ((0.5, -0.6, 0.6), 0.15, 0.04), ((0.1, 0.1, -1.0), 0.08, 0.08))
+
+
+def surface_mesh(n_lat: int, n_lon: int, seed: int = 0):
+    """Triangle mesh of the synthetic surface (a scan stand-in for cfg4's STL input).
+
+    A UV-sphere tessellation (``n_lat`` rings × ``n_lon`` segments plus the two poles) whose
+    directions are first rotated by a seeded random rotation — two seeds give two different
+    tessellations (vertex sets) of the same surface, like two scans — then mapped onto
+    |x| = r(x/|x|) with four extra cusps (Gaussian lobes of height 0.08–0.2·R0 in fixed
+    directions) so that no rotation maps the shape close onto itself — the tooth-like scan the
+    reference's cfg4 registers; ``surface_points`` stays cusp-free (the goldens use it).
+    Returns ``(vertices V×3 f64, faces F×3 int64)``.
+    """
+    rng = np.random.default_rng(seed)
+    q = rng.standard_normal(4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    Rg = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                   [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                   [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    th = np.pi * (np.arange(1, n_lat + 1) / (n_lat + 1))
+    ph = 2.0 * np.pi * np.arange(n_lon) / n_lon
+    st, ct = np.sin(th)[:, None], np.cos(th)[:, None]
+    ring = np.stack([st * np.cos(ph)[None, :], st * np.sin(ph)[None, :], np.broadcast_to(ct, (n_lat, n_lon))],
+                    axis=2).reshape(-1, 3)
+    u = np.vstack([[0.0, 0.0, 1.0], ring, [0.0, 0.0, -1.0]]) @ Rg.T
+    g, _ = _bump(u)
+    cusp = np.zeros(len(u))
+    for d, hgt, w in _CUSPS:
+        d = np.asarray(d, np.float64) / np.linalg.norm(d)
+        cusp += hgt * np.exp(-np.sum((u - d) ** 2, axis=1) / w)
+    verts = u * (R0 * (1.0 + ALPHA * g + cusp))[:, None]
+    idx = 1 + np.arange(n_lat * n_lon).reshape(n_lat, n_lon)
+    nxt = np.roll(idx, -1, axis=1)
+    faces = [np.stack([np.zeros(n_lon, np.int64), idx[0], nxt[0]], axis=1)]
+    a, b, c, d = idx[:-1], nxt[:-1], idx[1:], nxt[1:]
+    faces.append(np.stack([a, c, b], axis=2).reshape(-1, 3))
+    faces.append(np.stack([b, c, d], axis=2).reshape(-1, 3))
+    south = len(verts) - 1
+    faces.append(np.stack([np.full(n_lon, south, np.int64), nxt[-1], idx[-1]], axis=1))
+    return verts, np.vstack(faces).astype(np.int64)

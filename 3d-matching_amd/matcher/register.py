@@ -17,12 +17,16 @@ from .ransac import global_registration, run_ransac
 
 
 def register(source, target, voxel_size=None, correspondences=None, ransac_iterations: int = 10000,
-             refine: bool = True, **ransac_kwargs):
-    """Return the refined ``RegistrationResult`` mapping ``source`` onto ``target``."""
+             refine: bool = True, iteration: int = 30, **ransac_kwargs):
+    """Return the refined ``RegistrationResult`` mapping ``source`` onto ``target``.
+
+    ``iteration``: RANSACConvergenceCriteria max_iteration of the feature path
+    (global_registration's own default, 30); ``ransac_iterations``: hypotheses of the
+    correspondence path."""
     v = voxel_size if voxel_size is not None else getattr(source, "voxel_size", 0.3)
     if correspondences is None and getattr(source, "pcd_fpfh", None) is not None \
             and getattr(target, "pcd_fpfh", None) is not None:
-        coarse = global_registration(source, target, v)
+        coarse = global_registration(source, target, v, iteration=iteration)
     elif correspondences is not None:
         coarse, _ = run_ransac(source, target, correspondences, voxel_size=v, max_iter=ransac_iterations,
                            **ransac_kwargs)

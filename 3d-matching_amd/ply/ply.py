@@ -18,6 +18,7 @@ preprocessing unless ``preprocess=True``.
 
 from __future__ import annotations
 
+import time
 from pathlib import Path
 
 import numpy as np
@@ -35,24 +36,44 @@ class Ply:
             raise TypeError(f"File is not a ply file: {self.path}")         # ply.py:49-51
         from m3d import plyio
 
+        t0 = time.perf_counter()
         pts, nrm = plyio.read_ply(self.path)
+        self.stage_ms = {"read": (time.perf_counter() - t0) * 1e3}
         if len(pts) == 0:
             raise ValueError(f"Point cloud is empty: {self.path}")          # ply.py:81-84
         self.pcd = PointCloud(pts, nrm)
         self._preprocess(voxel_size)
 
     def _preprocess(self, voxel_size: float) -> None:
+        """ply.py:53-66.  Wall time of each stage lands in ``stage_ms`` (every stage returns host
+        arrays, so the device work is complete when its timer stops)."""
         from m3d import prep
 
         v = voxel_size
+        ms = getattr(self, "stage_ms", None)
+        if ms is None:
+            ms = self.stage_ms = {}
+        t = time.perf_counter()
+
+        def lap(name):
+            nonlocal t
+            now = time.perf_counter()
+            ms[name] = (now - t) * 1e3
+            t = now
+
         down, _ = prep.voxel_down_sample(self.pcd.points, v)
+        lap("voxel_down_sample")
         down_n = prep.estimate_normals(down, 2 * v, 30)
+        lap("normals_down")
         self.pcd_down = PointCloud(down, down_n)
         self.pcd_fpfh = Feature(prep.compute_fpfh(down, down_n, 5 * v, 100).T)
+        lap("fpfh")
         noise = 0.05 * np.random.randn(*self.pcd_down.points.shape)      # ply.py:61-62
         self.pcd_down.points = self.pcd_down.points + noise
+        lap("noise")
         prev = self.pcd.normals if self.pcd.has_normals() else None
         self.pcd.normals = prep.estimate_normals(self.pcd.points, 2 * v, 30, normals=prev)
+        lap("normals_full")
 
     @classmethod
     def from_arrays(cls, points, normals=None, points_down=None, fpfh=None, voxel_size: float = 0.3,

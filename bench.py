@@ -81,6 +81,9 @@ def parse():
                     help="untimed RANSAC runs for at least this long before the timed ones")
     ap.add_argument("--no-ransac-api", action="store_true")
     ap.add_argument("--no-grid", action="store_true")
+    ap.add_argument("--no-cfg4", action="store_true")
+    ap.add_argument("--cfg4-mesh", type=int, default=300,
+                    help="cfg4 source mesh rings (segments = 2x; target mesh 10%% finer)")
     ap.add_argument("--shard", choices=["auto", "target", "source"], default="auto",
                     help="N>1 cfg1 sharding: target (MIN of the NN keys + claims, SUM of the terms), "
                          "source (target replicated, SUM of the terms only), or auto: the "
@@ -416,6 +419,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_ransac_api:
         ransac_api = bench_ransac_api(args)
 
+    # ------------------------------------------------------------------ cfg4: STL -> PLY -> register
+    cfg4 = None
+    if rank == 0 and world == 1 and not args.no_cfg4:
+        cfg4 = bench_cfg4(args)
+
     # ------------------------------------------------------------------ CPU baseline
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -455,6 +463,7 @@ def main():
                  else {k: v for k, v in cfg3.items() if k != "roofline"}),
         "ransac": ransac,
         "ransac_api": ransac_api,
+        "cfg4_synthetic": cfg4,
         "cpu_baseline": cpu,
         "check": cfg1["check"],
     }
@@ -463,6 +472,78 @@ def main():
     del comm
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_cfg4(args):
+    """cfg4 (BASELINE configs[4]) on generated scans: main.py:24-43's pipeline from STL files.
+    Two tessellations of the synthetic surface (source moved by T^-1) as binary STL ->
+    convert_stl-ply.py (m3d.plyio) -> Ply(path, 0.3) (ply.py:32-66, stages timed) ->
+    global_registration (ransac.py:20-59) at the reference's iteration=30 and at 30000 ->
+    refine_registration (icp.py:17-48).  One untimed pass on a small mesh first."""
+    import tempfile
+
+    import numpy as np
+    import torch
+
+    from m3d import plyio, synth
+    from matcher.icp import refine_registration
+    from matcher.ransac import global_registration
+    from ply import Ply
+
+    T = synth.random_rigid(31, rot_range=0.5, trans_range=0.5)
+    out = {"pipeline": "STL -> convert_stl-ply.py -> Ply(0.3) -> global_registration -> refine_registration",
+           "data": "generated meshes (m3d.synth.surface_mesh; the reference ships no scans)"}
+    with tempfile.TemporaryDirectory() as d:
+        for tag, nl in (("warm", 60), ("timed", args.cfg4_mesh)):
+            v_s, f_s = synth.surface_mesh(nl, 2 * nl, seed=1)
+            v_t, f_t = synth.surface_mesh(int(nl * 1.1), int(nl * 2.2), seed=2)
+            plyio.write_stl(f"{d}/src.stl", synth.apply(np.linalg.inv(T), v_s), f_s)
+            plyio.write_stl(f"{d}/tgt.stl", v_t, f_t)
+            t0 = time.perf_counter()
+            plyio.convert_stl_to_ply(f"{d}/src.stl", f"{d}/src.ply")
+            plyio.convert_stl_to_ply(f"{d}/tgt.stl", f"{d}/tgt.ply")
+            t_conv = time.perf_counter() - t0
+            np.random.seed(0)
+            src, tgt = Ply(f"{d}/src.ply", 0.3), Ply(f"{d}/tgt.ply", 0.3)
+            res = {}
+            for it in (30, 30000):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                coarse = global_registration(src, tgt, 0.3, iteration=it)
+                t1 = time.perf_counter()
+                fine = refine_registration(src, tgt, coarse.transformation, 0.3)
+                t2 = time.perf_counter()
+                res[it] = (coarse, fine, (t1 - t0) * 1e3, (t2 - t1) * 1e3)
+            if tag == "warm":
+                continue
+            out.update({
+                "src_vertices": len(v_s), "tgt_vertices": len(v_t),
+                "src_down": len(src.pcd_down.points), "tgt_down": len(tgt.pcd_down.points),
+                "convert_stl_ply_ms": t_conv * 1e3,
+                "ply_stage_ms": {"src": src.stage_ms, "tgt": tgt.stage_ms},
+            })
+            for it, (coarse, fine, tg, tr) in res.items():
+                out[f"iteration_{it}"] = {
+                    "global_registration_ms": tg, "refine_registration_ms": tr,
+                    "coarse_fitness": coarse.fitness, "fine_fitness": fine.fitness,
+                    "fine_max_abs_err_vs_T_true": float(np.abs(fine.transformation - T).max())}
+            # validation throughput: the same a6 call with confidence 1.0 (no early exit), so every
+            # checker-passing hypothesis of 30000 is validated (grid.hip validate_kernel batches)
+            from m3d import feature_ransac, prep
+            corr = feature_ransac.correspondences_from_features(src.pcd_fpfh, tgt.pcd_fpfh, True)
+            sp, tp = src.pcd_down.points, tgt.pcd_down.points
+            kw = dict(edge_length=0.9, distance=0.45, max_iteration=30000, confidence=1.0)
+            prep.ransac_on_correspondences(sp, tp, corr, 0.45, **kw)  # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fr = prep.ransac_on_correspondences(sp, tp, corr, 0.45, **kw)
+            dt = time.perf_counter() - t0
+            out["validation_throughput"] = {
+                "hypotheses": 30000, "correspondences": len(corr), "validations": fr.validations,
+                "ms": dt * 1e3, "validations_per_s": fr.validations / dt,
+                "point_evaluations_per_s": fr.validations * len(sp) / dt,
+                "best_fitness": fr.fitness}
+    return out
 
 
 def bench_ransac_api(args, budget_s=1.5):

@@ -115,6 +115,30 @@ def test_feature_ransac_matches_oracle():
     assert len(got.correspondence_set) == round(got.fitness * len(src))
 
 
+@pytest.mark.parametrize("bad_ratio,iters,seed,edge,nval", [(0.97, 2000, 5, None, 2000), (0.9, 2000, 6, 0.9, 5)])
+def test_feature_ransac_batched_validation_matches_oracle(bad_ratio, iters, seed, edge, nval):
+    """Batched validation (validate_kernel, batches of 64 → 128 → …) against the sequential
+    oracle.  Case 1: no checkers and a 0.03 radius on a 97 %-outlier set keep every fitness tiny,
+    so the early exit never comes and all 2000 hypotheses are validated in growing batches (ties
+    in fitness decided by rmse); case 2: an early exit inside the first batch."""
+    src, _ = synth.surface_points(3000, seed=seed)
+    T = synth.random_rigid(seed + 1, rot_range=0.5, trans_range=1.0)
+    tgt = synth.apply(T, src) + np.random.default_rng(seed + 2).normal(scale=0.01, size=src.shape)
+    rng = np.random.default_rng(seed + 3)
+    corr = np.c_[np.arange(3000), np.arange(3000)]
+    bad = rng.random(3000) < bad_ratio
+    corr[bad, 1] = rng.integers(0, 3000, int(bad.sum()))
+    kw = dict(max_iteration=iters, confidence=0.999, edge_length=edge, distance=None)
+    got = prep.ransac_on_correspondences(src, tgt, corr, 0.03, seed=seed, **kw)
+    ref = P.ransac_feature(src, tgt, corr, 0.03, lambda h: P.native_rows(seed, h, len(corr)), **kw)
+    assert ref["validations"] >= nval
+    assert got.validations == ref["validations"]
+    assert got.best_index == ref["best_index"]
+    assert got.fitness == ref["fitness"]
+    assert abs(got.inlier_rmse - ref["inlier_rmse"]) <= 1e-12 * max(1.0, ref["inlier_rmse"])
+    np.testing.assert_allclose(got.transformation, ref["transformation"], atol=1e-9)
+
+
 def test_feature_ransac_empty_cases():
     pts, _ = synth.surface_points(100, seed=1)
     out = prep.ransac_on_correspondences(pts, pts, np.zeros((2, 2), np.int32), 0.45)
@@ -141,3 +165,30 @@ def test_ply_pipeline_registers_synthetic_scan(tmp_path):
     assert coarse.fitness > 0.3
     fine = refine_registration(src, tgt, coarse.transformation, 0.3)
     np.testing.assert_allclose(fine.transformation, T, atol=5e-3)
+
+
+@pytest.mark.parametrize("iteration", [30, 30000])
+def test_cfg4_stl_pipeline(tmp_path, iteration):
+    """cfg4 from STL: two tessellations of one surface (two "scans", source moved by T⁻¹) written
+    as binary STL → convert_stl-ply.py:1-11 (m3d.plyio.convert_stl_to_ply: merged vertices →
+    ASCII PLY) → Ply(path, 0.3) (ply.py:32-66) → matcher.register (= main.py:24-43:
+    global_registration → refine_registration) on the GPU.  The reference ships no scans
+    (3d_data/.gitignore), so the meshes are generated (m3d.synth.surface_mesh)."""
+    from m3d import plyio
+    from matcher import register
+    from ply import Ply
+
+    T = synth.random_rigid(31, rot_range=0.5, trans_range=0.5)
+    v_src, f_src = synth.surface_mesh(180, 360, seed=1)
+    v_tgt, f_tgt = synth.surface_mesh(200, 400, seed=2)
+    plyio.write_stl(tmp_path / "src.stl", synth.apply(np.linalg.inv(T), v_src), f_src, binary=True)
+    plyio.write_stl(tmp_path / "tgt.stl", v_tgt, f_tgt, binary=True)
+    n_src = plyio.convert_stl_to_ply(tmp_path / "src.stl", tmp_path / "src.ply")
+    n_tgt = plyio.convert_stl_to_ply(tmp_path / "tgt.stl", tmp_path / "tgt.ply")
+    assert (n_src, n_tgt) == (len(v_src), len(v_tgt))  # shared STL corners merged back
+    np.random.seed(0)
+    src, tgt = Ply(tmp_path / "src.ply", 0.3), Ply(tmp_path / "tgt.ply", 0.3)
+    assert set(src.stage_ms) >= {"read", "voxel_down_sample", "normals_down", "fpfh", "noise", "normals_full"}
+    res = register(src, tgt, 0.3, iteration=iteration)
+    np.testing.assert_allclose(res.transformation, T, atol=5e-3)
+    assert res.fitness > 0.9

@@ -120,3 +120,24 @@ def test_ply_class_checks_like_reference(tmp_path):
     (tmp_path / "x.txt").write_text("x")
     with pytest.raises(TypeError):
         Ply(tmp_path / "x.txt")
+
+
+@pytest.mark.parametrize("binary", [True, False])
+def test_stl_writer_round_trip_on_generated_mesh(tmp_path, binary):
+    """m3d.synth.surface_mesh → write_stl → read_stl: a closed mesh (every edge in two faces),
+    vertices merged back exactly (float32 STL payload), faces preserved."""
+    from m3d import synth
+
+    v, f = synth.surface_mesh(20, 40, seed=4)
+    e = np.sort(np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]]), axis=1)
+    assert set(np.unique(np.unique(e, axis=0, return_counts=True)[1])) == {2}
+    plyio.write_stl(tmp_path / "m.stl", v, f, binary=binary)
+    vv, ff = plyio.read_stl(tmp_path / "m.stl")
+    v32 = v.astype(np.float32).astype(np.float64)
+    if binary:
+        np.testing.assert_array_equal(vv, v32)
+    else:  # ASCII holds 9 significant digits of each float32 coordinate
+        np.testing.assert_allclose(vv, v32, rtol=1e-8, atol=1e-12)
+    np.testing.assert_array_equal(ff, f)
+    assert plyio.convert_stl_to_ply(tmp_path / "m.stl", tmp_path / "m.ply") == len(v)
+    np.testing.assert_array_equal(plyio.read_ply(tmp_path / "m.ply")[0], vv)
