@@ -38,13 +38,13 @@ constexpr int kNNTile = 16;   // screen sub-tile (one branch per sub-tile)
 constexpr int kNNLds = 512;   // targets per LDS tile (8 KB, double-buffered)
 constexpr int kNNBlock = 256;
 constexpr int kTermsBlock = 256;
-constexpr int kTermsPtsDefault = 2;  // sources per terms thread (M3D_TERMS_PTS = 1|2|4|8, tuning):
+constexpr int kTermsPtsDefault = 2;  // sources per terms thread (M3D_TERMS_PTS = 1|2|4, tuning):
                                      // 2× fewer block partials for the last block to reduce
 static int terms_pts() {
   static const int v = [] {
     const char* e = getenv("M3D_TERMS_PTS");
     const int k = e ? atoi(e) : kTermsPtsDefault;
-    return (k == 1 || k == 2 || k == 4 || k == 8) ? k : kTermsPtsDefault;
+    return (k == 1 || k == 2 || k == 4) ? k : kTermsPtsDefault;
   }();
   return v;
 }
@@ -763,56 +763,115 @@ struct TermsArgs {
 // est: M3D_EST_POINT_TO_PLANE → slots 0..20 JTJ (upper, row-major), 21..26 JTr, 27 Σr²
 //      M3D_EST_POINT_TO_POINT → slots 0..2 Σp_c, 3..5 Σq_c, 6..14 Σ p_c q_cᵀ (row-major)
 // both: 28 count, 29 Σd²  (c = source centre: identical on every shard)
-// kWT: write the block partial through to memory (sc1 store) for the fused last-block reduce
-template <bool kWT>
+// kWT: write the block partial through to memory (sc1 store) for the fused last-block reduce.
+// kP sources per thread, in two load rounds so that a thread's chains overlap: (1) every
+// source's key / runner-up / fp64 point (or claim / dmin), (2) after the fp64 decision, every
+// winner's fp64 target (and normal); the rare ambiguous queries are resolved by the whole wave in
+// between (nnkey.h resolve_wave, one ballot when there are none).
+template <bool kWT, int kP>
 __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* __restrict__ s,
-                                            double* __restrict__ partials, int pts) {
+                                            double* __restrict__ partials) {
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
   double acc[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) acc[k] = 0.0;
-  for (int u = 0; u < pts; ++u) {
-    // every lane stays in the loop (resolve_wave is a whole-wave operation)
-    const int64_t i = ((int64_t)blockIdx.x * pts + u) * kTermsBlock + threadIdx.x;
-    const bool valid = i < a.ns;
-    const int64_t ii = valid ? i : 0;
-    const double* p = a.src64 + 3 * ii;
-    double vs[3];
-    q64_of(s->T, p, vs);
-    int64_t gj = -1;
-    double d2 = 0.0;
+  int64_t ii[kP];
+  bool valid[kP];
+  double vs[kP][3];
+  int64_t gj[kP];
+  double d2[kP];
+  bool fixed[kP];  // winner and d² already final (resolved in fp64, or given by the claim)
+  uint64_t k1[kP];
+  float n2[kP];
+#pragma unroll
+  for (int u = 0; u < kP; ++u) {
+    const int64_t i = ((int64_t)blockIdx.x * kP + u) * kTermsBlock + threadIdx.x;
+    valid[u] = i < a.ns;
+    ii[u] = valid[u] ? i : 0;
+    gj[u] = -1;
+    d2[u] = 0.0;
+    fixed[u] = true;
     if (a.claim == nullptr) {
-      const uint64_t k1 = valid ? (uint64_t)a.keys[ii] : (uint64_t)kKeyNone;
-      const float n2 = valid ? __uint_as_float(a.near2[ii]) : kInf;
-      if (valid && a.reset_keys != nullptr) {
-        a.reset_keys[ii] = kKeyNone;
-        a.near2[ii] = kNearNone;
-      }
-      winner_fp64(valid, k1, n2, s, a.g, a.tgt64, a.off, a.nt_shard, a.src32[ii], vs, gj, d2);
-    } else if (valid) {
-      const int32_t cj = a.claim[ii];
+      k1[u] = valid[u] ? (uint64_t)a.keys[ii[u]] : (uint64_t)kKeyNone;
+      n2[u] = valid[u] ? __uint_as_float(a.near2[ii[u]]) : kInf;
+    } else if (valid[u]) {
+      const int32_t cj = a.claim[ii[u]];
+      const int64_t dm = a.dmin[ii[u]];
       if (cj != 0x7FFFFFFF) {
-        gj = cj;
-        d2 = __longlong_as_double(a.dmin[ii]);
+        gj[u] = cj;
+        d2[u] = __longlong_as_double(dm);
       }
-      if (a.dprev != nullptr) a.dprev[ii] = a.dmin[ii];
+      if (a.dprev != nullptr) a.dprev[ii[u]] = dm;
     }
-    if (!valid) continue;
-    if (a.corr != nullptr) a.corr[i] = (int32_t)gj;
+    q64_of(s->T, a.src64 + 3 * ii[u], vs[u]);
+  }
+  if (a.claim == nullptr) {
+#pragma unroll
+    for (int u = 0; u < kP; ++u) {
+      if (valid[u] && a.reset_keys != nullptr) {
+        a.reset_keys[ii[u]] = kKeyNone;
+        a.near2[ii[u]] = kNearNone;
+      }
+      // nnkey.h winner_fp64, split: ambiguous queries resolved here by the wave, the others'
+      // candidate (k1's target) re-evaluated in fp64 after the batched target loads below
+      const float X = valid[u] && k1[u] != (uint64_t)kKeyNone ? search_bound(key_d2(k1[u]), s->band_e, s->r2_hi)
+                                                              : -1.0f;
+      const bool amb = X >= 0.0f && n2[u] <= X;
+      float qx = 0.0f, qy = 0.0f, qz = 0.0f;
+      if (amb) xform32(s->Rt32, a.src32[ii[u]], qx, qy, qz);
+      int64_t bj = -1;
+      double bd = 0.0;
+      resolve_wave(amb, a.g, a.tgt64, a.off, qx, qy, qz, X, vs[u], s->r2, bj, bd);
+      if (amb) {
+        gj[u] = bj;
+        d2[u] = bd;
+      } else if (valid[u] && key_real(k1[u])) {
+        const int64_t c = (int64_t)(uint32_t)k1[u];
+        if (c >= a.off && c < a.off + a.nt_shard) {
+          gj[u] = c;
+          fixed[u] = false;
+        }
+      }
+    }
+  }
+  double tq[kP][3], tn[kP][3];
+#pragma unroll
+  for (int u = 0; u < kP; ++u) {
+    const bool own = valid[u] && gj[u] >= a.off && gj[u] < a.off + a.nt_shard;
+    const int64_t l = own ? gj[u] - a.off : 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      tq[u][k] = a.tgt64[3 * l + k];
+      tn[u][k] = a.est == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kP; ++u) {
+    if (!valid[u]) continue;
+    if (!fixed[u]) {  // k1's target: the fp64 winner iff its d64 < r²
+      const double d = d2_64(vs[u], tq[u]);
+      if (d < s->r2) {
+        d2[u] = d;
+      } else {
+        gj[u] = -1;
+      }
+    }
+    const int64_t i = ii[u];
+    if (a.corr != nullptr) a.corr[i] = (int32_t)gj[u];
     if (a.sq != nullptr) {
-      const bool local = gj >= a.off && gj < a.off + a.nt_shard;
-      a.sq[a.minv[i]] = seed_rec(gj, local, a.tgt32 + (local ? gj - a.off : 0), d2);
+      const bool local = gj[u] >= a.off && gj[u] < a.off + a.nt_shard;
+      a.sq[a.minv[i]] = seed_rec(gj[u], local, a.tgt32 + (local ? gj[u] - a.off : 0), d2[u]);
     }
-    if (gj < a.off || gj >= a.off + a.nt_shard) continue;  // none, or another shard's target
-    const double* q = a.tgt64 + 3 * (gj - a.off);
-    const double d[3] = {vs[0] - q[0], vs[1] - q[1], vs[2] - q[2]};
+    if (gj[u] < a.off || gj[u] >= a.off + a.nt_shard) continue;  // none, or another shard's target
+    const double* q = tq[u];
+    const double d[3] = {vs[u][0] - q[0], vs[u][1] - q[1], vs[u][2] - q[2]};
     acc[28] += 1.0;
-    acc[29] += d2;
+    acc[29] += d2[u];
     if (a.est == M3D_EST_POINT_TO_PLANE) {
-      const double* n = a.nrm64 + 3 * (gj - a.off);
+      const double* n = tn[u];
       const double r = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
       double J[6];
-      cross3(vs, n, J);
+      cross3(vs[u], n, J);
       J[3] = n[0];
       J[4] = n[1];
       J[5] = n[2];
@@ -825,7 +884,7 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
       for (int x = 0; x < 6; ++x) acc[21 + x] += J[x] * r;
       acc[27] += r * r;
     } else {
-      const double pc[3] = {vs[0] - a.c[0], vs[1] - a.c[1], vs[2] - a.c[2]};
+      const double pc[3] = {vs[u][0] - a.c[0], vs[u][1] - a.c[1], vs[u][2] - a.c[2]};
       const double qc[3] = {q[0] - a.c[0], q[1] - a.c[1], q[2] - a.c[2]};
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
@@ -858,10 +917,11 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
   }
 }
 
+template <int kP>
 __global__ __launch_bounds__(kTermsBlock) void terms_kernel(TermsArgs a, const IcpState* __restrict__ s,
-                                                            double* __restrict__ partials, int pts) {
+                                                            double* __restrict__ partials) {
   if (s->done) return;
-  terms_block<false>(a, s, partials, pts);
+  terms_block<false, kP>(a, s, partials);
 }
 
 // Target-sharded evaluation, step 1 (m3d_icp_shard_nn): this shard's fp64 winner of every query
@@ -1031,13 +1091,14 @@ __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restri
 // write-through (sc1), drains it (vmcnt(0)) and one lane adds to the agent-scope ticket; the
 // block whose add returned nblocks − 1 reads every partial with sc1 loads.  No L2 write-back or
 // invalidate fences are needed.
+template <int kP>
 __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     TermsArgs a, IcpState* s, double* partials, int64_t nblocks, double* __restrict__ sums,
-    SolveParams sp, int pts, int do_solve) {
+    SolveParams sp, int do_solve) {
   // do_solve = 0: the sharded tail (m3d_icp_shard_terms) — terms + the fixed-order reduce into
   // `sums` in one launch; the caller all-reduces them and runs m3d_icp_solve
   if (s->done) return;
-  terms_block<true>(a, s, partials, pts);
+  terms_block<true, kP>(a, s, partials);
   __shared__ double red[kReduceGroups][kTermSlots];
   __shared__ int last;
   // the partial went out write-through (sc1): drain it, then one lane takes the ticket
@@ -1340,8 +1401,13 @@ hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* c
                                  const int64_t* dmin, hipStream_t st) {
   const int64_t ns = s->src->n;
   if (ns == 0) return hipMemsetAsync(s->partials, 0, sizeof(double) * kTermSlots, st);
-  terms_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(terms_args(s, off, claim, dmin, false),
-                                                             s->state, s->partials, terms_pts());
+  const TermsArgs ta = terms_args(s, off, claim, dmin, false);
+  const unsigned nb = (unsigned)s->nblocks;
+  switch (terms_pts()) {
+    case 1: terms_kernel<1><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials); break;
+    case 2: terms_kernel<2><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials); break;
+    default: terms_kernel<4><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials); break;
+  }
   return hipGetLastError();
 }
 
@@ -1364,6 +1430,17 @@ static SolveParams solve_params(const m3d_icp* s) {
 
 // sharded tail: terms (shard offset off; claim/dmin: the target-shard exchange results, or null
 // for a source shard) + reduce into sums, one launch
+static void launch_terms_solve(const TermsArgs& ta, const m3d_icp* s, double* sums, int do_solve,
+                               hipStream_t st) {
+  const unsigned nb = (unsigned)s->nblocks;
+  const SolveParams sp = solve_params(s);
+  switch (terms_pts()) {
+    case 1: terms_solve_kernel<1><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks, sums, sp, do_solve); break;
+    case 2: terms_solve_kernel<2><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks, sums, sp, do_solve); break;
+    default: terms_solve_kernel<4><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks, sums, sp, do_solve); break;
+  }
+}
+
 hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, const int32_t* claim,
                                    const int64_t* dmin, double* sums, bool reset_keys,
                                    hipStream_t st) {
@@ -1372,9 +1449,7 @@ hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, const int32_t*
     hipError_t e = launch_icp_terms_mode(s, off, claim, dmin, st);
     return e == hipSuccess ? launch_icp_reduce(s, sums, st) : e;
   }
-  terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
-      terms_args(s, off, claim, dmin, reset_keys), s->state, s->partials, s->nblocks, sums,
-      solve_params(s), terms_pts(), 0);
+  launch_terms_solve(terms_args(s, off, claim, dmin, reset_keys), s, sums, 0, st);
   return hipGetLastError();
 }
 
@@ -1390,9 +1465,7 @@ hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t
     if (e == hipSuccess) e = launch_icp_reduce(s, s->sums, st);
     return e == hipSuccess ? launch_icp_solve(s, s->sums, st) : e;
   }
-  terms_solve_kernel<<<(unsigned)s->nblocks, kTermsBlock, 0, st>>>(
-      terms_args(s, 0, nullptr, nullptr, reset_keys), s->state, s->partials, s->nblocks, s->sums,
-      solve_params(s), terms_pts(), 1);
+  launch_terms_solve(terms_args(s, 0, nullptr, nullptr, reset_keys), s, s->sums, 1, st);
   return hipGetLastError();
 }
 

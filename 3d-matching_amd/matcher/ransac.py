@@ -163,6 +163,9 @@ def evaluate_inlier_ratio_fast(p_src, p_tgt, transform, dist_thresh_sq) -> float
     return np.int64(cnt[0].item()) / len(p_src)
 
 
+_REPLAY_CHUNK = 4096  # rows per MT checkpoint of the replay sampler
+
+
 def run_ransac(src, tgt, correspondences, voxel_size: float = 0.3, max_iter: int = 10000,
            early_stop: bool = True, early_stop_threshold: float = 0.5,
            early_stop_confidence: float = 0.99, sampler: str = "replay", seed=None,
@@ -191,18 +194,27 @@ def run_ransac(src, tgt, correspondences, voxel_size: float = 0.3, max_iter: int
     params = RansacParams(max_iter=max_iter, thr=thr, mode=mode, early_stop=early_stop,
                           es_threshold=early_stop_threshold, es_confidence=early_stop_confidence)
     triples = None
-    state0 = None
+    checkpoints = None
     if sampler == "replay" and nc >= 3:
-        state0 = np.random.get_state()
-        triples, _ = replay_triples(nc, max_iter, state=state0)
+        # the rows in chunks, keeping the MT state at each chunk start: after the run the RNG is
+        # advanced from the checkpoint nearest the stop (< _REPLAY_CHUNK re-drawn rows), not
+        # replayed from the start
+        checkpoints = [np.random.get_state()]
+        parts = []
+        for h0 in range(0, max_iter, _REPLAY_CHUNK):
+            t, st = replay_triples(nc, min(_REPLAY_CHUNK, max_iter - h0), state=checkpoints[-1])
+            parts.append(t)
+            checkpoints.append(st)
+        triples = np.concatenate(parts) if parts else np.empty((0, 3), np.int32)
     elif sampler == "native":
         params.seed = 0 if seed is None else int(seed)
     elif sampler != "replay":
         raise ValueError("sampler must be 'replay' or 'native'")
     out = cs.run(params, triples=triples)
-    if state0 is not None:
+    if checkpoints is not None:
         # advance the global RNG by exactly the iterations the loop consumed
-        _, st = replay_triples(nc, out.iterations, state=state0)
+        k, rem = divmod(int(out.iterations), _REPLAY_CHUNK)
+        st = checkpoints[k] if rem == 0 else replay_triples(nc, rem, state=checkpoints[k])[1]
         np.random.set_state(st)
     res = RegistrationResult(out.transformation, out.fitness)
     return res, dict(best_index=out.best_index, iterations=out.iterations, best_count=out.best_count,

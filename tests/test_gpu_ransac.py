@@ -147,6 +147,25 @@ def test_matcher_ransac_replay_equals_reference_loop(golden, pts5k):
     assert np.random.rand() == after
 
 
+@pytest.mark.parametrize("max_iter", [5000, 8192])
+def test_replay_rng_advance_across_checkpoints(pts5k, max_iter):
+    """run_ransac's replay keeps an MT checkpoint every 4096 rows; without early stop the loop
+    consumes max_iter rows (one checkpoint + a remainder, or exactly two checkpoints) and the
+    global RNG must end where max_iter np.random.choice calls leave it."""
+    from matcher import ransac as M
+
+    corr = pts5k["corr_mid"]
+    np.random.seed(77)
+    _, info = M.run_ransac(pts5k["src"], pts5k["tgt"], corr, voxel_size=0.3, max_iter=max_iter,
+                           early_stop=False)
+    assert info["iterations"] == max_iter
+    after = np.random.rand()
+    np.random.seed(77)
+    for _ in range(max_iter):
+        np.random.choice(len(corr), 3, replace=False)
+    assert np.random.rand() == after
+
+
 def test_crash_kats_through_api(golden):
     from matcher import ransac as M
 
