@@ -229,65 +229,17 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     k1d = key_real_d2(k1);
     if (g.ncells > 0) {
       const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
-      const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
-      const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
-      const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
-      const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
-      const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
-      const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
-      const int ny = y1 - y0 + 1;
-      const int rows = ny * (z1 - z0 + 1);
+      int rows = 0, cand = 0;
+      grid_scan<kL, kR, kB>(g, qx, qy, qz, R, r2_hi, off, sub, k1, k1d, n2, &rows, &cand);
       if (stats != nullptr && sub == 0) {
         atomicAdd(&stats[0], 1ull);
         atomicAdd(&stats[1], (unsigned long long)rows);
+        atomicAdd(&stats[2], (unsigned long long)cand);
         if (seed != kKeyNone) atomicAdd(&stats[3], 1ull);
-      }
-      for (int r0 = 0; r0 < rows; r0 += kR) {
-        int32_t a[kR], b[kR];
-        int32_t len = 0;
-#pragma unroll
-        for (int k = 0; k < kR; ++k) {
-          const int r = r0 + k;
-          a[k] = b[k] = 0;
-          if (r < rows) {
-            const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
-            a[k] = g.start[row + x0];
-            b[k] = g.start[row + x1 + 1];
-          }
-          len = max(len, b[k] - a[k]);
-          if (stats != nullptr && sub == 0) atomicAdd(&stats[2], (unsigned long long)(b[k] - a[k]));
-        }
-        for (int32_t base = sub; base < len; base += kL * kB) {
-          float4 v[kR][kB];
-#pragma unroll
-          for (int k = 0; k < kR; ++k)
-#pragma unroll
-            for (int m = 0; m < kB; ++m) {
-              const int32_t j = a[k] + base + m * kL;
-              if (j < b[k]) v[k][m] = g.pts[j];
-            }
-#pragma unroll
-          for (int k = 0; k < kR; ++k)
-#pragma unroll
-            for (int m = 0; m < kB; ++m) {
-              const int32_t j = a[k] + base + m * kL;
-              if (j < b[k]) {
-                const float d2 = d2f(qx, qy, qz, v[k][m].x, v[k][m].y, v[k][m].z);
-                if (d2 <= r2_hi)
-                  near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(v[k][m].w))), d2);
-              }
-            }
-        }
       }
     }
   }
-#pragma unroll
-  for (int o = kL / 2; o > 0; o >>= 1) {
-    const uint64_t b1 = ((uint64_t)(uint32_t)__shfl_xor((int)(k1 >> 32), o, kL) << 32) |
-                        (uint32_t)__shfl_xor((int)(uint32_t)k1, o, kL);
-    const float bn2 = __shfl_xor(n2, o, kL);
-    near_merge(k1, k1d, n2, b1, bn2);
-  }
+  grid_merge_lanes<kL>(k1, k1d, n2);
   if (i >= 0 && sub == 0) {
     keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
     near2[i] = __float_as_uint(n2);

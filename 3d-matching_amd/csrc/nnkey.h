@@ -114,6 +114,77 @@ __device__ __forceinline__ int grid_coord(float x, float o, float inv_h, int n) 
   return (int)f;
 }
 
+// Grid scan of one query by kL cooperating lanes (grid.hip grid_nn_batched_kernel, icp.hip
+// grid_icp_kernel): every lane of the query sees every cell row of the box q ± R and takes the
+// row's points sub, sub + kL, …; the start offsets of kR rows are loaded together, then kR × kB
+// point loads per lane go out at once.  Each lane pushes the targets with d2f ≤ r2_hi into its
+// (k1, k1d, near2) state; grid_merge_lanes combines the kL states.
+template <int kL, int kR, int kB>
+__device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, float qz, float R,
+                                          float r2_hi, int64_t off, int sub, uint64_t& k1,
+                                          float& k1d, float& n2, int* nrows = nullptr,
+                                          int* ncand = nullptr) {
+  const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
+  const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
+  const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
+  const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
+  const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
+  const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
+  const int ny = y1 - y0 + 1;
+  const int rows = ny * (z1 - z0 + 1);
+  if (nrows != nullptr) *nrows = rows;
+  int cand = 0;
+  for (int r0 = 0; r0 < rows; r0 += kR) {
+    int32_t a[kR], b[kR];
+    int32_t len = 0;
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+      const int r = r0 + k;
+      a[k] = b[k] = 0;
+      if (r < rows) {
+        const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
+        a[k] = g.start[row + x0];
+        b[k] = g.start[row + x1 + 1];
+      }
+      len = max(len, b[k] - a[k]);
+      cand += b[k] - a[k];
+    }
+    for (int32_t base = sub; base < len; base += kL * kB) {
+      float4 v[kR][kB];
+#pragma unroll
+      for (int k = 0; k < kR; ++k)
+#pragma unroll
+        for (int m = 0; m < kB; ++m) {
+          const int32_t j = a[k] + base + m * kL;
+          if (j < b[k]) v[k][m] = g.pts[j];
+        }
+#pragma unroll
+      for (int k = 0; k < kR; ++k)
+#pragma unroll
+        for (int m = 0; m < kB; ++m) {
+          const int32_t j = a[k] + base + m * kL;
+          if (j < b[k]) {
+            const float d2 = d2f(qx, qy, qz, v[k][m].x, v[k][m].y, v[k][m].z);
+            if (d2 <= r2_hi)
+              near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(v[k][m].w))), d2);
+          }
+        }
+    }
+  }
+  if (ncand != nullptr) *ncand = cand;
+}
+
+template <int kL>
+__device__ __forceinline__ void grid_merge_lanes(uint64_t& k1, float& k1d, float& n2) {
+#pragma unroll
+  for (int o = kL / 2; o > 0; o >>= 1) {
+    const uint64_t b1 = ((uint64_t)(uint32_t)__shfl_xor((int)(k1 >> 32), o, kL) << 32) |
+                        (uint32_t)__shfl_xor((int)(uint32_t)k1, o, kL);
+    const float bn2 = __shfl_xor(n2, o, kL);
+    near_merge(k1, k1d, n2, b1, bn2);
+  }
+}
+
 // Exact fp64 decision for the ambiguous queries of a wave (every lane of the wave calls it, with
 // amb set on the lanes whose query needs it).  For each such query the whole wave scans the
 // cell box of q ± 1.001·√X (grid.hip header lemma: it holds every target with d2f ≤ X), lanes
