@@ -301,6 +301,37 @@ def compute_spfh(points, normals, idx, cnt):
     return spfh
 
 
+def spfh_edge_sensitive(points, normals, idx, cnt, delta=1e-12, delta_swap=2e-15):
+    """Test aid for the FPFH parity bar: True for a point whose SPFH may legitimately differ
+    between two correct fp64 implementations — one of its pair features lands within ``delta``
+    of a bin edge (the bin arguments 11·(f0 + π)/2π, 11·(f1 + 1)/2, 11·(f2 + 1)/2), or the
+    source/target swap test acos|a1| > acos|a2| has ||a1| − |a2|| < ``delta_swap``.  acos /
+    atan2 of two libms (numpy's and the device's ocml) may differ by an ulp or two (≈ 1e-16
+    relative: acos near π/2 has slope ≈ 1, so ≥ 10 ulps of acos for the swap test), which can
+    move only such a feature across the edge."""
+    p = np.asarray(points, np.float64)
+    nr = np.asarray(normals, np.float64)
+    out = np.zeros(len(p), bool)
+    for i in range(len(p)):
+        c = int(cnt[i])
+        for k in range(1, c):
+            j = idx[i, k]
+            dp = p[j] - p[i]
+            f3 = math.sqrt(_dot(dp, dp))
+            if f3 == 0.0:
+                continue
+            a1, a2 = _dot(nr[i], dp) / f3, _dot(nr[j], dp) / f3
+            if abs(abs(a1) - abs(a2)) < delta_swap:
+                out[i] = True
+                break
+            f = pair_features(p[i], nr[i], p[j], nr[j])
+            xs = (11 * (f[0] + math.pi) / (2.0 * math.pi), 11 * (f[1] + 1.0) * 0.5, 11 * (f[2] + 1.0) * 0.5)
+            if any(abs(x - round(x)) < delta for x in xs):
+                out[i] = True
+                break
+    return out
+
+
 def compute_fpfh(points, normals, radius, max_nn, nbrs=None):
     p = np.asarray(points, np.float64)
     nr = np.asarray(normals, np.float64)
