@@ -761,6 +761,17 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
     const double cell = max_dist * 1.001 / cell_div;
     int grc = ensure_grid(ctx, tgt, cell, nullptr, &tg);
     if (!grc) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
+    // Grid NN on a dense target: a seeded query's box is ~1–2 cells per axis, so the candidates
+    // it scans grow with the points per cell.  Shrink the target cell by div = ⌊√(m / 3.5)⌋
+    // (m = points per occupied cell at cell ≈ r; any cell size gives the same keys, grid.hip):
+    // measured (tools/grid_cell_sweep.sh) 1M × 1M (m ≈ 33) 206 → 128 µs per scan at div 3;
+    // cfg1 (m ≈ 3.9) and the 1M × 125k shard (m ≈ 4.7) are fastest at div 1.
+    if (!grc && params->nn_method == M3D_NN_GRID && getenv("M3D_GRID_CELL_DIV") == nullptr &&
+        tg->n_occ > 0) {
+      const double m = (double)tg->n_pts / (double)tg->n_occ;
+      const int div = std::min(4, std::max(1, (int)std::floor(std::sqrt(m / 3.5))));
+      if (div > 1) grc = ensure_grid(ctx, tgt, cell / div, nullptr, &tg);
+    }
     if (!grc && params->nn_method == M3D_NN_GRID && sg->mpts == nullptr) {
       hipError_t e = grid_morton(const_cast<Grid*>(sg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("morton order: ") + hipGetErrorString(e));

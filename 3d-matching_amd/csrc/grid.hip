@@ -96,6 +96,16 @@ __global__ __launch_bounds__(kGridBlock) void cell_start_kernel(const uint32_t* 
   start[c] = (int32_t)lo;
 }
 
+// occupied cells: sorted positions that start a new cell
+__global__ __launch_bounds__(kGridBlock) void count_occupied_kernel(const uint32_t* __restrict__ key,
+                                                                    int64_t n,
+                                                                    unsigned long long* __restrict__ occ) {
+  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  const bool first = k < n && (k == 0 || key[k] != key[k - 1]);
+  const unsigned long long b = __ballot(first);
+  if ((threadIdx.x & (kWave - 1)) == 0 && b != 0) atomicAdd(occ, (unsigned long long)__popcll(b));
+}
+
 __global__ __launch_bounds__(kGridBlock) void grid_gather_kernel(const float4* __restrict__ p,
                                                                  const int32_t* __restrict__ val,
                                                                  int64_t n,
@@ -493,8 +503,20 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   cell_start_kernel<<<(unsigned)((total + 1 + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
       kout, n, total, g->start);
   grid_gather_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, vout, n, g->pts);
+  // occupied-cell count (m3d_icp_create sizes the grid-NN cell from the points per occupied cell);
+  // the radix-sort temp storage (≥ 8 B) holds the counter
+  unsigned long long occ = 0;
   e = hipGetLastError();
+  if (e == hipSuccess && tmp_bytes >= sizeof(unsigned long long))
+    e = hipMemsetAsync(tmp, 0, sizeof(unsigned long long), st);
+  if (e == hipSuccess && tmp_bytes >= sizeof(unsigned long long)) {
+    count_occupied_kernel<<<blocks, kGridBlock, 0, st>>>(kout, n, reinterpret_cast<unsigned long long*>(tmp));
+    e = hipGetLastError();
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(&occ, tmp, sizeof(occ), hipMemcpyDeviceToHost, st);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(st);
+  g->n_occ = (int64_t)occ;
   g->order = vout;  // sorted point indices: the cloud's cell order
   vout = nullptr;
   d.start = g->start;

@@ -97,6 +97,7 @@ struct Grid {
   float4* mpts = nullptr;
   int32_t* minv = nullptr;
   int64_t n_pts = 0;
+  int64_t n_occ = 0;      // occupied cells (0: not counted)
   double cell = 0.0;      // cell size used
   double cell_req = 0.0;  // cell size requested
   // brute-force MFMA screen operands in this grid's cell order (icp.hip pack16_sorted), padded
