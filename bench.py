@@ -345,7 +345,7 @@ def main():
                 cfg3.update(sec)
             else:
                 g_bytes = 28 * n3 + 16 * c3
-                sec["roofline"] = {"bound": "hbm", "kernel": "grid_nn_kernel",
+                sec["roofline"] = {"bound": "hbm", "kernel": "grid_nn_batched_kernel",
                                    "achieved": g_bytes / (avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": g_bytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                    "bytes_per_launch": g_bytes}
