@@ -213,6 +213,7 @@ void m3d_destroy(m3d_ctx* ctx) {
   if (ctx->stats) hipFree(ctx->stats);
   if (ctx->rstate) hipFree(ctx->rstate);
   if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
+  if (ctx->pin) hipHostFree(ctx->pin);
   for (auto& v : ctx->ev)
     for (auto& pr : v) {
       hipEventDestroy(pr.first);
@@ -444,6 +445,87 @@ int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64
   return M3D_OK;
 }
 
+// ------------------------------------------------------------------------------- one hypothesis
+namespace {
+constexpr size_t kPinT = 0, kPinStatus = 128, kPinCount = 136, kPinBytes = 4096;
+int pin_ensure(m3d_ctx* ctx) {
+  if (ctx->pin != nullptr) return M3D_OK;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, kPinBytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return m3d_fail(ctx, M3D_ERR_OOM, "pinned staging hipHostMalloc failed");
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    hipHostFree(h);
+    return m3d_fail(ctx, M3D_ERR_HIP, "hipHostGetDevicePointer failed");
+  }
+  ctx->pin = h;
+  ctx->pin_dev = d;
+  return M3D_OK;
+}
+extern "C++" {
+template <class T>
+T* pin_at(const m3d_ctx* ctx, size_t o, bool dev) {
+  return reinterpret_cast<T*>(static_cast<char*>(dev ? ctx->pin_dev : ctx->pin) + o);
+}
+}  // extern "C++"
+}  // namespace
+
+int m3d_kabsch3_one(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triple, double* T_out,
+                    int32_t* status, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, cs != nullptr && triple != nullptr && T_out != nullptr, "invalid arguments");
+  hipSetDevice(ctx->device);
+  int rc = pin_ensure(ctx);
+  if (rc) return rc;
+  hipStream_t st = S(stream);
+  // the library's own staging: ordered after earlier scratch users on other streams
+  Arena a(ctx, st);
+  hipError_t e = launch_kabsch3_one(cs, triple, pin_at<double>(ctx, kPinT, true),
+                                    pin_at<int32_t>(ctx, kPinStatus, true), st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  memcpy(T_out, pin_at<double>(ctx, kPinT, false), sizeof(double) * 16);
+  if (status) *status = *pin_at<int32_t>(ctx, kPinStatus, false);
+  return M3D_OK;
+}
+
+int m3d_ransac_score_one(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, double thr, int mode,
+                         int64_t* count, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, cs != nullptr && T != nullptr && count != nullptr, "invalid arguments");
+  CHECK_ARG(ctx, mode == M3D_SCORE_SQUARED || mode == M3D_SCORE_NORM, "unknown score mode");
+  if (cs->nc == 0) {  // ransac.py:220-221
+    *count = 0;
+    return M3D_OK;
+  }
+  hipSetDevice(ctx->device);
+  int rc = pin_ensure(ctx);
+  if (rc) return rc;
+  hipStream_t st = S(stream);
+  hipError_t e;
+  {
+    Arena a(ctx, st);
+    size_t o[kScoreSlots];
+    score_layout(a, 1, o);
+    const size_t o_T = a.take(sizeof(double) * 16);
+    const size_t o_c = a.take(sizeof(int32_t));
+    rc = a.commit();
+    if (rc) return rc;
+    ScoreScratch s = score_bind(a, o);
+    double* T64 = a.at<double>(o_T);
+    int32_t* cnt = a.at<int32_t>(o_c);
+    e = launch_score_one_prep(cs, T, thr, mode, T64, s.hypf, cnt, s.mf, st);
+    if (e == hipSuccess) e = score_enqueue(ctx, cs, T64, 1, thr, mode, cnt, s, nullptr, st, true);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(pin_at<int32_t>(ctx, kPinCount, false), cnt, sizeof(int32_t),
+                         hipMemcpyDeviceToHost, st);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  *count = *pin_at<int32_t>(ctx, kPinCount, false);
+  return M3D_OK;
+}
+
 // ------------------------------------------------------------------------------- a4
 int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_params* p,
                          const int32_t* triples, int32_t* counts_out,
@@ -554,28 +636,16 @@ struct MT {
     key[623] = key[396] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
     pos = 0;
   }
-  uint32_t next() {
-    if (pos >= 624) gen();
-    uint32_t y = key[pos++];
+  static uint32_t temper(uint32_t y) {
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
     return y;
   }
-  // numpy random_interval(max) for max <= 0xffffffff (masked rejection)
-  uint32_t interval(uint32_t max) {
-    if (max == 0) return 0;
-    uint32_t mask = max;
-    mask |= mask >> 1;
-    mask |= mask >> 2;
-    mask |= mask >> 4;
-    mask |= mask >> 8;
-    mask |= mask >> 16;
-    uint32_t v;
-    while ((v = (next() & mask)) > max) {
-    }
-    return v;
+  uint32_t next() {
+    if (pos >= 624) gen();
+    return temper(key[pos++]);
   }
 };
 }  // namespace
@@ -584,31 +654,43 @@ int m3d_replay_triples(uint32_t* mt_key, int32_t* mt_pos, int64_t nc, int64_t H,
                        int32_t* triples_out) {
   if (!mt_key || !mt_pos || (H > 0 && !triples_out)) return M3D_ERR_INVALID;
   if (nc < 3 || nc > 0xffffffffll) return M3D_ERR_INVALID;
+  if (*mt_pos < 0 || *mt_pos > 624) return M3D_ERR_INVALID;
   MT mt;
   memcpy(mt.key, mt_key, sizeof(mt.key));
   mt.pos = *mt_pos;
   // legacy RandomState.choice(nc, 3, replace=False) == permutation(nc)[:3]; permutation shuffles
-  // arange(nc) with i = nc-1 .. 1, j = random_interval(i), swap(x[i], x[j]).  Only positions 0..2
-  // are needed; version stamps avoid re-initialising the O(nc) array per hypothesis.
-  std::vector<int64_t> val((size_t)nc);
-  std::vector<uint32_t> stamp((size_t)nc, 0u);
-  uint32_t cur = 0;
+  // arange(nc) with i = nc-1 .. 1, j_i = random_interval(i), swap(x[i], x[j_i]).  Only positions
+  // 0..2 are needed: the draws are stored (sequential writes), then each position is traced back
+  // through the swaps in reverse order (i = 1 .. nc-1: p == i → j_i, p == j_i → i), which lands
+  // on the initial index, i.e. the value.  Sequential passes, no O(nc) value array.
+  thread_local std::vector<uint32_t> jbuf;
+  if (jbuf.size() < (size_t)nc) jbuf.resize((size_t)nc);
+  uint32_t* j = jbuf.data();
   for (int64_t h = 0; h < H; ++h) {
-    ++cur;
-    if (cur == 0) {
-      std::fill(stamp.begin(), stamp.end(), 0u);
-      cur = 1;
+    // random_interval(i) for i = nc-1 .. 1, branch-free: every MT output is a candidate
+    // (y & mask(i), mask = 2^(⌊log2 i⌋+1) − 1) that is kept iff ≤ i — the rejection loop's
+    // outcome is unpredictable, a branch on it costs more than the generator
+    int64_t i = nc - 1;
+    while (i >= 1) {
+      if (mt.pos >= 624) mt.gen();
+      int k = mt.pos;
+      for (; k < 624 && i >= 1; ++k) {
+        const uint32_t v = MT::temper(mt.key[k]) & (0xFFFFFFFFu >> __builtin_clz((uint32_t)i));
+        j[i] = v;
+        i -= (int64_t)(v <= (uint32_t)i);
+      }
+      mt.pos = k;
     }
-    auto get = [&](int64_t k) { return stamp[k] == cur ? val[k] : k; };
-    for (int64_t i = nc - 1; i >= 1; --i) {
-      const int64_t j = (int64_t)mt.interval((uint32_t)i);
-      const int64_t vi = get(i), vj = get(j);
-      val[i] = vj;
-      stamp[i] = cur;
-      val[j] = vi;
-      stamp[j] = cur;
+    uint32_t p0 = 0, p1 = 1, p2 = 2;
+    for (int64_t i = 1; i < nc; ++i) {
+      const uint32_t ji = j[i], ii = (uint32_t)i;
+      p0 = p0 == ii ? ji : (p0 == ji ? ii : p0);
+      p1 = p1 == ii ? ji : (p1 == ji ? ii : p1);
+      p2 = p2 == ii ? ji : (p2 == ji ? ii : p2);
     }
-    for (int k = 0; k < 3; ++k) triples_out[3 * h + k] = (int32_t)get(k);
+    triples_out[3 * h + 0] = (int32_t)p0;
+    triples_out[3 * h + 1] = (int32_t)p1;
+    triples_out[3 * h + 2] = (int32_t)p2;
   }
   memcpy(mt_key, mt.key, sizeof(mt.key));
   *mt_pos = mt.pos;

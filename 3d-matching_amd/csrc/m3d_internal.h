@@ -128,6 +128,10 @@ struct m3d_ctx {
   hipEvent_t scratch_ev = nullptr;
   hipStream_t scratch_stream = nullptr;
   bool scratch_used = false;
+  // mapped pinned host memory for the one-hypothesis calls (m3d_kabsch3_one / _score_one):
+  // kernels write their few results straight into it (pin_dev), read after one stream sync
+  void* pin = nullptr;
+  void* pin_dev = nullptr;
 };
 
 struct m3d_corrset {
@@ -230,6 +234,12 @@ hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_
                           int64_t hyp0, int64_t H, double thr_sq, double* T_out, uint8_t* status,
                           HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st,
                           const ScoreFuse* fuse = nullptr);
+// one hypothesis, host operands by value (m3d_kabsch3_one / m3d_ransac_score_one)
+hipError_t launch_kabsch3_one(const m3d_corrset* cs, const int32_t* tri, double* T_out,
+                              int32_t* status, hipStream_t st);
+hipError_t launch_score_one_prep(const m3d_corrset* cs, const double* T, double thr, int mode,
+                                 double* T64, HypF32* hypf, int32_t* counts, const ScoreMf& mf,
+                                 hipStream_t st);
 hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
                               HypF32* hypf, ZeroArgs z, hipStream_t st);
 // MFMA scoring (score_mfma_kernel): per-batch hypothesis operands built from the fp64

@@ -994,6 +994,84 @@ hipError_t launch_score_prep(const m3d_corrset* cs, const double* T64, int64_t H
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------- one hypothesis
+// The per-call drop-in (compute_step_transformation / evaluate_inlier_ratio as
+// benchmark_ransac.py:105-113 calls them, one hypothesis per call): the triple and the transform
+// travel as kernel arguments and the transform comes back through mapped pinned memory, so a
+// call is one launch (a1) or two launches + one 4-B copy (a2/a3) and one stream sync, with no
+// staging copies.
+struct Tri3 {
+  int32_t i[3];
+};
+struct T16 {
+  double v[16];
+};
+
+__global__ void kabsch3_one_kernel(const double* __restrict__ p64, const double* __restrict__ q64,
+                                   int64_t nc, Tri3 tri, double* __restrict__ T_out,
+                                   int32_t* __restrict__ status) {
+  if (threadIdx.x != 0) return;
+  double T[16];
+  int st = M3D_HYP_OK;
+  if (nc < 3) {  // ransac.py:139-140
+    for (int k = 0; k < 16; ++k) T[k] = (k % 5 == 0) ? 1.0 : 0.0;
+    st = M3D_HYP_DEGENERATE;
+  } else {
+    double ps[3][3], qs[3][3];
+    for (int k = 0; k < 3; ++k) {
+      const int64_t r = (tri.i[k] < 0 || tri.i[k] >= nc) ? 0 : tri.i[k];
+      for (int c = 0; c < 3; ++c) {
+        ps[k][c] = p64[3 * r + c];
+        qs[k][c] = q64[3 * r + c];
+      }
+    }
+    st = kabsch3(ps, qs, T) ? M3D_HYP_NONFINITE : M3D_HYP_OK;
+  }
+  for (int k = 0; k < 16; ++k) T_out[k] = T[k];
+  *status = st;
+}
+
+// everything the score launch needs for one transform: the fp64 T (band rechecks), the fp32
+// screen block, the zeroed count and the MFMA operands (+ padding hypotheses) when it runs there
+__global__ __launch_bounds__(256) void score_one_prep_kernel(T16 T, GuardParams g,
+                                                             double* __restrict__ T64,
+                                                             HypF32* __restrict__ hypf,
+                                                             int32_t* __restrict__ counts,
+                                                             Hyp16Fuse hf) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j == 0) {
+    for (int k = 0; k < 16; ++k) T64[k] = T.v[k];
+    hypf[0] = make_hypf(T.v, g);
+    counts[0] = 0;
+  }
+  if (hf.on && j < hf.h_pad) hyp16_one(j == 0 ? T.v : nullptr, j == 0, j, hf.h_pad, hf.m, hf.hb16, hf.heps);
+}
+
+hipError_t launch_kabsch3_one(const m3d_corrset* cs, const int32_t* tri, double* T_out,
+                              int32_t* status, hipStream_t st) {
+  Tri3 t{{tri[0], tri[1], tri[2]}};
+  kabsch3_one_kernel<<<1, 64, 0, st>>>(cs->p64, cs->q64, cs->nc, t, T_out, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_one_prep(const m3d_corrset* cs, const double* T, double thr, int mode,
+                                 double* T64, HypF32* hypf, int32_t* counts, const ScoreMf& mf,
+                                 hipStream_t st) {
+  T16 t;
+  for (int k = 0; k < 16; ++k) t.v[k] = T[k];
+  Hyp16Fuse hf{};
+  hf.on = 0;
+  if (score_prep_params(cs, 1, thr, mode, mf, &hf.m, &hf.h_pad)) {
+    hf.hb16 = mf.hb16;
+    hf.heps = mf.heps;
+    hf.on = 1;
+  }
+  const int64_t n = hf.on ? hf.h_pad : 1;
+  score_one_prep_kernel<<<blocks_for(n, 256), 256, 0, st>>>(t, guard_of(cs, thr_sq_mode(thr, mode)),
+                                                            T64, hypf, counts, hf);
+  return hipGetLastError();
+}
+
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
                         const double* T64, double thr, int mode, int64_t* stats,
                         const int32_t* done, const ScoreMf& mf, hipStream_t st) {

@@ -28,7 +28,7 @@ COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2
 OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -84,6 +84,8 @@ SIGNATURES = {
     "m3d_corrset_size": (i64, [vp]),
     "m3d_kabsch3_batch": (C.c_int, [vp, vp, vp, u64, i64, i64, vp, vp, vp]),
     "m3d_ransac_score": (C.c_int, [vp, vp, vp, i64, dbl, C.c_int, vp, vp]),
+    "m3d_kabsch3_one": (C.c_int, [vp, vp, C.POINTER(i32), C.POINTER(dbl), C.POINTER(i32), vp]),
+    "m3d_ransac_score_one": (C.c_int, [vp, vp, C.POINTER(dbl), dbl, C.c_int, C.POINTER(i64), vp]),
     "m3d_ransac_run": (C.c_int, [vp, vp, C.POINTER(RansacParams), vp, C.POINTER(RansacResult), vp]),
     "m3d_ransac_run_async": (C.c_int, [vp, vp, C.POINTER(RansacParams), vp, vp, vp, vp]),
     "m3d_replay_triples": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(i32), i64, i64,

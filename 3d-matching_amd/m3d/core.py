@@ -167,6 +167,24 @@ class CorrSet:
                        "ransac_score")
         return counts
 
+    def kabsch3_one(self, triple):
+        """a1 for one row triple (host) → (T (4,4) ndarray, status): one launch, one sync
+        (m3d_kabsch3_one, the reference harness's per-call form)."""
+        tri = (C.c_int32 * 3)(*(int(v) for v in triple))
+        T = (C.c_double * 16)()
+        st = C.c_int32(0)
+        self.ctx.check(self.ctx.lib.m3d_kabsch3_one(self.ctx.h, self.h, tri, T, C.byref(st),
+                                                    stream_handle()), "kabsch3_one")
+        return np.array(T[:]).reshape(4, 4), int(st.value)
+
+    def score_one(self, T, thr: float, mode: int = _lib.SCORE_SQUARED) -> int:
+        """a2/a3 for one host transform → inlier count (m3d_ransac_score_one)."""
+        Tc = (C.c_double * 16)(*np.asarray(T, np.float64).reshape(16).tolist())
+        n = C.c_int64(0)
+        self.ctx.check(self.ctx.lib.m3d_ransac_score_one(self.ctx.h, self.h, Tc, float(thr), int(mode),
+                                                         C.byref(n), stream_handle()), "ransac_score_one")
+        return int(n.value)
+
     def run(self, params: "RansacParams", triples=None) -> "RansacOutcome":
         """a4 on the device: the step-RANSAC loop with best tracking and early stop."""
         p = params.to_c()
@@ -264,6 +282,53 @@ def replay_triples(nc: int, H: int, state=None):
     if use_global:
         np.random.set_state(new_state)
     return out, new_state
+
+
+_MT_STATE_KEY_BYTES = 624 * 4  # numpy mt19937_state: uint32 key[624]; int pos
+_choice3_fast = None
+
+
+def _mt_state_ptrs(bitgen):
+    addr = bitgen.ctypes.state_address
+    return (C.cast(addr, C.POINTER(C.c_uint32)),
+            C.cast(addr + _MT_STATE_KEY_BYTES, C.POINTER(C.c_int32)))
+
+
+def _choice3_selftest() -> bool:
+    """Whether numpy's MT19937 state can be advanced in place (layout check against numpy)."""
+    try:
+        lib = _lib.load()
+        a, b = np.random.RandomState(20240), np.random.RandomState(20240)
+        for n in (3, 50, 1025):
+            exp = a.choice(n, 3, replace=False)
+            key, pos = _mt_state_ptrs(b._bit_generator)
+            out = (C.c_int32 * 3)()
+            if lib.m3d_replay_triples(key, pos, n, 1, out) != 0 or list(out) != exp.tolist():
+                return False
+        sa, sb = a.get_state(), b.get_state()
+        return bool(np.array_equal(sa[1], sb[1]) and sa[2] == sb[2])
+    except Exception:
+        return False
+
+
+def choice3(nc: int) -> np.ndarray:
+    """``np.random.choice(nc, 3, replace=False)`` on the global legacy RNG (ransac.py:143): the
+    same three rows, and the RNG left in the same state.  numpy draws them through a full O(nc)
+    permutation; the library replays the same MT19937 draws branch-free and traces only the
+    first three positions (m3d_replay_triples), advancing numpy's state in place under its
+    lock.  Falls back to numpy's own call if the state layout check fails."""
+    global _choice3_fast
+    if _choice3_fast is None:
+        _choice3_fast = _choice3_selftest()
+    rs = np.random.mtrand._rand
+    bg = getattr(rs, "_bit_generator", None)
+    if not _choice3_fast or nc < 3 or type(bg).__name__ != "MT19937":
+        return np.random.choice(nc, 3, replace=False)
+    out = (C.c_int32 * 3)()
+    with bg.lock:
+        key, pos = _mt_state_ptrs(bg)
+        check(_lib.load().m3d_replay_triples(key, pos, int(nc), 1, out), None, "choice3")
+    return np.array(out[:], dtype=np.int64)
 
 
 # --------------------------------------------------------------------------------- ICP

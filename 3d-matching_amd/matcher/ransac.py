@@ -5,8 +5,10 @@ KTC-Security-Circle/3d-matching ``src/matcher/ransac.py``; the arithmetic runs i
 (HIP, gfx950) through the C ABI of ``include/m3d.h``.
 
 * ``compute_step_transformation`` (ransac.py:104-192): draws its 3 rows from the GLOBAL legacy
-  numpy RNG exactly like the reference (``np.random.choice(n, 3, replace=False)``), so a seeded
-  program sees the same hypotheses; the Kabsch estimate runs on the device.
+  numpy RNG exactly like the reference (``np.random.choice(n, 3, replace=False)``: the same rows
+  and the same RNG state afterwards, replayed natively by ``m3d.core.choice3``), so a seeded
+  program sees the same hypotheses; the Kabsch estimate runs on the device (one launch, one sync:
+  ``m3d_kabsch3_one``).
 * ``evaluate_inlier_ratio`` (ransac.py:195-236) and ``evaluate_inlier_ratio_fast``
   (ransac.py:239-277): exact counts (fp32 screen + fp64 guard-band recheck on the device).
 * ``compute_feature_correspondences`` (ransac.py:62-101): FPFH feature-space NN on the device
@@ -24,7 +26,7 @@ import numpy as np
 
 from m3d import _lib
 from m3d import cache as _cache
-from m3d.core import CorrSet, RansacParams, replay_triples
+from m3d.core import CorrSet, RansacParams, choice3, replay_triples
 from m3d.types import RegistrationResult
 
 __all__ = [
@@ -130,13 +132,13 @@ def compute_step_transformation(src, tgt, correspondences) -> RegistrationResult
     n_corres = len(corres_np)
     if n_corres < 3:
         return res
-    idxs = np.random.choice(n_corres, 3, replace=False)       # same RNG stream as the reference
+    idxs = choice3(n_corres)  # np.random.choice(n, 3, replace=False): same rows, same RNG state
     s_pts, t_pts = _down_points(src), _down_points(tgt)
     _check_gather(corres_np[idxs], len(s_pts), len(t_pts))     # only the sampled rows are read
     cs = _packed(s_pts, t_pts, np.asarray(corres_np, np.int32), need_all=False)
-    T, status = cs.kabsch3(1, triples=np.asarray(idxs, np.int32).reshape(1, 3))
-    if int(status[0].item()) == _lib.HYP_OK:
-        res.transformation = T[0].cpu().numpy()
+    T, status = cs.kabsch3_one(idxs)
+    if status == _lib.HYP_OK:
+        res.transformation = T
     return res
 
 
@@ -148,8 +150,8 @@ def evaluate_inlier_ratio(src, tgt, correspondences, transform, voxel_size) -> f
         return 0.0
     s_pts, t_pts = _down_points(src), _down_points(tgt)
     cs = _packed(s_pts, t_pts, np.asarray(corres, np.int32), need_all=True)
-    cnt = cs.score(np.asarray(transform, np.float64).reshape(1, 4, 4), dist_thresh, _lib.SCORE_NORM)
-    return np.int64(cnt[0].item()) / len(corres)
+    cnt = cs.score_one(transform, dist_thresh, _lib.SCORE_NORM)
+    return np.int64(cnt) / len(corres)
 
 
 def evaluate_inlier_ratio_fast(p_src, p_tgt, transform, dist_thresh_sq) -> float:
@@ -158,9 +160,8 @@ def evaluate_inlier_ratio_fast(p_src, p_tgt, transform, dist_thresh_sq) -> float
     if len(p_src) == 0:
         return 0.0
     cs = _cache.corrset_gathered(p_src, np.asarray(p_tgt, np.float64).reshape(-1, 3))
-    cnt = cs.score(np.asarray(transform, np.float64).reshape(1, 4, 4), dist_thresh_sq,
-                   _lib.SCORE_SQUARED)
-    return np.int64(cnt[0].item()) / len(p_src)
+    cnt = cs.score_one(transform, dist_thresh_sq, _lib.SCORE_SQUARED)
+    return np.int64(cnt) / len(p_src)
 
 
 _REPLAY_CHUNK = 4096  # rows per MT checkpoint of the replay sampler

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 5
+#define M3D_ABI_VERSION 6
 
 /* return codes */
 #define M3D_OK 0
@@ -113,6 +113,21 @@ int m3d_kabsch3_batch(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triple
  * of the reference formula (fp32 screen + fp64 recheck of pairs inside a proven guard band). */
 int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64_t H, double thr,
                      int mode, int32_t* counts, void* stream);
+
+/* a1 and a2/a3 for ONE hypothesis with host operands — the per-call form the reference harness
+ * uses (benchmark_ransac.py:105-113: one compute_step_transformation + one
+ * evaluate_inlier_ratio per iteration).  Synchronous; the operands travel as kernel arguments
+ * and the results come back through the context's mapped pinned memory (one launch + one
+ * stream sync for a1; two launches, a 4-B copy and one sync for a2/a3).
+ * m3d_kabsch3_one: triple [host] 3 int32 rows; T_out [host] 16 f64; status [host] (may be
+ * NULL) M3D_HYP_*.  Replaces compute_step_transformation (ransac.py:104-192) after its
+ * np.random.choice draw (ransac.py:143).
+ * m3d_ransac_score_one: T [host] 16 f64; *count [host] = inliers (thr / mode as in
+ * m3d_ransac_score).  Replaces evaluate_inlier_ratio[_fast] (ransac.py:195-277). */
+int m3d_kabsch3_one(m3d_ctx* ctx, const m3d_corrset* cs, const int32_t* triple, double* T_out,
+                    int32_t* status, void* stream);
+int m3d_ransac_score_one(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, double thr,
+                         int mode, int64_t* count, void* stream);
 
 /* a4: the step-RANSAC loop (_visualize_matcher.py:343-470; benchmark_ransac.py:87-125 when
  * early_stop == 0), run on the device in batches with no host round trip per batch. */

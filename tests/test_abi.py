@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, f"{s} missing from the ctypes signature table"
-    assert lib.m3d_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.m3d_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_no_device_here_is_reported_not_crashed():
@@ -63,6 +63,26 @@ def test_replay_triples_advance_global_rng():
     exp = np.array([np.random.choice(5000, 3, replace=False) for _ in range(10)])
     np.testing.assert_array_equal(tri, exp)
     assert np.random.rand() == after
+
+
+@pytest.mark.parametrize("nc", [3, 4, 7, 1024, 1025, 5000, 100000])
+def test_choice3_is_numpy_choice_on_the_global_rng(nc):
+    """matcher.ransac.compute_step_transformation draws through m3d.core.choice3: the rows of
+    np.random.choice(nc, 3, replace=False) (ransac.py:143) and the identical global RNG state."""
+    from m3d import core
+
+    np.random.seed(nc)
+    exp = [np.random.choice(nc, 3, replace=False) for _ in range(5)]
+    st_exp = np.random.get_state()
+    np.random.seed(nc)
+    got = [core.choice3(nc) for _ in range(5)]
+    st = np.random.get_state()
+    assert core._choice3_fast, "numpy MT19937 state layout check failed: fast path disabled"
+    for a, b in zip(exp, got):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(st_exp[1], st[1])
+    assert st_exp[2] == st[2]
+    assert np.random.rand() == (np.random.set_state(st_exp) or np.random.rand())
 
 
 def host_kabsch(a, b):

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import ransac_oracle as O
-from m3d import _lib
+from m3d import _lib, synth
 from m3d.core import CorrSet, RansacParams
 
 pytestmark = pytest.mark.gpu
@@ -435,3 +435,25 @@ print(json.dumps(out))
     pp, qq = src[corr[:, 0]], tgt[corr[:, 1]]
     np.testing.assert_array_equal(np.array(res["1"][str(_lib.SCORE_NORM)])[pick],
                                   O.inlier_counts(pp, qq, T.cpu().numpy()[pick], 0.45, 1))
+
+
+@pytest.mark.parametrize("nc", [3, 5, 2049, 100_000])
+def test_one_hypothesis_calls_equal_batched(nc):
+    """m3d_kabsch3_one / m3d_ransac_score_one (the per-call drop-in path: operands as kernel
+    arguments, results through mapped pinned memory) give the batched kernels' bits."""
+    src, tgt, corr, _ = synth.ransac_pair(nc, seed=11, noise_ratio=1.0)
+    cs = CorrSet(src, tgt, corr)
+    rng = np.random.RandomState(nc)
+    n = len(corr)
+    tri = np.array([rng.choice(n, 3, replace=False) for _ in range(16)], np.int32)
+    T, st = cs.kabsch3(len(tri), triples=tri)
+    T, st = T.cpu().numpy(), st.cpu().numpy()
+    for h in range(len(tri)):
+        T1, s1 = cs.kabsch3_one(tri[h])
+        assert s1 == st[h]
+        np.testing.assert_array_equal(T1, T[h])
+    Ts = np.concatenate([T, np.eye(4)[None], synth.random_rigid(3, rot_range=3.0, trans_range=50.0)[None]])
+    for thr, mode in ((0.45, _lib.SCORE_NORM), (0.2025, _lib.SCORE_SQUARED), (1e4, _lib.SCORE_NORM)):
+        ref = cs.score(Ts, thr, mode).cpu().numpy()
+        got = [cs.score_one(Ts[h], thr, mode) for h in range(len(Ts))]
+        np.testing.assert_array_equal(got, ref)
