@@ -75,7 +75,9 @@ def parse():
     ap.add_argument("--no-cfg3", action="store_true")
     ap.add_argument("--nc", type=int, default=100_000)
     ap.add_argument("--hyps", type=int, default=100_000, help="RANSAC hypotheses per GPU per run")
-    ap.add_argument("--ransac-steps", type=int, default=3)
+    ap.add_argument("--ransac-steps", type=int, default=20,
+                    help="timed RANSAC runs (~1.5 ms each): enough that the sync at either end "
+                         "of the timed region does not weigh on the per-run time")
     ap.add_argument("--no-ransac", action="store_true")
     ap.add_argument("--ransac-warmup-s", type=float, default=0.5,
                     help="untimed RANSAC runs for at least this long before the timed ones")
