@@ -765,6 +765,7 @@ void m3d_cloud_destroy(m3d_cloud* c) {
   hipFree(c->xyz64);
   hipFree(c->nrm64);
   hipFree(c->xyz32);
+  hipFree(c->rec64);
   delete c;
 }
 
@@ -858,6 +859,10 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
       hipError_t e = grid_morton(const_cast<Grid*>(sg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("morton order: ") + hipGetErrorString(e));
     }
+    if (!grc) {
+      hipError_t e = ensure_target_rec(tgt, nullptr);
+      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("target records: ") + hipGetErrorString(e));
+    }
     if (!grc && params->nn_method == M3D_NN_BRUTE && tg->mf16 == nullptr) {
       hipError_t e = build_mfma_tiles(tgt, const_cast<Grid*>(tg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("mfma tiles: ") + hipGetErrorString(e));
@@ -935,18 +940,31 @@ int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
   return M3D_OK;
 }
 
+namespace {
+// Whether an iteration's tail runs as ONE launch (terms + last-block reduce [+ solve]).  The
+// fused last block reduces every block partial alone, with 256 threads: past ~256 blocks the
+// separate 1024-thread reduce_kernel is faster (1M sources, grid loop: fused 60.7 µs against
+// terms 33.1 + reduce 8.8 + solve 6.5 µs, rocprof).  Where the fused tail hands the keys back
+// (brute force: the next scan then seeds itself, no keyinit launch) it stays fused.  Both forms
+// sum in the same fixed order: the same bits.
+bool fused_tail(const m3d_icp* s, bool keys_back) {
+  static const bool env = [] {
+    const char* e = getenv("M3D_ICP_FUSED");
+    return !(e && atoi(e) == 0);
+  }();
+  return env && (keys_back || s->nblocks <= 256);
+}
+}  // namespace
+
 int m3d_icp_step(m3d_icp* s, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;
   hipStream_t st = S(stream);
-  static const bool fused = [] {
-    const char* e = getenv("M3D_ICP_FUSED");
-    return !(e && atoi(e) == 0);
-  }();
+  // brute force: the fused tail hands the keys back as kKeyNone, the next NN seeds itself
+  const bool reset = s->params.nn_method != M3D_NN_GRID && s->src->n > 0;
+  const bool fused = fused_tail(s, reset);
   HIPX(ctx, enqueue_nn(s, 0, st, fused));
   if (fused) {
-    // brute force: the tail hands the keys back as kKeyNone, the next NN seeds itself
-    const bool reset = s->params.nn_method != M3D_NN_GRID && s->src->n > 0;
     KTimer kt(ctx, M3D_KERNEL_TERMS, st);
     HIPX(ctx, launch_icp_terms_solve(s, reset, st));
     s->keys_clean = reset;
@@ -997,13 +1015,9 @@ int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* dmin, const int3
   CHECK_ARG(ctx, claim != nullptr || off == 0, "a target shard (offset > 0) needs dmin and claim");
   hipStream_t st = S(stream);
   s->keys_clean = false;
-  static const bool fused = [] {
-    const char* e = getenv("M3D_ICP_FUSED");
-    return !(e && atoi(e) == 0);
-  }();
-  if (fused) {  // terms + fixed-order reduce in one launch (same bits as the two kernels)
-    // keys kept inside (source shard): hand them back as kKeyNone like m3d_icp_step
-    const bool reset = claim == nullptr && s->src->n > 0 && s->params.nn_method != M3D_NN_GRID;
+  // keys kept inside (source shard): the fused tail hands them back as kKeyNone like m3d_icp_step
+  const bool reset = claim == nullptr && s->src->n > 0 && s->params.nn_method != M3D_NN_GRID;
+  if (fused_tail(s, reset)) {  // terms + fixed-order reduce in one launch (same bits as the two kernels)
     KTimer kt(ctx, M3D_KERNEL_TERMS, st);
     HIPX(ctx, launch_icp_terms_reduce(s, off, claim, dmin, sums, reset, st));
     s->keys_clean = reset;

@@ -744,6 +744,7 @@ struct TermsArgs {
   int64_t ns;
   const double* tgt64;
   const double* nrm64;
+  const double* rec64;    // the target's 64-B records (point, normal), or null: tgt64 / nrm64
   int64_t nt_shard, off;
   const int64_t* keys;
   uint32_t* near2;
@@ -839,10 +840,21 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
   for (int u = 0; u < kP; ++u) {
     const bool own = valid[u] && gj[u] >= a.off && gj[u] < a.off + a.nt_shard;
     const int64_t l = own ? gj[u] - a.off : 0;
+    if (a.rec64 != nullptr) {
+      const double4 r0 = reinterpret_cast<const double4*>(a.rec64)[2 * l];
+      const double4 r1 = reinterpret_cast<const double4*>(a.rec64)[2 * l + 1];
+      tq[u][0] = r0.x;
+      tq[u][1] = r0.y;
+      tq[u][2] = r0.z;
+      tn[u][0] = r0.w;
+      tn[u][1] = r1.x;
+      tn[u][2] = r1.y;
+    } else {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      tq[u][k] = a.tgt64[3 * l + k];
-      tn[u][k] = a.est == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
+      for (int k = 0; k < 3; ++k) {
+        tq[u][k] = a.tgt64[3 * l + k];
+        tn[u][k] = a.est == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
+      }
     }
   }
 #pragma unroll
@@ -1370,6 +1382,36 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
 }
 
 
+__global__ __launch_bounds__(256) void pack_rec_kernel(const double* __restrict__ xyz,
+                                                       const double* __restrict__ nrm, int64_t n,
+                                                       double* __restrict__ rec) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double r[8];
+  for (int k = 0; k < 3; ++k) {
+    r[k] = xyz[3 * i + k];
+    r[3 + k] = nrm != nullptr ? nrm[3 * i + k] : 0.0;
+  }
+  r[6] = r[7] = 0.0;
+  for (int k = 0; k < 8; ++k) rec[8 * i + k] = r[k];
+}
+
+hipError_t ensure_target_rec(const m3d_cloud* c, hipStream_t st) {
+  if (c->rec64 != nullptr || c->n == 0) return hipSuccess;
+  double* rec = nullptr;
+  hipError_t e = hipMalloc(&rec, sizeof(double) * 8 * c->n);
+  if (e != hipSuccess) return e;
+  pack_rec_kernel<<<(unsigned)((c->n + 255) / 256), 256, 0, st>>>(c->xyz64, c->nrm64, c->n, rec);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    hipFree(rec);
+    return e;
+  }
+  c->rec64 = rec;
+  return hipSuccess;
+}
+
 static TermsArgs terms_args(const m3d_icp* s, int64_t off, const int32_t* claim,
                             const int64_t* dmin, bool reset_keys) {
   TermsArgs a;
@@ -1378,6 +1420,7 @@ static TermsArgs terms_args(const m3d_icp* s, int64_t off, const int32_t* claim,
   a.ns = s->src->n;
   a.tgt64 = s->tgt->xyz64;
   a.nrm64 = s->tgt->nrm64;
+  a.rec64 = s->tgt->rec64;
   a.nt_shard = s->tgt->n;
   a.off = off;
   a.keys = s->keys;

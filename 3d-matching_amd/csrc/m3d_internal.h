@@ -161,6 +161,10 @@ struct m3d_cloud {
   double s16 = 1.0;  // power-of-two scale of the fp16 MFMA screen operands (|s16·x|∞ ≤ 32)
   int center_given = 0;  // centre supplied by the caller (a frame shared by target shards)
   mutable std::vector<m3d::Grid*> grids;  // uniform grids built on demand, one per cell size
+  // target records for the ICP terms pass (icp.hip pack_rec): point + normal (zeros without
+  // normals) as 8 doubles per point, 64-B aligned, so the gather of a source's winner touches one
+  // 64-B segment instead of one in each of xyz64 and nrm64; built on first use as an ICP target
+  mutable double* rec64 = nullptr;
 };
 
 struct m3d_icp {
@@ -235,6 +239,7 @@ hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_
                           HypF32* hypf, const int32_t* done, ZeroArgs z, hipStream_t st,
                           const ScoreFuse* fuse = nullptr);
 // one hypothesis, host operands by value (m3d_kabsch3_one / m3d_ransac_score_one)
+hipError_t ensure_target_rec(const m3d_cloud* c, hipStream_t st);  // icp.hip: c->rec64
 hipError_t launch_kabsch3_one(const m3d_corrset* cs, const int32_t* tri, double* T_out,
                               int32_t* status, hipStream_t st);
 hipError_t launch_score_one_prep(const m3d_corrset* cs, const double* T, double thr, int mode,
