@@ -214,6 +214,7 @@ void m3d_destroy(m3d_ctx* ctx) {
   if (ctx->rstate) hipFree(ctx->rstate);
   if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
   if (ctx->pin) hipHostFree(ctx->pin);
+  if (ctx->one_ticket) hipFree(ctx->one_ticket);
   for (auto& v : ctx->ev)
     for (auto& pr : v) {
       hipEventDestroy(pr.first);
@@ -458,8 +459,15 @@ int pin_ensure(m3d_ctx* ctx) {
     hipHostFree(h);
     return m3d_fail(ctx, M3D_ERR_HIP, "hipHostGetDevicePointer failed");
   }
+  uint32_t* tk = nullptr;
+  if (hipMalloc(&tk, sizeof(uint32_t)) != hipSuccess || hipMemset(tk, 0, sizeof(uint32_t)) != hipSuccess) {
+    if (tk) hipFree(tk);
+    hipHostFree(h);
+    return m3d_fail(ctx, M3D_ERR_OOM, "ticket hipMalloc failed");
+  }
   ctx->pin = h;
   ctx->pin_dev = d;
+  ctx->one_ticket = tk;
   return M3D_OK;
 }
 extern "C++" {
@@ -505,24 +513,16 @@ int m3d_ransac_score_one(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, d
   hipError_t e;
   {
     Arena a(ctx, st);
-    size_t o[kScoreSlots];
-    score_layout(a, 1, o);
-    const size_t o_T = a.take(sizeof(double) * 16);
-    const size_t o_c = a.take(sizeof(int32_t));
+    const int64_t nb = count_one_blocks(cs->nc);
+    const size_t o_p = a.take(sizeof(int32_t) * nb);
     rc = a.commit();
     if (rc) return rc;
-    ScoreScratch s = score_bind(a, o);
-    double* T64 = a.at<double>(o_T);
-    int32_t* cnt = a.at<int32_t>(o_c);
-    e = launch_score_one_prep(cs, T, thr, mode, T64, s.hypf, cnt, s.mf, st);
-    if (e == hipSuccess) e = score_enqueue(ctx, cs, T64, 1, thr, mode, cnt, s, nullptr, st, true);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(pin_at<int32_t>(ctx, kPinCount, false), cnt, sizeof(int32_t),
-                         hipMemcpyDeviceToHost, st);
+    e = launch_count_one(cs, T, thr, mode, a.at<int32_t>(o_p), nb, ctx->one_ticket,
+                         pin_at<int64_t>(ctx, kPinCount, true), st);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
-  *count = *pin_at<int32_t>(ctx, kPinCount, false);
+  *count = *pin_at<int64_t>(ctx, kPinCount, false);
   return M3D_OK;
 }
 

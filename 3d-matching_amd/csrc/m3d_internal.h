@@ -132,6 +132,7 @@ struct m3d_ctx {
   // kernels write their few results straight into it (pin_dev), read after one stream sync
   void* pin = nullptr;
   void* pin_dev = nullptr;
+  uint32_t* one_ticket = nullptr;  // device: last-block ticket of count_one_kernel (kept at 0)
 };
 
 struct m3d_corrset {
@@ -242,9 +243,10 @@ hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_
 hipError_t ensure_target_rec(const m3d_cloud* c, hipStream_t st);  // icp.hip: c->rec64
 hipError_t launch_kabsch3_one(const m3d_corrset* cs, const int32_t* tri, double* T_out,
                               int32_t* status, hipStream_t st);
-hipError_t launch_score_one_prep(const m3d_corrset* cs, const double* T, double thr, int mode,
-                                 double* T64, HypF32* hypf, int32_t* counts, const ScoreMf& mf,
-                                 hipStream_t st);
+int64_t count_one_blocks(int64_t nc);
+hipError_t launch_count_one(const m3d_corrset* cs, const double* T, double thr, int mode,
+                            int32_t* partials, int64_t max_blocks, uint32_t* ticket, int64_t* out,
+                            hipStream_t st);
 hipError_t launch_hypf_from_T(const m3d_corrset* cs, const double* T, int64_t H, double thr_sq,
                               HypF32* hypf, ZeroArgs z, hipStream_t st);
 // MFMA scoring (score_mfma_kernel): per-batch hypothesis operands built from the fp64

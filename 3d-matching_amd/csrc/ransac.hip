@@ -1031,22 +1031,6 @@ __global__ void kabsch3_one_kernel(const double* __restrict__ p64, const double*
   *status = st;
 }
 
-// everything the score launch needs for one transform: the fp64 T (band rechecks), the fp32
-// screen block, the zeroed count and the MFMA operands (+ padding hypotheses) when it runs there
-__global__ __launch_bounds__(256) void score_one_prep_kernel(T16 T, GuardParams g,
-                                                             double* __restrict__ T64,
-                                                             HypF32* __restrict__ hypf,
-                                                             int32_t* __restrict__ counts,
-                                                             Hyp16Fuse hf) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j == 0) {
-    for (int k = 0; k < 16; ++k) T64[k] = T.v[k];
-    hypf[0] = make_hypf(T.v, g);
-    counts[0] = 0;
-  }
-  if (hf.on && j < hf.h_pad) hyp16_one(j == 0 ? T.v : nullptr, j == 0, j, hf.h_pad, hf.m, hf.hb16, hf.heps);
-}
-
 hipError_t launch_kabsch3_one(const m3d_corrset* cs, const int32_t* tri, double* T_out,
                               int32_t* status, hipStream_t st) {
   Tri3 t{{tri[0], tri[1], tri[2]}};
@@ -1054,22 +1038,68 @@ hipError_t launch_kabsch3_one(const m3d_corrset* cs, const int32_t* tri, double*
   return hipGetLastError();
 }
 
-hipError_t launch_score_one_prep(const m3d_corrset* cs, const double* T, double thr, int mode,
-                                 double* T64, HypF32* hypf, int32_t* counts, const ScoreMf& mf,
-                                 hipStream_t st) {
+// One transform against every correspondence: the reference formula itself in fp64 (numpy's
+// operation order, exact_inlier) — for a single hypothesis that is ~30 fp64 flop per pair, less
+// than the MFMA screen's 1024-hypothesis padding costs.  Block counts go out write-through, the
+// last block (ticket) adds them in block order and stores the total straight into the caller's
+// mapped pinned memory: one launch, no memset, no copy.
+constexpr int kOneBlock = 256, kOnePerThread = 4;
+__global__ __launch_bounds__(kOneBlock) void count_one_kernel(T16 T, const double* __restrict__ p64,
+                                                              const double* __restrict__ q64,
+                                                              int64_t nc, double thr, int mode,
+                                                              int32_t* partials, uint32_t* ticket,
+                                                              int64_t* out) {
+  __shared__ int32_t wsum[kOneBlock / 64];
+  __shared__ int last;
+  int32_t n = 0;
+#pragma unroll
+  for (int u = 0; u < kOnePerThread; ++u) {
+    const int64_t i = ((int64_t)blockIdx.x * kOnePerThread + u) * kOneBlock + threadIdx.x;
+    if (i < nc) n += exact_inlier(T.v, p64 + 3 * i, q64 + 3 * i, thr, mode) ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int32_t b = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __hip_atomic_store(&partials[blockIdx.x], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  int64_t t = 0;
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kOneBlock)
+    t += __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  __shared__ int64_t tw[kOneBlock / 64];
+  if ((threadIdx.x & 63) == 0) tw[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *out = tw[0] + tw[1] + tw[2] + tw[3];
+    *ticket = 0u;
+  }
+}
+
+hipError_t launch_count_one(const m3d_corrset* cs, const double* T, double thr, int mode,
+                            int32_t* partials, int64_t max_blocks, uint32_t* ticket, int64_t* out,
+                            hipStream_t st) {
   T16 t;
   for (int k = 0; k < 16; ++k) t.v[k] = T[k];
-  Hyp16Fuse hf{};
-  hf.on = 0;
-  if (score_prep_params(cs, 1, thr, mode, mf, &hf.m, &hf.h_pad)) {
-    hf.hb16 = mf.hb16;
-    hf.heps = mf.heps;
-    hf.on = 1;
-  }
-  const int64_t n = hf.on ? hf.h_pad : 1;
-  score_one_prep_kernel<<<blocks_for(n, 256), 256, 0, st>>>(t, guard_of(cs, thr_sq_mode(thr, mode)),
-                                                            T64, hypf, counts, hf);
+  const int64_t per = (int64_t)kOneBlock * kOnePerThread;
+  const int64_t nb = (cs->nc + per - 1) / per;
+  if (nb < 1 || nb > max_blocks) return hipErrorInvalidValue;
+  count_one_kernel<<<(unsigned)nb, kOneBlock, 0, st>>>(t, cs->p64, cs->q64, cs->nc, thr, mode, partials,
+                                                        ticket, out);
   return hipGetLastError();
+}
+
+int64_t count_one_blocks(int64_t nc) {
+  const int64_t per = (int64_t)kOneBlock * kOnePerThread;
+  return std::max<int64_t>(1, (nc + per - 1) / per);
 }
 
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,

@@ -118,7 +118,7 @@ int m3d_ransac_score(m3d_ctx* ctx, const m3d_corrset* cs, const double* T, int64
  * uses (benchmark_ransac.py:105-113: one compute_step_transformation + one
  * evaluate_inlier_ratio per iteration).  Synchronous; the operands travel as kernel arguments
  * and the results come back through the context's mapped pinned memory (one launch + one
- * stream sync for a1; two launches, a 4-B copy and one sync for a2/a3).
+ * stream sync each; a2/a3 evaluates the reference formula directly in fp64, numpy's order).
  * m3d_kabsch3_one: triple [host] 3 int32 rows; T_out [host] 16 f64; status [host] (may be
  * NULL) M3D_HYP_*.  Replaces compute_step_transformation (ransac.py:104-192) after its
  * np.random.choice draw (ransac.py:143).
