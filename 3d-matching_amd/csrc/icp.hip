@@ -60,14 +60,15 @@ struct FrameParams {
   int shared;  // the target's frame is shared by every shard (m3d_cloud_create_framed)
 };
 
-// Refresh the fp32 search transform and radius bound for the current T (device side).
-__device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
+// Refresh the fp32 search transform and radius bound for transform T (device side; T and
+// r2 = s->r2 passed in registers by the solve, which has them already).
+__device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const FrameParams& f) {
   const double* cs = f.cs;
   const double* ct = f.ct;
   const double pinf = f.pinf, qinf = f.qinf;
   double rowl1 = 0.0, tinf = 0.0;
   for (int i = 0; i < 3; ++i) {
-    const double* r = s->T + 4 * i;
+    const double* r = T + 4 * i;
     const double tp = fma(r[2], cs[2], fma(r[1], cs[1], r[0] * cs[0])) + r[3] - ct[i];
     for (int j = 0; j < 3; ++j) s->Rt32[3 * i + j] = (float)r[j];
     s->Rt32[9 + i] = (float)tp;
@@ -80,7 +81,7 @@ __device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
   // absolute coordinates (≤ 4 roundings of 2⁻⁵³ of the magnitudes involved)
   double tabs = 0.0, csinf = 0.0, ctinf = 0.0;
   for (int i = 0; i < 3; ++i) {
-    tabs = fmax(tabs, fabs(s->T[4 * i + 3]));
+    tabs = fmax(tabs, fabs(T[4 * i + 3]));
     csinf = fmax(csinf, fabs(cs[i]));
     ctinf = fmax(ctinf, fabs(ct[i]));
   }
@@ -91,16 +92,17 @@ __device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
   const float eqf = __double2float_ru(eq), bef = __double2float_ru(2.0 * eq * 1.01);
   s->eq = isfinite(eqf) ? eqf : FLT_MAX;
   s->band_e = isfinite(bef) ? bef : FLT_MAX;
-  const double r = sqrt(s->r2);
+  const double r = sqrt(r2);
   const double e = 2.0 * (3.0 * kU * (r + 1.7320508075688772 * E) * (r + 1.7320508075688772 * E) +
                           2.0 * 1.7320508075688772 * E * r + 3.0 * E * E);
-  float hi = __double2float_ru(s->r2 + e);
-  s->r2_hi = isfinite(hi) ? hi : FLT_MAX;
+  float hi = __double2float_ru(r2 + e);
+  if (!isfinite(hi)) hi = FLT_MAX;
+  s->r2_hi = hi;
   // Screen bound: |fl(|t|² − 2q·t) − (d² − |q|²)| + rounding of thr ≤ eps,
   // with |t|∞ ≤ qinf (target), |q|∞ ≤ Q = rowl1·pinf + |t'|∞ (query after the transform).
   const double Q = rowl1 * pinf + tinf;
   const double E1 = 5.0 * kU * (3.0 * qinf * qinf + 6.0 * Q * qinf);
-  const double es = 2.0 * (E1 + 6.0 * kU * (double)s->r2_hi + 12.0 * kU * Q * Q) + 1e-30;
+  const double es = 2.0 * (E1 + 6.0 * kU * (double)hi + 12.0 * kU * Q * Q) + 1e-30;
   const float esf = __double2float_ru(es);
   s->screen_eps = isfinite(esf) ? esf : FLT_MAX;
   // MFMA screen (nn_mfma_kernel): the same key from fp16 hi/lo operands scaled
@@ -118,13 +120,19 @@ __device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
   const double Esplit = 3.0 * u16 * u16 * P + 4.0 * sig * 3.0 * (As + Ts) + u16 * u16 * Ws + 2.0 * sig;
   const double Eacc = 32.0 * kU * 1.01 * (P + Ws);
   const double E1m = 1.05 * (Esplit + Eacc) / (S * S) + kU * 3.0 * qinf * qinf;
-  const double esm = 2.0 * (E1m + 6.0 * kU * (double)s->r2_hi + 12.0 * kU * Q * Q) + 1e-30;
+  const double esm = 2.0 * (E1m + 6.0 * kU * (double)hi + 12.0 * kU * Q * Q) + 1e-30;
   const float esmf = __double2float_ru(esm);
   s->screen_eps_m = isfinite(esmf) ? esmf : FLT_MAX;
   s->mfma_scale = (float)S;
   // operands must stay well inside the fp16 range (max 65504) and the bound finite
   s->mfma_ok = (As < 16384.0 && Ts < 16384.0 && Ws < 16384.0 && isfinite(esmf) &&
-                s->r2_hi < FLT_MAX && esmf < 0.25f * FLT_MAX) ? 1 : 0;
+                hi < FLT_MAX && esmf < 0.25f * FLT_MAX) ? 1 : 0;
+}
+
+__device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
+  double T[16];
+  for (int k = 0; k < 16; ++k) T[k] = s->T[k];
+  refresh_rt32_from(s, T, s->r2, f);
 }
 
 __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, double T3, double T4,
@@ -1024,16 +1032,29 @@ __device__ __forceinline__ void vec6_to_matrix_wave(const double x[6], double T[
 
 // One evaluation + update from the reduced sums.  Run by one whole wave: every lane computes
 // the same values (so its stores to *s agree) except the three sincos of vec6_to_matrix_wave.
+// Everything the solve reads is loaded up front: interleaved with its stores, each later load
+// of *s or sums (which the compiler must assume may alias) waited for the stores before it.
 __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp) {
-  const double count = sums[28];
+  double sm[30];
+#pragma unroll
+  for (int k = 0; k < 30; ++k) sm[k] = sums[k];
+  const int32_t evals = s->evals, iters = s->iters;
+  const double prev_fit = s->prev_fitness, prev_rmse = s->prev_rmse, r2 = s->r2;
+  const float eq = s->eq;
+  double T[16];
+  float rt[12];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) T[k] = s->T[k];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) rt[k] = s->Rt32[k];
+  const double count = sm[28];
   const double fit = count > 0.0 ? count / (double)sp.ns : 0.0;
-  const double rmse = count > 0.0 ? sqrt(sums[29] / count) : 0.0;
+  const double rmse = count > 0.0 ? sqrt(sm[29] / count) : 0.0;
   bool stop = false;
-  if (s->evals > 0 && fabs(s->prev_fitness - fit) < sp.rel_fit &&
-      fabs(s->prev_rmse - rmse) < sp.rel_rmse) {
+  if (evals > 0 && fabs(prev_fit - fit) < sp.rel_fit && fabs(prev_rmse - rmse) < sp.rel_rmse) {
     s->converged = 1;
     stop = true;
-  } else if (s->iters >= sp.max_iter) {
+  } else if (iters >= sp.max_iter) {
     stop = true;
   }
   s->fitness = fit;
@@ -1041,7 +1062,7 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   s->count = (int64_t)count;
   s->prev_fitness = fit;
   s->prev_rmse = rmse;
-  s->evals += 1;
+  s->evals = evals + 1;
   if (stop) {
     s->done = 1;
     return;
@@ -1049,8 +1070,9 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   double upd[16];
   for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
   // the search transform of the evaluation just reduced: seed_key's bound for the next one
-  for (int k = 0; k < 12; ++k) s->Rt32_prev[k] = s->Rt32[k];
-  s->eq_prev = s->eq;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) s->Rt32_prev[k] = rt[k];
+  s->eq_prev = eq;
   s->bound_ok = sp.f.shared;  // bounds compare keys across ranks: only in a shared frame
   if (count > 0.0) {
     if (sp.est == M3D_EST_POINT_TO_PLANE) {
@@ -1058,22 +1080,22 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
       int k = 0;
       for (int a = 0; a < 6; ++a)
         for (int c = a; c < 6; ++c) {
-          A[a * 6 + c] = sums[k];
-          A[c * 6 + a] = sums[k];
+          A[a * 6 + c] = sm[k];
+          A[c * 6 + a] = sm[k];
           ++k;
         }
-      for (int a = 0; a < 6; ++a) b[a] = -sums[21 + a];
+      for (int a = 0; a < 6; ++a) b[a] = -sm[21 + a];
       ldlt6_solve(A, b, x);
       vec6_to_matrix_wave(x, upd);
     } else {
       const double n = count;
       double mp[3], mq[3], Hm[9], R[9];
       for (int a = 0; a < 3; ++a) {
-        mp[a] = sums[a] / n;
-        mq[a] = sums[3 + a] / n;
+        mp[a] = sm[a] / n;
+        mq[a] = sm[3 + a] / n;
       }
       for (int a = 0; a < 3; ++a)
-        for (int c = 0; c < 3; ++c) Hm[3 * a + c] = sums[6 + 3 * a + c] / n - mp[a] * mq[c];
+        for (int c = 0; c < 3; ++c) Hm[3 * a + c] = sm[6 + 3 * a + c] / n - mp[a] * mq[c];
       rotation_from_cov(Hm, R);
       for (int a = 0; a < 3; ++a) {
         const double mpw[3] = {mp[0] + sp.c[0], mp[1] + sp.c[1], mp[2] + sp.c[2]};
@@ -1086,9 +1108,11 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   for (int k = 0; k < 16; ++k) finite = finite && isfinite(upd[k]);
   if (!finite)
     for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
-  matmul4(upd, s->T, s->T);
-  s->iters += 1;
-  refresh_rt32(s, sp.f);
+  matmul4(upd, T, T);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s->T[k] = T[k];
+  s->iters = iters + 1;
+  refresh_rt32_from(s, T, r2, sp.f);
 }
 
 __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
