@@ -1154,7 +1154,8 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
 #pragma unroll
   for (int u = 0; u < kG; ++u) gv[u] = 0.0;
   const int g0 = threadIdx.x / kTermSlots;
-  constexpr int kR = 4;  // rounds of kReduceGroups blocks in flight per batch (kR·kG loads)
+  constexpr int kR = 8;  // rounds of kReduceGroups blocks in flight per batch (kR·kG loads):
+                         // 256 blocks (cfg1: 196) in ONE batch of dependent loads
   for (int64_t b0 = 0; b0 < nblocks; b0 += kR * kReduceGroups) {
     double t[kR][kG];
 #pragma unroll
