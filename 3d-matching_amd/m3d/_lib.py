@@ -28,7 +28,7 @@ COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2
 OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -126,6 +126,10 @@ SIGNATURES = {
     "m3d_icp_source_shard_steps": (C.c_int, [vp, vp, i32, vp]),
     "m3d_ransac_best_allreduce": (C.c_int, [vp, vp, i64, vp, vp]),
     "m3d_ransac_run_sharded": (C.c_int, [vp, vp, vp, C.POINTER(RansacParams), C.POINTER(RansacResult), vp]),
+    "m3d_parse_ascii_rows": (C.c_int, [C.c_char_p, C.c_size_t, i64, i32, C.POINTER(dbl),
+                                       C.POINTER(C.c_size_t)]),
+    "m3d_format_ascii_rows": (C.c_int, [C.POINTER(dbl), i64, i32, vp, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "m3d_merge_vertices": (C.c_int, [C.POINTER(dbl), i64, C.POINTER(dbl), C.POINTER(i32), C.POINTER(i64)]),
     "m3d_debug_kabsch3_host":(C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
     "m3d_debug_ldlt6_host": (C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }

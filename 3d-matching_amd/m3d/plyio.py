@@ -18,6 +18,7 @@ milliseconds.
 
 from __future__ import annotations
 
+import ctypes as C
 import re
 from pathlib import Path
 
@@ -124,7 +125,27 @@ def read_ply(path):
     raise PlyError("PLY file has no vertex element")
 
 
+def _text_lib():
+    from . import _lib
+
+    return _lib.load()
+
+
 def _read_ascii_vertices(f, count, props):
+    if any(isinstance(t, tuple) for _, t in props):
+        raise PlyError("list properties in the vertex element are not supported")
+    # fast path: the library's from_chars parser over the rest of the file (csrc/hostio.cpp),
+    # the same correctly rounded doubles as numpy's; anything unusual falls back to numpy
+    pos = f.tell()
+    rest = f.read()
+    out = np.empty((count, len(props)), np.float64)
+    used = C.c_size_t(0)
+    rc = _text_lib().m3d_parse_ascii_rows(rest, len(rest), count, len(props),
+                                          out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(used))
+    if rc == 0:
+        f.seek(pos + used.value)
+        return {p: out[:, k] for k, (p, _) in enumerate(props)}
+    f.seek(pos)
     rows = []
     while len(rows) < count:
         line = f.readline()
@@ -156,9 +177,18 @@ def write_ply(path, points, normals=None, binary: bool = False, dtype="double"):
         f.write(("\n".join(head) + "\n").encode("ascii"))
         if binary:
             f.write(np.ascontiguousarray(data.astype("<" + np_t)).tobytes())
+        elif dtype == "double":  # shortest round-trip text per number (csrc/hostio.cpp)
+            data = np.ascontiguousarray(data)
+            cap = 32 * data.size + 1
+            buf = np.empty(cap, np.uint8)
+            n = C.c_size_t(0)
+            rc = _text_lib().m3d_format_ascii_rows(data.ctypes.data_as(C.POINTER(C.c_double)), len(data),
+                                                   data.shape[1], buf.ctypes.data, cap, C.byref(n))
+            if rc != 0:
+                raise PlyError("ASCII formatting failed")
+            f.write(memoryview(buf[:n.value]))
         else:
-            fmt = "%.17g" if dtype == "double" else "%.9g"
-            np.savetxt(f, data.astype(np_t), fmt=fmt)
+            np.savetxt(f, data.astype(np_t), fmt="%.9g")
 
 
 _STL_VERTEX = re.compile(rb"vertex\s+(\S+)\s+(\S+)\s+(\S+)")
@@ -181,9 +211,22 @@ def read_stl(path):
         if len(v) % 3:
             raise ValueError(f"{path}: ASCII STL vertex count is not a multiple of 3")
         tri = v.reshape(-1, 3, 3)
-    flat = np.ascontiguousarray(tri.reshape(-1, 3))
-    # exact-equality merge on the raw bytes of each (x, y, z) (one 1-D sort of 24-byte keys);
-    # +0.0 and -0.0 differ in bytes, so canonicalise them first
+    flat = np.ascontiguousarray(tri.reshape(-1, 3), dtype=np.float64)
+    # exact-equality merge in first-occurrence order: one hash pass in the library
+    # (csrc/hostio.cpp m3d_merge_vertices); the numpy sort below is the same merge
+    uniq = np.empty_like(flat)
+    inv = np.empty(len(flat), np.int32)
+    m = C.c_int64(0)
+    P = C.POINTER(C.c_double)
+    if _text_lib().m3d_merge_vertices(flat.ctypes.data_as(P), len(flat), uniq.ctypes.data_as(P),
+                                      inv.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(m)) == 0:
+        return uniq[: m.value].copy(), inv.astype(np.int64).reshape(-1, 3)
+    return _merge_numpy(flat)
+
+
+def _merge_numpy(flat):
+    """Exact-equality merge on the raw bytes of each (x, y, z) (one 1-D sort of 24-byte keys);
+    +0.0 and -0.0 differ in bytes, so they are canonicalised first."""
     flat = flat + 0.0
     key = flat.view(np.dtype((np.void, 24))).ravel()
     _, first, inverse = np.unique(key, return_index=True, return_inverse=True)

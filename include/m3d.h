@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 6
+#define M3D_ABI_VERSION 7
 
 /* return codes */
 #define M3D_OK 0
@@ -374,6 +374,26 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
  * of the math.  Never used by the product path. */
 int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16);
 int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6);
+
+/* ------------------------------------------------------------------ host text I/O (§8(f) rank 4) */
+
+/* ASCII number blocks of PLY files (m3d.plyio; replaces the C++ readers/writers the reference
+ * calls: o3d.io.read_point_cloud, src/ply/ply.py:80, and trimesh's ASCII PLY export,
+ * convert_stl-ply.py:1-11).  Host only, no device needed.
+ * m3d_parse_ascii_rows: `rows` non-blank lines of exactly `cols` numbers from buf[0, len) →
+ * out [host] rows×cols f64 (correctly rounded, as numpy's parser); *consumed = bytes used.
+ * M3D_ERR_INVALID on anything else (short file, extra or non-numeric tokens).
+ * m3d_format_ascii_rows: rows×cols f64 → text, one row per line, each number the shortest
+ * representation that reads back to the same double; cap ≥ 32·rows·cols. */
+int m3d_parse_ascii_rows(const char* buf, size_t len, int64_t rows, int32_t cols, double* out,
+                         size_t* consumed);
+int m3d_format_ascii_rows(const double* data, int64_t rows, int32_t cols, char* out, size_t cap,
+                          size_t* written);
+/* STL corner merge (convert_stl-ply.py:3-6, trimesh.load_mesh): xyz [host] n×3 f64 corners →
+ * uniq [host] (≤ n)×3 f64 unique vertices in first-occurrence order (exact equality, -0.0 ≡ +0.0),
+ * inverse [host] n int32 (corner → vertex id), *n_unique. */
+int m3d_merge_vertices(const double* xyz, int64_t n, double* uniq, int32_t* inverse,
+                       int64_t* n_unique);
 
 #ifdef __cplusplus
 }

@@ -141,3 +141,74 @@ def test_stl_writer_round_trip_on_generated_mesh(tmp_path, binary):
     np.testing.assert_array_equal(ff, f)
     assert plyio.convert_stl_to_ply(tmp_path / "m.stl", tmp_path / "m.ply") == len(v)
     np.testing.assert_array_equal(plyio.read_ply(tmp_path / "m.ply")[0], vv)
+
+
+def test_native_ascii_parser_equals_numpy():
+    """csrc/hostio.cpp (m3d_parse_ascii_rows): the doubles numpy's own parser returns, on
+    extreme magnitudes, integers, signed zeros, tabs, CRLF, blank lines and trailing spaces."""
+    import ctypes as C
+
+    from m3d import _lib
+
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    vals = np.concatenate([rng.normal(size=600) * 10.0 ** rng.integers(-300, 300, 600),
+                           [0.0, -0.0, 1.0, -7.0, 5e-324, 1.7976931348623157e308, 0.1, 1 / 3]])
+    vals = vals[: len(vals) // 3 * 3].reshape(-1, 3)
+    lines = []
+    for k, row in enumerate(vals):
+        sep = "\t" if k % 5 == 0 else " "
+        txt = sep.join(repr(float(v)) if k % 2 else f"{v:.17g}" for v in row)
+        lines.append(txt + ("  " if k % 7 == 0 else "") + ("\r\n" if k % 3 == 0 else "\n"))
+        if k % 11 == 0:
+            lines.append("\n")
+    buf = "".join(lines).encode() + b"trailing element data\n"
+    out = np.empty_like(vals)
+    used = C.c_size_t(0)
+    assert lib.m3d_parse_ascii_rows(buf, len(buf), len(vals), 3,
+                                    out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(used)) == 0
+    exp = np.loadtxt([l for l in lines if l.strip()], dtype=np.float64)
+    np.testing.assert_array_equal(out.view(np.uint64), exp.view(np.uint64))  # bit for bit
+    assert buf[used.value:] == b"trailing element data\n"
+    # short input, extra tokens and non-numbers are refused (plyio then uses numpy)
+    for bad, rows in ((b"1 2 3\n", 2), (b"1 2 3 4\n", 1), (b"1 2 x\n", 1), (b"+1 2 3\n", 1)):
+        assert lib.m3d_parse_ascii_rows(bad, len(bad), rows, 3, out.ctypes.data_as(C.POINTER(C.c_double)),
+                                        C.byref(used)) != 0
+
+
+def test_native_ascii_writer_round_trips_and_plus_sign_fallback(tmp_path):
+    rng = np.random.default_rng(4)
+    pts = rng.normal(size=(1000, 3)) * 10.0 ** rng.integers(-200, 200, (1000, 1))
+    pts[0] = [-0.0, 5e-324, 1.7976931348623157e308]
+    p = tmp_path / "w.ply"
+    plyio.write_ply(p, pts, binary=False, dtype="double")
+    got, _ = plyio.read_ply(p)
+    np.testing.assert_array_equal(got.view(np.uint64), pts.view(np.uint64))
+    # a file the native parser refuses ('+' signs) still reads through numpy
+    q = tmp_path / "plus.ply"
+    q.write_text("ply\nformat ascii 1.0\nelement vertex 2\nproperty double x\nproperty double y\n"
+                 "property double z\nend_header\n+1.5 2 3\n4 +5e1 6\n")
+    got, _ = plyio.read_ply(q)
+    np.testing.assert_array_equal(got, [[1.5, 2, 3], [4, 50, 6]])
+
+
+def test_native_vertex_merge_equals_numpy_merge():
+    """csrc/hostio.cpp m3d_merge_vertices = plyio._merge_numpy: first-occurrence order, exact
+    equality with -0.0 ≡ +0.0, on shared corners, duplicates and signed zeros."""
+    from m3d import synth
+
+    v, f = synth.surface_mesh(40, 80, seed=5)
+    corners = v[f].reshape(-1, 3).astype(np.float32).astype(np.float64)
+    corners[::97] = [-0.0, 0.0, 1.0]
+    corners[1::101] = [0.0, -0.0, 1.0]
+    ref_v, ref_f = plyio._merge_numpy(corners)
+    import ctypes as C
+
+    uniq = np.empty_like(corners)
+    inv = np.empty(len(corners), np.int32)
+    m = C.c_int64(0)
+    P = C.POINTER(C.c_double)
+    assert plyio._text_lib().m3d_merge_vertices(corners.ctypes.data_as(P), len(corners), uniq.ctypes.data_as(P),
+                                                inv.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(m)) == 0
+    np.testing.assert_array_equal(uniq[: m.value], ref_v)
+    np.testing.assert_array_equal(inv.reshape(-1, 3), ref_f)
