@@ -102,9 +102,24 @@ __device__ __forceinline__ double d2_exact(const double* a, const double* b) {
   return (dx * dx + dy * dy) + dz * dz;
 }
 
+// fp32 prefilter of a candidate against an exact fp64 threshold thr (inclusive): with e the
+// bound on |fp32 distance − fp64 distance| of two centred points (both coordinate roundings,
+// √3·2·u·rmax), any point whose fp64 d² ≤ thr has a directly computed fp32 d² (three roundings
+// of relative u each, covered by the 4e-6 factors) ≤ this bound — so a candidate above it can be
+// skipped without its fp64 gather.
+__device__ __forceinline__ float prefilter_bound(double thr, double e) {
+  const double b = (sqrt(thr) + e) * (1.0 + 4e-6);
+  const float f = __double2float_ru(b * b * (1.0 + 4e-6));
+  return isfinite(f) ? f : FLT_MAX;
+}
+
 // Block = L lanes (one query each); dynamic LDS: d²[k][L] doubles then idx[k][L] ints.
+// Candidates are screened in fp32 from the grid's own sorted points first (prefilter_bound of
+// r² and, once k are held, of the k-th d²): most of a box lies outside the sphere, and past the
+// first k most candidates cannot enter the list, so the exact path (fp64 gather + insertion)
+// runs for few.  The list is exactly the one without the screen.
 __global__ void hybrid_search_kernel(const double* __restrict__ xyz64, const float4* __restrict__ xyz32,
-                                     int64_t n, GridDev g, float Rf, double r2, int k,
+                                     int64_t n, GridDev g, float Rf, double r2, double eabs, int k,
                                      int32_t* __restrict__ out_idx, double* __restrict__ out_d2,
                                      int32_t* __restrict__ out_cnt) {
   extern __shared__ double lds[];
@@ -116,6 +131,7 @@ __global__ void hybrid_search_kernel(const double* __restrict__ xyz64, const flo
   const double q[3] = {xyz64[3 * i], xyz64[3 * i + 1], xyz64[3 * i + 2]};
   const float4 qf = xyz32[i];
   int cnt = 0;
+  float bf = prefilter_bound(r2, eabs);
   if (g.ncells > 0) {
     const int x0 = prep_coord(qf.x - Rf, g.o[0], g.inv_h, g.n[0]);
     const int x1 = prep_coord(qf.x + Rf, g.o[0], g.inv_h, g.n[0]);
@@ -128,7 +144,10 @@ __global__ void hybrid_search_kernel(const double* __restrict__ xyz64, const flo
         const int64_t row = ((int64_t)cz * g.n[1] + cy) * g.n[0];
         const int32_t j0 = g.start[row + x0], j1 = g.start[row + x1 + 1];
         for (int32_t j = j0; j < j1; ++j) {
-          const int32_t t = __float_as_int(g.pts[j].w);
+          const float4 tp = g.pts[j];
+          const float fx = qf.x - tp.x, fy = qf.y - tp.y, fz = qf.z - tp.z;
+          if ((fx * fx + fy * fy) + fz * fz > bf) continue;
+          const int32_t t = __float_as_int(tp.w);
           const double d2 = d2_exact(xyz64 + 3 * (int64_t)t, q);
           if (!(d2 < r2)) continue;
           int pos;
@@ -150,6 +169,7 @@ __global__ void hybrid_search_kernel(const double* __restrict__ xyz64, const flo
           }
           ld[pos * L + lane] = d2;
           li[pos * L + lane] = t;
+          if (cnt == k) bf = prefilter_bound(ld[(k - 1) * L + lane], eabs);
         }
       }
   }
@@ -158,6 +178,143 @@ __global__ void hybrid_search_kernel(const double* __restrict__ xyz64, const flo
     out_d2[i * k + s] = s < cnt ? ld[s * L + lane] : 0.0;
   }
   out_cnt[i] = cnt;
+}
+
+// The same search with ONE WAVE per query (k ≤ 64·kS): the wave reads the box's cell rows 64
+// points at a time (coalesced: the rows are contiguous in the sorted grid), screens them in fp32
+// against prefilter_bound of the current threshold, evaluates the survivors' exact fp64 d², and
+// inserts the qualifying ones into a sorted list held across the lanes (entry e in lane e % 64,
+// slot e / 64): position = number of held entries below the candidate (a ballot), entries at
+// and above it move up one place (a lane shift), the k-th entry sets the next threshold.  The
+// list order is the total order (d², index), so it is the per-lane kernel's list exactly, with
+// every candidate read once per wave instead of once per lane and no divergent insertion chains.
+__device__ __forceinline__ bool key_less(double d, int32_t t, double D, int32_t T) {
+  return d < D || (d == D && t < T);
+}
+
+// lane l ← lane l − 1 across the whole wave (gfx9 DPP wave_shr:1; lane 0 keeps `old`): a VALU
+// move, no LDS round trip like ds_bpermute
+__device__ __forceinline__ int32_t wave_shr1(int32_t old, int32_t v) {
+  return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double wave_shr1(double old, double v) {
+  const uint64_t o = (uint64_t)__double_as_longlong(old), x = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)wave_shr1((int32_t)(uint32_t)o, (int32_t)(uint32_t)x);
+  const uint32_t hi = (uint32_t)wave_shr1((int32_t)(uint32_t)(o >> 32), (int32_t)(uint32_t)(x >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t x = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)(x >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <int kS>
+__global__ __launch_bounds__(256) void hybrid_search_wave_kernel(
+    const double* __restrict__ xyz64, const float4* __restrict__ xyz32, int64_t n, GridDev g,
+    float Rf, double r2, double eabs, int k, int32_t* __restrict__ out_idx,
+    double* __restrict__ out_d2, int32_t* __restrict__ out_cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;  // wave-uniform
+  const double q[3] = {xyz64[3 * i], xyz64[3 * i + 1], xyz64[3 * i + 2]};
+  const float4 qf = xyz32[i];
+  double D[kS];
+  int32_t T[kS];
+#pragma unroll
+  for (int u = 0; u < kS; ++u) {
+    D[u] = 0.0;
+    T[u] = -1;
+  }
+  int cnt = 0;             // entries held (wave-uniform)
+  double thr = r2;         // exact threshold: r² until k are held, then the k-th entry (inclusive)
+  int32_t thr_t = INT32_MAX;
+  float bf = prefilter_bound(r2, eabs);
+  if (g.ncells > 0) {
+    const int x0 = prep_coord(qf.x - Rf, g.o[0], g.inv_h, g.n[0]);
+    const int x1 = prep_coord(qf.x + Rf, g.o[0], g.inv_h, g.n[0]);
+    const int y0 = prep_coord(qf.y - Rf, g.o[1], g.inv_h, g.n[1]);
+    const int y1 = prep_coord(qf.y + Rf, g.o[1], g.inv_h, g.n[1]);
+    const int z0 = prep_coord(qf.z - Rf, g.o[2], g.inv_h, g.n[2]);
+    const int z1 = prep_coord(qf.z + Rf, g.o[2], g.inv_h, g.n[2]);
+    for (int cz = z0; cz <= z1; ++cz)
+      for (int cy = y0; cy <= y1; ++cy) {
+        const int64_t row = ((int64_t)cz * g.n[1] + cy) * g.n[0];
+        const int32_t j0 = g.start[row + x0], j1 = g.start[row + x1 + 1];
+        for (int32_t jb = j0; jb < j1; jb += 64) {
+          const int32_t j = jb + lane;
+          bool cand = false;
+          double d = 0.0;
+          int32_t t = -1;
+          if (j < j1) {
+            const float4 tp = g.pts[j];
+            const float fx = qf.x - tp.x, fy = qf.y - tp.y, fz = qf.z - tp.z;
+            if ((fx * fx + fy * fy) + fz * fz <= bf) {
+              t = __float_as_int(tp.w);
+              d = d2_exact(xyz64 + 3 * (int64_t)t, q);
+              cand = d < r2 && (cnt < k ? true : key_less(d, t, thr, thr_t));
+            }
+          }
+          uint64_t m = __ballot(cand);
+          while (m != 0) {
+            const int src = __builtin_ctzll(m);
+            m &= m - 1;
+            const double x = readlane_f64(d, src);
+            const int32_t xt = __builtin_amdgcn_readlane(t, src);
+            if (cnt == k && !key_less(x, xt, thr, thr_t)) continue;  // the threshold moved
+            int pos = 0;
+#pragma unroll
+            for (int u = 0; u < kS; ++u) {
+              const int e = u * 64 + lane;
+              pos += __popcll(__ballot(e < cnt && key_less(D[u], T[u], x, xt)));
+            }
+            // move entries pos .. up by one place (slot u takes lane 63 of slot u − 1)
+#pragma unroll
+            for (int u = kS - 1; u >= 0; --u) {
+              // lane 0 of slot u takes lane 63 of slot u − 1 (a uniform read), the others
+              // their left neighbour
+              const double d63 = u > 0 ? readlane_f64(D[u > 0 ? u - 1 : 0], 63) : 0.0;
+              const int32_t t63 = u > 0 ? __builtin_amdgcn_readlane(T[u > 0 ? u - 1 : 0], 63) : -1;
+              const double dc = wave_shr1(d63, D[u]);
+              const int32_t tc = wave_shr1(t63, T[u]);
+              const int e = u * 64 + lane;
+              if (e > pos) {
+                D[u] = dc;
+                T[u] = tc;
+              } else if (e == pos) {
+                D[u] = x;
+                T[u] = xt;
+              }
+            }
+            cnt = cnt < k ? cnt + 1 : k;
+            if (cnt == k) {
+              const int u = (k - 1) / 64, l = (k - 1) % 64;
+              double dk = D[0];
+              int32_t tk = T[0];
+#pragma unroll
+              for (int v = 0; v < kS; ++v)
+                if (v == u) {
+                  dk = D[v];
+                  tk = T[v];
+                }
+              thr = readlane_f64(dk, l);
+              thr_t = __builtin_amdgcn_readlane(tk, l);
+              bf = prefilter_bound(thr, eabs);
+            }
+          }
+        }
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < kS; ++u) {
+    const int e = u * 64 + lane;
+    if (e < k) {
+      out_idx[i * k + e] = e < cnt ? T[u] : -1;
+      out_d2[i * k + e] = e < cnt ? D[u] : 0.0;
+    }
+  }
+  if (lane == 0) out_cnt[i] = cnt;
 }
 
 // ------------------------------------------------------------------------------- normals
@@ -559,8 +716,22 @@ hipError_t hybrid_search(const m3d_cloud* c, const Grid* g, double radius, int k
   const float Rf = (float)Rd * (1.0f + 1e-6f);
   const int L = k <= 40 ? 64 : (k <= 80 ? 32 : (k <= 160 ? 16 : 8));
   const size_t lds = (size_t)k * L * (sizeof(double) + sizeof(int32_t));
-  hybrid_search_kernel<<<(unsigned)((c->n + L - 1) / L), L, lds, st>>>(
-      c->xyz64, c->xyz32, c->n, g->dev, Rf, radius * radius, k, idx, d2, cnt);
+  const double eabs = 3.4641016151377544 * c->rmax * 5.9604644775390625e-08 * 1.01;
+  static const int mode = [] {  // M3D_HYBRID_WAVE=0: the per-lane kernel (A/B)
+    const char* e = getenv("M3D_HYBRID_WAVE");
+    return e ? atoi(e) : 1;
+  }();
+  const unsigned wb = (unsigned)((c->n + 3) / 4);  // 4 waves (queries) per 256-thread block
+  if (mode != 0 && k <= 64) {
+    hybrid_search_wave_kernel<1><<<wb, 256, 0, st>>>(c->xyz64, c->xyz32, c->n, g->dev, Rf,
+                                                     radius * radius, eabs, k, idx, d2, cnt);
+  } else if (mode != 0 && k <= 128) {
+    hybrid_search_wave_kernel<2><<<wb, 256, 0, st>>>(c->xyz64, c->xyz32, c->n, g->dev, Rf,
+                                                     radius * radius, eabs, k, idx, d2, cnt);
+  } else {
+    hybrid_search_kernel<<<(unsigned)((c->n + L - 1) / L), L, lds, st>>>(
+        c->xyz64, c->xyz32, c->n, g->dev, Rf, radius * radius, eabs, k, idx, d2, cnt);
+  }
   return hipGetLastError();
 }
 
