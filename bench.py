@@ -529,6 +529,7 @@ def bench_cfg4(args):
                     "global_registration_ms": tg, "refine_registration_ms": tr,
                     "coarse_fitness": coarse.fitness, "fine_fitness": fine.fitness,
                     "fine_max_abs_err_vs_T_true": float(np.abs(fine.transformation - T).max())}
+            out["reference_suite"] = reference_suite(src, tgt, f"{d}/src.ply", f"{d}/tgt.ply")
             # validation throughput: the same a6 call (EdgeLength 0.9 + Distance 0.45 checkers) with
             # a 0.03 validation radius below the 0.05 point noise, so no hypothesis reaches the
             # early exit and every checker-passing one of 30000 is validated (grid.hip
@@ -549,6 +550,61 @@ def bench_cfg4(args):
                 "point_evaluations_per_s": fr.validations * len(sp) / dt,
                 "best_fitness": fr.fitness}
     return out
+
+
+# benchmark_results.txt (the reference's own published profile; hardware and input sizes unstated)
+PUBLISHED_MS = {"ply_loading": 791.23, "correspondence_computation": 8.98, "ransac_iteration": 0.76,
+                "evaluate_inliers": 0.50, "compute_transformation": 0.24, "deep_copy": 3.83,
+                "full_ransac": 21.12}
+
+
+def reference_suite(src, tgt, src_path, tgt_path, iterations=100):
+    """benchmark_ransac.py:223-275 (run_comprehensive_benchmark) through the drop-in, on the cfg4
+    scans: ply_loading (two Ply(path) calls, :45-47), correspondence_computation
+    (compute_feature_correspondences, :76-77), ransac_iteration / compute_transformation /
+    evaluate_inliers (100 × a1 + a2, :105-113), deep_copy (copy.deepcopy(src.pcd), :141-142),
+    full_ransac (global_registration, iteration 30, :193-194) — wall ms beside the published
+    benchmark_results.txt (hardware and input sizes unstated there)."""
+    import copy
+
+    import numpy as np
+    import torch
+
+    from matcher.ransac import (compute_feature_correspondences, compute_step_transformation,
+                                evaluate_inlier_ratio, global_registration)
+    from ply import Ply
+
+    def wall(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        return r, (time.perf_counter() - t0) * 1e3
+
+    np.random.seed(0)
+    (s2, t2), load_ms = wall(lambda: (Ply(src_path, 0.3), Ply(tgt_path, 0.3)))
+    corres, corr_ms = wall(lambda: compute_feature_correspondences(s2, t2, noise_ratio=0.0))
+    a = b = 0.0
+    for _ in range(iterations):
+        res, ta = wall(lambda: compute_step_transformation(s2, t2, corres))
+        _, tb = wall(lambda: evaluate_inlier_ratio(s2, t2, corres, res.transformation, 0.3))
+        a += ta
+        b += tb
+    cp = 0.0
+    for _ in range(iterations):
+        cp += wall(lambda: copy.deepcopy(s2.pcd))[1]
+    full, full_ms = wall(lambda: global_registration(s2, t2, voxel_size=0.3, iteration=30))
+    got = {"ply_loading": load_ms, "correspondence_computation": corr_ms,
+           "ransac_iteration": (a + b) / iterations, "evaluate_inliers": b / iterations,
+           "compute_transformation": a / iterations, "deep_copy": cp / iterations,
+           "full_ransac": full_ms}
+    return {"harness": "benchmark_ransac.py run_comprehensive_benchmark (voxel 0.3, noise 0.0, 100 "
+                       "iterations, full RANSAC 30) through matcher/ply on the cfg4 scans",
+            "points": [len(s2.pcd.points), len(t2.pcd.points)],
+            "down_points": [len(s2.pcd_down.points), len(t2.pcd_down.points)],
+            "correspondences": int(len(corres)), "full_ransac_fitness": float(full.fitness),
+            "ms": got, "published_ms": PUBLISHED_MS,
+            "speedup_vs_published": {k: PUBLISHED_MS[k] / v for k, v in got.items() if v > 0}}
 
 
 def bench_ransac_api(args, budget_s=1.5):
