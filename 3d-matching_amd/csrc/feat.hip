@@ -54,14 +54,34 @@ __global__ __launch_bounds__(kFnnBlock) void feature_nn_kernel(const double* __r
     for (int e = threadIdx.x; e < tn * kFeatDim; e += kFnnBlock)
       tile[e / kFeatDim][e % kFeatDim] = fr[t0 * kFeatDim + e];
     __syncthreads();
-    for (int r = 0; r < tn; ++r) {
+    // four references per step: four independent dimension-order chains (each d² still sums
+    // its 33 terms in the oracle's order) instead of one 33-long dependent fp64 chain
+    int r = 0;
+    for (; r + 4 <= tn; r += 4) {
+      double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+#pragma unroll
+      for (int j = 0; j < kFeatDim; ++j) {
+        const double t0 = a[j] - tile[r][j], t1 = a[j] - tile[r + 1][j];
+        const double t2 = a[j] - tile[r + 2][j], t3 = a[j] - tile[r + 3][j];
+        d0 += t0 * t0;
+        d1 += t1 * t1;
+        d2 += t2 * t2;
+        d3 += t3 * t3;
+      }
+      // references in increasing index: strict < keeps the lowest
+      if (d0 < bd) { bd = d0; bi = (int32_t)(t0 + r); }
+      if (d1 < bd) { bd = d1; bi = (int32_t)(t0 + r + 1); }
+      if (d2 < bd) { bd = d2; bi = (int32_t)(t0 + r + 2); }
+      if (d3 < bd) { bd = d3; bi = (int32_t)(t0 + r + 3); }
+    }
+    for (; r < tn; ++r) {
       double d = 0.0;
 #pragma unroll
       for (int j = 0; j < kFeatDim; ++j) {
         const double t = a[j] - tile[r][j];
         d += t * t;
       }
-      if (d < bd) {  // references visited in increasing index: strict < keeps the lowest
+      if (d < bd) {
         bd = d;
         bi = (int32_t)(t0 + r);
       }
@@ -96,8 +116,9 @@ hipError_t feature_nn(const double* fq, int64_t nq, const double* fr, int64_t nr
                       hipStream_t st) {
   if (nq == 0) return hipSuccess;
   const int64_t bx = (nq + kFnnBlock - 1) / kFnnBlock;
-  // ≥ ~2048 blocks: slice the references (slices of ≥ 4 tiles)
-  int64_t S = std::max<int64_t>(1, std::min<int64_t>((2048 + bx - 1) / bx, (nr + 4 * kFnnTile - 1) / (4 * kFnnTile)));
+  // ≥ ~2048 blocks (≥ 4 waves per SIMD: each lane's chains are latency-bound): slice the
+  // references, slices of ≥ 1 tile
+  int64_t S = std::max<int64_t>(1, std::min<int64_t>((2048 + bx - 1) / bx, (nr + kFnnTile - 1) / kFnnTile));
   S = std::min<int64_t>(S, 65535);
   int64_t slice = (nr + S - 1) / S;
   slice = (slice + kFnnTile - 1) / kFnnTile * kFnnTile;
