@@ -997,9 +997,8 @@ hipError_t launch_score_prep(const m3d_corrset* cs, const double* T64, int64_t H
 // ------------------------------------------------------------------------------- one hypothesis
 // The per-call drop-in (compute_step_transformation / evaluate_inlier_ratio as
 // benchmark_ransac.py:105-113 calls them, one hypothesis per call): the triple and the transform
-// travel as kernel arguments and the transform comes back through mapped pinned memory, so a
-// call is one launch (a1) or two launches + one 4-B copy (a2/a3) and one stream sync, with no
-// staging copies.
+// travel as kernel arguments and the results go straight into mapped pinned memory, so a call
+// is one launch and one stream sync, with no staging copies (a2/a3: count_one_kernel below).
 struct Tri3 {
   int32_t i[3];
 };
