@@ -22,6 +22,14 @@ GOLDEN = ROOT / "tests" / "golden"
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP path through libm3d.so)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    # the C-ABI / host-code tests load libm3d.so: build it in-tree first when a fresh checkout
+    # has none (hipcc cross-compiles gfx950 without a GPU; __graft_entry__.build() does the same)
+    lib = PKG / "m3d" / "libm3d.so"
+    if not lib.exists() and os.environ.get("M3D_NO_AUTOBUILD") != "1":
+        import subprocess
+
+        subprocess.run(["make", "-C", str(PKG / "csrc"), "-j", str(min(8, os.cpu_count() or 1))],
+                       check=False, stdout=subprocess.DEVNULL)
 
 
 @pytest.fixture(scope="session")
