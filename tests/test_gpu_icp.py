@@ -377,6 +377,30 @@ def test_icp_cfg1_matches_oracle(nn):
     np.testing.assert_allclose(r.transformation, T_true, atol=5e-4)
 
 
+def test_icp_cfg1_point_to_point_matches_oracle():
+    """cfg1's pair with TransformationEstimationPointToPoint (a10: Umeyama over the 15 centred
+    sums, rotation_from_cov shared with a1), 30 fixed iterations, grid NN: correspondences
+    equal to the oracle's exact NN at every evaluation, final transform / fitness / rmse against
+    the oracle's own run."""
+    src, tgt, nrm, _ = synth.icp_pair(100_000, 100_000, seed=0)
+    lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
+                 max_iteration=30, nn="grid", estimation=_lib.EST_POINT_TO_POINT)
+    lp.reset(np.eye(4))
+    tree = cKDTree(tgt)
+    for it in range(31):
+        T = lp.result().transformation
+        lp.step()
+        ref_j, _ = I.nn_exact(tree, tgt, I.transform_points(T, src), 0.12)
+        np.testing.assert_array_equal(lp.correspondences().cpu().numpy(), ref_j, err_msg=f"evaluation {it}")
+    r = lp.result()
+    ref = I.registration_icp(src, tgt, 0.12, init=np.eye(4), estimation="point_to_point",
+                             relative_fitness=-1, relative_rmse=-1, max_iteration=30)
+    assert r.iterations == ref["iterations"] == 30
+    np.testing.assert_allclose(r.transformation, ref["transformation"], rtol=0, atol=1e-9)
+    assert r.fitness == ref["fitness"]
+    assert abs(r.inlier_rmse - ref["inlier_rmse"]) < 1e-12
+
+
 def test_fused_tail_beyond_256_blocks_equals_separate():
     """Past 256 terms blocks the fused tail's last block reduces the partials in several batches
     (brute force keeps the fused form: it hands the keys back) and the grid loop switches to the
