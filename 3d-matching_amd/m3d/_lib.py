@@ -149,6 +149,14 @@ def load() -> C.CDLL:
     if not LIB_PATH.exists():
         raise ImportError(f"{LIB_PATH} not built: run `make -C {LIB_PATH.parent.parent / 'csrc'}` "
                           "(hipcc --offload-arch=gfx950)")
+    # torch first: PyTorch-ROCm ships its own HIP/HSA runtime libraries.  Imported first, they
+    # are the copies libm3d.so binds to (same sonames) and the process has ONE runtime; loaded
+    # after libm3d.so (e.g. plyio's host text helpers before any device call), torch brings up a
+    # second runtime and libm3d's then reports no device (measured on the MI355X box).
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - host-only use without torch
+        pass
     lib = C.CDLL(os.fspath(LIB_PATH))
     lib.m3d_abi_version.restype = C.c_int
     if lib.m3d_abi_version() != ABI_VERSION:

@@ -41,7 +41,12 @@ class Context:
         h = C.c_void_p()
         rc = lib.m3d_create(device, C.byref(h))
         if rc == _lib.M3D_ERR_NODEVICE:
-            raise RuntimeError(f"device {device} is not a gfx950 (MI355X) GPU")
+            n = C.c_int(-1)
+            lib.m3d_device_count(C.byref(n))
+            torch = _torch()
+            arch = torch.cuda.get_device_properties(device).gcnArchName if torch.cuda.is_available() else "?"
+            raise RuntimeError(f"device {device} is not a gfx950 (MI355X) GPU (libm3d sees {n.value} "
+                               f"device(s); torch: {arch})")
         check(rc, None, "m3d_create")
         self.h = h
         self.lib = lib

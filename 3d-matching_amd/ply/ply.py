@@ -48,6 +48,7 @@ class Ply:
         """ply.py:53-66.  Wall time of each stage lands in ``stage_ms`` (every stage returns host
         arrays, so the device work is complete when its timer stops)."""
         from m3d import prep
+        from m3d.core import Cloud, to_device
 
         v = voxel_size
         ms = getattr(self, "stage_ms", None)
@@ -61,18 +62,23 @@ class Ply:
             ms[name] = (now - t) * 1e3
             t = now
 
-        down, _ = prep.voxel_down_sample(self.pcd.points, v)
+        # the full cloud goes to the device once (down-sampling, then its normals), the
+        # down-sampled one once (its normals, then FPFH: the noise is added after, ply.py:61-62)
+        p_dev = to_device(self.pcd.points)
+        down, _ = prep.voxel_down_sample(p_dev, v)
         lap("voxel_down_sample")
-        down_n = prep.estimate_normals(down, 2 * v, 30)
+        c_down = Cloud(down)
+        down_n = prep.estimate_normals(c_down, 2 * v, 30)
         lap("normals_down")
         self.pcd_down = PointCloud(down, down_n)
-        self.pcd_fpfh = Feature(prep.compute_fpfh(down, down_n, 5 * v, 100).T)
+        self.pcd_fpfh = Feature(prep.compute_fpfh(c_down, down_n, 5 * v, 100).T)
         lap("fpfh")
         noise = 0.05 * np.random.randn(*self.pcd_down.points.shape)      # ply.py:61-62
         self.pcd_down.points = self.pcd_down.points + noise
         lap("noise")
         prev = self.pcd.normals if self.pcd.has_normals() else None
-        self.pcd.normals = prep.estimate_normals(self.pcd.points, 2 * v, 30, normals=prev)
+        # existing normals orient the estimate like Open3D (the cloud carries them)
+        self.pcd.normals = prep.estimate_normals(Cloud(p_dev, prev), 2 * v, 30)
         lap("normals_full")
 
     @classmethod

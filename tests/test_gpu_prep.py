@@ -223,3 +223,25 @@ def test_cfg4_stl_pipeline(tmp_path, iteration):
     res = register(src, tgt, 0.3, iteration=iteration)
     np.testing.assert_allclose(res.transformation, T, atol=5e-3)
     assert res.fitness > 0.9
+
+
+@pytest.mark.gpu
+def test_host_text_io_before_any_device_call(tmp_path):
+    """A fresh process whose first libm3d use is host-side (ASCII PLY write) must still see the
+    device afterwards: libm3d.so has to bind to the HIP runtime torch brings (m3d/_lib.py)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import numpy as np\n"
+        "from m3d import plyio, synth\n"
+        "from ply import Ply\n"
+        "pts, _ = synth.surface_points(20000, seed=21)\n"
+        "plyio.write_ply(%r, pts, binary=False)\n"
+        "print(len(Ply(%r, 0.3).pcd_down.points))\n"
+    ) % (str(root / "3d-matching_amd"), str(tmp_path / "a.ply"), str(tmp_path / "a.ply"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert int(r.stdout.split()[-1]) > 0
