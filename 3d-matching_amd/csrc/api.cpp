@@ -664,33 +664,73 @@ int m3d_replay_triples(uint32_t* mt_key, int32_t* mt_pos, int64_t nc, int64_t H,
   // through the swaps in reverse order (i = 1 .. nc-1: p == i → j_i, p == j_i → i), which lands
   // on the initial index, i.e. the value.  Sequential passes, no O(nc) value array.
   thread_local std::vector<uint32_t> jbuf;
-  if (jbuf.size() < (size_t)nc) jbuf.resize((size_t)nc);
+  if (jbuf.size() < (size_t)nc + 64) jbuf.resize((size_t)nc + 64);
   uint32_t* j = jbuf.data();
+  uint32_t tk[624];  // the tempered outputs of the current key block
+  auto temper_block = [&](int from) {
+    for (int k = from; k < 624; ++k) tk[k] = MT::temper(mt.key[k]);  // vectorised
+  };
+  if (mt.pos < 624) temper_block(mt.pos);
   for (int64_t h = 0; h < H; ++h) {
     // random_interval(i) for i = nc-1 .. 1, branch-free: every MT output is a candidate
     // (y & mask(i), mask = 2^(⌊log2 i⌋+1) − 1) that is kept iff ≤ i — the rejection loop's
-    // outcome is unpredictable, a branch on it costs more than the generator
+    // outcome is unpredictable, a branch on it costs more than the generator.  The mask is
+    // constant while i stays above mask >> 1, so the dependency chain per output is the compare
+    // and the decrement.
     int64_t i = nc - 1;
     while (i >= 1) {
-      if (mt.pos >= 624) mt.gen();
-      int k = mt.pos;
-      for (; k < 624 && i >= 1; ++k) {
-        const uint32_t v = MT::temper(mt.key[k]) & (0xFFFFFFFFu >> __builtin_clz((uint32_t)i));
-        j[i] = v;
-        i -= (int64_t)(v <= (uint32_t)i);
+      const uint32_t mask = 0xFFFFFFFFu >> __builtin_clz((uint32_t)i);
+      const int64_t lo = (int64_t)(mask >> 1);
+      while (i > lo) {
+        if (mt.pos >= 624) {
+          mt.gen();
+          temper_block(0);
+        }
+        // at least i − lo more outputs are needed before i reaches lo (each output lowers i by
+        // at most one), so that many run without a bound check
+        const int k0 = mt.pos;
+        const int n = (int)std::min<int64_t>(624 - k0, i - lo);
+        uint32_t ii = (uint32_t)i;
+        for (int k = k0; k < k0 + n; ++k) {
+          const uint32_t v = tk[k] & mask;
+          j[ii] = v;
+          ii -= (uint32_t)(v <= ii);
+        }
+        mt.pos = k0 + n;
+        i = ii;
       }
-      mt.pos = k;
     }
-    uint32_t p0 = 0, p1 = 1, p2 = 2;
-    for (int64_t i = 1; i < nc; ++i) {
-      const uint32_t ji = j[i], ii = (uint32_t)i;
-      p0 = p0 == ii ? ji : (p0 == ji ? ii : p0);
-      p1 = p1 == ii ? ji : (p1 == ji ? ii : p1);
-      p2 = p2 == ii ? ji : (p2 == ji ? ii : p2);
+    // trace positions 0..2 back through the swaps (i ascending).  After step i a traced
+    // position p is ≤ i, so from i = 3 on it can only move when j_i == p (then p := i): a
+    // vectorised search for the next index whose draw equals one of the three positions
+    uint32_t p[3] = {0, 1, 2};
+    for (int64_t a = 1; a < std::min<int64_t>(nc, 3); ++a) {
+      const uint32_t ji = j[a], ia = (uint32_t)a;
+      for (int q = 0; q < 3; ++q) p[q] = p[q] == ia ? ji : (p[q] == ji ? ia : p[q]);
     }
-    triples_out[3 * h + 0] = (int32_t)p0;
-    triples_out[3 * h + 1] = (int32_t)p1;
-    triples_out[3 * h + 2] = (int32_t)p2;
+    int64_t a = 3;
+    constexpr int kW = 32;
+    while (a < nc) {
+      const int64_t e = std::min<int64_t>(nc, a + kW);
+      uint32_t any = 0;
+      if (e - a == kW) {
+        const uint32_t p0 = p[0], p1 = p[1], p2 = p[2];
+        for (int t = 0; t < kW; ++t) {
+          const uint32_t v = j[a + t];
+          any |= (uint32_t)(v == p0) | (uint32_t)(v == p1) | (uint32_t)(v == p2);
+        }
+      } else {
+        any = 1;
+      }
+      if (any) {
+        for (int64_t b = a; b < e; ++b)
+          for (int q = 0; q < 3; ++q) p[q] = j[b] == p[q] ? (uint32_t)b : p[q];
+      }
+      a = e;
+    }
+    triples_out[3 * h + 0] = (int32_t)p[0];
+    triples_out[3 * h + 1] = (int32_t)p[1];
+    triples_out[3 * h + 2] = (int32_t)p[2];
   }
   memcpy(mt_key, mt.key, sizeof(mt.key));
   *mt_pos = mt.pos;
