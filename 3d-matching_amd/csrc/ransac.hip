@@ -527,6 +527,12 @@ __device__ __forceinline__ float vmin3a(float a, float b, float c) {
   return __builtin_elementwise_minimum(__builtin_elementwise_minimum(fabsf(a), fabsf(b)), fabsf(c));
 }
 
+#ifndef M3D_SCORE_PERM_COUNT
+#define M3D_SCORE_PERM_COUNT 1
+#endif
+// units of score_mfma_kernel's per-lane outlier counter (the v_perm count adds 8 per outlier)
+constexpr uint32_t kOutlUnit = M3D_SCORE_PERM_COUNT ? 8u : 1u;
+
 // grid: x = hypothesis blocks of shyps<kSMG>(), y = correspondence slices of slice_len (multiple
 // of kSTile); block = 8 waves, wave w owns hypotheses hb + (w·kSMG + g)·32 + (lane & 31).
 template <int kSMG>
@@ -606,9 +612,19 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
         for (int r = 0; r < 16; ++r) v[r] = fnmsq(dz[r], fnmsq(dy[r], fnmsq(dx[r], t2r)));
         // v > 0 ⇔ inlier (outside the band): count sign bits (outliers) per lane
         uint32_t s = 0;
+#if M3D_SCORE_PERM_COUNT
+        // v_perm selectors 9 / 11 give a byte of 0xFF when S1 / S0 is negative: two sign masks
+        // per word, counted by v_bcnt (accumulating) — 8 per outlier, so outl holds 8× the count
+        // (2 VALU per 2 values instead of 2 shifts + an add3)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2)
+          s += __builtin_popcount(__builtin_amdgcn_perm(__float_as_uint(v[r]),
+                                                        __float_as_uint(v[r + 1]), 0x0C0C0B09u));
+#else
 #pragma unroll
         for (int r = 0; r < 16; r += 2)
           s += (__float_as_uint(v[r]) >> 31) + (__float_as_uint(v[r + 1]) >> 31);
+#endif
         outl[g] += s;
         const float m0 = vmin3a(v[0], v[1], v[2]), m1 = vmin3a(v[3], v[4], v[5]);
         const float m2 = vmin3a(v[6], v[7], v[8]), m3 = vmin3a(v[9], v[10], v[11]);
@@ -642,7 +658,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
               const bool in = hyp[g] < H && i < ex.nc &&
                               exact_inlier(ex.T64 + 16 * hyp[g], ex.p64 + 3 * i, ex.q64 + 3 * i,
                                            ex.thr, ex.mode);
-              outl[g] += (in ? 0u : 1u) - sgn;
+              outl[g] += kOutlUnit * ((in ? 0u : 1u) - sgn);
             }
             ++slot;
           }
@@ -660,7 +676,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   const uint32_t rows = tiles_seen * (kSTile / 2);  // each lane half sees half of every 32-row block
 #pragma unroll
   for (int g = 0; g < kSMG; ++g) {
-    const uint32_t in = 2 * rows - (outl[g] + (uint32_t)__shfl_xor((int)outl[g], 32));
+    const uint32_t in = 2 * rows - (outl[g] + (uint32_t)__shfl_xor((int)outl[g], 32)) / kOutlUnit;
     if (h == 0 && hyp[g] < H && in != 0) atomicAdd(&counts[hyp[g]], (int32_t)in);
   }
   // the queued guard-band pairs, one per thread: fp64 in numpy order, count correction
