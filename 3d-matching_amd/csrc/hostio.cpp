@@ -9,6 +9,7 @@
 #include <cstring>
 #include <system_error>
 #include <vector>
+#include <algorithm>
 
 #include "../../include/m3d.h"
 
@@ -70,39 +71,86 @@ int m3d_format_ascii_rows(const double* data, int64_t rows, int32_t cols, char* 
 // STL → unique vertices (convert_stl-ply.py: trimesh.load_mesh merges a mesh's shared
 // corners).  Exact equality of the (x, y, z) bytes after -0.0 → +0.0, ids in first-occurrence
 // order — what plyio's numpy sort-based merge computes, in one hash pass: open addressing over a
-// power-of-two table ≥ 2n, 24-byte keys compared with memcmp.
+// power-of-two table of (32-bit hash tag, id) slots kept at ≤ 50 % load (it starts at n / 4
+// slots — a closed mesh has ~n / 6 distinct corners — and doubles when half full), so the table
+// stays cache-sized and a probe only reads the stored vertex when the tags agree; the slots of
+// the vertices 8 ahead are prefetched.
+namespace {
+struct MergeSlot {
+  uint32_t tag;
+  int32_t id;  // −1: empty
+};
+inline uint64_t vertex_hash(const uint64_t b[3]) {
+  uint64_t h = b[0] * 0x9E3779B97F4A7C15ull;
+  h = (h ^ (h >> 29) ^ b[1]) * 0xBF58476D1CE4E5B9ull;
+  h = (h ^ (h >> 31) ^ b[2]) * 0x94D049BB133111EBull;
+  return h ^ (h >> 32);
+}
+inline void vertex_bits(const double* xyz, double v[3], uint64_t b[3]) {
+  for (int k = 0; k < 3; ++k) {
+    v[k] = xyz[k] + 0.0;  // -0.0 + 0.0 = +0.0
+    memcpy(&b[k], &v[k], 8);
+  }
+}
+}  // namespace
+
 int m3d_merge_vertices(const double* xyz, int64_t n, double* uniq, int32_t* inverse,
                        int64_t* n_unique) {
   if (n < 0 || n > INT32_MAX || (n > 0 && (xyz == nullptr || uniq == nullptr || inverse == nullptr)) ||
       n_unique == nullptr)
     return M3D_ERR_INVALID;
-  uint64_t cap = 16;
-  while (cap < 2 * (uint64_t)n) cap <<= 1;
-  std::vector<int32_t> table(cap, -1);
+  uint64_t cap = 1024;
+  while (cap < (uint64_t)n / 4) cap <<= 1;
+  std::vector<MergeSlot> table(cap, MergeSlot{0u, -1});
+  std::vector<uint64_t> hashes;  // only for rehashing: the hash of each unique vertex
+  hashes.reserve((size_t)(cap / 2));
+  constexpr int64_t kAhead = 8;
+  uint64_t hq[kAhead];  // hashes of vertices i .. i + kAhead − 1 (ring)
+  for (int64_t i = 0; i < std::min<int64_t>(n, kAhead); ++i) {
+    double v[3];
+    uint64_t b[3];
+    vertex_bits(xyz + 3 * i, v, b);
+    hq[i] = vertex_hash(b);
+    __builtin_prefetch(&table[hq[i] & (cap - 1)]);
+  }
   int64_t m = 0;
   for (int64_t i = 0; i < n; ++i) {
     double v[3];
     uint64_t b[3];
-    for (int k = 0; k < 3; ++k) {
-      v[k] = xyz[3 * i + k] + 0.0;  // -0.0 + 0.0 = +0.0
-      memcpy(&b[k], &v[k], 8);
+    vertex_bits(xyz + 3 * i, v, b);
+    const uint64_t h = hq[i % kAhead];
+    if (i + kAhead < n) {
+      double v2[3];
+      uint64_t b2[3];
+      vertex_bits(xyz + 3 * (i + kAhead), v2, b2);
+      const uint64_t h2 = vertex_hash(b2);
+      hq[i % kAhead] = h2;
+      __builtin_prefetch(&table[h2 & (cap - 1)]);
     }
-    uint64_t h = b[0] * 0x9E3779B97F4A7C15ull;
-    h = (h ^ (h >> 29) ^ b[1]) * 0xBF58476D1CE4E5B9ull;
-    h = (h ^ (h >> 31) ^ b[2]) * 0x94D049BB133111EBull;
-    h ^= h >> 32;
+    const uint32_t tag = (uint32_t)(h >> 32);
     uint64_t s = h & (cap - 1);
     for (;;) {
-      const int32_t id = table[s];
-      if (id < 0) {
-        table[s] = (int32_t)m;
+      const MergeSlot e = table[s];
+      if (e.id < 0) {
+        table[s] = MergeSlot{tag, (int32_t)m};
         memcpy(uniq + 3 * m, v, sizeof(v));
+        hashes.push_back(h);
         inverse[i] = (int32_t)m;
         ++m;
+        if ((uint64_t)m * 2 > cap) {  // grow: reinsert every unique vertex by its stored hash
+          cap <<= 1;
+          std::vector<MergeSlot> t2(cap, MergeSlot{0u, -1});
+          for (int64_t u = 0; u < m; ++u) {
+            uint64_t s2 = hashes[(size_t)u] & (cap - 1);
+            while (t2[s2].id >= 0) s2 = (s2 + 1) & (cap - 1);
+            t2[s2] = MergeSlot{(uint32_t)(hashes[(size_t)u] >> 32), (int32_t)u};
+          }
+          table.swap(t2);
+        }
         break;
       }
-      if (memcmp(uniq + 3 * (int64_t)id, v, sizeof(v)) == 0) {
-        inverse[i] = id;
+      if (e.tag == tag && memcmp(uniq + 3 * (int64_t)e.id, v, sizeof(v)) == 0) {
+        inverse[i] = e.id;
         break;
       }
       s = (s + 1) & (cap - 1);

@@ -212,3 +212,24 @@ def test_native_vertex_merge_equals_numpy_merge():
                                                 inv.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(m)) == 0
     np.testing.assert_array_equal(uniq[: m.value], ref_v)
     np.testing.assert_array_equal(inv.reshape(-1, 3), ref_f)
+
+
+@pytest.mark.parametrize("n,k", [(12, 3), (300000, 100000), (200001, 7)])
+def test_native_vertex_merge_table_growth(n, k):
+    """The merge table starts at n / 4 slots and doubles at half load: mostly-unique inputs
+    (several doublings), few-unique inputs and tiny inputs all equal the numpy merge."""
+    import ctypes as C
+
+    rng = np.random.default_rng(n)
+    base = rng.integers(-50, 50, size=(k, 3)).astype(np.float64) * 0.5
+    base[rng.random(k) < 0.1, 0] = -0.0
+    flat = np.ascontiguousarray(base[rng.integers(0, k, n)])
+    uniq = np.empty_like(flat)
+    inv = np.empty(n, np.int32)
+    m = C.c_int64(0)
+    P = C.POINTER(C.c_double)
+    assert plyio._text_lib().m3d_merge_vertices(flat.ctypes.data_as(P), n, uniq.ctypes.data_as(P),
+                                                inv.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(m)) == 0
+    ref_v, ref_f = plyio._merge_numpy(flat)
+    np.testing.assert_array_equal(uniq[: m.value], ref_v)
+    np.testing.assert_array_equal(inv, ref_f.reshape(-1))
