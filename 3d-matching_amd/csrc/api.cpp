@@ -1158,18 +1158,31 @@ struct DevTmp {
   ~DevTmp() { hipFree(p); }
 };
 
+// the grids of a hybrid search: cell = radius, plus the finer first-stage grid when the cloud is
+// dense enough (prep.hip hybrid_fine_radius; both cached on the cloud)
+int search_grids(m3d_ctx* ctx, const m3d_cloud* c, double radius, int k, hipStream_t st,
+                 const Grid** g, const Grid** gf, double* hf) {
+  int rc = ensure_grid(ctx, c, radius, st, g);
+  if (rc) return rc;
+  *gf = nullptr;
+  *hf = hybrid_fine_radius(*g, radius, k);
+  if (*hf > 0.0) rc = ensure_grid(ctx, c, *hf, st, gf);
+  return rc;
+}
+
 // hybrid neighbourhoods of every point of `c` (grid cell = radius)
 int neighbourhoods(m3d_ctx* ctx, const m3d_cloud* c, double radius, int k, hipStream_t st,
                    DevTmp<int32_t>& idx, DevTmp<double>& d2, DevTmp<int32_t>& cnt) {
-  const Grid* g = nullptr;
-  int rc = ensure_grid(ctx, c, radius, st, &g);
+  const Grid *g = nullptr, *gf = nullptr;
+  double hf = 0.0;
+  int rc = search_grids(ctx, c, radius, k, st, &g, &gf, &hf);
   if (rc) return rc;
   const int64_t n = std::max<int64_t>(c->n, 1);
   rc = dev_alloc(ctx, &idx.p, n * k);
   if (!rc) rc = dev_alloc(ctx, &d2.p, n * k);
   if (!rc) rc = dev_alloc(ctx, &cnt.p, n);
   if (rc) return rc;
-  HIPX(ctx, hybrid_search(c, g, radius, k, idx.p, d2.p, cnt.p, st));
+  HIPX(ctx, hybrid_search(c, g, radius, k, idx.p, d2.p, cnt.p, st, gf, hf));
   return M3D_OK;
 }
 }  // namespace
@@ -1199,10 +1212,11 @@ int m3d_hybrid_search(m3d_ctx* ctx, const m3d_cloud* cloud, double radius, int32
   CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
-  const Grid* g = nullptr;
-  int rc = ensure_grid(ctx, cloud, radius, st, &g);
+  const Grid *g = nullptr, *gf = nullptr;
+  double hf = 0.0;
+  int rc = search_grids(ctx, cloud, radius, max_nn, st, &g, &gf, &hf);
   if (rc) return rc;
-  HIPX(ctx, hybrid_search(cloud, g, radius, max_nn, idx, d2, count, st));
+  HIPX(ctx, hybrid_search(cloud, g, radius, max_nn, idx, d2, count, st, gf, hf));
   HIPX(ctx, hipStreamSynchronize(st));
   return M3D_OK;
 }

@@ -312,8 +312,12 @@ hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st);
 hipError_t voxel_down_sample(const double* xyz, const double* nrm, int64_t n, double voxel,
                              double* out_xyz, double* out_nrm, int64_t* out_n, hipStream_t st,
                              std::string* why);
+// hybrid (radius + max_nn) neighbour lists; gf / hfine: optional first-stage grid and radius
+// (hybrid_fine_radius), the result is the same list
+double hybrid_fine_radius(const Grid* g, double radius, int k);
 hipError_t hybrid_search(const m3d_cloud* c, const Grid* g, double radius, int k, int32_t* idx,
-                         double* d2, int32_t* cnt, hipStream_t st);
+                         double* d2, int32_t* cnt, hipStream_t st, const Grid* gf = nullptr,
+                         double hfine = 0.0);
 hipError_t launch_normals(const m3d_cloud* c, const int32_t* nbr, int k, const int32_t* cnt,
                           const double* prev, double* out, hipStream_t st);
 hipError_t launch_fpfh(const m3d_cloud* c, const double* nrm, const int32_t* nbr, const double* d2,

@@ -210,11 +210,17 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// Two-stage form (gf.ncells > 0): the wave first searches the box of radius h on a finer grid
+// gf (hybrid_search picks h so that ~2.5k points are expected within it).  The box holds every
+// point within h of the query (the same covering argument as for r), so if k entries are then
+// held and the k-th d² is below h²(1 − 1e-12), every unscanned point — exact distance > h, its
+// fp64 d² at least h²(1 − 4u) — is beyond the k-th entry: the list is final.  Otherwise the list
+// is discarded and the radius-r box is searched as before.  Either way the list is the same.
 template <int kS>
 __global__ __launch_bounds__(256) void hybrid_search_wave_kernel(
     const double* __restrict__ xyz64, const float4* __restrict__ xyz32, int64_t n, GridDev g,
-    float Rf, double r2, double eabs, int k, int32_t* __restrict__ out_idx,
-    double* __restrict__ out_d2, int32_t* __restrict__ out_cnt) {
+    float Rf, double r2, double eabs, int k, GridDev gf, float Hf, double h2safe,
+    int32_t* __restrict__ out_idx, double* __restrict__ out_d2, int32_t* __restrict__ out_cnt) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;  // wave-uniform
@@ -231,7 +237,8 @@ __global__ __launch_bounds__(256) void hybrid_search_wave_kernel(
   double thr = r2;         // exact threshold: r² until k are held, then the k-th entry (inclusive)
   int32_t thr_t = INT32_MAX;
   float bf = prefilter_bound(r2, eabs);
-  if (g.ncells > 0) {
+  auto scan = [&](const GridDev& g, float Rf) {
+    if (g.ncells <= 0) return;
     const int x0 = prep_coord(qf.x - Rf, g.o[0], g.inv_h, g.n[0]);
     const int x1 = prep_coord(qf.x + Rf, g.o[0], g.inv_h, g.n[0]);
     const int y0 = prep_coord(qf.y - Rf, g.o[1], g.inv_h, g.n[1]);
@@ -305,7 +312,24 @@ __global__ __launch_bounds__(256) void hybrid_search_wave_kernel(
           }
         }
       }
+  };
+  bool done = false;
+  if (gf.ncells > 0) {
+    scan(gf, Hf);
+    done = cnt == k && thr < h2safe;  // wave-uniform
+    if (!done) {
+#pragma unroll
+      for (int u = 0; u < kS; ++u) {
+        D[u] = 0.0;
+        T[u] = -1;
+      }
+      cnt = 0;
+      thr = r2;
+      thr_t = INT32_MAX;
+      bf = prefilter_bound(r2, eabs);
+    }
   }
+  if (!done) scan(g, Rf);
 #pragma unroll
   for (int u = 0; u < kS; ++u) {
     const int e = u * 64 + lane;
@@ -708,12 +732,44 @@ hipError_t voxel_down_sample(const double* xyz, const double* nrm, int64_t n, do
   return e;
 }
 
-hipError_t hybrid_search(const m3d_cloud* c, const Grid* g, double radius, int k, int32_t* idx,
-                         double* d2, int32_t* cnt, hipStream_t st) {
-  if (c->n == 0) return hipSuccess;
-  // fp32 box half-width: r plus the centring/rounding error of both fp32 coordinates
+// the fp32 box half-width that covers every point within `radius` (fp64) of a query: the
+// radius plus the centring/rounding error of both fp32 coordinates
+static float box_half_width(const m3d_cloud* c, double radius) {
   const double Rd = (radius + 2.0 * c->rmax * 5.9604644775390625e-08 * 1.01) * (1.0 + 1e-6);
-  const float Rf = (float)Rd * (1.0f + 1e-6f);
+  return (float)Rd * (1.0f + 1e-6f);
+}
+
+double hybrid_fine_radius(const Grid* g, double radius, int k) {
+  // M3D_HYBRID_FINE=0: single-stage search (A/B); otherwise the expected-count factor below
+  static const double c = [] {
+    const char* e = getenv("M3D_HYBRID_FINE");
+    return e ? atof(e) : 0.3;
+  }();
+  if (!(c > 0.0) || k > 128 || g == nullptr || g->n_occ <= 0) return 0.0;
+  // m = points per occupied radius-cell.  On a scanned surface ≈ 8 m (h / r)² points lie within
+  // h (measured: the cfg4 scan, 1144 points within r against m = 139), so h = r·√(c·k / m)
+  // expects ≈ 2.5 k of them at c = 0.3.  The cost of the search is mostly the insertions, about
+  // k·(1 + ln(N / k)) for N points within the searched radius, so a small h pays even though a
+  // query with fewer than k points within it searches again; worth a second grid only well
+  // below r.
+  const double m = (double)g->n_pts / (double)g->n_occ;
+  const double h = radius * sqrt(c * k / m);
+  return h <= 0.6 * radius ? h : 0.0;
+}
+
+hipError_t hybrid_search(const m3d_cloud* c, const Grid* g, double radius, int k, int32_t* idx,
+                         double* d2, int32_t* cnt, hipStream_t st, const Grid* gf, double hfine) {
+  if (c->n == 0) return hipSuccess;
+  const float Rf = box_half_width(c, radius);
+  GridDev gfd{};
+  gfd.ncells = 0;
+  float Hf = 0.0f;
+  double h2safe = 0.0;
+  if (gf != nullptr && hfine > 0.0 && hfine < radius) {
+    gfd = gf->dev;
+    Hf = box_half_width(c, hfine);
+    h2safe = hfine * hfine * (1.0 - 1e-12);
+  }
   const int L = k <= 40 ? 64 : (k <= 80 ? 32 : (k <= 160 ? 16 : 8));
   const size_t lds = (size_t)k * L * (sizeof(double) + sizeof(int32_t));
   const double eabs = 3.4641016151377544 * c->rmax * 5.9604644775390625e-08 * 1.01;
@@ -724,10 +780,12 @@ hipError_t hybrid_search(const m3d_cloud* c, const Grid* g, double radius, int k
   const unsigned wb = (unsigned)((c->n + 3) / 4);  // 4 waves (queries) per 256-thread block
   if (mode != 0 && k <= 64) {
     hybrid_search_wave_kernel<1><<<wb, 256, 0, st>>>(c->xyz64, c->xyz32, c->n, g->dev, Rf,
-                                                     radius * radius, eabs, k, idx, d2, cnt);
+                                                     radius * radius, eabs, k, gfd, Hf, h2safe,
+                                                     idx, d2, cnt);
   } else if (mode != 0 && k <= 128) {
     hybrid_search_wave_kernel<2><<<wb, 256, 0, st>>>(c->xyz64, c->xyz32, c->n, g->dev, Rf,
-                                                     radius * radius, eabs, k, idx, d2, cnt);
+                                                     radius * radius, eabs, k, gfd, Hf, h2safe,
+                                                     idx, d2, cnt);
   } else {
     hybrid_search_kernel<<<(unsigned)((c->n + L - 1) / L), L, lds, st>>>(
         c->xyz64, c->xyz32, c->n, g->dev, Rf, radius * radius, eabs, k, idx, d2, cnt);

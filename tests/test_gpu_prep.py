@@ -40,10 +40,17 @@ def test_voxel_down_sample_rejects_bad_voxel():
         prep.voxel_down_sample(np.array([[0.0, 0, 0], [1e9, 0, 0]]), 1e-3)
 
 
-@pytest.mark.parametrize("case", ["surface", "duplicates", "plane", "offset"])
+@pytest.mark.parametrize("case", ["surface", "duplicates", "plane", "offset", "dense"])
 def test_hybrid_search_exact(case):
+    """Lists equal the oracle's bit for bit.  "plane" and "dense" are dense enough for the
+    two-stage search (prep.hip hybrid_fine_radius: a finer first grid, full search again when
+    fewer than k points lie within its radius), "plane" at k = 30 with many such repeats."""
     rng = np.random.default_rng(3)
-    if case == "surface":
+    radii = [(0.6, 30), (1.5, 100)]
+    if case == "dense":
+        pts, _ = synth.surface_points(60000, seed=7)
+        radii = [(0.6, 30), (1.0, 100)]
+    elif case == "surface":
         pts, _ = synth.surface_points(8000, seed=1)
     elif case == "duplicates":
         pts = np.repeat(rng.normal(size=(400, 3)), 5, axis=0)
@@ -51,7 +58,7 @@ def test_hybrid_search_exact(case):
         pts = np.c_[rng.uniform(-2, 2, (5000, 2)), np.zeros(5000)]
     else:
         pts = synth.surface_points(5000, seed=2)[0] + np.array([2e4, -1e4, 5e3])
-    for radius, k in [(0.6, 30), (1.5, 100)]:
+    for radius, k in radii:
         gi, gd, gc = prep.hybrid_search(pts, radius, k)
         ri, rd, rc = P.hybrid_search(pts, radius, k)
         np.testing.assert_array_equal(gc, rc)
