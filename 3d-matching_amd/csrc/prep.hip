@@ -307,9 +307,11 @@ __global__ __launch_bounds__(256) void hybrid_search_wave_kernel(
                 }
               thr = readlane_f64(dk, l);
               thr_t = __builtin_amdgcn_readlane(tk, l);
-              bf = prefilter_bound(thr, eabs);
             }
           }
+          // the fp32 screen bound follows the k-th entry once per chunk (the entries above were
+          // tested against the exact thr; bf only screens the next chunk)
+          if (cnt == k) bf = prefilter_bound(thr, eabs);
         }
       }
   };
