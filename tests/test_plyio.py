@@ -233,3 +233,39 @@ def test_native_vertex_merge_table_growth(n, k):
     ref_v, ref_f = plyio._merge_numpy(flat)
     np.testing.assert_array_equal(uniq[: m.value], ref_v)
     np.testing.assert_array_equal(inv, ref_f.reshape(-1))
+
+
+def test_native_ascii_parser_large_input():
+    """A multi-megabyte vertex block: the same doubles, blank lines and CRLF anywhere, the rows
+    stop exactly at the declared count even when numeric rows (faces) follow, and errors deep
+    inside or a short block are reported."""
+    import ctypes as C
+
+    from m3d import _lib
+
+    lib = _lib.load()
+    rng = np.random.default_rng(11)
+    n = 60000
+    vals = rng.normal(size=(n, 3)) * 10.0 ** rng.integers(-5, 5, (n, 1))
+    lines = []
+    for k, row in enumerate(vals):
+        lines.append(" ".join(repr(float(v)) for v in row) + ("\r\n" if k % 3 == 0 else "\n"))
+        if k % 97 == 0:
+            lines.append(" \t\n")
+    faces = "".join(f"3 {k} {k + 1} {k + 2}\n" for k in range(500))
+    buf = "".join(lines).encode() + faces.encode()
+    assert len(buf) > 1 << 20
+    out = np.empty_like(vals)
+    used = C.c_size_t(0)
+    P = C.POINTER(C.c_double)
+    assert lib.m3d_parse_ascii_rows(buf, len(buf), n, 3, out.ctypes.data_as(P), C.byref(used)) == 0
+    np.testing.assert_array_equal(out, vals)
+    assert buf[used.value:] == faces.encode()
+    # a bad row deep inside, and a declared count beyond the rows present, are refused
+    bad = bytearray(buf)
+    pos = len(buf) * 2 // 3
+    pos = buf.index(b"\n", pos) + 1
+    bad[pos:pos + 1] = b"x"
+    assert lib.m3d_parse_ascii_rows(bytes(bad), len(bad), n, 3, out.ctypes.data_as(P), C.byref(used)) != 0
+    short = "".join(lines).encode()
+    assert lib.m3d_parse_ascii_rows(short, len(short), n + 1, 3, out.ctypes.data_as(P), C.byref(used)) != 0
