@@ -215,6 +215,7 @@ void m3d_destroy(m3d_ctx* ctx) {
   if (ctx->scratch_ev) hipEventDestroy(ctx->scratch_ev);
   if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->one_ticket) hipFree(ctx->one_ticket);
+  if (ctx->prep) hipFree(ctx->prep);
   for (auto& v : ctx->ev)
     for (auto& pr : v) {
       hipEventDestroy(pr.first);
@@ -1170,19 +1171,51 @@ int search_grids(m3d_ctx* ctx, const m3d_cloud* c, double radius, int k, hipStre
   return rc;
 }
 
+// Neighbour lists of the synchronous preprocessing calls (estimate_normals, compute_fpfh): a
+// context-owned device buffer, grown on demand and reused — the lists of a 180k-point cloud at
+// k = 30 take 65 MB, whose hipMalloc + hipFree per call cost more than the normals kernel.  Safe
+// to reuse because those entry points synchronise their stream before returning and a context
+// serves one host thread (m3d.h).
+struct NbrLists {
+  int32_t* idx = nullptr;
+  double* d2 = nullptr;
+  int32_t* cnt = nullptr;
+  double* extra = nullptr;  // caller's n × extra_per_point doubles (FPFH: the SPFH rows)
+};
+
+int prep_lists(m3d_ctx* ctx, int64_t n, int k, int64_t extra_per_point, NbrLists* L) {
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bi = up(sizeof(int32_t) * (size_t)n * k), bd = up(sizeof(double) * (size_t)n * k);
+  const size_t bc = up(sizeof(int32_t) * (size_t)n), be = up(sizeof(double) * (size_t)(n * extra_per_point));
+  const size_t need = bi + bd + bc + be;
+  if (need > ctx->prep_bytes) {
+    if (ctx->prep) hipFree(ctx->prep);
+    ctx->prep = nullptr;
+    ctx->prep_bytes = 0;
+    if (hipMalloc(&ctx->prep, need) != hipSuccess) {
+      ctx->prep = nullptr;
+      return m3d_fail(ctx, M3D_ERR_OOM, "hipMalloc: neighbour lists");
+    }
+    ctx->prep_bytes = need;
+  }
+  char* b = static_cast<char*>(ctx->prep);
+  L->idx = reinterpret_cast<int32_t*>(b);
+  L->d2 = reinterpret_cast<double*>(b + bi);
+  L->cnt = reinterpret_cast<int32_t*>(b + bi + bd);
+  L->extra = reinterpret_cast<double*>(b + bi + bd + bc);
+  return M3D_OK;
+}
+
 // hybrid neighbourhoods of every point of `c` (grid cell = radius)
 int neighbourhoods(m3d_ctx* ctx, const m3d_cloud* c, double radius, int k, hipStream_t st,
-                   DevTmp<int32_t>& idx, DevTmp<double>& d2, DevTmp<int32_t>& cnt) {
+                   int64_t extra_per_point, NbrLists* L) {
   const Grid *g = nullptr, *gf = nullptr;
   double hf = 0.0;
   int rc = search_grids(ctx, c, radius, k, st, &g, &gf, &hf);
   if (rc) return rc;
-  const int64_t n = std::max<int64_t>(c->n, 1);
-  rc = dev_alloc(ctx, &idx.p, n * k);
-  if (!rc) rc = dev_alloc(ctx, &d2.p, n * k);
-  if (!rc) rc = dev_alloc(ctx, &cnt.p, n);
+  rc = prep_lists(ctx, std::max<int64_t>(c->n, 1), k, extra_per_point, L);
   if (rc) return rc;
-  HIPX(ctx, hybrid_search(c, g, radius, k, idx.p, d2.p, cnt.p, st, gf, hf));
+  HIPX(ctx, hybrid_search(c, g, radius, k, L->idx, L->d2, L->cnt, st, gf, hf));
   return M3D_OK;
 }
 }  // namespace
@@ -1228,11 +1261,10 @@ int m3d_estimate_normals(m3d_ctx* ctx, const m3d_cloud* cloud, double radius, in
   CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
-  DevTmp<int32_t> idx, cnt;
-  DevTmp<double> d2;
-  int rc = neighbourhoods(ctx, cloud, radius, max_nn, st, idx, d2, cnt);
+  NbrLists L;
+  int rc = neighbourhoods(ctx, cloud, radius, max_nn, st, 0, &L);
   if (rc) return rc;
-  HIPX(ctx, launch_normals(cloud, idx.p, max_nn, cnt.p, cloud->nrm64, normals_out, st));
+  HIPX(ctx, launch_normals(cloud, L.idx, max_nn, L.cnt, cloud->nrm64, normals_out, st));
   HIPX(ctx, hipStreamSynchronize(st));
   return M3D_OK;
 }
@@ -1245,12 +1277,10 @@ int m3d_compute_fpfh(m3d_ctx* ctx, const m3d_cloud* cloud, const double* normals
   CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
-  DevTmp<int32_t> idx, cnt;
-  DevTmp<double> d2, spfh;
-  int rc = neighbourhoods(ctx, cloud, radius, max_nn, st, idx, d2, cnt);
-  if (!rc) rc = dev_alloc(ctx, &spfh.p, std::max<int64_t>(cloud->n, 1) * 33);
+  NbrLists L;
+  int rc = neighbourhoods(ctx, cloud, radius, max_nn, st, 33, &L);
   if (rc) return rc;
-  HIPX(ctx, launch_fpfh(cloud, normals, idx.p, d2.p, max_nn, cnt.p, spfh.p, fpfh_out, st));
+  HIPX(ctx, launch_fpfh(cloud, normals, L.idx, L.d2, max_nn, L.cnt, L.extra, fpfh_out, st));
   HIPX(ctx, hipStreamSynchronize(st));
   return M3D_OK;
 }

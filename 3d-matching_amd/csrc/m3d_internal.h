@@ -133,6 +133,9 @@ struct m3d_ctx {
   void* pin = nullptr;
   void* pin_dev = nullptr;
   uint32_t* one_ticket = nullptr;  // device: last-block ticket of count_one_kernel (kept at 0)
+  // neighbour lists of the synchronous preprocessing calls (api.cpp prep_lists), grown on demand
+  void* prep = nullptr;
+  size_t prep_bytes = 0;
 };
 
 struct m3d_corrset {
