@@ -10,20 +10,84 @@
 #include <system_error>
 #include <vector>
 #include <algorithm>
+#include <thread>
 
 #include "../../include/m3d.h"
 
 namespace {
 inline bool is_blank(char c) { return c == ' ' || c == '\t' || c == '\r'; }
+
+// Exact fast path for the plain decimals of point files: [-]digits[.digits][(e|E)[±]digits]
+// with at most 19 significant digits w and a decimal exponent |q| ≤ 27.  w and 10^|q| are exact
+// in the x87 80-bit format (64-bit significand; 5^27 < 2^64), so w·10^q (or w / 10^−q) is ONE
+// correctly rounded extended-precision operation; converting that to double is a second
+// rounding, which can differ from the correctly rounded double only when the extended result
+// lies within one extended ulp of a point halfway between two doubles (its low 11 significand
+// bits 0x3FF–0x401) — those, and everything outside the form, return nullptr and take
+// std::from_chars.  Results in this range are normal doubles (|x| in [1e-27, 1e46]).
+const long double kPow10L[28] = {1e0L,  1e1L,  1e2L,  1e3L,  1e4L,  1e5L,  1e6L,  1e7L,  1e8L,  1e9L,
+                                 1e10L, 1e11L, 1e12L, 1e13L, 1e14L, 1e15L, 1e16L, 1e17L, 1e18L, 1e19L,
+                                 1e20L, 1e21L, 1e22L, 1e23L, 1e24L, 1e25L, 1e26L, 1e27L};
+
+inline const char* parse_decimal_fast(const char* p, const char* e, double* out) {
+  const char* s = p;
+  const bool neg = s < e && *s == '-';
+  s += neg;
+  // w < 10^18 before each digit keeps w < 10^19 < 2^64: at most 19 significant digits
+  constexpr uint64_t kW18 = 1000000000000000000ull;
+  uint64_t w = 0;
+  int q = 0;
+  const char* const ds = s;
+  while (s < e && (unsigned)(*s - '0') < 10) {
+    if (w >= kW18) return nullptr;
+    w = w * 10 + (unsigned)(*s++ - '0');
+  }
+  bool any = s > ds;
+  if (s < e && *s == '.') {
+    const char* const fs = ++s;
+    while (s < e && (unsigned)(*s - '0') < 10) {
+      if (w >= kW18) return nullptr;
+      w = w * 10 + (unsigned)(*s++ - '0');
+    }
+    q = -(int)(s - fs);
+    any |= s > fs;
+  }
+  if (!any) return nullptr;
+  if (s < e && (*s == 'e' || *s == 'E')) {
+    ++s;
+    bool eneg = false;
+    if (s < e && (*s == '-' || *s == '+')) eneg = *s++ == '-';
+    int x = 0, xd = 0;
+    while (s < e && (unsigned)(*s - '0') < 10 && xd < 5) x = x * 10 + (*s++ - '0'), ++xd;
+    if (xd == 0 || xd == 5) return nullptr;
+    q += eneg ? -x : x;
+  }
+  double v;
+  if (w == 0) {
+    v = 0.0;
+  } else if (q == 0) {
+    v = (double)w;  // one correctly rounded conversion
+  } else {
+    if (q > 27 || q < -27) return nullptr;
+    const long double L = q > 0 ? (long double)w * kPow10L[q] : (long double)w / kPow10L[-q];
+    uint64_t m;
+    memcpy(&m, &L, sizeof(m));  // x87 extended: the 64-bit significand comes first
+    const uint64_t lo = m & 0x7FF;
+    if (lo >= 0x3FF && lo <= 0x401) return nullptr;
+    v = (double)L;
+  }
+  *out = neg ? -v : v;
+  return s;
+}
 }  // namespace
 
 extern "C" {
 
-int m3d_parse_ascii_rows(const char* buf, size_t len, int64_t rows, int32_t cols, double* out,
-                         size_t* consumed) {
-  if ((len > 0 && buf == nullptr) || rows < 0 || cols <= 0 || (rows > 0 && out == nullptr) ||
-      consumed == nullptr)
-    return M3D_ERR_INVALID;
+namespace {
+// serial parse of `rows` rows from [buf, buf + len): the rows' numbers into out, *consumed = bytes
+// up to and including the last row's newline
+int parse_rows_serial(const char* buf, size_t len, int64_t rows, int32_t cols, double* out,
+                      size_t* consumed) {
   const char* p = buf;
   const char* const e = buf + len;
   int64_t r = 0;
@@ -35,11 +99,16 @@ int m3d_parse_ascii_rows(const char* buf, size_t len, int64_t rows, int32_t cols
       if (p >= e || *p == '\n') break;
       if (c == cols) return M3D_ERR_INVALID;  // more numbers on the row than properties
       double v;
-      const std::from_chars_result res = std::from_chars(p, e, v);
-      if (res.ec != std::errc() || (res.ptr < e && !is_blank(*res.ptr) && *res.ptr != '\n'))
+      const char* end = parse_decimal_fast(p, e, &v);
+      if (end == nullptr) {
+        const std::from_chars_result res = std::from_chars(p, e, v);
+        if (res.ec != std::errc()) return M3D_ERR_INVALID;
+        end = res.ptr;
+      }
+      if (end < e && !is_blank(*end) && *end != '\n')
         return M3D_ERR_INVALID;  // not a plain number (the caller falls back to numpy)
       out[r * cols + c++] = v;
-      p = res.ptr;
+      p = end;
     }
     if (p < e) ++p;  // the newline
     if (c == 0) continue;  // blank line
@@ -47,6 +116,71 @@ int m3d_parse_ascii_rows(const char* buf, size_t len, int64_t rows, int32_t cols
     ++r;
   }
   *consumed = (size_t)(p - buf);
+  return M3D_OK;
+}
+
+// rows (lines holding anything but blanks) in [b, e): the serial parser's row rule
+int64_t count_rows(const char* b, const char* e) {
+  int64_t n = 0;
+  bool any = false;
+  for (const char* p = b; p < e; ++p) {
+    const char c = *p;
+    if (c == '\n') {
+      n += any;
+      any = false;
+    } else {
+      any |= !is_blank(c);
+    }
+  }
+  return n + any;
+}
+}  // namespace
+
+// Large inputs are parsed by several threads: the buffer is cut into chunks at line starts, each
+// thread counts its chunk's rows, the prefix sums place every chunk's rows in `out` (and find the
+// chunk holding the last row to parse), then the chunks are parsed in parallel.  (The fast
+// decimal path scales across threads; std::from_chars of this libstdc++ hardly does.)
+int m3d_parse_ascii_rows(const char* buf, size_t len, int64_t rows, int32_t cols, double* out,
+                         size_t* consumed) {
+  if ((len > 0 && buf == nullptr) || rows < 0 || cols <= 0 || (rows > 0 && out == nullptr) ||
+      consumed == nullptr)
+    return M3D_ERR_INVALID;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int T = (int)std::min<size_t>({(size_t)16, (size_t)hw, len / ((size_t)1 << 18)});
+  if (T < 2 || rows < 4096) return parse_rows_serial(buf, len, rows, cols, out, consumed);
+  std::vector<size_t> cut((size_t)T + 1, len);
+  cut[0] = 0;
+  for (int t = 1; t < T; ++t) {
+    const size_t c = std::max(cut[t - 1], len / T * (size_t)t);
+    const void* nl = c < len ? memchr(buf + c, '\n', len - c) : nullptr;
+    cut[t] = nl ? (size_t)((const char*)nl - buf) + 1 : len;
+  }
+  std::vector<int64_t> nrow((size_t)T, 0);
+  std::vector<int> rc((size_t)T, M3D_OK);
+  std::vector<size_t> used((size_t)T, 0);
+  auto run = [&](auto&& body) {
+    std::vector<std::thread> th;
+    th.reserve((size_t)T - 1);
+    for (int t = 1; t < T; ++t) th.emplace_back(body, t);
+    body(0);
+    for (auto& x : th) x.join();
+  };
+  run([&](int t) { nrow[t] = count_rows(buf + cut[t], buf + cut[t + 1]); });
+  std::vector<int64_t> first((size_t)T + 1, 0);
+  for (int t = 0; t < T; ++t) first[t + 1] = first[t] + nrow[t];
+  if (first[T] < rows) return M3D_ERR_INVALID;  // fewer rows than declared
+  run([&](int t) {
+    const int64_t want = std::min(nrow[t], rows - first[t]);
+    if (want <= 0) return;
+    rc[t] = parse_rows_serial(buf + cut[t], cut[t + 1] - cut[t], want, cols, out + first[t] * cols,
+                              &used[t]);
+  });
+  int last = 0;
+  for (int t = 0; t < T; ++t) {
+    if (rc[t] != M3D_OK) return rc[t];
+    if (first[t] < rows) last = t;
+  }
+  *consumed = cut[last] + used[last];
   return M3D_OK;
 }
 

@@ -269,3 +269,34 @@ def test_native_ascii_parser_large_input():
     assert lib.m3d_parse_ascii_rows(bytes(bad), len(bad), n, 3, out.ctypes.data_as(P), C.byref(used)) != 0
     short = "".join(lines).encode()
     assert lib.m3d_parse_ascii_rows(short, len(short), n + 1, 3, out.ctypes.data_as(P), C.byref(used)) != 0
+
+
+def test_native_ascii_parser_fast_path_exact():
+    """hostio.cpp's fast decimal path (≤ 19 significant digits, |exponent| ≤ 27, one x87
+    extended operation, results near a double halfway point sent to std::from_chars) returns the
+    correctly rounded double: random values in the formats point files use, exact ties between
+    two doubles, 19 / 20-digit mantissas, signed zeros and exponent spellings — bit for bit
+    against Python's float() (correctly rounded), on a block large enough for the threaded path."""
+    import ctypes as C
+
+    from m3d import _lib
+
+    lib = _lib.load()
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(-10, 10, 40000), rng.normal(size=20000) * 10.0 ** rng.integers(-12, 12, 20000),
+                        rng.uniform(-5, 5, 20000).astype(np.float32).astype(np.float64)])
+    fmts = ["{!r}", "{:.17g}", "{:.16g}", "{:.15g}", "{:.9g}", "{:.6f}", "{:.3e}", "{:.12E}"]
+    toks = [fmts[k % len(fmts)].format(float(v)) for k, v in enumerate(x)]
+    toks += ["9007199254740993e1", "9007199254740993", "9007199254740995e-1", "4503599627370497.5",
+             "1234567890123456789", "12345678901234567890", "0.1234567890123456789", "-0.0", "0.000",
+             ".5", "5.", "1e5", "1E+05", "2.5e-27", "2.5e27", "7e-28", "7e28", "123456789012345678e-27"]
+    toks += toks[-18:] * 2
+    toks = toks[: len(toks) // 3 * 3]
+    buf = ("\n".join(" ".join(toks[i:i + 3]) for i in range(0, len(toks), 3)) + "\n").encode()
+    rows = len(toks) // 3
+    out = np.empty((rows, 3))
+    used = C.c_size_t(0)
+    assert lib.m3d_parse_ascii_rows(buf, len(buf), rows, 3, out.ctypes.data_as(C.POINTER(C.c_double)),
+                                    C.byref(used)) == 0
+    exp = np.array([float(t) for t in toks]).reshape(-1, 3)
+    np.testing.assert_array_equal(out.view(np.uint64), exp.view(np.uint64))
