@@ -184,21 +184,63 @@ int m3d_parse_ascii_rows(const char* buf, size_t len, int64_t rows, int32_t cols
   return M3D_OK;
 }
 
+namespace {
+// rows [r0, r1) as text into [p, e): nullptr if it does not fit
+char* format_rows(const double* data, int64_t r0, int64_t r1, int32_t cols, char* p, char* e) {
+  for (int64_t r = r0; r < r1; ++r)
+    for (int32_t c = 0; c < cols; ++c) {
+      if (e - p < 32) return nullptr;  // a double takes at most 24 characters
+      const std::to_chars_result res = std::to_chars(p, e, data[r * cols + c]);
+      if (res.ec != std::errc()) return nullptr;
+      p = res.ptr;
+      *p++ = (c + 1 < cols) ? ' ' : '\n';
+    }
+  return p;
+}
+}  // namespace
+
+// Large blocks are formatted by several threads into their own buffers (std::to_chars is
+// locale-free), then copied into `out` in row order.
 int m3d_format_ascii_rows(const double* data, int64_t rows, int32_t cols, char* out, size_t cap,
                           size_t* written) {
   if (rows < 0 || cols <= 0 || (rows > 0 && (data == nullptr || out == nullptr)) || written == nullptr)
     return M3D_ERR_INVALID;
-  char* p = out;
-  char* const e = out + cap;
-  for (int64_t r = 0; r < rows; ++r)
-    for (int32_t c = 0; c < cols; ++c) {
-      if (e - p < 32) return M3D_ERR_INVALID;  // a double takes at most 24 characters
-      const std::to_chars_result res = std::to_chars(p, e, data[r * cols + c]);
-      if (res.ec != std::errc()) return M3D_ERR_INVALID;
-      p = res.ptr;
-      *p++ = (c + 1 < cols) ? ' ' : '\n';
-    }
-  *written = (size_t)(p - out);
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int T = (int)std::min<int64_t>({(int64_t)16, (int64_t)hw, rows * cols / 32768});
+  if (T < 2) {
+    char* p = format_rows(data, 0, rows, cols, out, out + cap);
+    if (p == nullptr) return M3D_ERR_INVALID;
+    *written = (size_t)(p - out);
+    return M3D_OK;
+  }
+  std::vector<std::vector<char>> part((size_t)T);
+  std::vector<size_t> len((size_t)T, 0);
+  std::vector<int> ok((size_t)T, 1);
+  auto body = [&](int t) {
+    const int64_t r0 = rows * t / T, r1 = rows * (t + 1) / T;
+    part[t].resize((size_t)(r1 - r0) * (size_t)cols * 25 + 32);
+    char* b = part[t].data();
+    char* p = format_rows(data, r0, r1, cols, b, b + part[t].size());
+    ok[t] = p != nullptr;
+    len[t] = p ? (size_t)(p - b) : 0;
+  };
+  std::vector<std::thread> th;
+  th.reserve((size_t)T - 1);
+  for (int t = 1; t < T; ++t) th.emplace_back(body, t);
+  body(0);
+  for (auto& x : th) x.join();
+  size_t total = 0;
+  for (int t = 0; t < T; ++t) {
+    if (!ok[t]) return M3D_ERR_INVALID;
+    total += len[t];
+  }
+  if (total > cap) return M3D_ERR_INVALID;
+  size_t off = 0;
+  for (int t = 0; t < T; ++t) {
+    memcpy(out + off, part[t].data(), len[t]);
+    off += len[t];
+  }
+  *written = total;
   return M3D_OK;
 }
 
