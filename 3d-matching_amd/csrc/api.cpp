@@ -1183,22 +1183,29 @@ struct NbrLists {
   double* extra = nullptr;  // caller's n × extra_per_point doubles (FPFH: the SPFH rows)
 };
 
-int prep_lists(m3d_ctx* ctx, int64_t n, int k, int64_t extra_per_point, NbrLists* L) {
-  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t bi = up(sizeof(int32_t) * (size_t)n * k), bd = up(sizeof(double) * (size_t)n * k);
-  const size_t bc = up(sizeof(int32_t) * (size_t)n), be = up(sizeof(double) * (size_t)(n * extra_per_point));
-  const size_t need = bi + bd + bc + be;
+// the context's preprocessing buffer with at least `need` bytes (grown, never shrunk)
+int prep_buffer(m3d_ctx* ctx, size_t need, char** out) {
   if (need > ctx->prep_bytes) {
     if (ctx->prep) hipFree(ctx->prep);
     ctx->prep = nullptr;
     ctx->prep_bytes = 0;
     if (hipMalloc(&ctx->prep, need) != hipSuccess) {
       ctx->prep = nullptr;
-      return m3d_fail(ctx, M3D_ERR_OOM, "hipMalloc: neighbour lists");
+      return m3d_fail(ctx, M3D_ERR_OOM, "hipMalloc: preprocessing scratch");
     }
     ctx->prep_bytes = need;
   }
-  char* b = static_cast<char*>(ctx->prep);
+  *out = static_cast<char*>(ctx->prep);
+  return M3D_OK;
+}
+
+int prep_lists(m3d_ctx* ctx, int64_t n, int k, int64_t extra_per_point, NbrLists* L) {
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bi = up(sizeof(int32_t) * (size_t)n * k), bd = up(sizeof(double) * (size_t)n * k);
+  const size_t bc = up(sizeof(int32_t) * (size_t)n), be = up(sizeof(double) * (size_t)(n * extra_per_point));
+  char* b = nullptr;
+  const int rc = prep_buffer(ctx, bi + bd + bc + be, &b);
+  if (rc) return rc;
   L->idx = reinterpret_cast<int32_t*>(b);
   L->d2 = reinterpret_cast<double*>(b + bi);
   L->cnt = reinterpret_cast<int32_t*>(b + bi + bd);
@@ -1230,8 +1237,12 @@ int m3d_voxel_down_sample(m3d_ctx* ctx, const double* xyz, const double* normals
   CHECK_ARG(ctx, n == 0 || (xyz && out_xyz), "null device pointer");
   hipSetDevice(ctx->device);
   std::string why;
+  // scratch from the context's preprocessing buffer: the call synchronises before returning
+  char* scratch = nullptr;
+  int rc = n > 0 ? prep_buffer(ctx, voxel_scratch_bytes(n), &scratch) : M3D_OK;
+  if (rc) return rc;
   hipError_t e = voxel_down_sample(xyz, normals, n, voxel_size, out_xyz, normals ? out_normals : nullptr,
-                                   out_n, S(stream), &why);
+                                   out_n, scratch, S(stream), &why);
   if (e != hipSuccess)
     return m3d_fail(ctx, why.empty() ? M3D_ERR_HIP : M3D_ERR_INVALID,
                     why.empty() ? std::string("voxel_down_sample: ") + hipGetErrorString(e) : why);

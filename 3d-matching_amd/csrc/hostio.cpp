@@ -6,6 +6,7 @@
 // std::to_chars (the shortest representation that reads back to the same double).
 #include <charconv>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <system_error>
 #include <vector>
@@ -16,6 +17,16 @@
 
 namespace {
 inline bool is_blank(char c) { return c == ' ' || c == '\t' || c == '\r'; }
+
+// threads of the text helpers: min(16, hardware threads, M3D_HOST_THREADS if set)
+int host_threads() {
+  static const int t = [] {
+    int v = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = getenv("M3D_HOST_THREADS")) v = std::max(1, std::min(v, atoi(e)));
+    return v;
+  }();
+  return t;
+}
 
 // Exact fast path for the plain decimals of point files: [-]digits[.digits][(e|E)[±]digits]
 // with at most 19 significant digits w and a decimal exponent |q| ≤ 27.  w and 10^|q| are exact
@@ -145,8 +156,7 @@ int m3d_parse_ascii_rows(const char* buf, size_t len, int64_t rows, int32_t cols
   if ((len > 0 && buf == nullptr) || rows < 0 || cols <= 0 || (rows > 0 && out == nullptr) ||
       consumed == nullptr)
     return M3D_ERR_INVALID;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int T = (int)std::min<size_t>({(size_t)16, (size_t)hw, len / ((size_t)1 << 18)});
+  const int T = (int)std::min<size_t>((size_t)host_threads(), len / ((size_t)1 << 18));
   if (T < 2 || rows < 4096) return parse_rows_serial(buf, len, rows, cols, out, consumed);
   std::vector<size_t> cut((size_t)T + 1, len);
   cut[0] = 0;
@@ -205,8 +215,7 @@ int m3d_format_ascii_rows(const double* data, int64_t rows, int32_t cols, char* 
                           size_t* written) {
   if (rows < 0 || cols <= 0 || (rows > 0 && (data == nullptr || out == nullptr)) || written == nullptr)
     return M3D_ERR_INVALID;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int T = (int)std::min<int64_t>({(int64_t)16, (int64_t)hw, rows * cols / 32768});
+  const int T = (int)std::min<int64_t>((int64_t)host_threads(), rows * cols / 32768);
   if (T < 2) {
     char* p = format_rows(data, 0, rows, cols, out, out + cap);
     if (p == nullptr) return M3D_ERR_INVALID;

@@ -312,9 +312,10 @@ hipError_t launch_validate(const Grid* qgrid, int64_t ns, const double* src64, c
 hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st);
 
 // preprocessing (prep.hip) and feature matching (feat.hip)
+size_t voxel_scratch_bytes(int64_t n);  // device scratch voxel_down_sample needs for n points
 hipError_t voxel_down_sample(const double* xyz, const double* nrm, int64_t n, double voxel,
-                             double* out_xyz, double* out_nrm, int64_t* out_n, hipStream_t st,
-                             std::string* why);
+                             double* out_xyz, double* out_nrm, int64_t* out_n, void* scratch,
+                             hipStream_t st, std::string* why);
 // hybrid (radius + max_nn) neighbour lists; gf / hfine: optional first-stage grid and radius
 // (hybrid_fine_radius), the result is the same list
 double hybrid_fine_radius(const Grid* g, double radius, int k);

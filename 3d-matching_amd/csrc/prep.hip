@@ -665,20 +665,56 @@ static void free_all(std::initializer_list<void*> ps) {
   for (void* p : ps) hipFree(p);
 }
 
+// Device scratch of voxel_down_sample for n points (the caller's buffer, api.cpp): block
+// partials of the bounds, 64-bit keys (in / sorted / unique), indices (in / sorted), run counts,
+// offsets, the run count, and hipcub's temporary storage.
+namespace {
+struct VoxelScratch {
+  size_t part, kin, kout, uniq, vin, vout, counts, offs, nruns, tmp, total, tmp_bytes;
+};
+VoxelScratch voxel_layout(int64_t n, int nb) {
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  VoxelScratch L{};
+  size_t tb = 0, tb2 = 0, tb3 = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                     (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 63, (hipStream_t)0);
+  hipcub::DeviceRunLengthEncode::Encode(nullptr, tb2, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                        (int32_t*)nullptr, (int32_t*)nullptr, (int)n, (hipStream_t)0);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, (int32_t*)nullptr, (int32_t*)nullptr, (int)n,
+                                   (hipStream_t)0);
+  L.tmp_bytes = std::max({tb, tb2, tb3, (size_t)1});
+  size_t o = 0;
+  L.part = o, o += up(sizeof(double) * 6 * (size_t)nb);
+  L.kin = o, o += up(8 * (size_t)n);
+  L.kout = o, o += up(8 * (size_t)n);
+  L.uniq = o, o += up(8 * (size_t)n);
+  L.vin = o, o += up(4 * (size_t)n);
+  L.vout = o, o += up(4 * (size_t)n);
+  L.counts = o, o += up(4 * (size_t)n);
+  L.offs = o, o += up(4 * (size_t)n);
+  L.nruns = o, o += up(4);
+  L.tmp = o, o += up(L.tmp_bytes);
+  L.total = o;
+  return L;
+}
+int voxel_blocks(int64_t n) { return (int)std::min<int64_t>(1024, (n + kPrepBlock - 1) / kPrepBlock); }
+}  // namespace
+
+size_t voxel_scratch_bytes(int64_t n) { return n > 0 ? voxel_layout(n, voxel_blocks(n)).total : 0; }
+
 hipError_t voxel_down_sample(const double* xyz, const double* nrm, int64_t n, double voxel,
-                             double* out_xyz, double* out_nrm, int64_t* out_n, hipStream_t st,
-                             std::string* why) {
+                             double* out_xyz, double* out_nrm, int64_t* out_n, void* scratch,
+                             hipStream_t st, std::string* why) {
   *out_n = 0;
   if (n == 0) return hipSuccess;
-  const int nb = (int)std::min<int64_t>(1024, (n + kPrepBlock - 1) / kPrepBlock);
-  double* part = nullptr;
-  hipError_t e = hipMalloc(&part, sizeof(double) * 6 * nb);
-  if (e != hipSuccess) return e;
+  const int nb = voxel_blocks(n);
+  const VoxelScratch L = voxel_layout(n, nb);
+  char* S = static_cast<char*>(scratch);
+  double* part = reinterpret_cast<double*>(S + L.part);
   minmax3d_kernel<<<nb, kPrepBlock, 0, st>>>(xyz, n, part);
   std::vector<double> hp(6 * (size_t)nb);
-  e = hipMemcpyAsync(hp.data(), part, sizeof(double) * 6 * nb, hipMemcpyDeviceToHost, st);
+  hipError_t e = hipMemcpyAsync(hp.data(), part, sizeof(double) * 6 * nb, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  hipFree(part);
   if (e != hipSuccess) return e;
   double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
   for (int b = 0; b < nb; ++b)
@@ -695,32 +731,26 @@ hipError_t voxel_down_sample(const double* xyz, const double* nrm, int64_t n, do
       return hipErrorInvalidValue;
     }
   }
-  uint64_t *kin = nullptr, *kout = nullptr, *uniq = nullptr;
-  int32_t *vin = nullptr, *vout = nullptr, *counts = nullptr, *offs = nullptr, *nruns = nullptr;
-  void* tmp = nullptr;
-  size_t tb = 0, tb2 = 0, tb3 = 0;
-  auto cleanup = [&]() { free_all({kin, kout, uniq, vin, vout, counts, offs, nruns, tmp}); };
-  if ((e = hipMalloc(&kin, 8 * n)) != hipSuccess || (e = hipMalloc(&kout, 8 * n)) != hipSuccess ||
-      (e = hipMalloc(&uniq, 8 * n)) != hipSuccess || (e = hipMalloc(&vin, 4 * n)) != hipSuccess ||
-      (e = hipMalloc(&vout, 4 * n)) != hipSuccess || (e = hipMalloc(&counts, 4 * n)) != hipSuccess ||
-      (e = hipMalloc(&offs, 4 * n)) != hipSuccess || (e = hipMalloc(&nruns, 4)) != hipSuccess) {
-    cleanup();
-    return e;
-  }
+  uint64_t* kin = reinterpret_cast<uint64_t*>(S + L.kin);
+  uint64_t* kout = reinterpret_cast<uint64_t*>(S + L.kout);
+  uint64_t* uniq = reinterpret_cast<uint64_t*>(S + L.uniq);
+  int32_t* vin = reinterpret_cast<int32_t*>(S + L.vin);
+  int32_t* vout = reinterpret_cast<int32_t*>(S + L.vout);
+  int32_t* counts = reinterpret_cast<int32_t*>(S + L.counts);
+  int32_t* offs = reinterpret_cast<int32_t*>(S + L.offs);
+  int32_t* nruns = reinterpret_cast<int32_t*>(S + L.nruns);
+  void* tmp = S + L.tmp;
+  size_t tb = L.tmp_bytes;
   const unsigned blocks = (unsigned)((n + kPrepBlock - 1) / kPrepBlock);
   voxel_key_kernel<<<blocks, kPrepBlock, 0, st>>>(xyz, n, vmin[0], vmin[1], vmin[2], voxel, kin, vin);
-  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, (int)n, 0, 63, st);
-  if (e == hipSuccess)
-    e = hipcub::DeviceRunLengthEncode::Encode(nullptr, tb2, kout, uniq, counts, nruns, (int)n, st);
-  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, counts, offs, (int)n, st);
-  if (e == hipSuccess) e = hipMalloc(&tmp, std::max({tb, tb2, tb3, (size_t)1}));
-  if (e == hipSuccess)
-    e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)n, 0, 63, st);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)n, 0, 63, st);
   // counts past the number of runs stay zero, so the scan is well defined over all n entries
   if (e == hipSuccess) e = hipMemsetAsync(counts, 0, 4 * n, st);
+  tb = L.tmp_bytes;
   if (e == hipSuccess)
-    e = hipcub::DeviceRunLengthEncode::Encode(tmp, tb2, kout, uniq, counts, nruns, (int)n, st);
-  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb3, counts, offs, (int)n, st);
+    e = hipcub::DeviceRunLengthEncode::Encode(tmp, tb, kout, uniq, counts, nruns, (int)n, st);
+  tb = L.tmp_bytes;
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, counts, offs, (int)n, st);
   if (e == hipSuccess) {
     voxel_mean_kernel<<<blocks, kPrepBlock, 0, st>>>(xyz, nrm, vout, counts, offs, nruns, out_xyz,
                                                      out_nrm);
@@ -729,7 +759,6 @@ hipError_t voxel_down_sample(const double* xyz, const double* nrm, int64_t n, do
   int32_t h_runs = 0;
   if (e == hipSuccess) e = hipMemcpyAsync(&h_runs, nruns, 4, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  cleanup();
   *out_n = h_runs;
   return e;
 }
