@@ -264,6 +264,67 @@ __global__ __launch_bounds__(256) void hybrid_search_wave_kernel(
             }
           }
           uint64_t m = __ballot(cand);
+          if constexpr (kS == 1) {
+            // Many candidates at once (the list is filling): merge them in one step instead of
+            // one insertion each.  Every element's place in the union of the held list and the
+            // chunk's candidates is its rank (the keys (d², index) are distinct): a list entry
+            // is preceded by its own index and the candidates below it, a candidate by the list
+            // entries below it (binary search over the sorted list) and the candidates below
+            // it.  Elements ranked below k are written to LDS at their rank and read back.
+            const int c = __popcll(m);
+            if (c >= 3) {
+              __shared__ double s_d[4][64];
+              __shared__ int32_t s_t[4][64];
+              const int w = threadIdx.x >> 6;
+              int rl = lane, rc = 0;
+              for (uint64_t mm = m; mm != 0; mm &= mm - 1) {
+                const int s = __builtin_ctzll(mm);
+                const double x = readlane_f64(d, s);
+                const int32_t xt = __builtin_amdgcn_readlane(t, s);
+                rl += key_less(x, xt, D[0], T[0]) ? 1 : 0;
+                rc += key_less(x, xt, d, t) ? 1 : 0;
+              }
+              int lo = 0, hi = cnt;  // list entries below this lane's candidate: the first
+              for (int it = 0; it < 7; ++it) {  // index whose key is not below it
+                const int mid = (lo + hi) >> 1;
+                const int src = mid < 64 ? mid : 63;
+                const double dm = __shfl(D[0], src);
+                const int32_t tm = __shfl(T[0], src);
+                if (lo < hi) {
+                  if (key_less(dm, tm, d, t))
+                    lo = mid + 1;
+                  else
+                    hi = mid;
+                }
+              }
+              rc += lo;
+              const int ncnt = cnt + c < k ? cnt + c : k;
+              if (lane < cnt && rl < k) {
+                s_d[w][rl] = D[0];
+                s_t[w][rl] = T[0];
+              }
+              if (cand && rc < k) {
+                s_d[w][rc] = d;
+                s_t[w][rc] = t;
+              }
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+              if (lane < ncnt) {
+                D[0] = s_d[w][lane];
+                T[0] = s_t[w][lane];
+              }
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+              cnt = ncnt;
+              if (cnt == k) {
+                thr = readlane_f64(D[0], k - 1);
+                thr_t = __builtin_amdgcn_readlane(T[0], k - 1);
+              }
+              m = 0;
+            }
+          }
           while (m != 0) {
             const int src = __builtin_ctzll(m);
             m &= m - 1;
