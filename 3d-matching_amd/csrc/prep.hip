@@ -835,12 +835,13 @@ double hybrid_fine_radius(const Grid* g, double radius, int k) {
   // M3D_HYBRID_FINE=0: single-stage search (A/B); otherwise the expected-count factor below
   static const double c = [] {
     const char* e = getenv("M3D_HYBRID_FINE");
-    return e ? atof(e) : 0.3;
+    return e ? atof(e) : 0.5;
   }();
   if (!(c > 0.0) || k > 128 || g == nullptr || g->n_occ <= 0) return 0.0;
   // m = points per occupied radius-cell.  On a scanned surface ≈ 8 m (h / r)² points lie within
   // h (measured: the cfg4 scan, 1144 points within r against m = 139), so h = r·√(c·k / m)
-  // expects ≈ 2.5 k of them at c = 0.3.  The cost of the search is mostly the insertions, about
+  // expects ≈ 4 k of them at c = 0.5 (measured best of 0.3 / 0.5 / 0.8 once chunks merge in one
+  // step; 0.3 before that).  The cost of the search is mostly the insertions, about
   // k·(1 + ln(N / k)) for N points within the searched radius, so a small h pays even though a
   // query with fewer than k points within it searches again; worth a second grid only well
   // below r.
