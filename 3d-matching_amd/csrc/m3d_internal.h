@@ -48,8 +48,9 @@ struct RansacState {
   int64_t iterations;
   int64_t rechecked;
   int32_t done;
-  int32_t pad[3];
-  uint64_t batch_key;  // select_best_kernel → select_kernel (no-early-stop batches)
+  uint32_t ticket;     // select_best_kernel's block ticket (the last block finalises the batch)
+  int32_t pad[2];
+  uint64_t batch_key;  // select_best_kernel's blocks → its last block (no-early-stop batches)
 };
 
 // ICP loop state (device resident), Open3D RegistrationICP semantics.

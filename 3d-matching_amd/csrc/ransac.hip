@@ -720,14 +720,31 @@ __device__ __forceinline__ int64_t required_iters(double ratio, double conf, int
   return (int64_t)v;  // int() truncation (v >= 0 here)
 }
 
+// Batch end without early stop: the batch's best (count desc, index asc — the first strict
+// improvement of the sequential walk) is order-free, given as one packed key.
+__device__ void finish_batch(RansacState* __restrict__ rs, uint64_t key, int64_t h_begin, int64_t n,
+                             int64_t max_iter, const double* __restrict__ T_batch) {
+  const BestPair bb{(int64_t)(key >> 32), h_begin + (int64_t)(0xFFFFFFFFu - (uint32_t)key)};
+  const BestPair fin = combine(BestPair{rs->best_count, rs->best_index}, bb);
+  if (fin.i != rs->best_index && fin.i >= h_begin) {
+    for (int k = 0; k < 16; ++k) rs->T_best[k] = T_batch[16 * (fin.i - h_begin) + k];
+  }
+  rs->best_count = fin.c;
+  rs->best_index = fin.i;
+  rs->iterations = h_begin + n;
+  if (rs->iterations >= max_iter) rs->done = 1;
+}
+
 // Batch best for the no-early-stop select: key = (count << 32) | (2³² − 1 − k), k the batch
 // position, so the MAX is the highest count at the lowest position; one 64-bit atomicMax per
 // wave into rs->batch_key (0 = empty: below every real key).  Many blocks — a single-block
-// reduction of 1e5 counts was latency-bound at 20–40 µs.
+// reduction of 1e5 counts was latency-bound at 20–40 µs.  The last block to take a ticket reads
+// and clears the key and finishes the batch (one launch fewer than a separate select_kernel).
 constexpr int kSelBestBlock = 256, kSelBestPer = 8;
-__global__ __launch_bounds__(kSelBestBlock) void select_best_kernel(const int32_t* __restrict__ counts,
-                                                                    int64_t n, RansacState* __restrict__ rs) {
-  if (rs->done) return;
+__global__ __launch_bounds__(kSelBestBlock) void select_best_kernel(
+    const int32_t* __restrict__ counts, int64_t h_begin, int64_t n, int64_t max_iter,
+    const double* __restrict__ T_batch, RansacState* __restrict__ rs) {
+  if (rs->done) return;  // same value for every block: either all take a ticket or none does
   uint64_t best = 0;
   const int64_t base = (int64_t)blockIdx.x * kSelBestBlock * kSelBestPer + threadIdx.x;
   int32_t v[kSelBestPer];
@@ -747,6 +764,16 @@ __global__ __launch_bounds__(kSelBestBlock) void select_best_kernel(const int32_
   }
   if ((threadIdx.x & 63) == 0 && best != 0)
     atomicMax((unsigned long long*)&rs->batch_key, (unsigned long long)best);
+  __threadfence();
+  __syncthreads();
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = atomicAdd(&rs->ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  const uint64_t key = atomicExch((unsigned long long*)&rs->batch_key, 0ull);  // for the next batch
+  rs->ticket = 0;
+  finish_batch(rs, key, h_begin, n, max_iter, T_batch);
 }
 
 __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict__ counts,
@@ -771,22 +798,8 @@ __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict_
   if (t == 0) done_s = rs->done;
   __syncthreads();
   if (done_s) return;
-  if (!early) {
-    // no stop to find: the batch's best (count desc, index asc — the first strict improvement
-    // of the sequential walk) is order-free; select_best_kernel left it as one packed key
-    if (t == 0) {
-      const uint64_t key = rs->batch_key;
-      rs->batch_key = 0;  // for the next batch
-      const BestPair bb{(int64_t)(key >> 32), h_begin + (int64_t)(0xFFFFFFFFu - (uint32_t)key)};
-      const BestPair fin = combine(BestPair{rs->best_count, rs->best_index}, bb);
-      if (fin.i != rs->best_index && fin.i >= h_begin) {
-        for (int k = 0; k < 16; ++k) rs->T_best[k] = T_batch[16 * (fin.i - h_begin) + k];
-      }
-      rs->best_count = fin.c;
-      rs->best_index = fin.i;
-      rs->iterations = h_begin + n;
-      if (rs->iterations >= max_iter) rs->done = 1;
-    }
+  if (!early) {  // n == 0 only: select_best_kernel finishes non-empty batches
+    if (t == 0) finish_batch(rs, rs->batch_key, h_begin, n, max_iter, T_batch);
     return;
   }
   BestPair carry{rs->best_count, rs->best_index};  // running best before the current chunk
@@ -1193,7 +1206,9 @@ hipError_t launch_select(const int32_t* counts, int64_t h_begin, int64_t n, int6
                          const double* T_batch, RansacState* rs, hipStream_t st) {
   if (!early_stop && n > 0) {
     const int64_t per = (int64_t)kSelBestBlock * kSelBestPer;
-    select_best_kernel<<<(unsigned)((n + per - 1) / per), kSelBestBlock, 0, st>>>(counts, n, rs);
+    select_best_kernel<<<(unsigned)((n + per - 1) / per), kSelBestBlock, 0, st>>>(
+        counts, h_begin, n, max_iter, T_batch, rs);
+    return hipGetLastError();
   }
   select_kernel<<<1, 1024, 0, st>>>(counts, h_begin, n, nc, max_iter, early_stop, es_thr, es_conf,
                                     T_batch, rs);
@@ -1210,7 +1225,8 @@ __global__ void ransac_init_kernel(RansacState* __restrict__ rs, const int64_t* 
   rs->iterations = 0;
   rs->rechecked = stats != nullptr ? stats[0] : 0;  // copy_result reports the difference
   rs->done = done;
-  for (int k = 0; k < 3; ++k) rs->pad[k] = 0;
+  rs->ticket = 0;
+  for (int k = 0; k < 2; ++k) rs->pad[k] = 0;
   rs->batch_key = 0;
 }
 
