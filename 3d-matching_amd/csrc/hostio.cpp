@@ -11,6 +11,7 @@
 #include <system_error>
 #include <vector>
 #include <algorithm>
+#include <limits>
 #include <thread>
 
 #include "../../include/m3d.h"
@@ -40,7 +41,26 @@ const long double kPow10L[28] = {1e0L,  1e1L,  1e2L,  1e3L,  1e4L,  1e5L,  1e6L,
                                  1e10L, 1e11L, 1e12L, 1e13L, 1e14L, 1e15L, 1e16L, 1e17L, 1e18L, 1e19L,
                                  1e20L, 1e21L, 1e22L, 1e23L, 1e24L, 1e25L, 1e26L, 1e27L};
 
+// The fast path needs the x87 format (64-bit significand stored first) AND the FPU running at
+// extended precision: compiled out where long double is anything else (IEEE quad, plain
+// double), switched off at run time when the precision-control word rounds to 53 bits.
+constexpr bool kX87Long = std::numeric_limits<long double>::digits == 64 &&
+                          std::numeric_limits<long double>::radix == 2;
+
+bool x87_extended_active() {
+  static const bool ok = [] {
+    volatile long double one = 1.0L, tiny = 1.0L;
+    for (int i = 0; i < 63; ++i) tiny = tiny / 2.0L;  // 2^-63: representable only at 64 bits
+    return kX87Long && (long double)(one + tiny) != one;
+  }();
+  return ok;
+}
+
 inline const char* parse_decimal_fast(const char* p, const char* e, double* out) {
+  if constexpr (!kX87Long) {
+    return nullptr;
+  }
+  if (!x87_extended_active()) return nullptr;
   const char* s = p;
   const bool neg = s < e && *s == '-';
   s += neg;

@@ -82,8 +82,15 @@ __global__ __launch_bounds__(kPrepBlock) void voxel_mean_kernel(
   for (int32_t k = 0; k < c; ++k) {
     const int64_t i = order[b + k];
     for (int a = 0; a < 3; ++a) sp[a] += p[3 * i + a];
-    if (nrm != nullptr)
-      for (int a = 0; a < 3; ++a) sn[a] += nrm[3 * i + a];
+    if (nrm != nullptr) {
+      // AccumulatedPoint::AddPoint: a normal with a NaN component is skipped (still counted)
+      const double n0 = nrm[3 * i], n1 = nrm[3 * i + 1], n2 = nrm[3 * i + 2];
+      if (!(isnan(n0) || isnan(n1) || isnan(n2))) {
+        sn[0] += n0;
+        sn[1] += n1;
+        sn[2] += n2;
+      }
+    }
   }
   for (int a = 0; a < 3; ++a) out_p[3 * v + a] = sp[a] / (double)c;
   if (nrm != nullptr && out_n != nullptr)

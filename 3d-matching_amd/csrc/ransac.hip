@@ -724,6 +724,11 @@ __device__ __forceinline__ int64_t required_iters(double ratio, double conf, int
 // improvement of the sequential walk) is order-free, given as one packed key.
 __device__ void finish_batch(RansacState* __restrict__ rs, uint64_t key, int64_t h_begin, int64_t n,
                              int64_t max_iter, const double* __restrict__ T_batch) {
+  if (key == 0) {  // empty batch (n == 0): no candidate, only the iteration count moves
+    rs->iterations = h_begin + n;
+    if (rs->iterations >= max_iter) rs->done = 1;
+    return;
+  }
   const BestPair bb{(int64_t)(key >> 32), h_begin + (int64_t)(0xFFFFFFFFu - (uint32_t)key)};
   const BestPair fin = combine(BestPair{rs->best_count, rs->best_index}, bb);
   if (fin.i != rs->best_index && fin.i >= h_begin) {
@@ -798,8 +803,8 @@ __global__ __launch_bounds__(1024) void select_kernel(const int32_t* __restrict_
   if (t == 0) done_s = rs->done;
   __syncthreads();
   if (done_s) return;
-  if (!early) {  // n == 0 only: select_best_kernel finishes non-empty batches
-    if (t == 0) finish_batch(rs, rs->batch_key, h_begin, n, max_iter, T_batch);
+  if (!early) {  // n == 0 only (key 0: no candidate): select_best_kernel finishes non-empty batches
+    if (t == 0) finish_batch(rs, 0ull, h_begin, n, max_iter, T_batch);
     return;
   }
   BestPair carry{rs->best_count, rs->best_index};  // running best before the current chunk

@@ -135,9 +135,14 @@ def read_ply(path):
 
 
 def _text_lib():
-    from . import _lib
+    """libm3d's host text routines, or None when the library cannot be loaded (no build, no
+    HIP/RCCL runtime): the numpy paths beside each call site give the same values."""
+    try:
+        from . import _lib
 
-    return _lib.load()
+        return _lib.load()
+    except (ImportError, OSError):
+        return None
 
 
 def _read_ascii_vertices(f, count, props):
@@ -150,8 +155,9 @@ def _read_ascii_vertices(f, count, props):
     rest = f.read()
     out = np.empty((count, len(props)), np.float64)
     used = C.c_size_t(0)
-    rc = _text_lib().m3d_parse_ascii_rows(rest, len(rest), count, len(props),
-                                          out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(used))
+    lib = _text_lib()
+    rc = -1 if lib is None else lib.m3d_parse_ascii_rows(
+        rest, len(rest), count, len(props), out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(used))
     if rc == 0:
         f.seek(pos + used.value)
         cols = {p: out[:, k] for k, (p, _) in enumerate(props)}
@@ -189,6 +195,9 @@ def write_ply(path, points, normals=None, binary: bool = False, dtype="double"):
         f.write(("\n".join(head) + "\n").encode("ascii"))
         if binary:
             f.write(np.ascontiguousarray(data.astype("<" + np_t)).tobytes())
+        elif dtype == "double" and _text_lib() is None:
+            # shortest round-trip text per number, as the library writes it (Python's repr)
+            f.write("".join(" ".join(map(repr, row)) + "\n" for row in data.tolist()).encode("ascii"))
         elif dtype == "double":  # shortest round-trip text per number (csrc/hostio.cpp)
             data = np.ascontiguousarray(data)
             cap = 32 * data.size + 1
@@ -230,7 +239,8 @@ def read_stl(path):
     inv = np.empty(len(flat), np.int32)
     m = C.c_int64(0)
     P = C.POINTER(C.c_double)
-    if _text_lib().m3d_merge_vertices(flat.ctypes.data_as(P), len(flat), uniq.ctypes.data_as(P),
+    lib = _text_lib()
+    if lib is not None and lib.m3d_merge_vertices(flat.ctypes.data_as(P), len(flat), uniq.ctypes.data_as(P),
                                       inv.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(m)) == 0:
         return uniq[: m.value].copy(), inv.astype(np.int64).reshape(-1, 3)
     return _merge_numpy(flat)

@@ -127,7 +127,8 @@ def compute_feature_correspondences(src, tgt, mutual_filter: bool = False,
 
 def compute_step_transformation(src, tgt, correspondences) -> RegistrationResult:
     """ransac.py:104-192 — 3-point Kabsch with identity fallback (fitness stays 0.0)."""
-    corres_np = _corr_array(correspondences)
+    c = np.asarray(correspondences)
+    corres_np = np.zeros((0, 2), np.int32) if c.size == 0 else c.reshape(-1, 2)
     res = RegistrationResult(np.eye(4), 0.0)
     n_corres = len(corres_np)
     if n_corres < 3:
@@ -135,7 +136,12 @@ def compute_step_transformation(src, tgt, correspondences) -> RegistrationResult
     idxs = choice3(n_corres)  # np.random.choice(n, 3, replace=False): same rows, same RNG state
     s_pts, t_pts = _down_points(src), _down_points(tgt)
     _check_gather(corres_np[idxs], len(s_pts), len(t_pts))     # only the sampled rows are read
-    cs = _packed(s_pts, t_pts, np.asarray(corres_np, np.int32), need_all=False)
+    if corres_np.dtype != np.int32:
+        # rows the reference never reads may hold anything, wider than int32 included: packed
+        # as 0 (the sampled rows were checked above)
+        ok = _in_range(corres_np, len(s_pts), len(t_pts))
+        corres_np = np.where(ok[:, None], corres_np, 0).astype(np.int32)
+    cs = _packed(s_pts, t_pts, corres_np, need_all=False)
     T, status = cs.kabsch3_one(idxs)
     if status == _lib.HYP_OK:
         res.transformation = T

@@ -4,8 +4,9 @@
 by the device path of ``m3d.prep``:
 
 1. read the PLY (``m3d.plyio``; Open3D ``read_point_cloud``)                       ply.py:80
-2. ``pcd_down`` = voxel down-sample (voxel_size)                                     ply.py:106
-3. ``pcd_down`` normals: hybrid search (2·v, 30)                                     ply.py:110-112
+2. ``pcd_down`` = voxel down-sample (voxel_size); file normals, when present, are averaged
+   per voxel like Open3D's VoxelDownSample                                           ply.py:106
+3. ``pcd_down`` normals: hybrid search (2·v, 30), oriented by those averaged normals ply.py:110-112
 4. ``pcd_fpfh`` = FPFH on ``pcd_down`` (hybrid 5·v, 100) — an Open3D-style ``Feature``
    (``.data`` 33×N)                                                                  ply.py:117-120
 5. Gaussian noise N(0, 0.05²) on ``pcd_down`` points from the GLOBAL numpy RNG, after the
@@ -65,9 +66,12 @@ class Ply:
         # the full cloud goes to the device once (down-sampling, then its normals), the
         # down-sampled one once (its normals, then FPFH: the noise is added after, ply.py:61-62)
         p_dev = to_device(self.pcd.points)
-        down, _ = prep.voxel_down_sample(p_dev, v)
+        prev = self.pcd.normals if self.pcd.has_normals() else None
+        # VoxelDownSample carries the file's normals (their plain per-voxel mean) into pcd_down,
+        # and EstimateNormals then orients each new normal by that mean (ply.py:106-112)
+        down, down_prev = prep.voxel_down_sample(p_dev, v, normals=prev)
         lap("voxel_down_sample")
-        c_down = Cloud(down)
+        c_down = Cloud(down, down_prev)
         down_n = prep.estimate_normals(c_down, 2 * v, 30)
         lap("normals_down")
         self.pcd_down = PointCloud(down, down_n)
@@ -76,7 +80,6 @@ class Ply:
         noise = 0.05 * np.random.randn(*self.pcd_down.points.shape)      # ply.py:61-62
         self.pcd_down.points = self.pcd_down.points + noise
         lap("noise")
-        prev = self.pcd.normals if self.pcd.has_normals() else None
         # existing normals orient the estimate like Open3D (the cloud carries them)
         self.pcd.normals = prep.estimate_normals(Cloud(p_dev, prev), 2 * v, 30)
         lap("normals_full")

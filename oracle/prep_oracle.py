@@ -63,7 +63,13 @@ def voxel_down_sample(points, voxel, normals=None):
             acc[m] += a[starts[m] + k]
         return acc / counts[:, None].astype(np.float64)
 
-    out_n = None if normals is None else seg_mean(np.asarray(normals, np.float64))
+    # AccumulatedPoint::AddPoint skips a normal with a NaN component; the mean still divides by
+    # every point of the voxel (GetAverageNormal, no re-normalisation)
+    if normals is None:
+        out_n = None
+    else:
+        nr = np.asarray(normals, np.float64)
+        out_n = seg_mean(np.where(np.isnan(nr).any(axis=1)[:, None], 0.0, nr))
     return seg_mean(p), out_n
 
 

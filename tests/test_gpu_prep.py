@@ -205,6 +205,72 @@ def test_ply_pipeline_registers_synthetic_scan(tmp_path):
     np.testing.assert_allclose(fine.transformation, T, atol=5e-3)
 
 
+def _ply_oracle(pts, nrm, v):
+    """ply.py:106-120 on the oracle: voxel down-sample carrying the file normals (per-voxel
+    mean), EstimateNormals(2v, 30) oriented by them, FPFH(5v, 100)."""
+    down, dprev = P.voxel_down_sample(pts, v, nrm)
+    dn = P.estimate_normals(down, 2 * v, 30, prev_normals=dprev)
+    return down, dprev, dn, P.compute_fpfh(down, dn, 5 * v, 100), (P.hybrid_search(down, 5 * v, 100), dn)
+
+
+def _fpfh_bar(got, ref, pts, nrm, nbrs):
+    """test_fpfh_matches_oracle's two tiers."""
+    idx, _, cnt = nbrs
+    sens = P.spfh_edge_sensitive(pts, nrm, idx, cnt)
+    clean = ~sens.copy()
+    for i in range(len(pts)):
+        if np.any(sens[idx[i, : int(cnt[i])]]):
+            clean[i] = False
+    assert clean.mean() >= 0.35, clean.mean()
+    np.testing.assert_allclose(got[clean], ref[clean], rtol=1e-12, atol=1e-12)
+    row_ok = np.all(np.abs(got - ref) <= 1e-6 * np.maximum(1.0, np.abs(ref)), axis=1)
+    assert row_ok.mean() >= 0.995, row_ok.mean()
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_ply_with_file_normals_follows_open3d(tmp_path, flip):
+    """A PLY that carries nx/ny/nz: Open3D's VoxelDownSample averages the file normals into
+    pcd_down, and EstimateNormals orients each new normal by that average (ply.py:80,106-112);
+    the full-resolution normals follow the file's (ply.py:133).  pcd_down normals within 1e-9 of
+    the oracle and FPFH at test_fpfh_matches_oracle's bars; with every file normal flipped, both
+    normal sets flip and every normal agrees in sign with the (averaged) file normal."""
+    from m3d import plyio
+    from ply import Ply
+
+    v = 0.5
+    pts, nrm = synth.surface_points(20000, seed=21)
+    if flip:
+        nrm = -nrm
+    plyio.write_ply(tmp_path / "n.ply", pts, nrm, binary=True)
+    np.random.seed(3)
+    ply = Ply(tmp_path / "n.ply", v)
+    down, dprev, dn, fpfh, (nbrs, _) = _ply_oracle(pts, nrm, v)
+    np.random.seed(3)
+    noise = 0.05 * np.random.randn(*down.shape)            # ply.py:61-62, after the features
+    np.testing.assert_array_equal(ply.pcd_down.points, down + noise)
+    np.testing.assert_allclose(ply.pcd_down.normals, dn, atol=1e-9)
+    assert np.all(np.sum(ply.pcd_down.normals * dprev, axis=1) >= 0.0)
+    _fpfh_bar(ply.pcd_fpfh.data.T, fpfh, down, dn, nbrs)
+    assert np.all(np.sum(ply.pcd.normals * nrm, axis=1) >= 0.0)
+    # without file normals the estimate's sign is the eigen solver's; the file's sign wins here
+    plain = P.estimate_normals(down, 2 * v, 30)
+    s = np.sign(np.sum(plain * dprev, axis=1))
+    np.testing.assert_allclose(ply.pcd_down.normals, plain * np.where(s == 0, 1.0, s)[:, None], atol=1e-9)
+    assert (s < 0).mean() > 0.05  # the orientation step changes a visible share of the normals
+
+
+def test_voxel_down_sample_skips_nan_normals():
+    """AccumulatedPoint::AddPoint (Open3D geometry/DownSample.cpp) adds a normal only when none
+    of its components is NaN, but divides by every point of the voxel."""
+    pts = np.array([[0.0, 0, 0], [0.1, 0, 0], [5.0, 0, 0]])
+    nrm = np.array([[0.0, 0, 1], [np.nan, 0, 0], [1.0, 0, 0]])
+    got, gn = prep.voxel_down_sample(pts, 1.0, nrm)
+    ref, rn = P.voxel_down_sample(pts, 1.0, nrm)
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(gn, rn)
+    np.testing.assert_array_equal(gn, [[0.0, 0, 0.5], [1.0, 0, 0]])
+
+
 @pytest.mark.parametrize("iteration", [30, 30000])
 def test_cfg4_stl_pipeline(tmp_path, iteration):
     """cfg4 from STL: two tessellations of one surface (two "scans", source moved by T⁻¹) written

@@ -222,6 +222,16 @@ def test_negative_and_out_of_range_indices():
     np.random.seed(5)  # choice(4, 3) = [0, 1, 2]: row 3 is never read
     r = M.compute_step_transformation(pts, pts, bad)
     np.testing.assert_allclose(r.transformation, np.eye(4), atol=1e-9)
+    # an unread int64 row beyond int32 range is harmless too, and the draw still happens
+    wide = bad.astype(np.int64)
+    wide[3, 1] = 1 << 40
+    np.random.seed(5)
+    r = M.compute_step_transformation(pts, pts, wide)
+    np.testing.assert_allclose(r.transformation, np.eye(4), atol=1e-9)
+    after = np.random.rand()
+    np.random.seed(5)
+    np.random.choice(4, 3, replace=False)
+    assert np.random.rand() == after
 
 
 @pytest.mark.parametrize("nc", [1, 2, 3, 5, 63, 2047, 2048, 2049, 10007])
@@ -457,3 +467,83 @@ def test_one_hypothesis_calls_equal_batched(nc):
         ref = cs.score(Ts, thr, mode).cpu().numpy()
         got = [cs.score_one(Ts[h], thr, mode) for h in range(len(Ts))]
         np.testing.assert_array_equal(got, ref)
+
+
+@pytest.fixture(scope="module")
+def ply_pair():
+    """A synthetic Ply pair through the device preprocessing (ply.py:32-66): two samplings of
+    the synthetic surface, the target moved by a known pose (the reference's 3d_data/ scans are
+    absent)."""
+    from ply import Ply
+
+    T = synth.random_rigid(41, rot_range=0.4, trans_range=0.5)
+    a, _ = synth.surface_points(20000, seed=42)
+    b, _ = synth.surface_points(20000, seed=43)
+    np.random.seed(1)
+    return (Ply.from_arrays(a, voxel_size=0.3, preprocess=True),
+            Ply.from_arrays(synth.apply(T, b), voxel_size=0.3, preprocess=True))
+
+
+def test_crash_script_noise_ratios(ply_pair):
+    """test_ransac_crash.py:227-236 as asserts: noise ratios 0/1/5/10/100 through
+    compute_feature_correspondences give Nc·(1 + r) int32 rows, every index in range, and the
+    noise-free rows all present (ransac.py:89-99 appends and shuffles)."""
+    from matcher import ransac as M
+
+    src, tgt = ply_pair
+    ns, nt = len(src.pcd_down.points), len(tgt.pcd_down.points)
+    base = M.compute_feature_correspondences(src, tgt, noise_ratio=0.0)
+    assert base.dtype == np.int32 and base.shape == (ns, 2)      # one row per source (no mutual)
+    key = lambda c: np.sort(c[:, 0].astype(np.int64) * nt + c[:, 1])
+    for r in (0.0, 1.0, 5.0, 10.0, 100.0):
+        np.random.seed(int(r) + 7)
+        c = M.compute_feature_correspondences(src, tgt, noise_ratio=r)
+        assert c.dtype == np.int32 and c.shape == (ns + int(ns * r), 2), (r, c.shape)
+        assert c[:, 0].min() >= 0 and c[:, 0].max() < ns and c[:, 1].min() >= 0 and c[:, 1].max() < nt
+        # multiset containment of the feature rows: the noise rows are extra
+        kc, kb = key(c), key(base)
+        pos = np.searchsorted(kc, kb)
+        assert np.all(kc[np.minimum(pos, len(kc) - 1)] == kb)
+        # the injected rows follow the reference's recipe on the global RNG
+        np.random.seed(int(r) + 7)
+        ref = O.inject_noise_legacy(base, ns, nt, r)
+        np.testing.assert_array_equal(c, ref)
+
+
+def test_crash_script_numerical_stability(ply_pair):
+    """test_ransac_crash.py:239-274 as asserts: 1000 compute_step_transformation +
+    evaluate_inlier_ratio(…, 0.3) calls on the Ply pair — every fitness finite (the script asks
+    ≥ 95 %), each transform the oracle's (1e-9, rank-2 samples) and each ratio the oracle's exactly,
+    and the global RNG advanced by exactly 1000 np.random.choice(n, 3, replace=False) draws."""
+    from matcher import ransac as M
+
+    src, tgt = ply_pair
+    sp, tp = np.asarray(src.pcd_down.points), np.asarray(tgt.pcd_down.points)
+    corr = M.compute_feature_correspondences(src, tgt, noise_ratio=0.0)
+    np.random.seed(123)
+    ref_rng = np.random.RandomState(123)
+    for _ in range(1000):
+        res = M.compute_step_transformation(src, tgt, corr)
+        f = M.evaluate_inlier_ratio(src, tgt, corr, res.transformation, 0.3)
+        assert np.isfinite(f) and np.all(np.isfinite(res.transformation))
+        idx = ref_rng.choice(len(corr), 3, replace=False)
+        T_ref, _ = O.kabsch3(sp[corr[idx, 0]], tp[corr[idx, 1]])
+        if not rank_deficient(sp[corr[idx, 0]], tp[corr[idx, 1]]):
+            np.testing.assert_allclose(res.transformation, T_ref, atol=1e-9)
+        assert f == O.evaluate_inlier_ratio(sp, tp, corr, res.transformation, 0.3)
+    assert np.random.rand() == ref_rng.rand()
+
+
+def test_crash_script_large_transformation(ply_pair):
+    """test_ransac_crash.py:277-294 as an assert: R ×1000 and t = (1000, 1000, 1000) give the
+    oracle's ratio on the Ply pair's correspondences (0.0 here, exactly)."""
+    from matcher import ransac as M
+
+    src, tgt = ply_pair
+    corr = M.compute_feature_correspondences(src, tgt, noise_ratio=0.0)
+    big = np.eye(4)
+    big[:3, :3] *= 1000.0
+    big[:3, 3] = [1000, 1000, 1000]
+    f = M.evaluate_inlier_ratio(src, tgt, corr, big, 0.3)
+    assert f == O.evaluate_inlier_ratio(src.pcd_down.points, tgt.pcd_down.points, corr, big, 0.3)
+    assert f == 0.0

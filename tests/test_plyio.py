@@ -327,3 +327,30 @@ def test_native_ascii_writer_threaded_equals_serial():
     assert whole == pieces
     back = np.array(whole.split(), dtype=np.float64).reshape(-1, 3)
     np.testing.assert_array_equal(back.view(np.uint64), data.view(np.uint64))
+
+
+def test_text_paths_without_the_library(tmp_path, monkeypatch):
+    """No loadable libm3d (no build, no HIP/RCCL runtime): ASCII PLY read / write and the STL
+    vertex merge take their numpy paths and give the same values as the library's."""
+    rng = np.random.default_rng(5)
+    pts = rng.normal(size=(300, 3)) * 7
+    nrm = rng.normal(size=(300, 3))
+    with_lib = tmp_path / "lib.ply"
+    plyio.write_ply(with_lib, pts, nrm, binary=False)
+    ref = plyio.read_ply(with_lib)
+    tri = rng.normal(size=(40, 3))
+    faces = rng.integers(0, 40, (90, 3))
+    plyio.write_stl(tmp_path / "m.stl", tri, faces, binary=True)
+    ref_stl = plyio.read_stl(tmp_path / "m.stl")
+
+    monkeypatch.setattr(plyio, "_text_lib", lambda: None)
+    no_lib = tmp_path / "nolib.ply"
+    plyio.write_ply(no_lib, pts, nrm, binary=False)
+    assert no_lib.read_bytes() == with_lib.read_bytes()   # shortest round-trip text both ways
+    for path in (with_lib, no_lib):
+        got = plyio.read_ply(path)
+        np.testing.assert_array_equal(got[0], ref[0])
+        np.testing.assert_array_equal(got[1], ref[1])
+    got_stl = plyio.read_stl(tmp_path / "m.stl")
+    np.testing.assert_array_equal(got_stl[0], ref_stl[0])
+    np.testing.assert_array_equal(got_stl[1], ref_stl[1])
