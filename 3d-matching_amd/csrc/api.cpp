@@ -803,6 +803,8 @@ void m3d_cloud_destroy(m3d_cloud* c) {
     grid_free(g);
     delete g;
   }
+  for (auto& m : c->morton) m3d_cloud_destroy(m.second);
+  hipFree(c->slot);
   hipFree(c->xyz64);
   hipFree(c->nrm64);
   hipFree(c->xyz32);
@@ -835,26 +837,66 @@ int ensure_grid(m3d_ctx* ctx, const m3d_cloud* c, double cell, hipStream_t st, c
   return M3D_OK;
 }
 
+// The ICP source in Morton slot order for cell size `cell` (grid.hip morton_copy), built once and
+// cached on the caller's cloud; sg = the caller's grid at that cell size.
+int ensure_morton_source(m3d_ctx* ctx, const m3d_cloud* c, const Grid* sg, double cell,
+                         const m3d_cloud** out, const Grid** gout) {
+  for (auto& m : c->morton)
+    if (m.first == cell && m.second->n == c->n) {
+      *out = m.second;
+      *gout = m.second->grids.front();
+      return M3D_OK;
+    }
+  hipError_t e = grid_morton(const_cast<Grid*>(sg), nullptr);
+  m3d_cloud* mc = new m3d_cloud();
+  mc->ctx = ctx;
+  Grid* g = new Grid();
+  mc->grids.push_back(g);
+  if (e == hipSuccess) e = morton_copy(c, sg, mc, g, nullptr);
+  if (e != hipSuccess) {
+    m3d_cloud_destroy(mc);
+    return m3d_fail(ctx, M3D_ERR_HIP, std::string("morton source: ") + hipGetErrorString(e));
+  }
+  c->morton.emplace_back(cell, mc);
+  *out = mc;
+  *gout = g;
+  return M3D_OK;
+}
+
 // NN evaluation for the current transform → s->keys (brute: keyinit + scan; grid: one kernel).
 // self_seed (m3d_icp_step's fused loop): when the previous fused tail left every key at
 // kKeyNone (s->keys_clean), the brute-force scan seeds itself and the keyinit launch is skipped.
-hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = false) {
+// [q0, q1): a slot range of the sources (q1 < 0: all), see icp_nn_splits.
+hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = false, int64_t q0 = 0,
+                      int64_t q1 = -1) {
   m3d_ctx* ctx = s->ctx;
-  const bool seeded = self_seed && s->keys_clean && off == 0;
+  const bool whole = q0 == 0 && (q1 < 0 || q1 == s->src->n);
+  const bool seeded = self_seed && s->keys_clean && off == 0 && whole;
   s->keys_clean = false;
   if (s->params.nn_method == M3D_NN_GRID) {
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->sgrid, s->tgrid, off, s->state, s->keys,
-                          s->near2, s->sq, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st);
+                          s->near2, s->sq, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st, q0, q1);
   }
   if (!seeded) {
-    hipError_t e = launch_icp_keyinit(s, off, st);
+    hipError_t e = launch_icp_keyinit(s, off, st, q0, q1);
     if (e != hipSuccess) return e;
   }
   KTimer kt(ctx, M3D_KERNEL_NN, st);
-  return launch_icp_nn(s, off, seeded, st);
+  return launch_icp_nn(s, off, seeded, st, q0, q1);
 }
 }  // namespace
+
+extern "C++" {
+namespace m3d {
+int icp_shard_nn_range(m3d_icp* s, int64_t off, int64_t q0, int64_t q1, int64_t* dkeys, hipStream_t st) {
+  hipError_t e = enqueue_nn(s, off, st, false, q0, q1);
+  if (e == hipSuccess) e = launch_shard_winner(s, off, dkeys, st, q0, q1);
+  if (e != hipSuccess) return m3d_fail(s->ctx, M3D_ERR_HIP, std::string("shard NN: ") + hipGetErrorString(e));
+  return M3D_OK;
+}
+}  // namespace m3d
+}  // extern "C++"
 
 int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
                    const m3d_icp_params* params, m3d_icp** out) {
@@ -872,6 +914,7 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
             "unknown nn_method");
   hipSetDevice(ctx->device);
   const Grid *tg = nullptr, *sg = nullptr;
+  const m3d_cloud* src_m = nullptr;
   {
     // Grid NN: cell ≈ the search radius, a query visits 3 cells per axis.  Brute force: the
     // same grids only ORDER the points (targets and queries in cell order make the MFMA
@@ -896,10 +939,10 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
       const int div = std::min(4, std::max(1, (int)std::floor(std::sqrt(m / 3.5))));
       if (div > 1) grc = ensure_grid(ctx, tgt, cell / div, nullptr, &tg);
     }
-    if (!grc && params->nn_method == M3D_NN_GRID && sg->mpts == nullptr) {
-      hipError_t e = grid_morton(const_cast<Grid*>(sg), nullptr);
-      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("morton order: ") + hipGetErrorString(e));
-    }
+    // the loop runs on the source in Morton slot order (its grid derived from sg)
+    const m3d_cloud* ms = nullptr;
+    if (!grc) grc = ensure_morton_source(ctx, src, sg, cell, &ms, &sg);
+    if (!grc) src_m = ms;
     if (!grc) {
       hipError_t e = ensure_target_rec(tgt, nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("target records: ") + hipGetErrorString(e));
@@ -912,13 +955,21 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   }
   m3d_icp* s = new m3d_icp();
   s->ctx = ctx;
-  s->src = src;
+  s->src = src_m;
+  s->user_src = src;
   s->tgt = tgt;
   s->params = *params;
   s->max_dist = max_dist;
   s->nblocks = terms_blocks(src->n);
   s->tgrid = tg;
-  s->qorder = sg->order;
+  // brute-force query order: the Morton slots themselves (compact 64-query waves, contiguous
+  // slot ranges for the split exchange of the target-shard loop); M3D_NN_QORDER=cell: the source
+  // grid's row-major cell order (round 2)
+  static const bool cell_order = [] {
+    const char* e = getenv("M3D_NN_QORDER");
+    return e && strcmp(e, "cell") == 0;
+  }();
+  s->qorder = cell_order ? sg->order : nullptr;
   s->sgrid = sg;
   int rc = dev_alloc(ctx, &s->state, 1);
   if (!rc) rc = dev_alloc(ctx, &s->keys, std::max<int64_t>(src->n, 1));
@@ -1040,6 +1091,16 @@ int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* dkeys, void* stream) {
   return M3D_OK;
 }
 
+int m3d_icp_shard_nn_range(m3d_icp* s, int64_t off, int64_t q0, int64_t q1, int64_t* dkeys, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  m3d_ctx* ctx = s->ctx;
+  CHECK_ARG(ctx, off >= 0, "negative shard offset");
+  CHECK_ARG(ctx, dkeys != nullptr, "null dkeys");
+  CHECK_ARG(ctx, 0 <= q0 && q0 <= q1 && q1 <= s->src->n, "slot range outside [0, ns]");
+  CHECK_ARG(ctx, icp_nn_range_ok(s), "this loop's NN cannot run on a slot range (fp32 VALU / per-query form)");
+  return icp_shard_nn_range(s, off, q0, q1, dkeys, S(stream));
+}
+
 int m3d_icp_shard_claim(m3d_icp* s, const int64_t* dmin, int32_t* claim, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   CHECK_ARG(s->ctx, dmin != nullptr && claim != nullptr, "null exchange buffer");
@@ -1103,7 +1164,14 @@ const int32_t* m3d_icp_corr(const m3d_icp* s) { return s ? s->corr : nullptr; }
 int m3d_icp_copy_corr(const m3d_icp* s, int32_t* dst, void* stream) {
   if (!s || !dst) return M3D_ERR_INVALID;
   if (s->src->n == 0) return M3D_OK;
-  HIPX(s->ctx, hipMemcpyAsync(dst, s->corr, sizeof(int32_t) * s->src->n, hipMemcpyDeviceToDevice,
+  HIPX(s->ctx, launch_scatter_i32(s->corr, s->src->slot, s->src->n, dst, S(stream)));
+  return M3D_OK;
+}
+
+int m3d_icp_copy_slots(const m3d_icp* s, int32_t* dst, void* stream) {
+  if (!s || !dst) return M3D_ERR_INVALID;
+  if (s->src->n == 0) return M3D_OK;
+  HIPX(s->ctx, hipMemcpyAsync(dst, s->src->slot, sizeof(int32_t) * s->src->n, hipMemcpyDeviceToDevice,
                               S(stream)));
   return M3D_OK;
 }
@@ -1120,8 +1188,7 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
   for (int k = 0; !rc && k <= params->max_iteration; ++k) rc = m3d_icp_step(s, stream);
   if (!rc) rc = m3d_icp_result_get(s, out, stream);
   if (!rc && corr_idx && src->n > 0) {
-    hipError_t e = hipMemcpyAsync(corr_idx, s->corr, sizeof(int32_t) * src->n,
-                                  hipMemcpyDeviceToDevice, S(stream));
+    hipError_t e = launch_scatter_i32(s->corr, s->src->slot, src->n, corr_idx, S(stream));
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));
     if (e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   }
@@ -1387,7 +1454,7 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
     const int64_t n = std::min<int64_t>(bsz, npass - c0);
     e = launch_val_states(s, T.p, dlist.p + c0, n, vst.p, st);
     if (e == hipSuccess)
-      e = launch_validate(s->sgrid, ns, src->xyz64, s->tgrid, tgt->xyz64, tgt->n, vst.p, n, vpart.p,
+      e = launch_validate(s->sgrid, ns, s->src->xyz64, s->tgrid, tgt->xyz64, tgt->n, vst.p, n, vpart.p,
                           vres.p, st);
     hs.resize(2 * (size_t)n);
     if (e == hipSuccess)
@@ -1426,7 +1493,7 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
       if (e == hipSuccess) e = enqueue_nn(s, 0, st);
       if (e == hipSuccess) e = launch_icp_terms_mode(s, 0, nullptr, nullptr, st);
       if (e == hipSuccess)
-        e = hipMemcpyAsync(corr_set_out, s->corr, 4 * ns, hipMemcpyDeviceToDevice, st);
+        e = launch_scatter_i32(s->corr, s->src->slot, ns, corr_set_out, st);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
   }

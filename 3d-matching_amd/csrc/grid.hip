@@ -212,14 +212,14 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const IcpState* __restrict__ s, int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
     const float4* __restrict__ sq, const int32_t* __restrict__ prev,
     const int64_t* __restrict__ dprev, const float4* __restrict__ tgt32, int64_t nt_shard,
-    int64_t nblocks, unsigned long long* __restrict__ stats) {
+    int64_t nblocks, unsigned long long* __restrict__ stats, int64_t q0) {
   // stats (M3D_GRID_STATS=1, diagnostics only, else null): [0] queries, [1] cell rows,
   // [2] candidate points, [3] queries with a seed
   if (s->done) return;
   const int64_t per = (nblocks + 7) / 8;
   const int64_t blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
   if (blk >= nblocks) return;
-  const int64_t t = (blk * kGridBlock + threadIdx.x) / kL;
+  const int64_t t = q0 + (blk * kGridBlock + threadIdx.x) / kL;  // queries [q0, ns) in Morton order
   const int sub = threadIdx.x & (kL - 1);
   const float r2_hi = s->r2_hi, be = s->band_e;
   const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
@@ -583,11 +583,101 @@ hipError_t grid_morton(Grid* g, hipStream_t st) {
   return grid_fail(e, kin, kout, vin, vout, tmp);
 }
 
+// ------------------------------------------------------------------------------- Morton copy
+// The ICP loop's source in the Morton order of its grid (m3d_icp_create): slot k holds source
+// point mpts[k].w.  Every per-source array of the loop (keys, runner-ups, correspondences, seeds,
+// exchange buffers) is then indexed by slot, so the grid scan's key writes and seed reads and the
+// terms pass's source loads are coalesced and its winner gathers spatially coherent; the ABI
+// translates back to source order (m3d_icp_copy_corr).  The copy's grid is derived from the
+// source's, not rebuilt: the same cells and starts; within a cell the Morton sort kept index order,
+// so a cell's points are consecutive ascending slots and the cell-ordered arrays only change their
+// index bits (minv: source index → slot).
+__global__ __launch_bounds__(kGridBlock) void morton_copy_points_kernel(
+    const double* __restrict__ xyz64, const double* __restrict__ nrm64,
+    const float4* __restrict__ xyz32, const float4* __restrict__ mpts, int64_t n,
+    double* __restrict__ oxyz64, double* __restrict__ onrm64, float4* __restrict__ oxyz32,
+    int32_t* __restrict__ slot, float4* __restrict__ ompts, int32_t* __restrict__ ominv) {
+  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (k >= n) return;
+  const float4 m = mpts[k];
+  const int64_t j = __float_as_int(m.w);
+  slot[k] = (int32_t)j;
+  for (int a = 0; a < 3; ++a) oxyz64[3 * k + a] = xyz64[3 * j + a];
+  if (onrm64 != nullptr)
+    for (int a = 0; a < 3; ++a) onrm64[3 * k + a] = nrm64[3 * j + a];
+  oxyz32[k] = xyz32[j];
+  ompts[k] = make_float4(m.x, m.y, m.z, __int_as_float((int32_t)k));
+  ominv[k] = (int32_t)k;
+}
+
+__global__ __launch_bounds__(kGridBlock) void morton_copy_cells_kernel(
+    const float4* __restrict__ pts, const int32_t* __restrict__ order, const int32_t* __restrict__ minv,
+    int64_t n, float4* __restrict__ opts, int32_t* __restrict__ oorder) {
+  const int64_t j = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (j >= n) return;
+  const float4 v = pts[j];
+  opts[j] = make_float4(v.x, v.y, v.z, __int_as_float(minv[__float_as_int(v.w)]));
+  oorder[j] = minv[order[j]];
+}
+
+hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Grid* gout,
+                       hipStream_t st) {
+  const int64_t n = src->n;
+  if (sg->mpts == nullptr || sg->minv == nullptr || sg->n_pts != n) return hipErrorInvalidValue;
+  out->n = n;
+  out->n_pad = src->n_pad;
+  for (int k = 0; k < 3; ++k) out->center[k] = src->center[k];
+  out->rmax = src->rmax;
+  out->s16 = src->s16;
+  out->center_given = src->center_given;
+  gout->dev = sg->dev;
+  gout->n_pts = n;
+  gout->n_occ = sg->n_occ;
+  gout->cell = sg->cell;
+  gout->cell_req = sg->cell_req;
+  const size_t n1 = (size_t)std::max<int64_t>(n, 1);
+  const int64_t ncells = sg->dev.ncells;
+  hipError_t e;
+  if ((e = hipMalloc(&out->xyz64, sizeof(double) * 3 * n1)) != hipSuccess ||
+      (src->nrm64 != nullptr && (e = hipMalloc(&out->nrm64, sizeof(double) * 3 * n1)) != hipSuccess) ||
+      (e = hipMalloc(&out->xyz32, sizeof(float4) * (size_t)std::max<int64_t>(src->n_pad, 1))) != hipSuccess ||
+      (e = hipMalloc(&out->slot, sizeof(int32_t) * n1)) != hipSuccess ||
+      (e = hipMalloc(&gout->mpts, sizeof(float4) * n1)) != hipSuccess ||
+      (e = hipMalloc(&gout->minv, sizeof(int32_t) * n1)) != hipSuccess)
+    return e;
+  if (n == 0) return hipSuccess;
+  if ((e = hipMalloc(&gout->start, sizeof(int32_t) * (size_t)(ncells + 1))) != hipSuccess ||
+      (e = hipMalloc(&gout->pts, sizeof(float4) * n1)) != hipSuccess ||
+      (e = hipMalloc(&gout->order, sizeof(int32_t) * n1)) != hipSuccess)
+    return e;
+  const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
+  morton_copy_points_kernel<<<blocks, kGridBlock, 0, st>>>(src->xyz64, src->nrm64, src->xyz32, sg->mpts,
+                                                           n, out->xyz64, out->nrm64, out->xyz32,
+                                                           out->slot, gout->mpts, gout->minv);
+  morton_copy_cells_kernel<<<blocks, kGridBlock, 0, st>>>(sg->pts, sg->order, sg->minv, n, gout->pts,
+                                                          gout->order);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // the pads of the centred fp32 copy (far points) and the cell starts are the source's
+  if (src->n_pad > n &&
+      (e = hipMemcpyAsync(out->xyz32 + n, src->xyz32 + n, sizeof(float4) * (size_t)(src->n_pad - n),
+                          hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    return e;
+  if (ncells > 0 && (e = hipMemcpyAsync(gout->start, sg->start, sizeof(int32_t) * (size_t)(ncells + 1),
+                                        hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    return e;
+  gout->dev.start = gout->start;
+  gout->dev.pts = gout->pts;
+  return hipStreamSynchronize(st);
+}
+
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, const Grid* g,
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
                           const float4* sq, const int32_t* prev, const int64_t* dprev,
-                          const float4* tgt32, int64_t nt_shard, hipStream_t st) {
-  if (ns == 0) return hipSuccess;
+                          const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0,
+                          int64_t q1) {
+  const int64_t ns_all = ns;
+  if (q1 >= 0) ns = q1;
+  if (ns <= q0) return hipSuccess;
   static const bool batched = [] {  // M3D_GRID_BATCHED=0: the per-query kernel above (A/B)
     const char* e = getenv("M3D_GRID_BATCHED");
     return !(e && atoi(e) == 0);
@@ -610,9 +700,9 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
       return p;
     }();
     if (gstats != nullptr) (void)hipMemsetAsync(gstats, 0, 4 * sizeof(unsigned long long), st);
-    const int64_t nb = (ns * L + kGridBlock - 1) / kGridBlock;
+    const int64_t nb = ((ns - q0) * L + kGridBlock - 1) / kGridBlock;
     const unsigned launch = (unsigned)((nb + 7) / 8 * 8);
-#define M3D_GB(LV, RV, BV) grid_nn_batched_kernel<LV, RV, BV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats)
+#define M3D_GB(LV, RV, BV) grid_nn_batched_kernel<LV, RV, BV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0)
 #define M3D_GBL(RV, BV) if (L == 1) M3D_GB(1, RV, BV); else if (L == 2) M3D_GB(2, RV, BV); else if (L == 4) M3D_GB(4, RV, BV); else if (L == 8) M3D_GB(8, RV, BV); else M3D_GB(16, RV, BV)
     if (RB == 22) { M3D_GBL(2, 2); } else if (RB == 41) { M3D_GBL(4, 1); } else if (RB == 42) { M3D_GBL(4, 2); } else { M3D_GBL(2, 4); }
 #undef M3D_GBL
@@ -626,6 +716,7 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
     }
     return hipGetLastError();
   }
+  if (q0 != 0 || ns != ns_all) return hipErrorInvalidValue;  // per-query form: every source
   const int32_t* order = qgrid != nullptr ? qgrid->order : nullptr;
   const unsigned blocks = (unsigned)((ns * L + kGridBlock - 1) / kGridBlock);
   if (L == 1)

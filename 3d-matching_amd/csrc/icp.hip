@@ -196,10 +196,10 @@ __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__
                                                       const int32_t* __restrict__ prev,
                                                       const int64_t* __restrict__ dprev,
                                                       int64_t* __restrict__ keys,
-                                                      uint32_t* __restrict__ near2) {
-  // keys ← seed_key (nnkey.h), near2 ← none
+                                                      uint32_t* __restrict__ near2, int64_t q0) {
+  // keys ← seed_key (nnkey.h), near2 ← none; sources [q0, ns)
   if (s->done) return;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = q0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= ns) return;
   const float* Rt = s->Rt32;  // uniform → scalar loads (a local copy went to scratch)
   const float4 p = src32[i];
@@ -470,11 +470,11 @@ __device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
                               const int32_t* __restrict__ order, const float4* __restrict__ tgt32,
                               int64_t jb, int64_t je, int64_t off, const IcpState* __restrict__ s,
                               int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
-                              const SeedArgs& sa) {
+                              const SeedArgs& sa, int64_t q0) {
   const float* Rt = s->Rt32;
   const float r2_hi = s->r2_hi;
   for (int qs = threadIdx.x; qs < mqueries<kMG>(); qs += kMBlock) {
-    const int64_t slot = (int64_t)blockIdx.x * mqueries<kMG>() + qs;
+    const int64_t slot = q0 + (int64_t)blockIdx.x * mqueries<kMG>() + qs;
     if (slot >= ns) return;
     const int64_t i = order != nullptr ? (int64_t)order[slot] : slot;
     float qx, qy, qz;
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           uint32_t* __restrict__ near2,
                                                           uint64_t exp_mask,
                                                           unsigned long long* __restrict__ stats,
-                                                          int strided, SeedArgs sa) {
+                                                          int strided, SeedArgs sa, int64_t q0) {
   // exp_mask: all ones; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
   // (profiling experiment only: the keys are then wrong).  stats (M3D_NN_STATS=1, diagnostics
   // only, else null): [0] flagged (group, sub-tile) steps, [1] all steps.
@@ -539,7 +539,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   if (!s->mfma_ok) {
     const int64_t jb = (int64_t)blockIdx.y * slice_len;
     nn_slice_scan<kMG>(src32, ns, order, tgt32, jb, min(nt_pad, jb + slice_len), off, s, keys,
-                       near2, sa);
+                       near2, sa, q0);
     return;
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -556,12 +556,13 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   half8 bq[kMG];
 #pragma unroll
   for (int g = 0; g < kMG; ++g) {
-    const int64_t slot = (int64_t)blockIdx.x * mqueries<kMG>() + (wave * kMG + g) * 32 + c;
-    const int64_t i = slot < ns ? (order != nullptr ? (int64_t)order[slot] : slot) : ns;
+    // queries: positions [q0, ns) of the visit order (order, or the slots themselves)
+    const int64_t slot = q0 + (int64_t)blockIdx.x * mqueries<kMG>() + (wave * kMG + g) * 32 + c;
+    const int64_t i = slot < ns ? (order != nullptr ? (int64_t)order[slot] : slot) : -1;
     qi[g] = i;
     n2[g] = kInf;
     float X = -1.0f;  // inactive: negative threshold, never hits
-    if (i < ns) {
+    if (i >= 0) {
       const float4 p = src32[i];
       xform32(Rt, p, qx[g], qy[g], qz[g]);
       const int64_t key = start_key(sa, s, i, p, qx[g], qy[g], qz[g], off, keys);
@@ -691,7 +692,7 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   }
 #pragma unroll
   for (int g = 0; g < kMG; ++g) {
-    if (h != 0 || qi[g] >= ns) continue;
+    if (h != 0 || qi[g] < 0) continue;
     const bool pk = publish_k1(sa, k1[g], k10[g]);
     if (pk || n2[g] < kInf)
       near_publish((unsigned long long*)&keys[qi[g]], &near2[qi[g]], k1[g], n2[g], pk);
@@ -952,9 +953,9 @@ __global__ __launch_bounds__(256) void shard_winner_kernel(
     const double* __restrict__ tgt64, int64_t nt_shard, int64_t off, GridDev g,
     const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
     const uint32_t* __restrict__ near2, int32_t* __restrict__ lidx, int64_t* __restrict__ ld64,
-    int64_t* __restrict__ dkey) {
+    int64_t* __restrict__ dkey, int64_t q0) {
   if (s->done) return;
-  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i0 = q0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool valid = i0 < ns;
   const int64_t i = valid ? i0 : 0;
   double Q[3];
@@ -1199,6 +1200,7 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(const double* __restri
                                                           const IcpState* __restrict__ s,
                                                           const int64_t* __restrict__ keys,
                                                           const uint32_t* __restrict__ near2,
+                                                          const int32_t* __restrict__ slot,
                                                           int32_t* __restrict__ idx,
                                                           double* __restrict__ d2out) {
   const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1211,8 +1213,15 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(const double* __restri
   winner_fp64(valid, valid ? (uint64_t)keys[i] : (uint64_t)kKeyNone,
               valid ? __uint_as_float(near2[i]) : kInf, s, g, tgt64, 0, nt, src32[i], Q, gj, d);
   if (!valid) return;
-  idx[i] = (int32_t)gj;
-  if (d2out != nullptr) d2out[i] = gj >= 0 ? d : INFINITY;
+  const int64_t o = slot != nullptr ? (int64_t)slot[i] : i;  // slot → the caller's source order
+  idx[o] = (int32_t)gj;
+  if (d2out != nullptr) d2out[o] = gj >= 0 ? d : INFINITY;
+}
+
+__global__ void scatter_i32_kernel(const int32_t* __restrict__ v, const int32_t* __restrict__ slot,
+                                   int64_t n, int32_t* __restrict__ dst) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) dst[slot[k]] = v[k];
 }
 
 __global__ void keys_to_idx_kernel(const int64_t* __restrict__ keys, int64_t n,
@@ -1255,12 +1264,12 @@ hipError_t launch_val_states(const m3d_icp* s, const double* T_dev, const int32_
   return hipGetLastError();
 }
 
-hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t off, hipStream_t st) {
-  const int64_t ns = s->src->n;
-  if (ns == 0) return hipSuccess;
-  keyinit_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(
+hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t off, hipStream_t st, int64_t q0, int64_t q1) {
+  const int64_t ns = q1 < 0 ? s->src->n : q1;
+  if (ns <= q0) return hipSuccess;
+  keyinit_kernel<<<(unsigned)((ns - q0 + 255) / 256), 256, 0, st>>>(
       s->src->xyz32, ns, s->tgt->xyz32, s->tgt->n, off, s->state, s->corr, s->dprev, s->keys,
-      s->near2);
+      s->near2, q0);
   return hipGetLastError();
 }
 
@@ -1286,13 +1295,22 @@ static bool icp_nn_uses_mfma(const m3d_icp* s) {
   return mfma_env && s->tgrid != nullptr && s->tgrid->mf16 != nullptr;
 }
 
+bool icp_nn_range_ok(const m3d_icp* s) {
+  if (s->params.nn_method == M3D_NN_GRID) {
+    const char* e = getenv("M3D_GRID_BATCHED");
+    return !(e && atoi(e) == 0) && s->sgrid != nullptr && s->sgrid->mpts != nullptr;
+  }
+  return icp_nn_uses_mfma(s) && s->qorder == nullptr;
+}
+
 // Brute-force NN into s->keys (after launch_icp_keyinit, or self_seed: keys all kKeyNone, see
 // SeedArgs).  MFMA tiles present: nn_mfma_kernel alone (its exact in-kernel scan covers
 // transforms whose operands do not fit fp16); otherwise the fp32 VALU nn_kernel.
-hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStream_t st) {
-  const int64_t ns = s->src->n;
+hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStream_t st, int64_t q0,
+                         int64_t q1) {
+  const int64_t ns = q1 < 0 ? s->src->n : q1;  // queries: visit positions [q0, ns)
   const int64_t nt_pad = s->tgt->n_pad;
-  if (ns == 0 || s->tgt->n == 0) return hipSuccess;
+  if (ns <= q0 || s->tgt->n == 0) return hipSuccess;
   static const int Q = [] {
     const char* e = getenv("M3D_NN_Q");
     const int v = e ? atoi(e) : kNNQDefault;
@@ -1339,7 +1357,7 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
     const int64_t tt = (int64_t)TH * kMTile;
     if (tg->mf_npad % tt != 0) return hipErrorInvalidValue;  // pack16 pads to kMTilePad
     const int64_t mq = MG == 4 ? mqueries<4>() : (MG == 2 ? mqueries<2>() : mqueries<1>());
-    dim3 gm = nn_grid((ns + mq - 1) / mq, tg->mf_npad, tt, &slice);
+    dim3 gm = nn_grid((ns - q0 + mq - 1) / mq, tg->mf_npad, tt, &slice);
     if (strided && fill) {
       // Strided tiles decouple grid.y from slice boundaries: pick S in [S0, 2·S0] so that the
       // block count fills the resident block slots in whole rounds (the last partial round of
@@ -1373,7 +1391,7 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
 #define M3D_NN_LAUNCH(MGV, THV)                                                                  \
   nn_mfma_kernel<MGV, THV><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,         \
                                                    tg->mf32, tg->mf_npad, slice, off, s->state,    \
-                                                   s->keys, s->near2, exp_mask, nn_stats, strided, sa)
+                                                   s->keys, s->near2, exp_mask, nn_stats, strided, sa, q0)
     if (MG == 4) {
       if (TH == 2) M3D_NN_LAUNCH(4, 2); else M3D_NN_LAUNCH(4, 1);
     } else if (MG == 2) {
@@ -1391,6 +1409,7 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
     }
     return hipGetLastError();
   }
+  if (q0 != 0 || ns != s->src->n) return hipErrorInvalidValue;  // the VALU form scans every source
   if (self_seed) {  // the fp32 VALU kernel reads its starting keys
     const hipError_t e = launch_icp_keyinit(s, off, st);
     if (e != hipSuccess) return e;
@@ -1542,16 +1561,25 @@ hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStr
   if (ns == 0) return hipSuccess;
   nn_finalize_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(
       s->src->xyz64, s->src->xyz32, ns, s->tgt->xyz64, s->tgt->n, s->tgrid->dev, s->state, s->keys,
-      s->near2, idx, d2);
+      s->near2, s->src->slot, idx, d2);
   return hipGetLastError();
 }
 
-hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hipStream_t st) {
-  const int64_t ns = s->src->n;
-  if (ns == 0) return hipSuccess;
-  shard_winner_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(
+hipError_t launch_scatter_i32(const int32_t* v, const int32_t* slot, int64_t n, int32_t* dst,
+                              hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (slot == nullptr) return hipMemcpyAsync(dst, v, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st);
+  scatter_i32_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(v, slot, n, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hipStream_t st,
+                               int64_t q0, int64_t q1) {
+  const int64_t ns = q1 < 0 ? s->src->n : q1;
+  if (ns <= q0) return hipSuccess;
+  shard_winner_kernel<<<(unsigned)((ns - q0 + 255) / 256), 256, 0, st>>>(
       s->src->xyz64, s->src->xyz32, ns, s->tgt->xyz64, s->tgt->n, off, s->tgrid->dev, s->state,
-      s->keys, s->near2, s->lidx, s->ld64, dkey);
+      s->keys, s->near2, s->lidx, s->ld64, dkey, q0);
   return hipGetLastError();
 }
 

@@ -170,11 +170,19 @@ struct m3d_cloud {
   // normals) as 8 doubles per point, 64-B aligned, so the gather of a source's winner touches one
   // 64-B segment instead of one in each of xyz64 and nrm64; built on first use as an ICP target
   mutable double* rec64 = nullptr;
+  // ICP sources: copies of this cloud in the Morton order of its grid, one per cell size (grid.hip
+  // morton_copy), built on first use by m3d_icp_create; in a copy, slot[k] = the index in this
+  // (parent) cloud of the copy's point k
+  mutable std::vector<std::pair<double, m3d_cloud*>> morton;
+  int32_t* slot = nullptr;
 };
 
 struct m3d_icp {
   m3d_ctx* ctx = nullptr;
+  // the loop's source: the caller's cloud in Morton slot order (user_src->morton); every per-source
+  // array below is indexed by slot, src->slot maps a slot to the caller's point index
   const m3d_cloud* src = nullptr;
+  const m3d_cloud* user_src = nullptr;
   const m3d_cloud* tgt = nullptr;
   m3d_icp_params params{};
   double max_dist = 0.0;
@@ -197,6 +205,7 @@ struct m3d_icp {
   const m3d::Grid* tgrid = nullptr;  // grid NN: the target's grid (owned by the target cloud)
   int64_t ns_total = 0;  // source-sharded multi-GPU: sources over all ranks (fitness denominator)
   // exchange buffers of the library-driven multi-GPU loops (m3d_icp_*shard_steps), lazily
+  bool xready = false;      // exchange buffers allocated and every rank agreed (comm.cpp)
   int64_t* xdk = nullptr;   // ns: d64 keys, MIN-reduced
   int32_t* xcl = nullptr;   // ns: claims, MIN-reduced
   double* xsums = nullptr;  // kTermSlots, SUM-reduced
@@ -275,10 +284,24 @@ hipError_t launch_copy_result(const RansacState* rs, int64_t nc, const int64_t* 
                               m3d_ransac_result* out_dev, hipStream_t st);
 hipError_t launch_ransac_pack_key(const m3d_ransac_result* r, int64_t hyp0, int64_t* key,
                                   hipStream_t st);
+// m3d_ransac_run_sharded: buf[0] ← this rank's key (r == null: a failed rank, 0); after the MAX,
+// buf[1..19] ← the SUM payload (ransac.hip ransac_shard_pack_kernel)
+hipError_t launch_ransac_shard_key(const m3d_ransac_result* r, int64_t hyp0, int64_t* buf,
+                                   hipStream_t st);
+hipError_t launch_ransac_shard_pack(const m3d_ransac_result* r, int64_t hyp0, int64_t* buf,
+                                    hipStream_t st);
+// target-shard loop pieces (api.cpp): the NN + this shard's winners of source slots [q0, q1), and
+// whether the loop's NN can run on a slot range (grid NN; brute force with MFMA tiles in slot order)
+int icp_shard_nn_range(m3d_icp* s, int64_t off, int64_t q0, int64_t q1, int64_t* dkeys, hipStream_t st);
+bool icp_nn_range_ok(const m3d_icp* s);
 
 // ICP
-hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_t st);
-hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, bool self_seed, hipStream_t st);
+// [q0, q1): the sources (slots; brute force: positions of s->qorder) one launch evaluates,
+// q1 < 0 = all (the target-shard loop splits its sources to overlap the exchange, comm.cpp)
+hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_t st, int64_t q0 = 0,
+                              int64_t q1 = -1);
+hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, bool self_seed, hipStream_t st,
+                         int64_t q0 = 0, int64_t q1 = -1);
 hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st);
 // claim/dmin: target-shard exchange results (m3d_icp_shard_claim), or null
 hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* claim,
@@ -286,7 +309,8 @@ hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* c
 hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, const int32_t* claim,
                                    const int64_t* dmin, double* sums, bool reset_keys,
                                    hipStream_t st);
-hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hipStream_t st);
+hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hipStream_t st,
+                               int64_t q0 = 0, int64_t q1 = -1);
 hipError_t launch_shard_claim(const m3d_icp* s, const int64_t* dmin, int32_t* claim, hipStream_t st);
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g);
@@ -297,8 +321,14 @@ void grid_free(Grid* g);
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, const Grid* g,
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
                           const float4* sq, const int32_t* prev, const int64_t* dprev,
-                          const float4* tgt32, int64_t nt_shard, hipStream_t st);
+                          const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0 = 0,
+                          int64_t q1 = -1);
 hipError_t grid_morton(Grid* g, hipStream_t st);
+// the Morton-slot copy of an ICP source (out, gout freshly allocated structs; see grid.hip)
+hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Grid* gout, hipStream_t st);
+// dst[slot[k]] = v[k], k < n (slot-ordered loop arrays → the caller's source order)
+hipError_t launch_scatter_i32(const int32_t* v, const int32_t* slot, int64_t n, int32_t* dst,
+                              hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);
 hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st);
 // a6 batched validation: states[k] ← evaluation state of T[list[k]] (icp_set_T semantics), then

@@ -1261,4 +1261,37 @@ hipError_t launch_ransac_pack_key(const m3d_ransac_result* r, int64_t hyp0, int6
   return hipGetLastError();
 }
 
+// m3d_ransac_run_sharded, after MAX(buf[0]) over ranks: the SUM payload buf[1..19] = this rank's
+// iterations, rechecked, the bits of its best T if its key is the global one (else 0: exactly one
+// rank holds the winner, ids are disjoint, so the integer SUM is the winner's bits, -0.0
+// included) and the failed-rank count.  A rank whose local run failed (r == null) contributes
+// zeros and 1: every rank learns of the failure from the same collective, none waits forever.
+__global__ void ransac_shard_pack_kernel(const m3d_ransac_result* __restrict__ r, int64_t hyp0,
+                                         int64_t* __restrict__ buf) {
+  const int t = threadIdx.x;
+  int64_t lkey = 0;
+  if (r != nullptr) {
+    const int64_t c = r->best_count, bi = r->best_index;
+    lkey = (c < 0 || bi < 0) ? 0 : (int64_t)(((uint64_t)c << 32) | (0xFFFFFFFFull - (uint64_t)(hyp0 + bi)));
+  }
+  const bool win = lkey != 0 && lkey == buf[0];
+  if (t < 16) buf[3 + t] = win ? __double_as_longlong(r->T[t]) : 0;
+  if (t == 16) buf[1] = r != nullptr ? r->iterations : 0;
+  if (t == 17) buf[2] = r != nullptr ? r->rechecked : 0;
+  if (t == 18) buf[19] = r != nullptr ? 0 : 1;
+}
+
+hipError_t launch_ransac_shard_key(const m3d_ransac_result* r, int64_t hyp0, int64_t* buf,
+                                   hipStream_t st) {
+  if (r == nullptr) return hipMemsetAsync(buf, 0, sizeof(int64_t), st);
+  ransac_pack_key_kernel<<<1, 64, 0, st>>>(r, hyp0, buf);
+  return hipGetLastError();
+}
+
+hipError_t launch_ransac_shard_pack(const m3d_ransac_result* r, int64_t hyp0, int64_t* buf,
+                                    hipStream_t st) {
+  ransac_shard_pack_kernel<<<1, 64, 0, st>>>(r, hyp0, buf);
+  return hipGetLastError();
+}
+
 }  // namespace m3d

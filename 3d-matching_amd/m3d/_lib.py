@@ -18,6 +18,7 @@ M3D_ERR_INVALID = -1
 M3D_ERR_HIP = -2
 M3D_ERR_OOM = -3
 M3D_ERR_NODEVICE = -4
+M3D_ERR_COMM = -5
 
 HYP_OK, HYP_DEGENERATE, HYP_NONFINITE = 0, 1, 2
 SCORE_SQUARED, SCORE_NORM = 0, 1
@@ -28,7 +29,7 @@ COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2
 OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -103,6 +104,7 @@ SIGNATURES = {
     "m3d_icp_step": (C.c_int, [vp, vp]),
     "m3d_icp_steps": (C.c_int, [vp, C.c_int32, vp]),
     "m3d_icp_shard_nn": (C.c_int, [vp, i64, vp, vp]),
+    "m3d_icp_shard_nn_range": (C.c_int, [vp, i64, i64, i64, vp, vp]),
     "m3d_icp_shard_claim": (C.c_int, [vp, vp, vp, vp]),
     "m3d_icp_shard_terms": (C.c_int, [vp, i64, vp, vp, vp, vp]),
     "m3d_icp_solve": (C.c_int, [vp, vp, vp]),
@@ -110,6 +112,7 @@ SIGNATURES = {
     "m3d_icp_set_source_total": (C.c_int, [vp, i64]),
     "m3d_icp_corr": (vp, [vp]),
     "m3d_icp_copy_corr": (C.c_int, [vp, vp, vp]),
+    "m3d_icp_copy_slots": (C.c_int, [vp, vp, vp]),
     "m3d_voxel_down_sample": (C.c_int, [vp, vp, vp, i64, dbl, vp, vp, C.POINTER(i64), vp]),
     "m3d_hybrid_search": (C.c_int, [vp, vp, dbl, i32, vp, vp, vp, vp]),
     "m3d_estimate_normals": (C.c_int, [vp, vp, dbl, i32, vp, vp]),
@@ -126,6 +129,8 @@ SIGNATURES = {
     "m3d_icp_source_shard_steps": (C.c_int, [vp, vp, i32, vp]),
     "m3d_ransac_best_allreduce": (C.c_int, [vp, vp, i64, vp, vp]),
     "m3d_ransac_run_sharded": (C.c_int, [vp, vp, vp, C.POINTER(RansacParams), C.POINTER(RansacResult), vp]),
+    "m3d_comm_poisoned": (C.c_int, [vp]),
+    "m3d_debug_comm_inject": (C.c_int, [vp, C.c_int]),
     "m3d_parse_ascii_rows": (C.c_int, [C.c_char_p, C.c_size_t, i64, i32, C.POINTER(dbl),
                                        C.POINTER(C.c_size_t)]),
     "m3d_format_ascii_rows": (C.c_int, [C.POINTER(dbl), i64, i32, vp, C.c_size_t, C.POINTER(C.c_size_t)]),
@@ -139,6 +144,10 @@ _lib = None
 
 class M3DError(RuntimeError):
     pass
+
+
+class M3DCommError(M3DError):
+    """A peer rank failed, or the communicator was aborted after a failure (M3D_ERR_COMM)."""
 
 
 def load() -> C.CDLL:
@@ -178,4 +187,6 @@ def check(rc: int, ctx=None, what: str = "") -> None:
         msg = raw.decode() if raw else ""
     if rc == M3D_ERR_INVALID:
         raise ValueError(f"{what}: {msg}" if msg else what)
+    if rc == M3D_ERR_COMM:
+        raise M3DCommError(f"{what} failed (code {rc}): {msg}")
     raise M3DError(f"{what} failed (code {rc}): {msg}")

@@ -49,6 +49,16 @@ class LibComm:
             self.ctx.lib.m3d_comm_destroy(h)
             self.h = None
 
+    @property
+    def poisoned(self) -> bool:
+        """True once the communicator was aborted after a failure (calls raise M3DCommError)."""
+        return self.ctx.lib.m3d_comm_poisoned(self.h) == 1
+
+    def inject_failure(self, what: int):
+        """Test hook (m3d_debug_comm_inject): 1 fails the next local run of run_sharded, 2 the
+        next ICP shard-loop iteration."""
+        self.ctx.check(self.ctx.lib.m3d_debug_comm_inject(self.h, int(what)), "m3d_debug_comm_inject")
+
     def _ar(self, t, op):
         import torch
 

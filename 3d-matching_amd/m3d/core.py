@@ -465,6 +465,11 @@ class IcpLoop:
         self.ctx.check(self.ctx.lib.m3d_icp_shard_nn(self.h, int(offset), ptr(dkeys), stream_handle()),
                        "icp_shard_nn")
 
+    def shard_nn_range(self, offset: int, q0: int, q1: int, dkeys):
+        """shard_nn for the source slots [q0, q1) (the split exchange's pieces)."""
+        self.ctx.check(self.ctx.lib.m3d_icp_shard_nn_range(self.h, int(offset), int(q0), int(q1), ptr(dkeys),
+                                                           stream_handle()), "icp_shard_nn_range")
+
     def shard_claim(self, dmin, claim):
         """Target shard, after MIN(dkeys): claim (cuda int32, ns) = own winner's index where it
         has the global d², else INT32_MAX; MIN-reduce it over ranks."""
@@ -500,6 +505,14 @@ class IcpLoop:
         self.ctx.check(self.ctx.lib.m3d_icp_result_get(self.h, C.byref(r), stream_handle()), "icp_result")
         return IcpOutcome(np.array(r.T[:]).reshape(4, 4), r.fitness, r.inlier_rmse,
                           r.num_correspondences, r.iterations, bool(r.converged))
+
+    def source_slots(self):
+        """Slot → source point index (int32 torch cuda): the loop holds its source in the Morton
+        order of the source grid; exchange buffers (dkeys / claims) are indexed by slot."""
+        torch = _torch()
+        out = torch.empty((max(self.src.n, 1),), dtype=torch.int32, device="cuda")
+        self.ctx.check(self.ctx.lib.m3d_icp_copy_slots(self.h, ptr(out), stream_handle()), "icp_copy_slots")
+        return out[: self.src.n]
 
     def correspondences(self):
         """Current correspondence target per source point (int32, -1 = none), torch cuda."""

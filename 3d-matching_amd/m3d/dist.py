@@ -28,11 +28,20 @@ tests); ``m3d.comm.LibComm`` issues RCCL from inside libm3d.so on the library's 
 
 The drivers are backend-agnostic: the GPU backend is ``m3d.core.IcpLoop``; the CPU tests plug in
 an oracle-backed backend and run the identical protocol over gloo.
+
+Failure contract (the native loops' in comm.cpp): the drivers' setup (the backend's reset) is
+followed by one MAX of a failed flag, so a rank that fails before the first exchange raises its
+own error and its peers ``M3DCommError`` — no rank is left inside an all-reduce its peers never
+join; ``ransac_sharded`` is fail-soft (a failed local run still joins the exchanges with neutral
+values and a failure count).  Source slots: per-source exchange buffers follow the backend's own
+source order (``IcpLoop``: its Morton slots, identical on every rank that holds the same source).
 """
 
 from __future__ import annotations
 
 import numpy as np
+
+from ._lib import M3DCommError
 
 KEY_NONE = 0x7FFFFFFFFFFFFFFF
 CLAIM_NONE = 0x7FFFFFFF
@@ -64,6 +73,25 @@ class TorchComm:
         import torch.distributed as dist
 
         self._ar(t, dist.ReduceOp.MAX)
+
+    def min_async(self, t):
+        """In-place MIN started in the background; returns a handle with .wait()."""
+        import torch.distributed as dist
+
+        return dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group, async_op=True)
+
+
+def agree(comm, exc, device):
+    """Setup agreement: MAX over ranks of "my setup failed".  Re-raises this rank's own exception,
+    or M3DCommError when only a peer failed."""
+    import torch
+
+    flag = torch.tensor([0 if exc is None else 1], dtype=torch.int32, device=device)
+    comm.max_(flag)
+    if exc is not None:
+        raise exc
+    if int(flag.item()) != 0:
+        raise M3DCommError("a peer rank failed before the collective loop")
 
 
 def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
@@ -108,23 +136,53 @@ def unpack_best_key(key: int) -> tuple[int, int]:
     return int(key) >> 32, _LOW - (int(key) & _LOW)
 
 
+def split_point(ns: int) -> int:
+    """The two source halves of the split exchange meet on a 4096-slot boundary (comm.cpp)."""
+    return (ns // 2 + 4095) // 4096 * 4096 if ns >= 2 * 4096 else ns
+
+
 class ShardedIcp:
     """Target-sharded ICP driver: backend has shard_nn / shard_claim / shard_terms / solve /
-    reset / result."""
+    reset / result (and shard_nn_range for split=True).
 
-    def __init__(self, backend, offset: int, ns: int, device, comm=None):
+    split=True: the half-split exchange of m3d_icp_shard_steps — the first source half's MIN runs
+    (async) while the second half's NN runs; the same keys, so the same result."""
+
+    def __init__(self, backend, offset: int, ns: int, device, comm=None, split: bool = False):
         import torch
 
         self.b = backend
         self.off = int(offset)
         self.comm = comm or TorchComm()
+        self.device = device
+        self.ns = int(ns)
+        # split: True → split_point(ns); an int → that slot (tests); False → one piece
+        h = split_point(self.ns) if split is True else (int(split) if split else self.ns)
+        self.h = h if 0 < h < self.ns else self.ns
+        self.split = self.h < self.ns
         self.dkeys = torch.empty(ns, dtype=torch.int64, device=device)
         self.claim = torch.empty(ns, dtype=torch.int32, device=device)
         self.sums = torch.empty(32, dtype=torch.float64, device=device)
 
+    def _nn_exchange(self):
+        if not self.split:
+            self.b.shard_nn(self.off, self.dkeys)
+            self.comm.min_(self.dkeys)
+            return
+        h = self.h
+        self.b.shard_nn_range(self.off, 0, h, self.dkeys)
+        a = self.dkeys[:h]
+        start = getattr(self.comm, "min_async", None)
+        work = start(a) if start is not None else None
+        if work is None:
+            self.comm.min_(a)
+        self.b.shard_nn_range(self.off, h, self.ns, self.dkeys)
+        if work is not None:
+            work.wait()
+        self.comm.min_(self.dkeys[h:])
+
     def iteration(self):
-        self.b.shard_nn(self.off, self.dkeys)
-        self.comm.min_(self.dkeys)
+        self._nn_exchange()
         self.b.shard_claim(self.dkeys, self.claim)
         self.comm.min_(self.claim)
         self.b.shard_terms(self.off, self.dkeys, self.claim, self.sums)
@@ -133,7 +191,12 @@ class ShardedIcp:
 
     def run(self, init, max_iteration: int):
         """Open3D loop structure: Eval + up to max_iteration updates (max_iteration + 1 passes)."""
-        self.b.reset(init)
+        err = None
+        try:
+            self.b.reset(init)
+        except Exception as e:  # noqa: BLE001 - re-raised by agree() after the peers learned of it
+            err = e
+        agree(self.comm, err, self.device)
         for _ in range(max_iteration + 1):
             self.iteration()
         return self.b.result()
@@ -150,6 +213,7 @@ class SourceShardedIcp:
 
         self.b = backend
         self.comm = comm or TorchComm()
+        self.device = device
         self.b.set_source_total(ns_total)
         self.sums = torch.empty(32, dtype=torch.float64, device=device)
 
@@ -160,7 +224,12 @@ class SourceShardedIcp:
         self.b.solve(self.sums)
 
     def run(self, init, max_iteration: int):
-        self.b.reset(init)
+        err = None
+        try:
+            self.b.reset(init)
+        except Exception as e:  # noqa: BLE001 - re-raised by agree()
+            err = e
+        agree(self.comm, err, self.device)
         for _ in range(max_iteration + 1):
             self.iteration()
         return self.b.result()
@@ -177,10 +246,21 @@ def ransac_sharded(cs, params, comm=None):
     if params.early_stop:
         raise ValueError("ransac_sharded runs without early stop: set params.early_stop = False")
     comm = comm or TorchComm()
-    out = cs.run(params)
-    gid = params.hyp0 + out.best_index
-    key = torch.tensor([best_key(out.best_count, gid)], dtype=torch.int64, device=cs.device)
+    err, k = None, 0
+    try:
+        out = cs.run(params)
+        if out.best_index >= 0:
+            k = best_key(out.best_count, params.hyp0 + out.best_index)
+    except Exception as e:  # noqa: BLE001 - fail-soft: join the exchanges, raise after them
+        err = e
+    key = torch.tensor([k], dtype=torch.int64, device=cs.device)
     comm.max_(key)
+    failed = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=cs.device)
+    comm.sum_(failed)
+    if err is not None:
+        raise err
+    if int(failed.item()) != 0:
+        raise M3DCommError(f"{int(failed.item())} peer rank(s) failed their local run")
     count, wid = unpack_best_key(int(key.item()))
     T, _ = cs.kabsch3(1, seed=params.seed, hyp0=wid)
     return count, wid, T[0].cpu().numpy()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 7
+#define M3D_ABI_VERSION 8
 
 /* return codes */
 #define M3D_OK 0
@@ -43,6 +43,7 @@ extern "C" {
 #define M3D_ERR_HIP (-2)      /* HIP runtime error */
 #define M3D_ERR_OOM (-3)      /* device allocation failed */
 #define M3D_ERR_NODEVICE (-4) /* no usable gfx950 device */
+#define M3D_ERR_COMM (-5)     /* a peer rank failed, or the communicator was aborted (ABI 8) */
 
 /* per-hypothesis status (ransac.py:134-140,184-192) */
 #define M3D_HYP_OK 0
@@ -250,10 +251,18 @@ int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream);
  *   m3d_icp_shard_terms(s, off, dmin, claim, sums)  terms of the owned winners; sums [device]
  *                                        32 f64                               → all-reduce SUM
  *   m3d_icp_solve(s, sums)               identical update on every rank.
+ * Every per-source exchange buffer (dkeys, dmin, claim) is indexed by the loop's SOURCE SLOT: the
+ * loop keeps its source in the Morton order of the source's grid (coalesced per-source arrays);
+ * m3d_icp_copy_slots gives slot → source index.  Ranks that share one source cloud (the target
+ * shard) get the same slots.
  * Source shard (SURVEY §8(e) "ICP alternative"): `src` is this rank's source shard, `tgt` the
  * whole target: m3d_icp_shard_nn(s, 0, NULL) + m3d_icp_shard_terms(s, 0, NULL, NULL, sums),
  * SUM of the sums, m3d_icp_solve; the fitness denominator is m3d_icp_set_source_total's. */
 int m3d_icp_shard_nn(m3d_icp* s, int64_t shard_offset, int64_t* dkeys, void* stream);
+/* m3d_icp_shard_nn for the source slots [q0, q1) only (dkeys entries outside stay untouched): the
+ * pieces of the split exchange (ABI 8).  M3D_ERR_INVALID when the loop's NN has no range form. */
+int m3d_icp_shard_nn_range(m3d_icp* s, int64_t shard_offset, int64_t q0, int64_t q1, int64_t* dkeys,
+                           void* stream);
 int m3d_icp_shard_claim(m3d_icp* s, const int64_t* dmin, int32_t* claim, void* stream);
 int m3d_icp_shard_terms(m3d_icp* s, int64_t shard_offset, const int64_t* dmin, const int32_t* claim,
                         double* sums, void* stream);
@@ -275,13 +284,23 @@ typedef struct m3d_comm m3d_comm;
 #define M3D_OP_MAX 2
 /* id_out [host] M3D_COMM_ID_BYTES bytes (ncclGetUniqueId), called on rank 0. */
 int m3d_comm_unique_id(uint8_t* id_out);
-/* Collective over the world's ranks (every rank calls it with the same id).  Synchronous. */
+/* Collective over the world's ranks (every rank calls it with the same id).  Synchronous.  Every
+ * buffer the library's collectives use is allocated here or before a loop's first collective.
+ * Failure contract (ABI 8): a loop object's first multi-GPU call allocates its exchange buffers
+ * and all ranks agree on the outcome (a rank whose setup failed returns its error, its peers
+ * M3D_ERR_COMM — nobody enters the loop); m3d_ransac_run_sharded is fail-soft (a failed local run
+ * still joins the collectives, every rank returns an error); a launch or RCCL error inside a
+ * collective loop aborts the communicator (ncclCommAbort) and every later call on it returns
+ * M3D_ERR_COMM — peers already waiting in a collective cannot be reached from that rank, so the
+ * caller must then tear down every rank (torch.distributed.run does when a worker fails). */
 int m3d_comm_init(m3d_ctx* ctx, const uint8_t* id, int rank, int world, m3d_comm** out);
 void m3d_comm_destroy(m3d_comm* c);
 /* In-place all-reduce of buf [device] count elements of dtype M3D_DT_* with op M3D_OP_*. */
 int m3d_comm_allreduce(m3d_comm* c, void* buf, int64_t count, int dtype, int op, void* stream);
 /* n iterations of target-sharded ICP (the protocol of "Multi-GPU pieces" above) with the MIN /
- * MIN / SUM all-reduces issued inside; every rank calls it with its shard offset. */
+ * MIN / SUM all-reduces issued inside; every rank calls it with its shard offset.  The sources
+ * are split into two slot halves: the first half's d64 MIN runs on a library-owned exchange
+ * stream while the second half's NN runs on `stream` (M3D_SHARD_SPLIT=0: one piece). */
 int m3d_icp_shard_steps(m3d_icp* s, m3d_comm* c, int64_t shard_offset, int32_t n, void* stream);
 /* n iterations of source-sharded ICP (one SUM of the 32 term slots per iteration). */
 int m3d_icp_source_shard_steps(m3d_icp* s, m3d_comm* c, int32_t n, void* stream);
@@ -290,18 +309,25 @@ int m3d_icp_source_shard_steps(m3d_icp* s, m3d_comm* c, int32_t n, void* stream)
  * (best_count << 32) | (2³² − 1 − (hyp0 + best_index)): highest count, lowest global id. */
 int m3d_ransac_best_allreduce(m3d_comm* c, const m3d_ransac_result* result_dev, int64_t hyp0,
                               int64_t* key_dev, void* stream);
-/* The whole hypothesis-sharded run, synchronous: out holds the global winner (T recomputed
- * from its id by the native sampler; best_index = global id; iterations and rechecked summed
- * over ranks).  params->early_stop must be 0 and the native sampler is used. */
+/* The whole hypothesis-sharded run, synchronous (one host sync): out holds the global winner
+ * (its transform's bits from the winning rank via an integer SUM; best_index = global id;
+ * iterations and rechecked summed over ranks).  params->early_stop must be 0 and the native
+ * sampler is used.  Scratch is the communicator's (no allocation per call). */
 int m3d_ransac_run_sharded(m3d_ctx* ctx, m3d_comm* c, const m3d_corrset* cs,
                            const m3d_ransac_params* params, m3d_ransac_result* out, void* stream);
+/* 1 once the communicator was aborted after a failure (M3D_ERR_COMM from then on), else 0. */
+int m3d_comm_poisoned(const m3d_comm* c);
 
 /* Read the loop state (synchronises the stream). */
 int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream);
-/* Device pointer to the current correspondence index array (ns int32, -1 = none). */
+/* Device pointer to the current correspondence index array (ns int32, -1 = none) in SOURCE SLOT
+ * order (see m3d_icp_copy_slots); m3d_icp_copy_corr gives it in source order. */
 const int32_t* m3d_icp_corr(const m3d_icp* s);
-/* Copy the current correspondence array to dst [device] (ns int32). */
+/* Copy the current correspondence array to dst [device] (ns int32, source order: dst[i] = target
+ * index of source point i, -1 = none). */
 int m3d_icp_copy_corr(const m3d_icp* s, int32_t* dst, void* stream);
+/* dst [device] ns int32: dst[k] = the source point index held in slot k (ABI 8). */
+int m3d_icp_copy_slots(const m3d_icp* s, int32_t* dst, void* stream);
 
 /* ------------------------------------------------------------------ preprocessing
  * Open3D 0.19 semantics restated (oracle/prep_oracle.py); all fp64. */
@@ -374,6 +400,9 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
  * of the math.  Never used by the product path. */
 int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16);
 int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6);
+/* Failure injection for the multi-GPU failure tests: what = 1 fails this rank's next local run of
+ * m3d_ransac_run_sharded, 2 its next ICP shard-loop iteration (0 clears). */
+int m3d_debug_comm_inject(m3d_comm* c, int what);
 
 /* ------------------------------------------------------------------ host text I/O (§8(f) rank 4) */
 

@@ -58,6 +58,17 @@ class OracleShard:
         if dkeys is not None:
             dkeys.copy_(torch.from_numpy(D.pack_d64(self.ld, self.lj >= 0)))
 
+    def shard_nn_range(self, off, q0, q1, dkeys):
+        """The split exchange's piece: sources [q0, q1) only (entries outside stay untouched)."""
+        if self.done:
+            return
+        j, d2 = self._local(off)
+        if q0 == 0:
+            self.lj, self.ld = j.copy(), d2.copy()
+        else:
+            self.lj[q0:q1], self.ld[q0:q1] = j[q0:q1], d2[q0:q1]
+        dkeys[q0:q1].copy_(torch.from_numpy(D.pack_d64(d2[q0:q1], j[q0:q1] >= 0)))
+
     def shard_claim(self, dmin, claim):
         if self.done:
             return
@@ -108,21 +119,26 @@ class OracleShard:
         return self.T, self.fitness, self.rmse, self.iters
 
 
-def _icp_worker(rank, world, port, path):
+def _icp_worker(rank, world, port, path, split=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     src, tgt, nrm, _ = synth.icp_pair(4000, 6001, seed=21)
     off, cnt = D.shard_bounds(len(tgt), world, rank)
     b = OracleShard(src, tgt[off:off + cnt], nrm[off:off + cnt], 0.12, 8)
-    drv = D.ShardedIcp(b, off, len(src), "cpu")
+    drv = D.ShardedIcp(b, off, len(src), "cpu", split=split)
+    assert drv.split == bool(split)
     T, fit, rmse, iters = drv.run(np.eye(4), 8)
     np.savez(f"{path}/rank{rank}.npz", T=T, fit=fit, rmse=rmse, iters=iters)
     dist.destroy_process_group()
 
 
-def test_sharded_icp_protocol_matches_single_process(tmp_path):
+@pytest.mark.parametrize("split", [False, 1733])
+def test_sharded_icp_protocol_matches_single_process(tmp_path, split):
+    """Target shards over gloo equal the single-process oracle, with the exchange in one piece
+    and split (the first slot half's MIN in flight — async — while the second half's NN runs,
+    m3d_icp_shard_steps' schedule)."""
     world = 2
-    mp.spawn(_icp_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_icp_worker, args=(world, free_port(), str(tmp_path), split), nprocs=world, join=True)
     src, tgt, nrm, _ = synth.icp_pair(4000, 6001, seed=21)
     ref = I.registration_icp(src, tgt, 0.12, np.eye(4), tgt_normals=nrm, relative_fitness=-1,
                              relative_rmse=-1, max_iteration=8)
@@ -207,3 +223,59 @@ def test_shard_bounds_cover(n, world):
     for (o1, c1), (o2, _) in zip(spans, spans[1:]):
         assert o1 + c1 == o2
     assert sum(c for _, c in spans) == n
+
+
+class _FailingShard(OracleShard):
+    def reset(self, init):
+        raise RuntimeError("injected setup failure")
+
+
+class _RansacStub:
+    """CorrSet stand-in for the fail-soft protocol test: a fixed local best, or a failing run."""
+
+    device = "cpu"
+
+    def __init__(self, count, fail):
+        self.count, self.fail = count, fail
+
+    def run(self, params):
+        if self.fail:
+            raise RuntimeError("injected run failure")
+        from types import SimpleNamespace
+        return SimpleNamespace(best_index=3, best_count=self.count)
+
+    def kabsch3(self, n, seed, hyp0):
+        return torch.eye(4, dtype=torch.float64)[None], None
+
+
+def _failure_worker(rank, world, port, path, what):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    src, tgt, nrm, _ = synth.icp_pair(500, 600, seed=3)
+    got = "ok"
+    try:
+        if what == "setup":
+            cls = _FailingShard if rank == 1 else OracleShard
+            D.ShardedIcp(cls(src, tgt, nrm, 0.12, 2), 0, len(src), "cpu").run(np.eye(4), 2)
+        else:
+            from m3d.core import RansacParams
+            p = RansacParams(max_iter=10, seed=1, thr=0.45, early_stop=False, hyp0=10 * rank)
+            D.ransac_sharded(_RansacStub(5 + rank, fail=rank == 1), p)
+    except Exception as e:  # noqa: BLE001
+        got = type(e).__name__ + ": " + str(e)
+    with open(f"{path}/rank{rank}.txt", "w") as f:
+        f.write(got)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("what", ["setup", "ransac"])
+def test_rank_failure_reaches_every_rank(tmp_path, what):
+    """A failure on one rank before (ICP setup) or during (the local RANSAC run) the exchange:
+    every rank raises from the same call instead of waiting in an all-reduce forever — the
+    failing rank its own error, the peer M3DCommError (m3d.dist.agree / the fail-soft RANSAC
+    exchange, the protocol of comm.cpp)."""
+    mp.spawn(_failure_worker, args=(2, free_port(), str(tmp_path), what), nprocs=2, join=True)
+    r0 = (tmp_path / "rank0.txt").read_text()
+    r1 = (tmp_path / "rank1.txt").read_text()
+    assert r0.startswith("M3DCommError"), r0
+    assert r1.startswith("RuntimeError: injected"), r1

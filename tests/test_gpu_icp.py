@@ -338,8 +338,10 @@ def test_target_shard_duplicates_across_shards_lowest_index():
     src = tgt[:4000:3] + 1e-3
     seen = {}
 
-    def keep(it, lp, kmin, cmin):
-        seen[it] = cmin.cpu().numpy().copy()
+    def keep(it, lp, kmin, cmin):  # claims are indexed by the loop's source slot
+        got = np.empty(len(src), np.int64)
+        got[lp.source_slots().cpu().numpy()] = cmin.cpu().numpy()
+        seen[it] = got
 
     run_target_shards(src, tgt, nrm, [0, 2500, 8000], 0, "grid", r=0.3, check_keys=keep)
     ref_j, _ = I.nn_exact(cKDTree(tgt), tgt, src, 0.3)

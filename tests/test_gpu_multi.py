@@ -47,7 +47,9 @@ def test_cfg3_geometry_eight_shards_match_unsharded():
     first = {}
 
     def check(it, lp, kmin, cmin):
-        got = cmin.cpu().numpy().astype(np.int64)
+        slot_claims = cmin.cpu().numpy().astype(np.int64)   # indexed by the loop's source slot
+        got = np.empty_like(slot_claims)
+        got[lp.source_slots().cpu().numpy()] = slot_claims
         got[got == 0x7FFFFFFF] = -1
         np.testing.assert_array_equal(got, ref_corr[it], err_msg=f"evaluation {it}")
         if it == 0:
@@ -182,3 +184,56 @@ def test_lib_ransac_sharded_world1_matches_run(comm1):
     np.testing.assert_array_equal(sh.transformation, one.transformation)
     with pytest.raises(ValueError):
         cs.run_sharded(comm1, RansacParams(max_iter=10, seed=4, thr=0.45, early_stop=True))
+
+
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_split_exchange_driver_matches_single_device(comm1, nn):
+    """The half-split target-shard schedule through the Python driver (IcpLoop.shard_nn_range
+    pieces, m3d.dist.ShardedIcp(split=True)) over the library communicator: the same bits as the
+    fused single-device loop, at a ragged split point and at the default one."""
+    from m3d import dist as D
+
+    src, tgt, nrm, _ = synth.icp_pair(30_001, 40_000, seed=44)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=5, nn=nn)
+    full = icp(s, t, 0.12, np.eye(4), **kw)
+    for split in (True, 12_345):
+        lp = IcpLoop(s, t, 0.12, **kw)
+        r = D.ShardedIcp(lp, 0, len(src), "cuda", comm=comm1, split=split).run(np.eye(4), 5)
+        np.testing.assert_array_equal(r.transformation, full.transformation)
+        assert (r.fitness, r.inlier_rmse) == (full.fitness, full.inlier_rmse)
+
+
+def test_comm_failure_contract_world1():
+    """Failure injection (m3d_debug_comm_inject) at world size 1: a failed local RANSAC run
+    raises from run_sharded without poisoning the communicator (fail-soft exchange; the next run
+    is exact); a failure inside an ICP shard loop aborts the communicator — that call raises, and
+    every later call raises M3DCommError."""
+    from m3d._lib import M3DCommError, M3DError
+    from m3d.comm import LibComm, unique_id
+
+    c = LibComm(0, 1, uid=unique_id())
+    s, t, cc, _ = synth.ransac_pair(20_000, seed=6, noise_ratio=1.0)
+    cs = CorrSet(s, t, cc)
+    p = RansacParams(max_iter=2000, seed=4, thr=0.45, mode=_lib.SCORE_NORM, early_stop=False)
+    one = cs.run(p)
+    c.inject_failure(1)
+    with pytest.raises(M3DError, match="injected"):
+        cs.run_sharded(c, p)
+    assert not c.poisoned
+    sh = cs.run_sharded(c, p)
+    assert (sh.best_index, sh.best_count) == (one.best_index, one.best_count)
+    np.testing.assert_array_equal(sh.transformation, one.transformation)
+    src, tgt, nrm, _ = synth.icp_pair(20_000, 20_000, seed=45)
+    lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
+                 max_iteration=4, nn="grid")
+    lp.reset(np.eye(4))
+    lp.shard_steps(c, 0, 1)
+    c.inject_failure(2)
+    with pytest.raises(M3DError, match="injected"):
+        lp.shard_steps(c, 0, 2)
+    assert c.poisoned
+    with pytest.raises(M3DCommError):
+        lp.shard_steps(c, 0, 1)
+    with pytest.raises(M3DCommError):
+        cs.run_sharded(c, p)
