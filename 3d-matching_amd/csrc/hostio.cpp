@@ -11,7 +11,10 @@
 #include <system_error>
 #include <vector>
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <limits>
+#include <mutex>
 #include <thread>
 
 #include "../../include/m3d.h"
@@ -362,6 +365,176 @@ int m3d_merge_vertices(const double* xyz, int64_t n, double* uniq, int32_t* inve
     }
   }
   *n_unique = m;
+  return M3D_OK;
+}
+
+// Content keys of the drop-in's cache (m3d.cache "content" policy): the reference's per-call API
+// (ransac.py:195-236 per hypothesis) hands the same arrays over again and again, and an EXACT
+// cache must notice any in-place edit, so every call keys each array by its full content.  At
+// Nc = 1e5 that is ~5.6 MB per call; one thread of xxh3 took ~0.11 ms of a 0.15 ms call.  Here
+// the arrays are cut into fixed 64 KB chunks hashed with XXH64 (Y. Collet's published algorithm)
+// by a persistent pool, then each array's chunk hashes are hashed twice (two seeds) into its
+// 128-bit key: the result does not depend on the thread count.
+namespace {
+constexpr uint64_t kP1 = 11400714785074694791ull, kP2 = 14029467366897019727ull,
+                   kP3 = 1609587929392839161ull, kP4 = 9650029242287828579ull,
+                   kP5 = 2870177450012600261ull;
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t rd64(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+inline uint64_t xx_round(uint64_t acc, uint64_t in) { return rotl64(acc + in * kP2, 31) * kP1; }
+inline uint64_t xx_merge(uint64_t acc, uint64_t v) { return (acc ^ xx_round(0, v)) * kP1 + kP4; }
+
+uint64_t xxh64(const uint8_t* p, size_t len, uint64_t seed) {
+  const uint8_t* const end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
+    const uint8_t* const limit = end - 32;
+    do {
+      v1 = xx_round(v1, rd64(p));
+      v2 = xx_round(v2, rd64(p + 8));
+      v3 = xx_round(v3, rd64(p + 16));
+      v4 = xx_round(v4, rd64(p + 24));
+      p += 32;
+    } while (p <= limit);
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = xx_merge(xx_merge(xx_merge(xx_merge(h, v1), v2), v3), v4);
+  } else {
+    h = seed + kP5;
+  }
+  h += (uint64_t)len;
+  for (; p + 8 <= end; p += 8) h = rotl64(h ^ xx_round(0, rd64(p)), 27) * kP1 + kP4;
+  if (p + 4 <= end) {
+    uint32_t w;
+    memcpy(&w, p, 4);
+    h = rotl64(h ^ ((uint64_t)w * kP1), 23) * kP2 + kP3;
+    p += 4;
+  }
+  for (; p < end; ++p) h = rotl64(h ^ ((uint64_t)*p * kP5), 11) * kP1;
+  h ^= h >> 33;
+  h *= kP2;
+  h ^= h >> 29;
+  h *= kP3;
+  h ^= h >> 32;
+  return h;
+}
+
+constexpr size_t kHashChunk = (size_t)1 << 16;
+
+struct HashJob {
+  const uint8_t* p;
+  size_t len;
+  uint64_t seed;
+  uint64_t* out;
+};
+
+// Persistent workers (created on first use); a job list is handed out with one atomic counter,
+// the caller works too and waits for the last chunk.
+class HashPool {
+ public:
+  static HashPool& get() {
+    static HashPool* pool = new HashPool();  // never destroyed: workers outlive static teardown
+    return *pool;
+  }
+  void run(const std::vector<HashJob>& jobs) {
+    std::lock_guard<std::mutex> one(run_mu_);  // one batch at a time
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      jobs_ = &jobs;
+      next_.store(0);
+      left_.store((int64_t)jobs.size());
+      ++gen_;
+    }
+    cv_.notify_all();
+    work(&jobs);
+    std::unique_lock<std::mutex> lk(mu_);
+    // every chunk done AND every worker that joined this batch out of work(): the job list is
+    // the caller's and dies with this call
+    done_cv_.wait(lk, [&] { return left_.load() == 0 && active_ == 0; });
+    jobs_ = nullptr;
+  }
+
+ private:
+  HashPool() {
+    const int n = std::max(0, std::min(host_threads(), 8) - 1);
+    for (int t = 0; t < n; ++t)
+      std::thread([this] { loop(); }).detach();
+  }
+  void work(const std::vector<HashJob>* js) {
+    for (;;) {
+      const int64_t k = next_.fetch_add(1);
+      if (k >= (int64_t)js->size()) return;
+      const HashJob& j = (*js)[(size_t)k];
+      *j.out = xxh64(j.p, j.len, j.seed);
+      if (left_.fetch_sub(1) == 1) {
+        std::lock_guard<std::mutex> lk(mu_);
+        done_cv_.notify_all();
+      }
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::vector<HashJob>* js;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen && jobs_ != nullptr; });
+        seen = gen_;
+        js = jobs_;
+        ++active_;
+      }
+      work(js);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        --active_;
+      }
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::vector<HashJob>* jobs_ = nullptr;
+  std::atomic<int64_t> next_{0}, left_{0};
+  uint64_t gen_ = 0;
+  int active_ = 0;  // workers inside work() for the current batch (guarded by mu_)
+};
+}  // namespace
+
+uint64_t m3d_debug_xxh64(const void* p, size_t len, uint64_t seed) {
+  return xxh64(static_cast<const uint8_t*>(p), len, seed);
+}
+
+int m3d_content_keys(const void* const* bufs, const size_t* lens, int32_t n, uint64_t* keys) {
+  if (n < 0 || (n > 0 && (bufs == nullptr || lens == nullptr || keys == nullptr))) return M3D_ERR_INVALID;
+  std::vector<size_t> first((size_t)n + 1, 0);
+  for (int32_t i = 0; i < n; ++i) {
+    if (lens[i] > 0 && bufs[i] == nullptr) return M3D_ERR_INVALID;
+    first[(size_t)i + 1] = first[(size_t)i] + (lens[i] + kHashChunk - 1) / kHashChunk;
+  }
+  std::vector<uint64_t> ch(first[(size_t)n]);
+  std::vector<HashJob> jobs;
+  jobs.reserve(ch.size());
+  for (int32_t i = 0; i < n; ++i) {
+    const uint8_t* b = static_cast<const uint8_t*>(bufs[i]);
+    for (size_t c = first[(size_t)i], off = 0; off < lens[i]; ++c, off += kHashChunk)
+      jobs.push_back(HashJob{b + off, std::min(kHashChunk, lens[i] - off), (uint64_t)c - first[(size_t)i],
+                             &ch[c]});
+  }
+  if (jobs.size() >= 4 && host_threads() > 1) {
+    HashPool::get().run(jobs);
+  } else {
+    for (const HashJob& j : jobs) *j.out = xxh64(j.p, j.len, j.seed);
+  }
+  for (int32_t i = 0; i < n; ++i) {
+    const uint8_t* c0 = reinterpret_cast<const uint8_t*>(ch.data() + first[(size_t)i]);
+    const size_t cl = 8 * (first[(size_t)i + 1] - first[(size_t)i]);
+    keys[2 * i] = xxh64(c0, cl, 0x9E3779B97F4A7C15ull ^ (uint64_t)lens[i]);
+    keys[2 * i + 1] = xxh64(c0, cl, 0xC2B2AE3D27D4EB4Full + (uint64_t)lens[i]);
+  }
   return M3D_OK;
 }
 

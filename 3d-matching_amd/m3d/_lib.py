@@ -135,6 +135,8 @@ SIGNATURES = {
                                        C.POINTER(C.c_size_t)]),
     "m3d_format_ascii_rows": (C.c_int, [C.POINTER(dbl), i64, i32, vp, C.c_size_t, C.POINTER(C.c_size_t)]),
     "m3d_merge_vertices": (C.c_int, [C.POINTER(dbl), i64, C.POINTER(dbl), C.POINTER(i32), C.POINTER(i64)]),
+    "m3d_content_keys": (C.c_int, [C.POINTER(vp), C.POINTER(C.c_size_t), i32, C.POINTER(u64)]),
+    "m3d_debug_xxh64": (u64, [vp, C.c_size_t, u64]),
     "m3d_debug_kabsch3_host":(C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
     "m3d_debug_ldlt6_host": (C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }

@@ -5,8 +5,10 @@ benchmark_ransac.py:105-113 call compute_step_transformation / evaluate_inlier_r
 of times with the same arrays.  Packing (gather + centring + fp32/fp16 conversion) is O(N)
 device work plus one host sync, so packed objects are cached.  Two key policies:
 
-* "content" (default, exact): a hash of the array CONTENTS (xxh3-128, ~10 GB/s): a mutated array
-  gets a new key, never a stale object.  At Nc = 1e5 this hashes ~6 MB per call.
+* "content" (default, exact): a hash of the array CONTENTS: a mutated array gets a new key, never
+  a stale object.  At Nc = 1e5 that is ~5.6 MB per call: arrays of ≥ 64 KB are keyed by the
+  library's parallel hash (csrc/hostio.cpp m3d_content_keys: 64 KB chunks, XXH64, a persistent
+  thread pool; all the arrays of one call in one batch), smaller ones by xxh3-128.
 * "identity" (opt-in, ``set_policy("identity")`` or M3D_CACHE=identity): an array's content hash
   is remembered per buffer identity (data pointer, shape, strides, dtype) together with a sampled
   signature (xxh3 of ~4k elements spread over the buffer plus its first and last 256 bytes); the
@@ -20,6 +22,7 @@ repeated call does no O(Nc) host work beyond the key.
 
 from __future__ import annotations
 
+import ctypes as C
 import os
 from collections import OrderedDict
 
@@ -54,6 +57,47 @@ def _full(a: np.ndarray) -> str:
     return x.hexdigest()
 
 
+_NATIVE_MIN = 1 << 16
+_native_lib = None
+
+
+def _native():
+    """libm3d's m3d_content_keys, or None (library not loadable: xxh3 keys only)."""
+    global _native_lib
+    if _native_lib is None:
+        try:
+            from . import _lib
+
+            _native_lib = _lib.load()
+        except (ImportError, OSError):
+            _native_lib = False
+    return _native_lib or None
+
+
+def _content_keys(arrays) -> list:
+    """Exact content keys of several arrays; the large ones hashed together by the library."""
+    out = [None] * len(arrays)
+    big = []
+    for i, a in enumerate(arrays):
+        if a is None:
+            out[i] = "none"
+        elif a.nbytes >= _NATIVE_MIN and _native() is not None:
+            big.append(i)
+        else:
+            out[i] = _full(a)
+    if big:
+        arrs = [np.ascontiguousarray(arrays[i]) for i in big]
+        n = len(arrs)
+        bufs = (C.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        lens = (C.c_size_t * n)(*[a.nbytes for a in arrs])
+        keys = (C.c_uint64 * (2 * n))()
+        if _native().m3d_content_keys(bufs, lens, n, keys) != 0:
+            raise RuntimeError("m3d_content_keys failed")
+        for k, (i, a) in enumerate(zip(big, arrs)):
+            out[i] = f"{a.dtype.str}{a.shape}:{keys[2 * k]:016x}{keys[2 * k + 1]:016x}"
+    return out
+
+
 def _sampled(a: np.ndarray) -> str:
     flat = a.reshape(-1)
     x = xxhash.xxh3_64()
@@ -78,12 +122,12 @@ def array_key(a) -> str:
         if hit is not None and hit[0] == sig:
             _ident.move_to_end(ident)
             return hit[1]
-        h = _full(a)
+        h = _content_keys([a])[0]
         _ident[ident] = (sig, h)
         while len(_ident) > 4 * _MAX:
             _ident.popitem(last=False)
         return h
-    return _full(a)
+    return _content_keys([a])[0]
 
 
 def _get(key, make):
@@ -105,6 +149,8 @@ def _get(key, make):
 
 
 def corr_key(src_pts, tgt_pts, corr) -> tuple:
+    if _POLICY == "content":  # one batch for the three arrays
+        return ("cs",) + tuple(_content_keys([np.asarray(src_pts), np.asarray(tgt_pts), np.asarray(corr)]))
     return ("cs", array_key(src_pts), array_key(tgt_pts), array_key(corr))
 
 
@@ -137,7 +183,8 @@ def corrset(src_pts, tgt_pts, corr) -> CorrSet:
 def corrset_gathered(p_src, p_tgt) -> CorrSet:
     p_src = np.asarray(p_src, np.float64)
     p_tgt = np.asarray(p_tgt, np.float64)
-    return _get(("csg", array_key(p_src), array_key(p_tgt)), lambda: CorrSet(p_src=p_src, p_tgt=p_tgt))
+    keys = _content_keys([p_src, p_tgt]) if _POLICY == "content" else [array_key(p_src), array_key(p_tgt)]
+    return _get(("csg",) + tuple(keys), lambda: CorrSet(p_src=p_src, p_tgt=p_tgt))
 
 
 def cloud(points, normals=None) -> Cloud:

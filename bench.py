@@ -313,6 +313,53 @@ def main():
                          "terms_avg_launch_ms": g_terms_ms},
         }
 
+    # ------------------------------------------------------------------ cfg1 strong scaling
+    # BASELINE metric as worded ("100k<->100k pts, 1/2/4/8 GPU"): the FIXED cfg1 pair over the N
+    # GPUs — sources sharded ns/N per rank against the replicated target, SUM of the 32 term slots
+    # (SURVEY §8(e) "ICP alternative"), value = ICP iterations/s of that one problem.  N = 1: the
+    # headline run itself (the same workload), so SCALE's N = 1 line equals BENCH.
+    cfg1_strong = None
+    if world == 1:
+        cfg1_strong = {"value": cfg1["value"], "ms_per_step": cfg1["ms_per_step"],
+                       "grid_value": None if icp_grid is None else icp_grid["value"],
+                       "note": "N = 1: the headline cfg1 run (same workload)"}
+    else:
+        s1, t1, n1, T1 = synth.icp_pair(ns, nt, seed=0)  # the N = 1 pair
+        o1, c1 = D.shard_bounds(ns, world, rank)
+        s1c, t1c = Cloud(s1[o1:o1 + c1]), Cloud(t1, n1)
+        cfg1_strong = {"workload": f"cfg1 fixed pair: {ns}<->{nt}, {iters} iterations, sources sharded "
+                                   f"over {world} GPUs ({c1} on rank {rank}), target replicated, SUM terms",
+                       "scaling": "strong", "unit": "ICP iter/s (one 100k x 100k problem)"}
+        for nn in ("brute",) + (() if args.no_grid else ("grid",)):
+            lp = IcpLoop(s1c, t1c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters, nn=nn)
+            lp.set_source_total(ns)
+            run = icp_runner(lp, iters, "source", 0, ns)
+            for _ in range(args.warmup):
+                run()
+            torch.cuda.synchronize()
+            e1, _, prof = timed(run, args.steps, (K_NN, K_TERMS))
+            rs1 = lp.result()
+            sec = {"value": iters * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3,
+                   "nn_avg_launch_ms": max_over_ranks(prof[K_NN][0] / max(prof[K_NN][1], 1)),
+                   "fitness": rs1.fitness, "max_abs_err_vs_T_true": float(np.abs(rs1.transformation - T1).max())}
+            if nn == "brute":
+                cfg1_strong.update(sec)
+            else:
+                cfg1_strong["grid_value"] = sec["value"]
+                cfg1_strong["grid"] = sec
+            del lp
+        del s1c, t1c
+
+    # ------------------------------------------------------------------ cfg1 cold call
+    # What the reference pays per refine_registration call (icp.py:42-48 builds its KD-tree every
+    # call): fresh device clouds (H2D + centring + fp32 packing), the loop object (grids, Morton
+    # source copy, fp16 MFMA tiles, target records) and the 50 iterations, per stage (synchronised
+    # between stages); plus the drop-in refine_registration on fresh Ply-likes (grid NN, Open3D's
+    # default convergence criteria).
+    cfg1_cold = None
+    if rank == 0 and world == 1:
+        cfg1_cold = bench_cold(args, src, tgt_all[:nt], nrm_all[:nt], r, iters)
+
     # ------------------------------------------------------------------ cfg3: 1M <-> 1M, strong
     cfg3 = None
     if not args.no_cfg3 or args.config == "cfg3":
@@ -398,6 +445,30 @@ def main():
         pairs = nc * hyps_per_launch
         sc_algo = SCORE_FLOP_PER_PAIR * pairs / (sc_avg * 1e-3) / 1e12
         sc_issued = SCORE_MFMA_FLOP_PER_PAIR * pairs / (sc_avg * 1e-3) / 1e12
+        # the FIXED H = 1e5 batch split over the ranks (hypothesis ids [off, off + cnt) per rank,
+        # MAX of the packed key): strong scaling of one cfg2 run; N = 1: the run above
+        ransac_strong = {"value": world * H * args.ransac_steps / rel, "ms_per_run": rel / args.ransac_steps * 1e3,
+                         "hyps_per_run": H, "note": "N = 1: the cfg2 run above (same workload)"}
+        if world > 1:
+            o2, c2 = D.shard_bounds(H, world, rank)
+            p2 = RansacParams(max_iter=c2, seed=42, thr=thr, mode=_lib.SCORE_NORM, early_stop=False, hyp0=o2)
+
+            def ransac_strong_run():
+                cs.run_async(p2, res_buf)
+                if comm_name == "libm3d-rccl":
+                    cs.best_allreduce(comm, res_buf, o2, key)
+                else:
+                    key.copy_(res_buf[19:20] * (1 << 32) + (0xFFFFFFFF - (o2 + res_buf[17:18])))
+                    comm.max_(key)
+
+            for _ in range(3):
+                ransac_strong_run()
+            torch.cuda.synchronize()
+            rs_el, _, _ = timed(ransac_strong_run, args.ransac_steps, ())
+            kc, kid = D.unpack_best_key(int(key.item()))
+            ransac_strong = {"value": H * args.ransac_steps / rs_el, "ms_per_run": rs_el / args.ransac_steps * 1e3,
+                             "hyps_per_run": H, "hyps_on_rank": c2, "best_id": kid, "best_count": kc,
+                             "workload": f"cfg2 fixed batch: {H} hypotheses split over {world} GPUs, MAX key"}
         ransac = {
             "metric": "RANSAC hypotheses/sec (cfg2: Nc=1e5, a1+a2, no early stop)",
             "value": world * H * args.ransac_steps / rel, "unit": "hyp/s",
@@ -414,6 +485,7 @@ def main():
                          "note": "27-flop/pair algorithmic rate / dense FP16 MFMA peak (the residuals "
                                  "run on the matrix pipe, DESIGN.md 3.2a)"},
             "kabsch_avg_launch_ms": kb_ms / max(kb_n, 1),
+            "strong": ransac_strong,
         }
 
     # ------------------------------------------------------------------ drop-in per-call path
@@ -461,6 +533,8 @@ def main():
         "ms_per_step_with_kernel_events": cfg1["ms_per_step_with_kernel_events"],
         "cfg1": {k: v for k, v in cfg1.items() if k != "roofline"} if args.config == "cfg3" else None,
         "icp_grid": icp_grid,
+        "cfg1_strong": cfg1_strong,
+        "cfg1_cold": cfg1_cold,
         "cfg3": (cfg3 if args.config != "cfg3" or cfg3 is None
                  else {k: v for k, v in cfg3.items() if k != "roofline"}),
         "ransac": ransac,
@@ -474,6 +548,59 @@ def main():
     del comm
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_cold(args, src, tgt, nrm, r, iters, reps=3):
+    """cfg1 from nothing on the device: per-stage wall ms (median of `reps` after one warm call)."""
+    import numpy as np
+    import torch
+
+    from m3d import cache
+    from m3d.core import Cloud, IcpLoop
+    from matcher.icp import refine_registration
+    from ply import Ply
+
+    def once(nn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sc, tc = Cloud(src), Cloud(tgt, nrm)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        lp = IcpLoop(sc, tc, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters, nn=nn)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        lp.reset(np.eye(4))
+        lp.steps(iters + 1)
+        lp.result()
+        t3 = time.perf_counter()
+        return {"clouds_ms": (t1 - t0) * 1e3, "loop_create_ms": (t2 - t1) * 1e3,
+                "iterations_ms": (t3 - t2) * 1e3, "total_ms": (t3 - t0) * 1e3}
+
+    def refine():
+        cache.clear()
+        a, b = Ply.from_arrays(src), Ply.from_arrays(tgt, nrm)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = refine_registration(a, b, np.eye(4), 0.3)
+        t1 = time.perf_counter()
+        return (t1 - t0) * 1e3, res
+
+    out = {"workload": f"cfg1 pair {len(src)}<->{len(tgt)}, {iters} iterations, every device object built "
+                       "inside the timed region"}
+    for nn in ("brute", "grid"):
+        once(nn)
+        runs = [once(nn) for _ in range(reps)]
+        out[nn] = {k: float(np.median([x[k] for x in runs])) for k in runs[0]}
+    refine()
+    ms = []
+    for _ in range(reps):
+        t, res = refine()
+        ms.append(t)
+    out["refine_registration_ms"] = float(np.median(ms))
+    out["refine_registration_iterations_note"] = ("Open3D default criteria (1e-6, 1e-6, 30), grid NN; "
+                                                  f"fitness {res.fitness:.4f}")
+    cache.clear()
+    return out
 
 
 def bench_cfg4(args):

@@ -400,6 +400,8 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
  * of the math.  Never used by the product path. */
 int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16);
 int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6);
+/* XXH64 of [p, p + len) (the chunk hash of m3d_content_keys; known-answer tests). */
+uint64_t m3d_debug_xxh64(const void* p, size_t len, uint64_t seed);
 /* Failure injection for the multi-GPU failure tests: what = 1 fails this rank's next local run of
  * m3d_ransac_run_sharded, 2 its next ICP shard-loop iteration (0 clears). */
 int m3d_debug_comm_inject(m3d_comm* c, int what);
@@ -423,6 +425,11 @@ int m3d_format_ascii_rows(const double* data, int64_t rows, int32_t cols, char* 
  * inverse [host] n int32 (corner → vertex id), *n_unique. */
 int m3d_merge_vertices(const double* xyz, int64_t n, double* uniq, int32_t* inverse,
                        int64_t* n_unique);
+/* Content keys of the drop-in's exact cache (m3d.cache): keys [host] 2·n uint64, the 128-bit key
+ * of each buffer [host] bufs[i], lens[i] bytes — its 64 KB chunks hashed (XXH64, chunk index as
+ * seed) by a persistent host thread pool, the chunk hashes hashed again with two seeds.  The
+ * same bytes give the same key whatever the thread count. */
+int m3d_content_keys(const void* const* bufs, const size_t* lens, int32_t n, uint64_t* keys);
 
 #ifdef __cplusplus
 }

@@ -547,3 +547,33 @@ def test_crash_script_large_transformation(ply_pair):
     f = M.evaluate_inlier_ratio(src, tgt, corr, big, 0.3)
     assert f == O.evaluate_inlier_ratio(src.pcd_down.points, tgt.pcd_down.points, corr, big, 0.3)
     assert f == 0.0
+
+
+def test_drop_in_sees_in_place_mutation_between_calls():
+    """The per-call drop-in caches packed device objects by exact content (m3d.cache): editing
+    the caller's arrays IN PLACE between calls (same buffers, same shapes) must give the
+    reference's answer for the new contents, never the stale cached one — at Nc = 1e5, where the
+    keys come from the library's parallel hash."""
+    from matcher import ransac as M
+    from ply import Ply
+
+    s, t, corr, T = synth.ransac_pair(100_000, seed=8)
+    src, tgt = Ply.from_arrays(s), Ply.from_arrays(t)
+    sp, tp = src.pcd_down.points, tgt.pcd_down.points
+    assert M.evaluate_inlier_ratio(src, tgt, corr, T, 0.3) == O.evaluate_inlier_ratio(sp, tp, corr, T, 0.3)
+    sp[corr[:5000, 0]] += 1.0                       # move 5000 matched source points away
+    f1 = M.evaluate_inlier_ratio(src, tgt, corr, T, 0.3)
+    assert f1 == O.evaluate_inlier_ratio(sp, tp, corr, T, 0.3) and f1 < 0.96
+    corr[:20000, 1] = corr[20000:40000, 1]          # rewire 20000 correspondences in place
+    f2 = M.evaluate_inlier_ratio(src, tgt, corr, T, 0.3)
+    assert f2 == O.evaluate_inlier_ratio(sp, tp, corr, T, 0.3) and f2 < f1
+    tp[:] = tp[::-1].copy()                         # permute the target in place
+    f3 = M.evaluate_inlier_ratio(src, tgt, corr, T, 0.3)
+    assert f3 == O.evaluate_inlier_ratio(sp, tp, corr, T, 0.3)
+    # compute_step_transformation reads the edited rows too
+    np.random.seed(3)
+    r = M.compute_step_transformation(src, tgt, corr)
+    ref_rng = np.random.RandomState(3)
+    idx = ref_rng.choice(len(corr), 3, replace=False)
+    T_ref, _ = O.kabsch3(sp[corr[idx, 0]], tp[corr[idx, 1]])
+    np.testing.assert_allclose(r.transformation, T_ref, atol=1e-9)
