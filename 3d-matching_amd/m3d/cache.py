@@ -6,7 +6,7 @@ of times with the same arrays.  Packing (gather + centring + fp32/fp16 conversio
 device work plus one host sync, so packed objects are cached.  Two key policies:
 
 * "content" (default, exact): a hash of the array CONTENTS: a mutated array gets a new key, never
-  a stale object.  At Nc = 1e5 that is ~5.6 MB per call: arrays of ≥ 64 KB are keyed by the
+  a stale object.  At Nc = 1e5 that is ~5.6 MB per call: arrays of ≥ 256 KB are keyed by the
   library's parallel hash (csrc/hostio.cpp m3d_content_keys: 64 KB chunks, XXH64, a persistent
   thread pool; all the arrays of one call in one batch), smaller ones by xxh3-128.
 * "identity" (opt-in, ``set_policy("identity")`` or M3D_CACHE=identity): an array's content hash
@@ -57,7 +57,7 @@ def _full(a: np.ndarray) -> str:
     return x.hexdigest()
 
 
-_NATIVE_MIN = 1 << 16
+_NATIVE_MIN = 1 << 18  # below this one xxh3 pass beats waking the pool (5k-row arrays: 120 KB)
 _native_lib = None
 
 
