@@ -98,9 +98,13 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_substr: str):
-    """HBM bytes per launch from the newest committed PMC summary (profiles/pmc_*.json)."""
-    files = sorted((ROOT / "profiles").glob("pmc_*.json"))
+def pmc_traffic(kernel_substr: str, shape: str = ""):
+    """HBM bytes per launch from the newest committed PMC summary (profiles/pmc_rNN.json at the
+    bench's cfg1 / cfg2 shapes; shape="1m": profiles/pmc_rNN_1m.json, the 1M x 1M grid)."""
+    import re
+
+    pat = re.compile(r"pmc_r\d+" + (f"_{shape}" if shape else "") + r"\.json$")
+    files = sorted(f for f in (ROOT / "profiles").glob("pmc_*.json") if pat.search(f.name))
     for f in reversed(files):
         try:
             d = json.loads(f.read_text())
@@ -397,7 +401,8 @@ def main():
                 sec["roofline"] = {"bound": "hbm", "kernel": "grid_nn_batched_kernel",
                                    "achieved": g_bytes / (avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": g_bytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                   "bytes_per_launch": g_bytes}
+                                   "bytes_per_launch": g_bytes,
+                                   "traffic": pmc_traffic("grid_nn", "1m")[0] if world == 1 else None}
                 cfg3["grid"] = sec
             del lp
         del s3c, t3c
