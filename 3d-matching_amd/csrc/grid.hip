@@ -682,11 +682,15 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
     const char* e = getenv("M3D_GRID_BATCHED");
     return !(e && atoi(e) == 0);
   }();
-  static const int L = [] {
+  // lanes per query: M3D_GRID_LANES, else by size — 4 while the queries fill about one occupancy
+  // round (cfg1: 15.1 µs vs 18.3 at 2), 2 beyond (1M × 125k 71.6 → 60.1 µs, 1M × 1M 117.7 →
+  // 112.1 µs: twice the queries in flight per wave)
+  static const int L_env = [] {
     const char* e = getenv("M3D_GRID_LANES");
-    const int v = e ? atoi(e) : kGridLanesDefault;
-    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : kGridLanesDefault;
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
   }();
+  const int L = L_env ? L_env : ((ns - q0) > 300000 ? 2 : kGridLanesDefault);
   static const int RB = [] {  // M3D_GRID_RB = kR·10 + kB (tuning): 22, 41, 42, 24
     const char* e = getenv("M3D_GRID_RB");
     const int v = e ? atoi(e) : 22;
