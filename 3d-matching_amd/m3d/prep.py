@@ -86,13 +86,22 @@ def compute_fpfh(points, normals, radius: float, max_nn: int = 100):
     return out[: c.n].cpu().numpy()
 
 
+def _feature_rows(f):
+    """N×33 feature rows from an Open3D-style Feature (``.data`` is 33×N) or an array."""
+    if not isinstance(f, np.ndarray) and hasattr(f, "data"):
+        return np.ascontiguousarray(np.asarray(f.data, np.float64).T)
+    return f
+
+
 def feature_correspondences(f_src, f_tgt, mutual_filter: bool = False,
                             mutual_consistent_ratio: float = 0.1) -> np.ndarray:
-    """CorrespondencesFromFeatures on N×33 feature rows → (M, 2) int32 (source, target)."""
+    """CorrespondencesFromFeatures (ransac.py:85) on N×33 feature rows, or on Open3D-style
+    Features (33×N ``.data``) → (M, 2) int32 (source, target)."""
     torch = _torch()
     ctx = context()
-    fs = to_device(np.asarray(f_src, np.float64), shape_tail=None)
-    ft = to_device(np.asarray(f_tgt, np.float64), shape_tail=None)
+    f_src, f_tgt = _feature_rows(f_src), _feature_rows(f_tgt)
+    fs = to_device(f_src, shape_tail=None)
+    ft = to_device(f_tgt, shape_tail=None)
     if fs.ndim != 2 or ft.ndim != 2 or fs.shape[1] != ft.shape[1]:
         raise ValueError("features must be N×33 arrays")
     ns, nt = fs.shape[0], ft.shape[0]

@@ -13,7 +13,7 @@ KTC-Security-Circle/3d-matching ``src/matcher/ransac.py``; the arithmetic runs i
   (ransac.py:239-277): exact counts (fp32 screen + fp64 guard-band recheck on the device).
 * ``compute_feature_correspondences`` (ransac.py:62-101): FPFH feature-space NN on the device
   plus the reference's outlier injection on the global numpy RNG.
-* ``global_registration`` (ransac.py:20-59): see ``m3d.feature_ransac``.
+* ``global_registration`` (ransac.py:20-59): ``m3d.prep`` feature correspondences + a6.
 
 Additions (batched, device-resident): ``run_ransac`` runs the whole step-RANSAC loop of
 ``_visualize_matcher.py:343-470`` on the GPU; ``register`` is the coarse-to-fine façade
@@ -99,20 +99,28 @@ def _packed(s_pts: np.ndarray, t_pts: np.ndarray, corr: np.ndarray, need_all: bo
 def global_registration(src, tgt, voxel_size: float, iteration: int = 30) -> RegistrationResult:
     """ransac.py:20-59: feature-matching RANSAC (mutual filter, Point-to-Point, ransac_n=3,
     EdgeLength(0.9) + Distance(1.5·v) checkers, RANSACConvergenceCriteria(iteration, 0.999))."""
-    from m3d import feature_ransac
+    # Open3D RegistrationRANSACBasedOnFeatureMatching = CorrespondencesFromFeatures (mutual) +
+    # RegistrationRANSACBasedOnCorrespondence.  Open3D draws each hypothesis' rows from its global
+    # RNG inside an OpenMP loop (not reproducible run to run); here the rows come from the counter
+    # sampler (seed, hypothesis id) and the early exit follows the sequential semantics.
+    from m3d import prep
 
     dist_thresh = voxel_size * 1.5
-    return feature_ransac.registration_ransac_based_on_feature_matching(
-        _down_points(src), _down_points(tgt), src.pcd_fpfh, tgt.pcd_fpfh, True, dist_thresh,
-        ransac_n=3, edge_length=0.9, distance=dist_thresh, max_iteration=iteration, confidence=0.999)
+    if dist_thresh <= 0.0:  # Open3D: an empty RegistrationResult for a non-positive distance
+        return RegistrationResult()
+    corres = prep.feature_correspondences(src.pcd_fpfh, tgt.pcd_fpfh, True)
+    out = prep.ransac_on_correspondences(_down_points(src), _down_points(tgt), corres, dist_thresh,
+                                         ransac_n=3, edge_length=0.9, distance=dist_thresh,
+                                         max_iteration=iteration, confidence=0.999)
+    return RegistrationResult(out.transformation, out.fitness, out.inlier_rmse, out.correspondence_set)
 
 
 def compute_feature_correspondences(src, tgt, mutual_filter: bool = False,
                                     noise_ratio: float = 0.0) -> np.ndarray:
     """ransac.py:62-101.  Returns an (N,2) int32 array (the Vector2iVector's numpy view)."""
-    from m3d import feature_ransac
+    from m3d import prep
 
-    corres_np = feature_ransac.correspondences_from_features(src.pcd_fpfh, tgt.pcd_fpfh, mutual_filter)
+    corres_np = prep.feature_correspondences(src.pcd_fpfh, tgt.pcd_fpfh, mutual_filter)
     if noise_ratio > 0:                                         # ransac.py:89-99
         n_original = len(corres_np)
         n_noise = int(n_original * noise_ratio)

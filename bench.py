@@ -666,8 +666,8 @@ def bench_cfg4(args):
             # a 0.03 validation radius below the 0.05 point noise, so no hypothesis reaches the
             # early exit and every checker-passing one of 30000 is validated (grid.hip
             # validate_kernel batches)
-            from m3d import feature_ransac, prep
-            corr = feature_ransac.correspondences_from_features(src.pcd_fpfh, tgt.pcd_fpfh, True)
+            from m3d import prep
+            corr = prep.feature_correspondences(src.pcd_fpfh, tgt.pcd_fpfh, True)
             sp, tp = src.pcd_down.points, tgt.pcd_down.points
             kw = dict(edge_length=0.9, distance=0.45, max_iteration=30000, confidence=0.999)
             prep.ransac_on_correspondences(sp, tp, corr, 0.03, **kw)  # warm
