@@ -1031,23 +1031,42 @@ __device__ __forceinline__ void vec6_to_matrix_wave(const double x[6], double T[
                     __shfl(sn, 1, kWave), __shfl(cs, 2, kWave), __shfl(sn, 2, kWave), T);
 }
 
-// One evaluation + update from the reduced sums.  Run by one whole wave: every lane computes
-// the same values (so its stores to *s agree) except the three sincos of vec6_to_matrix_wave.
-// Everything the solve reads is loaded up front: interleaved with its stores, each later load
-// of *s or sums (which the compiler must assume may alias) waited for the stores before it.
-__device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp) {
+// The state fields the solve reads, loaded by solve_in — in the fused tail before the partial
+// sums, so that their global round trip overlaps the reduction's.
+struct SolveIn {
+  int32_t evals, iters;
+  double prev_fit, prev_rmse, r2;
+  float eq;
+  double T[16];
+  float rt[12];
+};
+
+__device__ __forceinline__ void solve_in(const IcpState* s, SolveIn& in) {
+  in.evals = s->evals;
+  in.iters = s->iters;
+  in.prev_fit = s->prev_fitness;
+  in.prev_rmse = s->prev_rmse;
+  in.r2 = s->r2;
+  in.eq = s->eq;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) in.T[k] = s->T[k];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) in.rt[k] = s->Rt32[k];
+}
+
+__device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp, const SolveIn& in) {
   double sm[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) sm[k] = sums[k];
-  const int32_t evals = s->evals, iters = s->iters;
-  const double prev_fit = s->prev_fitness, prev_rmse = s->prev_rmse, r2 = s->r2;
-  const float eq = s->eq;
+  const int32_t evals = in.evals, iters = in.iters;
+  const double prev_fit = in.prev_fit, prev_rmse = in.prev_rmse, r2 = in.r2;
+  const float eq = in.eq;
   double T[16];
   float rt[12];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) T[k] = s->T[k];
+  for (int k = 0; k < 16; ++k) T[k] = in.T[k];
 #pragma unroll
-  for (int k = 0; k < 12; ++k) rt[k] = s->Rt32[k];
+  for (int k = 0; k < 12; ++k) rt[k] = in.rt[k];
   const double count = sm[28];
   const double fit = count > 0.0 ? count / (double)sp.ns : 0.0;
   const double rmse = count > 0.0 ? sqrt(sm[29] / count) : 0.0;
@@ -1119,7 +1138,9 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
 __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
                              SolveParams sp) {
   if (threadIdx.x >= kWave || s->done) return;
-  solve_state(sums, s, sp);
+  SolveIn in;
+  solve_in(s, in);
+  solve_state(sums, s, sp, in);
 }
 
 // Fused single-device iteration tail: terms → block partial → the last block to finish (ticket)
@@ -1148,6 +1169,8 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
   }
   __syncthreads();
   if (!last) return;
+  SolveIn in;
+  if (do_solve && threadIdx.x < kWave) solve_in(s, in);
   // every load of the other blocks' partials is an sc1 load (L2-coherent, bypasses L1)
   const int slot = threadIdx.x & (kTermSlots - 1);
   constexpr int kG = kReduceGroups / (kTermsBlock / kTermSlots);  // groups per thread
@@ -1187,7 +1210,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
   __syncthreads();
   if (threadIdx.x < kWave) {
     if (threadIdx.x == 0) s->ticket = 0;
-    if (do_solve) solve_state(red[0], s, sp);
+    if (do_solve) solve_state(red[0], s, sp, in);
   }
 }
 
