@@ -1,4 +1,4 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the N>1 protocols in m3d/dist.py.
+"""Multi-process (world_size 2 and 3, gloo, CPU) tests of the N>1 protocols in m3d/dist.py.
 
 The driver (ShardedIcp) is the code bench.py runs over RCCL; here its backend is an oracle-backed
 CPU implementation of the same calls (shard_nn / shard_claim / shard_terms / solve), so the
@@ -132,19 +132,18 @@ def _icp_worker(rank, world, port, path, split=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("split", [False, 1733])
-def test_sharded_icp_protocol_matches_single_process(tmp_path, split):
+@pytest.mark.parametrize("world,split", [(2, False), (2, 1733), (3, False), (3, 1733)])
+def test_sharded_icp_protocol_matches_single_process(tmp_path, world, split):
     """Target shards over gloo equal the single-process oracle, with the exchange in one piece
     and split (the first slot half's MIN in flight — async — while the second half's NN runs,
-    m3d_icp_shard_steps' schedule)."""
-    world = 2
+    m3d_icp_shard_steps' schedule); world 3 gives uneven shards (6001 targets)."""
     mp.spawn(_icp_worker, args=(world, free_port(), str(tmp_path), split), nprocs=world, join=True)
     src, tgt, nrm, _ = synth.icp_pair(4000, 6001, seed=21)
     ref = I.registration_icp(src, tgt, 0.12, np.eye(4), tgt_normals=nrm, relative_fitness=-1,
                              relative_rmse=-1, max_iteration=8)
     r0 = np.load(tmp_path / "rank0.npz")
-    r1 = np.load(tmp_path / "rank1.npz")
-    np.testing.assert_array_equal(r0["T"], r1["T"])  # every rank holds the identical transform
+    for r in range(1, world):  # every rank holds the identical transform
+        np.testing.assert_array_equal(r0["T"], np.load(tmp_path / f"rank{r}.npz")["T"])
     np.testing.assert_allclose(r0["T"], ref["transformation"], atol=1e-10)
     assert abs(float(r0["fit"]) - ref["fitness"]) < 1e-12
     assert int(r0["iters"]) == 8
@@ -162,15 +161,15 @@ def _icp_source_worker(rank, world, port, path):
     dist.destroy_process_group()
 
 
-def test_source_sharded_icp_protocol_matches_single_process(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_source_sharded_icp_protocol_matches_single_process(tmp_path, world):
     mp.spawn(_icp_source_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
     src, tgt, nrm, _ = synth.icp_pair(4001, 6000, seed=22)
     ref = I.registration_icp(src, tgt, 0.12, np.eye(4), tgt_normals=nrm, relative_fitness=-1,
                              relative_rmse=-1, max_iteration=8)
     r0 = np.load(tmp_path / "rank0.npz")
-    r1 = np.load(tmp_path / "rank1.npz")
-    np.testing.assert_array_equal(r0["T"], r1["T"])
+    for r in range(1, world):
+        np.testing.assert_array_equal(r0["T"], np.load(tmp_path / f"rank{r}.npz")["T"])
     np.testing.assert_allclose(r0["T"], ref["transformation"], atol=1e-10)
     assert abs(float(r0["fit"]) - ref["fitness"]) < 1e-12  # global denominator
     assert abs(float(r0["rmse"]) - ref["inlier_rmse"]) < 1e-12
@@ -190,13 +189,14 @@ def _ransac_worker(rank, world, port, path):
     dist.destroy_process_group()
 
 
-def test_ransac_best_key_allreduce_first_max(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_ransac_best_key_allreduce_first_max(tmp_path, world):
     rng = np.random.default_rng(0)
     counts = rng.integers(0, 50, 1001)
-    counts[[100, 700, 900]] = 77  # ties across both shards: the lowest id must win
+    counts[[100, 700, 900]] = 77  # ties across shards: the lowest id must win
     np.save(tmp_path / "counts.npy", counts)
-    mp.spawn(_ransac_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
-    for r in range(2):
+    mp.spawn(_ransac_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
         assert tuple(np.load(tmp_path / f"best{r}.npy")) == (77, 100)
 
 
