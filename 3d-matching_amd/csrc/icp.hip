@@ -519,7 +519,7 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 }
 
 template <int kMG, int kTH>
-__global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restrict__ src32,
+__global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) void nn_mfma_kernel(const float4* __restrict__ src32,
                                                           int64_t ns,
                                                           const int32_t* __restrict__ order,
                                                           const uint4* __restrict__ tgt16,
@@ -531,7 +531,8 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
                                                           uint32_t* __restrict__ near2,
                                                           uint64_t exp_mask,
                                                           unsigned long long* __restrict__ stats,
-                                                          int strided, SeedArgs sa, int64_t q0) {
+                                                          int strided, SeedArgs sa, int64_t q0,
+                                                          int defer) {
   // exp_mask: all ones; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
   // (profiling experiment only: the keys are then wrong).  stats (M3D_NN_STATS=1, diagnostics
   // only, else null): [0] flagged (group, sub-tile) steps, [1] all steps.
@@ -590,6 +591,17 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   }
   const floatx16 zacc = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
                          0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  // Deferred exact passes: a group whose every query starts from a real seed already screens
+  // with (nearly) its final threshold, so its flagged sub-tiles need not be resolved inside the
+  // tile — where one wave's exact pass holds the block's other 7 waves at the tile barrier —
+  // but can wait in a per-wave list (tile offset, flagged bits) until after the sweep.  The
+  // candidates evaluated are the same sub-tiles' rows, so the key is the same.
+  uint32_t dfr = 0;
+  if (defer) {
+#pragma unroll
+    for (int g = 0; g < kMG; ++g)
+      if (!((force >> (g * 8)) & 1u) && __all(qi[g] < 0 || key_real(k1[g]))) dfr |= 1u << g;
+  }
   // Tiles of kTH × 256 targets, [buffer][lane half][target]: a half-wave's 32 ds_read_b128 hit
   // 32 consecutive 16-B slots.  Thread t stages kTH elements (e = t + u·512: plane e / kTT, target
   // e % kTT; mf16 is stored as two planes, so the loads are coalesced).  The sweep runs the tile
@@ -601,6 +613,16 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
   static_assert(kMBlock == 2 * kMTile, "one 16-B operand half per thread per half tile");
   static_assert(kSub * kMG <= 64, "hit mask holds every (group, sub-tile)");
   __shared__ uint4 t16[2][2][kTT];
+  constexpr int kDefer = 16;  // deferred entries per wave (more: resolved in the tile as before)
+  constexpr bool kCanDefer = kSub * kMG <= 32;
+  __shared__ uint64_t dlist[kMBlock / 64][kDefer];
+  int dn = 0;
+  uint64_t dmask = 0;  // (group, sub-tile) bits of the deferring groups
+#pragma unroll
+  for (int g = 0; g < kMG; ++g)
+    if ((dfr >> g) & 1u) dmask |= kGMask << (g * kSub);
+  dmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(dmask >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dmask);  // wave-uniform: SGPRs
   // contiguous slice of slice_len targets per grid.y, or (strided) every gridDim.y-th tile
   const int64_t tstep = strided ? (int64_t)gridDim.y * kTT : (int64_t)kTT;
   const int64_t jb = strided ? (int64_t)blockIdx.y * kTT : (int64_t)blockIdx.y * slice_len;
@@ -662,6 +684,14 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
       atomicAdd(&stats[0], (unsigned long long)__builtin_popcountll(hm));
       atomicAdd(&stats[1], (unsigned long long)(kSub * kMG));
     }
+    if (kCanDefer) {
+      const uint64_t hd = hm & dmask & exp_mask;
+      if (hd != 0 && dn < kDefer) {
+        if (lane == 0) dlist[wave][dn] = ((uint64_t)(uint32_t)j0 << 32) | (uint32_t)hd;
+        ++dn;
+        hm &= ~hd;
+      }
+    }
 #pragma unroll
     for (int g = 0; g < kMG; ++g) {
       uint64_t mg = (hm >> (g * kSub)) & kGMask & exp_mask;
@@ -689,6 +719,23 @@ __global__ __launch_bounds__(kMBlock) void nn_mfma_kernel(const float4* __restri
     }
     __syncthreads();
     buf ^= 1;
+  }
+  // the deferred exact passes (rows from global memory: the tiles have left LDS)
+  for (int e = 0; e < dn; ++e) {
+    const uint64_t ent = dlist[wave][e];
+    const int64_t jt = (int64_t)(ent >> 32);
+#pragma unroll
+    for (int g = 0; g < kMG; ++g) {
+      uint64_t mg = ((ent & 0xFFFFFFFFull) >> (g * kSub)) & kGMask;
+      while (mg != 0) {
+        const int sub = __builtin_ctzll(mg);
+        mg &= mg - 1;
+        nn_exact_rows(tgt32 + jt + sub * 32, off, h, qx[g], qy[g], qz[g], r2_hi, k1[g], k1d[g], n2[g]);
+        const uint64_t o1 = shfl_xor64(k1[g], 32);
+        const float on2 = __shfl_xor(n2[g], 32);
+        near_merge(k1[g], k1d[g], n2[g], o1, on2);
+      }
+    }
   }
 #pragma unroll
   for (int g = 0; g < kMG; ++g) {
@@ -1411,10 +1458,15 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
       }
     }
     const SeedArgs sa{s->corr, s->tgt->xyz32, s->tgt->n, self_seed ? 1 : 0};
+    // seeded groups resolve their flagged sub-tiles after the sweep (M3D_NN_DEFER=0: in the tile)
+    static const int defer = [] {
+      const char* e = getenv("M3D_NN_DEFER");
+      return (e && atoi(e) == 0) ? 0 : 1;
+    }();
 #define M3D_NN_LAUNCH(MGV, THV)                                                                  \
   nn_mfma_kernel<MGV, THV><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,         \
                                                    tg->mf32, tg->mf_npad, slice, off, s->state,    \
-                                                   s->keys, s->near2, exp_mask, nn_stats, strided, sa, q0)
+                                                   s->keys, s->near2, exp_mask, nn_stats, strided, sa, q0, defer)
     if (MG == 4) {
       if (TH == 2) M3D_NN_LAUNCH(4, 2); else M3D_NN_LAUNCH(4, 1);
     } else if (MG == 2) {
