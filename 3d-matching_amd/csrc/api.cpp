@@ -999,6 +999,9 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
 
 void m3d_icp_destroy(m3d_icp* s) {
   if (!s) return;
+  for (hipGraphExec_t g : s->graph)
+    if (g != nullptr) hipGraphExecDestroy(g);
+  if (s->cap_stream != nullptr) hipStreamDestroy(s->cap_stream);
   hipFree(s->state);
   hipFree(s->keys);
   hipFree(s->near2);
@@ -1068,9 +1071,84 @@ int m3d_icp_step(m3d_icp* s, void* stream) {
   return M3D_OK;
 }
 
+namespace {
+// n steps as ONE graph launch: the sequence (NN scan [+ keyinit] + fused tail per step, 2–3
+// kernels each) is captured on a loop-owned stream the second time the same (n, keys_clean on
+// entry) is requested — a one-shot run never pays the capture — and then replayed on the
+// caller's stream — the per-kernel host enqueues and the stream's per-dispatch
+// gaps become one graph launch.  Every kernel argument is a device pointer into the loop's state,
+// so a replay computes exactly what the enqueued steps would (tests: test_gpu_icp graph cases).
+// Not used while kernel profiling records events, or after a failed capture (plain enqueues).
+bool icp_graphs_on() {
+  static const bool on = [] {
+    const char* e = getenv("M3D_ICP_GRAPH");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+int capture_steps(m3d_icp* s, int32_t n) {
+  if (s->cap_stream == nullptr &&
+      hipStreamCreateWithFlags(&s->cap_stream, hipStreamNonBlocking) != hipSuccess) {
+    s->cap_stream = nullptr;
+    return M3D_ERR_HIP;
+  }
+  const bool kc0 = s->keys_clean;
+  const int slot = kc0 ? 1 : 0;
+  if (hipStreamBeginCapture(s->cap_stream, hipStreamCaptureModeThreadLocal) != hipSuccess)
+    return M3D_ERR_HIP;
+  int rc = M3D_OK;
+  for (int32_t k = 0; k < n && rc == M3D_OK; ++k) rc = m3d_icp_step(s, s->cap_stream);
+  hipGraph_t g = nullptr;
+  const hipError_t ee = hipStreamEndCapture(s->cap_stream, &g);
+  const bool kc1 = s->keys_clean;
+  s->keys_clean = kc0;  // nothing ran yet
+  hipGraphExec_t ex = nullptr;
+  if (rc == M3D_OK && ee == hipSuccess && g != nullptr &&
+      hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess) {
+    if (s->graph[slot] != nullptr) hipGraphExecDestroy(s->graph[slot]);
+    s->graph[slot] = ex;
+    s->graph_n[slot] = n;
+    s->graph_kc_out[slot] = kc1;
+  } else {
+    rc = rc ? rc : M3D_ERR_HIP;
+  }
+  if (g != nullptr) hipGraphDestroy(g);
+  (void)hipGetLastError();
+  return rc;
+}
+}  // namespace
+
+int m3d_icp_prepare_steps(m3d_icp* s, int32_t n) {
+  if (!s) return M3D_ERR_INVALID;
+  CHECK_ARG(s->ctx, n >= 0, "n must be >= 0");
+  if (n < 2 || !icp_graphs_on() || s->graph_off) return M3D_OK;  // plain enqueues then
+  hipSetDevice(s->ctx->device);
+  if (capture_steps(s, n) != M3D_OK) {
+    s->graph_off = true;
+    (void)hipGetLastError();
+  }
+  return M3D_OK;
+}
+
 int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   CHECK_ARG(s->ctx, n >= 0, "n must be >= 0");
+  if (n >= 2 && icp_graphs_on() && !s->graph_off && !s->ctx->profiling) {
+    const int slot = s->keys_clean ? 1 : 0;
+    const bool have = s->graph[slot] != nullptr && s->graph_n[slot] == n;
+    const bool again = s->seen_n[slot] == n;
+    s->seen_n[slot] = n;
+    if (!have && again) {
+      hipSetDevice(s->ctx->device);
+      if (capture_steps(s, n) != M3D_OK) s->graph_off = true;
+    }
+    if ((have || again) && !s->graph_off) {
+      HIPX(s->ctx, hipGraphLaunch(s->graph[slot], S(stream)));
+      s->keys_clean = s->graph_kc_out[slot];
+      return M3D_OK;
+    }
+  }
   for (int32_t k = 0; k < n; ++k) {
     const int rc = m3d_icp_step(s, stream);
     if (rc) return rc;
@@ -1141,6 +1219,7 @@ int m3d_icp_set_source_total(m3d_icp* s, int64_t ns_total) {
   CHECK_ARG(s->ctx, ns_total >= 0 && (ns_total == 0 || ns_total >= s->src->n),
             "source total must be 0 or at least the shard's source count");
   s->ns_total = ns_total;
+  s->graph_n[0] = s->graph_n[1] = -1;  // the captured solve carries the fitness denominator
   return M3D_OK;
 }
 

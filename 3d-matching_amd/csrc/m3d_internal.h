@@ -209,6 +209,14 @@ struct m3d_icp {
   int64_t* xdk = nullptr;   // ns: d64 keys, MIN-reduced
   int32_t* xcl = nullptr;   // ns: claims, MIN-reduced
   double* xsums = nullptr;  // kTermSlots, SUM-reduced
+  // m3d_icp_steps replays: an n-step sequence captured into a HIP graph (api.cpp), one slot per
+  // keys_clean state on entry; a slot captures a sequence requested a second time
+  hipStream_t cap_stream = nullptr;
+  hipGraphExec_t graph[2] = {nullptr, nullptr};
+  int32_t graph_n[2] = {-1, -1};
+  bool graph_kc_out[2] = {false, false};  // keys_clean after the sequence
+  int32_t seen_n[2] = {-1, -1};           // the slot's last request (n)
+  bool graph_off = false;                 // a capture failed: plain enqueues from then on
 };
 
 // error plumbing ------------------------------------------------------------------------

@@ -29,7 +29,7 @@ COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2
 OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -103,6 +103,7 @@ SIGNATURES = {
     "m3d_icp_reset": (C.c_int, [vp, C.POINTER(dbl), vp]),
     "m3d_icp_step": (C.c_int, [vp, vp]),
     "m3d_icp_steps": (C.c_int, [vp, C.c_int32, vp]),
+    "m3d_icp_prepare_steps": (C.c_int, [vp, C.c_int32]),
     "m3d_icp_shard_nn": (C.c_int, [vp, i64, vp, vp]),
     "m3d_icp_shard_nn_range": (C.c_int, [vp, i64, i64, i64, vp, vp]),
     "m3d_icp_shard_claim": (C.c_int, [vp, vp, vp, vp]),

@@ -455,8 +455,13 @@ class IcpLoop:
         self.ctx.check(self.ctx.lib.m3d_icp_step(self.h, stream_handle()), "icp_step")
 
     def steps(self, n: int):
-        """n iterations enqueued by the library in one call (m3d_icp_steps)."""
+        """n iterations enqueued by the library in one call (m3d_icp_steps; a sequence requested
+        again is replayed from a captured HIP graph)."""
         self.ctx.check(self.ctx.lib.m3d_icp_steps(self.h, int(n), stream_handle()), "icp_steps")
+
+    def prepare_steps(self, n: int):
+        """Capture the n-step graph now for the current state (setup; m3d_icp_prepare_steps)."""
+        self.ctx.check(self.ctx.lib.m3d_icp_prepare_steps(self.h, int(n)), "icp_prepare_steps")
 
     def shard_nn(self, offset: int, dkeys):
         """This shard's NN.  dkeys (cuda int64, ns) → target shard: bits of the shard's fp64

@@ -227,6 +227,9 @@ def main():
             drv = D.SourceShardedIcp(loop, loop.src.n, ns_total, dev, comm=comm)
         elif mode == "target" and comm_name != "libm3d-rccl":
             drv = D.ShardedIcp(loop, off, loop.src.n, dev, comm=comm)
+        if mode == "single":  # setup beside the loop object: the steps' HIP graph, captured once
+            loop.reset(np.eye(4))
+            loop.prepare_steps(iters + 1)
 
         def run():
             loop.reset(np.eye(4))

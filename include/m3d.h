@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 8
+#define M3D_ABI_VERSION 9
 
 /* return codes */
 #define M3D_OK 0
@@ -233,8 +233,14 @@ int m3d_icp_reset(m3d_icp* s, const double* init_host, void* stream);
 /* One full iteration on one device: NN evaluation + estimation terms + solve/update. */
 int m3d_icp_step(m3d_icp* s, void* stream);
 /* n iterations (n × m3d_icp_step, enqueued from native code: no per-iteration host binding
- * overhead).  Iterations after convergence / max_iteration are device no-ops. */
+ * overhead).  Iterations after convergence / max_iteration are device no-ops.  A sequence of n
+ * steps requested a second time (from the same keys state) is captured into a HIP graph and
+ * replayed as one launch from then on (M3D_ICP_GRAPH=0: plain enqueues); the results are the
+ * same bits either way. */
 int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream);
+/* Capture the n-step graph now, for the loop's current state (setup work, e.g. before a timed
+ * region; nothing runs).  Later m3d_icp_steps(s, n) calls from that state replay it. */
+int m3d_icp_prepare_steps(m3d_icp* s, int32_t n);
 /* Multi-GPU pieces (icp.py:42-48 with the correspondence search split over ranks).
  * Result contract of every NN (nnkey.h): for each source point the lexicographic (d64, index)
  * minimum over the targets with d64 < r², d64 the fp64 d² of the fp64 transformed point —

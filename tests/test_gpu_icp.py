@@ -183,6 +183,53 @@ def test_step_loop_matches_run():
     assert r2.fitness == full.fitness and r2.iterations == 10
 
 
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_graph_replay_matches_enqueued_steps(nn):
+    """m3d_icp_steps captures an n-step sequence into a HIP graph the second time it is requested
+    (one graph per keys-clean state on entry) and replays it; it must compute what the steps
+    enqueued one by one compute, bit for bit: plain first calls, the capturing call, replays,
+    steps without a reset in between, another n, and with kernel profiling on (plain)."""
+    from m3d.core import context
+
+    src, tgt, nrm, _ = synth.icp_pair(30000, seed=13)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=80, nn=nn)
+    a = IcpLoop(s, t, 0.12, **kw)
+    b = IcpLoop(s, t, 0.12, **kw)
+
+    def state(lp):
+        r = lp.result()
+        return r.transformation, r.fitness, r.inlier_rmse, r.iterations, lp.correspondences().cpu().numpy()
+
+    def same(x, y):
+        np.testing.assert_array_equal(x[0], y[0])
+        assert x[1:4] == y[1:4]
+        np.testing.assert_array_equal(x[4], y[4])
+
+    def both(n):
+        a.steps(n)
+        for _ in range(n):
+            b.step()
+        same(state(a), state(b))
+
+    T0 = synth.random_rigid(5, rot_range=0.02, trans_range=0.03)
+    for rep in range(3):
+        for lp in (a, b):
+            lp.reset(T0 if rep != 1 else np.eye(4))
+        both(6)
+        both(6)  # without a reset: the keys-clean entry state (brute force) or the same one (grid)
+    both(3)
+    both(3)
+    both(3)
+    ctx = context()
+    ctx.profile(True)
+    a.steps(4)
+    ctx.profile(False)
+    for _ in range(4):
+        b.step()
+    same(state(a), state(b))
+
+
 @pytest.mark.parametrize("estimation", [_lib.EST_POINT_TO_PLANE, _lib.EST_POINT_TO_POINT])
 @pytest.mark.parametrize("nn", ["brute", "grid"])
 def test_fused_tail_matches_separate_kernels(nn, estimation):

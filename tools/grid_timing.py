@@ -35,6 +35,8 @@ for name, ns, nt_all, shard in (("cfg1 100k x 100k", 100_000, 100_000, 1), ("1M 
     t_ms, tn = ctx.profile_read(_lib.KERNEL_TERMS)
     ctx.profile(False)
     lp.reset(np.eye(4))
+    lp.steps(it + 1)  # a sequence requested twice is captured into a graph (m3d_icp_steps)
+    lp.reset(np.eye(4))
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
