@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--nt", type=int, default=100_000, help="target points per GPU (cfg1)")
     ap.add_argument("--icp-iters", type=int, default=50)
     ap.add_argument("--cfg3-n", type=int, default=1_000_000)
-    ap.add_argument("--cfg3-iters", type=int, default=10)
+    ap.add_argument("--cfg3-iters", type=int, default=50)  # as cfg1: the unseeded first evaluation amortised alike
     ap.add_argument("--cfg3-steps", type=int, default=2)
     ap.add_argument("--no-cfg3", action="store_true")
     ap.add_argument("--nc", type=int, default=100_000)
