@@ -539,10 +539,28 @@ template <int kSMG>
 __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
     const uint4* __restrict__ ca16, int64_t nc_pad, const uint4* __restrict__ hb16,
     const float* __restrict__ heps, int64_t h_pad, int64_t H, int64_t slice_len, float T2,
-    int32_t* __restrict__ counts, ExactArgs ex, const int32_t* __restrict__ done, float band_on) {
+    int32_t* __restrict__ counts, ExactArgs ex, const int32_t* __restrict__ done, float band_on, int xcd) {
   // band_on: 1; M3D_SCORE_EXP=1 passes −1 to time the screen without the fp64 band path
   // (profiling experiment only: counts are then those of the screen alone)
   if (done != nullptr && *done) return;
+  // xcd: the dispatch order is remapped so that each XCD (linear block id mod 8) walks one
+  // contiguous run of a group-major order — hypothesis blocks in 4 groups, within a group slice
+  // by slice — so an XCD's L2 holds its group's B operands (≈ 2.4 MB) and one correspondence
+  // slice at a time, instead of every XCD streaming every block's operands
+  int64_t bxi = blockIdx.x, byi = blockIdx.y;
+  if (xcd) {
+    const int64_t nbx = gridDim.x, nby = gridDim.y, nb = nbx * nby;
+    const int64_t b = blockIdx.x + blockIdx.y * nbx;
+    const int64_t k = b % 8, pos = b / 8;
+    const int64_t t = k * (nb / 8) + min(k, nb % 8) + pos;  // this XCD's run starts after the others'
+    constexpr int64_t kG = 4;
+    const int64_t gx = (nbx + kG - 1) / kG;
+    const int64_t g = min(t / (gx * nby), (nbx - 1) / gx);  // full groups hold gx × nby blocks
+    const int64_t r = t - g * gx * nby;
+    const int64_t w = min(gx, nbx - g * gx);
+    byi = r / w;
+    bxi = g * gx + r % w;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   s_half8 bx[kSMG], by[kSMG], bz[kSMG];
@@ -551,7 +569,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   int64_t hyp[kSMG];
 #pragma unroll
   for (int g = 0; g < kSMG; ++g) {
-    const int64_t j = (int64_t)blockIdx.x * shyps<kSMG>() + (wave * kSMG + g) * 32 + c;  // < h_pad
+    const int64_t j = bxi * shyps<kSMG>() + (wave * kSMG + g) * 32 + c;  // < h_pad
     hyp[g] = j;
     SH8 t;
     t.u = hb16[(3 * h + 0) * h_pad + j];
@@ -579,7 +597,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   // grid.y block y visits every gridDim.y-th correspondence tile (slice_len = 0) or a contiguous
   // slice of slice_len rows
   const int64_t tstep = slice_len == 0 ? (int64_t)gridDim.y * kSTile : (int64_t)kSTile;
-  const int64_t jb = slice_len == 0 ? (int64_t)blockIdx.y * kSTile : (int64_t)blockIdx.y * slice_len;
+  const int64_t jb = slice_len == 0 ? byi * kSTile : byi * slice_len;
   const int64_t je = slice_len == 0 ? nc_pad : min(nc_pad, jb + slice_len);
   const int p0 = threadIdx.x / kSTile, k0 = threadIdx.x % kSTile;  // planes p0 and p0 + 2
 #pragma unroll
@@ -1183,15 +1201,19 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
       return (e && atoi(e) == 1) ? -1.0f : 1.0f;
     }();
     const dim3 grid((unsigned)bx, (unsigned)sy);
+    static const int xcd = [] {  // M3D_SCORE_XCD=0: the plain (x, y) dispatch order
+      const char* e = getenv("M3D_SCORE_XCD");
+      return (e && atoi(e) == 0) ? 0 : 1;
+    }();
     if (MG == 4)
       score_mfma_kernel<4><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
-                                                     slice, T2, counts, ex, done, band_on);
+                                                     slice, T2, counts, ex, done, band_on, xcd);
     else if (MG == 2)
       score_mfma_kernel<2><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
-                                                     slice, T2, counts, ex, done, band_on);
+                                                     slice, T2, counts, ex, done, band_on, xcd);
     else
       score_mfma_kernel<1><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
-                                                     slice, T2, counts, ex, done, band_on);
+                                                     slice, T2, counts, ex, done, band_on, xcd);
     return hipGetLastError();
   }
   const int64_t per_launch = (int64_t)65535 * kScoreHyps;  // grid.y limit
