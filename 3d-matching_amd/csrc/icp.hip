@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <stdlib.h>
 
+#include "lds_dma.h"
 #include "linalg.h"
 #include "m3d_internal.h"
 #include "nnkey.h"
@@ -340,8 +341,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMGDefault = 2;  // 32-query groups per wave (M3D_NN_MG = 1|2|4 overrides, tuning)
 constexpr int kMTile = 256;   // targets per half tile (8 sub-tiles of 32)
-constexpr int kTHDefault = 1; // half tiles per LDS tile (M3D_NN_TH = 1 | 2; 2 measured 0.312 vs 0.290 ms: spills)
-constexpr int kMTilePad = 512;  // MFMA operand arrays are padded to a multiple of every tile size
+#ifndef M3D_NN_DMA
+#define M3D_NN_DMA 1  // 0: the register-staged tile prefetch
+#endif
+constexpr int kTHDefault = 4;  // half tiles per LDS tile (M3D_NN_TH = 1 | 2 | 4)
+constexpr int kMTilePad = 1024; // MFMA operand arrays are padded to a multiple of every tile size
 constexpr int kMBlock = 512;  // 8 waves × kMG × 32 = 512 queries per block: every target tile
                               // staged in LDS serves 512 queries (L2→LDS traffic per pair halved)
 template <int kMG>
@@ -614,8 +618,8 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
   static_assert(kSub * kMG <= 64, "hit mask holds every (group, sub-tile)");
   __shared__ uint4 t16[2][2][kTT];
   constexpr int kDefer = 16;  // deferred entries per wave (more: resolved in the tile as before)
-  constexpr bool kCanDefer = kSub * kMG <= 32;
-  __shared__ uint64_t dlist[kMBlock / 64][kDefer];
+  __shared__ uint64_t dlist[kMBlock / 64][kDefer];  // flagged (group, sub-tile) bits
+  __shared__ uint32_t dtile[kMBlock / 64][kDefer];  // their tile's first target
   int dn = 0;
   uint64_t dmask = 0;  // (group, sub-tile) bits of the deferring groups
 #pragma unroll
@@ -640,6 +644,17 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
   int buf = 0;
   for (int64_t j0 = jb; j0 < je; j0 += tstep) {
     const bool has_next = j0 + tstep < je;
+#if M3D_NN_DMA
+    // the next tile global → LDS by DMA while this one is swept (lds_dma.h): no prefetch
+    // registers (a wave's 64 elements are one plane's 64 consecutive targets)
+    if (has_next) {
+#pragma unroll
+      for (int u = 0; u < kTH; ++u) {
+        const int e = threadIdx.x + u * kMBlock;
+        lds_dma16(tgt16 + (e / kTT) * nt_pad + j0 + tstep + e % kTT, &t16[buf ^ 1][e / kTT][(e % kTT) & ~63]);
+      }
+    }
+#else
     uint4 pre[kTH];
     if (has_next) {
 #pragma unroll
@@ -648,6 +663,7 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
         pre[u] = tgt16[(e / kTT) * nt_pad + j0 + tstep + e % kTT];
       }
     }
+#endif
     // Sweep: MFMA + sign-OR test for the tile's sub-tiles, branch-free; a sub-tile that hits
     // anywhere in the wave sets a bit of the wave-uniform mask (SALU).  Software-pipelined: the
     // MFMA of step t+1 is issued before step t's tree, so a wave never waits on its own MFMA.
@@ -684,10 +700,13 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
       atomicAdd(&stats[0], (unsigned long long)__builtin_popcountll(hm));
       atomicAdd(&stats[1], (unsigned long long)(kSub * kMG));
     }
-    if (kCanDefer) {
+    {
       const uint64_t hd = hm & dmask & exp_mask;
       if (hd != 0 && dn < kDefer) {
-        if (lane == 0) dlist[wave][dn] = ((uint64_t)(uint32_t)j0 << 32) | (uint32_t)hd;
+        if (lane == 0) {
+          dlist[wave][dn] = hd;
+          dtile[wave][dn] = (uint32_t)j0;
+        }
         ++dn;
         hm &= ~hd;
       }
@@ -710,6 +729,9 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
       thr_operand(bt, X < 0.0f ? -1.0f : ((X - qq[g]) + eps) * S2, fg);
       if (h == 1) bq[g] = bt;  // the threshold only ever tightens: force stays as it was
     }
+#if M3D_NN_DMA
+    lds_dma_wait();
+#else
     if (has_next) {
 #pragma unroll
       for (int u = 0; u < kTH; ++u) {
@@ -717,16 +739,17 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
         t16[buf ^ 1][e / kTT][e % kTT] = pre[u];
       }
     }
+#endif
     __syncthreads();
     buf ^= 1;
   }
   // the deferred exact passes (rows from global memory: the tiles have left LDS)
   for (int e = 0; e < dn; ++e) {
     const uint64_t ent = dlist[wave][e];
-    const int64_t jt = (int64_t)(ent >> 32);
+    const int64_t jt = (int64_t)dtile[wave][e];
 #pragma unroll
     for (int g = 0; g < kMG; ++g) {
-      uint64_t mg = ((ent & 0xFFFFFFFFull) >> (g * kSub)) & kGMask;
+      uint64_t mg = (ent >> (g * kSub)) & kGMask;
       while (mg != 0) {
         const int sub = __builtin_ctzll(mg);
         mg &= mg - 1;
@@ -1418,11 +1441,11 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
       const char* e = getenv("M3D_NN_FILL");
       return !(e && atoi(e) == 0);
     }();
-    // target tile = TH × 256 (one barrier per tile; M3D_NN_TH = 1 | 2)
+    // target tile = TH × 256 (one barrier per tile; M3D_NN_TH = 1 | 2 | 4)
     static const int TH = [] {
       const char* e = getenv("M3D_NN_TH");
       const int v = e ? atoi(e) : kTHDefault;
-      return (v == 1 || v == 2) ? v : kTHDefault;
+      return (v == 1 || v == 2 || v == 4) ? v : kTHDefault;
     }();
     const int64_t tt = (int64_t)TH * kMTile;
     if (tg->mf_npad % tt != 0) return hipErrorInvalidValue;  // pack16 pads to kMTilePad
@@ -1470,9 +1493,9 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
     if (MG == 4) {
       if (TH == 2) M3D_NN_LAUNCH(4, 2); else M3D_NN_LAUNCH(4, 1);
     } else if (MG == 2) {
-      if (TH == 2) M3D_NN_LAUNCH(2, 2); else M3D_NN_LAUNCH(2, 1);
+      if (TH == 4) M3D_NN_LAUNCH(2, 4); else if (TH == 2) M3D_NN_LAUNCH(2, 2); else M3D_NN_LAUNCH(2, 1);
     } else {
-      if (TH == 2) M3D_NN_LAUNCH(1, 2); else M3D_NN_LAUNCH(1, 1);
+      if (TH == 4) M3D_NN_LAUNCH(1, 4); else if (TH == 2) M3D_NN_LAUNCH(1, 2); else M3D_NN_LAUNCH(1, 1);
     }
 #undef M3D_NN_LAUNCH
     if (nn_stats != nullptr) {

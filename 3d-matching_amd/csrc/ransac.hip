@@ -22,6 +22,7 @@
 #include <float.h>
 #include <stdlib.h>
 
+#include "lds_dma.h"
 #include "linalg.h"
 #include "m3d_internal.h"
 
@@ -530,6 +531,9 @@ __device__ __forceinline__ float vmin3a(float a, float b, float c) {
 #ifndef M3D_SCORE_PERM_COUNT
 #define M3D_SCORE_PERM_COUNT 1
 #endif
+#ifndef M3D_SCORE_DMA
+#define M3D_SCORE_DMA 1  // 0: the register-staged tile prefetch (measured 2-3 % slower)
+#endif
 // units of score_mfma_kernel's per-lane outlier counter (the v_perm count adds 8 per outlier)
 constexpr uint32_t kOutlUnit = M3D_SCORE_PERM_COUNT ? 8u : 1u;
 
@@ -609,11 +613,26 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   for (int64_t j0 = jb; j0 < je; j0 += tstep) {
     ++tiles_seen;
     const bool has_next = j0 + tstep < je;
+#if M3D_SCORE_DMA
+    // the next tile goes global → LDS by DMA (global_load_lds_dwordx4: wave-uniform base + lane ×
+    // 16 B; the a16 rows are lane-linear) while this tile is swept, so no prefetch registers.  The
+    // register prefetch (2 × uint4 live across the sweep) was spilled to scratch at the 128-VGPR
+    // cap: a scratch store + reload per tile (78 of the launch's 83 MB of HBM writes at H = 1e5)
+    // and a wait for the load before the sweep began.  The sweep issues no other vector-memory
+    // load (the rare in-place exact fallback's waits stay correct: lds_dma.h); the wait before
+    // the barrier below retires the copy.
+    if (has_next) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        lds_dma16(ca16 + (p0 + 2 * u) * nc_pad + j0 + tstep + k0, &a16[buf ^ 1][p0 + 2 * u][k0 & ~63]);
+    }
+#else
     uint4 pre[2];
     if (has_next) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) pre[u] = ca16[(p0 + 2 * u) * nc_pad + j0 + tstep + k0];
     }
+#endif
 #pragma unroll 2
     for (int sub = 0; sub < kSTile / 32; ++sub) {
       SH8 ax, ay, az;
@@ -683,10 +702,14 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
         }
       }
     }
+#if M3D_SCORE_DMA
+    lds_dma_wait();
+#else
     if (has_next) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) a16[buf ^ 1][p0 + 2 * u][k0] = pre[u];
     }
+#endif
     __syncthreads();
     buf ^= 1;
   }

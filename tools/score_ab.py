@@ -4,6 +4,7 @@ of pairs re-evaluated in fp64.  Run twice (M3D_SCORE_MFMA=1 / 0) and compare the
 import os
 import sys
 import time
+import zlib
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -35,8 +36,8 @@ def main():
     c = counts.cpu().numpy()
     print(f"{os.environ.get('AB_TAG', '')} mfma={os.environ.get('M3D_SCORE_MFMA', '1')} mg={os.environ.get('M3D_SCORE_MG', '2')} nc={nc} H={H} ms={dt * 1e3:.3f} "
           f"sum={int(c.sum())} mean_fit={c.mean() / nc:.4f} rechecked={int(s1 - s0)} "
-          f"hash={hash(c.tobytes()) & 0xffffffff:08x}")
-    np.save(f"gpurun_out/counts_{os.environ.get('M3D_SCORE_MFMA', '1')}.npy", c)
+          f"crc={zlib.crc32(c.tobytes()):08x}")
+    np.save(f"gpurun_out/counts_{os.environ.get('M3D_SCORE_MFMA', '1')}{os.environ.get('AB_TAG', '')}.npy", c)
 
 
 if __name__ == "__main__":
