@@ -1479,6 +1479,11 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
         }
         gm.y = (unsigned)best;
       }
+      static const int64_t gy_env = [] {  // M3D_NN_GY: grid.y override (tuning sweeps)
+        const char* e = getenv("M3D_NN_GY");
+        return e ? (int64_t)atoll(e) : (int64_t)0;
+      }();
+      if (gy_env > 0) gm.y = (unsigned)std::min<int64_t>(gy_env, ntiles);
     }
     const SeedArgs sa{s->corr, s->tgt->xyz32, s->tgt->n, self_seed ? 1 : 0};
     // seeded groups resolve their flagged sub-tiles after the sweep (M3D_NN_DEFER=0: in the tile)
