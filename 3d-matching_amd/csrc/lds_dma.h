@@ -14,13 +14,19 @@ namespace m3d {
 // the one being swept and waits for the DMA before the sweep's first ds_read.  The caller retires
 // the copy with lds_dma_wait() before the barrier that publishes the buffer; ordinary loads the
 // compiler issues meanwhile keep correct waits (an older pending copy only makes them stricter).
+// M0 is a register the compiler reserves (it never honours an M0 clobber), so the asm saves it
+// in an SGPR of its own and restores it after the copy: whatever the compiler keeps in M0 (a
+// v_writelane lane index, say) survives the call.
 __device__ __forceinline__ void lds_dma16(const void* src, void* wave_dst) {
   const uint32_t lds = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)wave_dst);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-               :
-               : "v"(src), "s"(lds)
-               : "memory", "m0");
+  uint32_t saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(src), "s"(lds)
+      : "memory");
 }
 
 // every copy this wave issued has landed in LDS

@@ -153,7 +153,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # M3D_BENCH_DIST=1 (under torch.distributed.run): take the N > 1 code path even at world 1 —
+    # the nccl process group, the libm3d RCCL communicator beside it and the sharded protocols —
+    # a rehearsal of the driver's multi-GPU runs on a one-GPU box (tools/gpu_dist1_rehearsal.sh)
+    multi = world > 1 or os.environ.get("M3D_BENCH_DIST") == "1"
+    if multi:
         # M3D_BENCH_SAME_DEVICE=1 + M3D_BENCH_BACKEND=gloo: every rank on cuda:0 over gloo — a
         # functional rehearsal of the N > 1 path on a one-GPU box (RCCL refuses two ranks on one
         # GPU, so that rehearsal uses --comm torch); the real runs are one rank per GPU
@@ -174,7 +178,7 @@ def main():
 
     ctx = context()
     comm, comm_name = None, "none"
-    if world > 1:
+    if multi:
         if args.comm == "lib":
             try:
                 from m3d.comm import LibComm
@@ -187,7 +191,7 @@ def main():
             comm, comm_name = D.TorchComm(), f"torch.distributed-{dist.get_backend()}"
 
     def barrier():
-        if world > 1:
+        if multi:
             dist.barrier()
             torch.cuda.synchronize()
 
@@ -255,7 +259,7 @@ def main():
         # replicated cloud costs 64 B per point
         budget = float(os.environ.get("M3D_TARGET_SHARD_BYTES", 64 * 2**30))
         shard = "target" if 64.0 * nt * world > budget else "source"
-    mode1 = "single" if world == 1 else shard
+    mode1 = "single" if not multi else shard
     if mode1 == "source":  # weak scaling: ns sources per rank against the whole (replicated) target
         src_all, tgt_all, nrm_all, T_true = synth.icp_pair(ns * world, nt, seed=0)
         src = src_all[rank * ns:(rank + 1) * ns]
@@ -264,7 +268,7 @@ def main():
     else:  # single device, or target-sharded: nt targets per rank, sources replicated
         src, tgt_all, nrm_all, T_true = synth.icp_pair(ns, nt * world, seed=0)
         off = rank * nt
-        tgt_c = (Cloud(tgt_all, nrm_all) if world == 1 else
+        tgt_c = (Cloud(tgt_all, nrm_all) if not multi else
                  Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0)))
     src_c = Cloud(src)
     K_NN, K_TERMS = _lib.KERNEL_NN, _lib.KERNEL_TERMS
@@ -289,7 +293,7 @@ def main():
         "ms_per_step_with_kernel_events": el_ev / args.steps * 1e3,
         "workload": (f"cfg1: {ns}<->{nt} synthetic pair per GPU, {iters} point-to-plane ICP "
                      f"iterations, brute-force NN (r={r:g}), "
-                     + ("1 GPU" if world == 1 else
+                     + ("1 GPU" if not multi else
                         (f"sources sharded over {world} GPUs ({ns} per GPU), target replicated (SUM terms)"
                          if mode1 == "source" else
                          f"target sharded over {world} GPUs ({nt} per GPU), sources replicated "
@@ -326,7 +330,7 @@ def main():
     # (SURVEY §8(e) "ICP alternative"), value = ICP iterations/s of that one problem.  N = 1: the
     # headline run itself (the same workload), so SCALE's N = 1 line equals BENCH.
     cfg1_strong = None
-    if world == 1:
+    if not multi:
         cfg1_strong = {"value": cfg1["value"], "ms_per_step": cfg1["ms_per_step"],
                        "grid_value": None if icp_grid is None else icp_grid["value"],
                        "note": "N = 1: the headline cfg1 run (same workload)"}
@@ -374,8 +378,8 @@ def main():
         s3, t3, nr3, T3 = synth.icp_pair(n3, n3, seed=0)
         o3, c3 = D.shard_bounds(n3, world, rank)
         s3c = Cloud(s3)
-        t3c = Cloud(t3, nr3) if world == 1 else Cloud(t3[o3:o3 + c3], nr3[o3:o3 + c3], center=t3.mean(axis=0))
-        mode3 = "single" if world == 1 else "target"
+        t3c = Cloud(t3, nr3) if not multi else Cloud(t3[o3:o3 + c3], nr3[o3:o3 + c3], center=t3.mean(axis=0))
+        mode3 = "single" if not multi else "target"
         cfg3 = {"metric": "ICP iterations/sec (cfg3: 1M<->1M pair, target sharded over the GPUs, strong scaling)",
                 "unit": "ICP iter/s (whole 1M x 1M problem)", "scaling": "strong",
                 "workload": f"cfg3: {n3}<->{n3} synthetic pair, {it3} point-to-plane iterations per step, "
@@ -425,7 +429,7 @@ def main():
         def ransac_run():
             # enqueued without a host round trip (m3d_ransac_run_async): runs go back to back
             cs.run_async(params, res_buf)
-            if world > 1:  # best over ranks: highest count, lowest global id (device-side key)
+            if multi:  # best over ranks: highest count, lowest global id (device-side key)
                 if comm_name == "libm3d-rccl":
                     cs.best_allreduce(comm, res_buf, rank * H, key)
                 else:
@@ -457,7 +461,7 @@ def main():
         # MAX of the packed key): strong scaling of one cfg2 run; N = 1: the run above
         ransac_strong = {"value": world * H * args.ransac_steps / rel, "ms_per_run": rel / args.ransac_steps * 1e3,
                          "hyps_per_run": H, "note": "N = 1: the cfg2 run above (same workload)"}
-        if world > 1:
+        if multi:
             o2, c2 = D.shard_bounds(H, world, rank)
             p2 = RansacParams(max_iter=c2, seed=42, thr=thr, mode=_lib.SCORE_NORM, early_stop=False, hyp0=o2)
 
@@ -535,7 +539,7 @@ def main():
         "dtype": "fp16-split MFMA NN screen + fp32 scan, exact fp64 NN decision, fp64 terms/solve",
         "data": "synthetic (m3d.synth: asymmetric closed surface, extent ~10, analytic normals)",
         "config": {"workload": head["workload"], "ns": ns, "nt_per_gpu": nt, "icp_iterations_per_step": iters,
-                   "max_corr": r, "parallelism": "single" if world == 1 else f"{mode1}-shard x{world}",
+                   "max_corr": r, "parallelism": "single" if not multi else f"{mode1}-shard x{world}",
                    "comm": comm_name},
         "roofline": head["roofline"],
         "ms_per_step_with_kernel_events": cfg1["ms_per_step_with_kernel_events"],
@@ -554,7 +558,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     del comm
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 
