@@ -388,7 +388,11 @@ constexpr int kSBlock = 512;                  // 8 waves
 template <int kSMG>
 constexpr int shyps() { return (kSBlock / 64) * kSMG * 32; }  // hypotheses per block
 constexpr int kSHypPad = shyps<4>();          // batch padding: a multiple of every variant's
-constexpr int kSTile = 256;                   // correspondences per LDS tile
+#ifndef M3D_SCORE_TILE
+#define M3D_SCORE_TILE 512
+#endif
+constexpr int kSTile = M3D_SCORE_TILE;        // correspondences per LDS tile (256 | 512)
+static_assert(kSTile % 64 == 0 && (4 * kSTile) % 512 == 0, "a wave stages 64 consecutive rows");
 constexpr double kU16 = 4.8828125e-04;        // 2^-11
 constexpr double kSig16 = 2.98023223876953125e-08;  // 2^-25: half the fp16 subnormal spacing
 constexpr float kPadQ = 30000.0f;             // padded rows: q far away (exact in fp16)
@@ -592,8 +596,8 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   float t2r;
   asm volatile("v_mov_b32 %0, %1" : "=v"(t2r) : "s"(T2));
   // [buffer][plane][correspondence]: plane 0 = p part (lane half 0 of every component),
-  // planes 1-3 = the q_x / q_y / q_z parts (lane half 1).  Thread t stages two of the tile's
-  // 4 × 256 16-B operands.
+  // planes 1-3 = the q_x / q_y / q_z parts (lane half 1).  The threads stage the tile's
+  // 4 × kSTile 16-B operands (kStage of them: below).
   __shared__ uint4 a16[2][4][kSTile];
   __shared__ uint32_t qn;                 // guard-band queue: entries used
   __shared__ uint2 qbuf[kSQueue];         // (correspondence, hypothesis | screen sign << 31)
@@ -603,9 +607,14 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   const int64_t tstep = slice_len == 0 ? (int64_t)gridDim.y * kSTile : (int64_t)kSTile;
   const int64_t jb = slice_len == 0 ? byi * kSTile : byi * slice_len;
   const int64_t je = slice_len == 0 ? nc_pad : min(nc_pad, jb + slice_len);
-  const int p0 = threadIdx.x / kSTile, k0 = threadIdx.x % kSTile;  // planes p0 and p0 + 2
+  // thread t stages elements e = t + u·kSBlock of the tile's 4 × kSTile operands: plane e / kSTile,
+  // row e % kSTile (a wave's 64 lanes: 64 consecutive rows of one plane)
+  constexpr int kStage = 4 * kSTile / kSBlock;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) a16[0][p0 + 2 * u][k0] = ca16[(p0 + 2 * u) * nc_pad + jb + k0];
+  for (int u = 0; u < kStage; ++u) {
+    const int e = threadIdx.x + u * kSBlock;
+    a16[0][e / kSTile][e % kSTile] = ca16[(e / kSTile) * nc_pad + jb + e % kSTile];
+  }
   __syncthreads();
   int buf = 0;
   const int pa = h == 0 ? 0 : 1;  // planes read by this lane for x, y, z: pa·(1 + comp)
@@ -623,14 +632,19 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
     // the barrier below retires the copy.
     if (has_next) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-        lds_dma16(ca16 + (p0 + 2 * u) * nc_pad + j0 + tstep + k0, &a16[buf ^ 1][p0 + 2 * u][k0 & ~63]);
+      for (int u = 0; u < kStage; ++u) {
+        const int e = threadIdx.x + u * kSBlock;
+        lds_dma16(ca16 + (e / kSTile) * nc_pad + j0 + tstep + e % kSTile, &a16[buf ^ 1][e / kSTile][(e % kSTile) & ~63]);
+      }
     }
 #else
-    uint4 pre[2];
+    uint4 pre[kStage];
     if (has_next) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) pre[u] = ca16[(p0 + 2 * u) * nc_pad + j0 + tstep + k0];
+      for (int u = 0; u < kStage; ++u) {
+        const int e = threadIdx.x + u * kSBlock;
+        pre[u] = ca16[(e / kSTile) * nc_pad + j0 + tstep + e % kSTile];
+      }
     }
 #endif
 #pragma unroll 2
@@ -707,7 +721,10 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
 #else
     if (has_next) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) a16[buf ^ 1][p0 + 2 * u][k0] = pre[u];
+      for (int u = 0; u < kStage; ++u) {
+        const int e = threadIdx.x + u * kSBlock;
+        a16[buf ^ 1][e / kSTile][e % kSTile] = pre[u];
+      }
     }
 #endif
     __syncthreads();
