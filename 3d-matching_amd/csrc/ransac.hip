@@ -231,9 +231,16 @@ __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__
       }
     st = kabsch3(ps, qs, T) ? M3D_HYP_NONFINITE : M3D_HYP_OK;
   }
-  for (int k = 0; k < 16; ++k) T_out[16 * h + k] = T[k];
+  if ((reinterpret_cast<uintptr_t>(T_out) & 15u) == 0) {  // 8 × 16-B stores (library buffers)
+    double2* To = reinterpret_cast<double2*>(T_out + 16 * h);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) To[k] = make_double2(T[2 * k], T[2 * k + 1]);
+  } else {  // a caller's buffer at an 8-B offset (m3d_kabsch3)
+    for (int k = 0; k < 16; ++k) T_out[16 * h + k] = T[k];
+  }
   if (status != nullptr) status[h] = (uint8_t)st;
-  hypf[h] = make_hypf(T, g);
+  // the fp32 VALU screen's block: not written when the MFMA screen scores this batch (hf.on)
+  if (hypf != nullptr) hypf[h] = make_hypf(T, g);
   if (hf.on) hyp16_one(T, true, h, hf.h_pad, hf.m, hf.hb16, hf.heps);
 }
 
@@ -1015,7 +1022,7 @@ hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_
   const int64_t n = hf.on ? hf.h_pad : H;
   kabsch3_kernel<<<blocks_for(n, 256), 256, 0, st>>>(cs->p64, cs->q64, cs->nc, triples, seed,
                                                      hyp0, H, guard_of(cs, thr_sq), T_out, status,
-                                                     hypf, done, z, hf);
+                                                     hf.on ? nullptr : hypf, done, z, hf);
   return hipGetLastError();
 }
 
