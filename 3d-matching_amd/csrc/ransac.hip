@@ -654,7 +654,10 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
       }
     }
 #endif
-#pragma unroll 2
+#ifndef M3D_SCORE_UNROLL
+#define M3D_SCORE_UNROLL 2
+#endif
+#pragma unroll M3D_SCORE_UNROLL
     for (int sub = 0; sub < kSTile / 32; ++sub) {
       SH8 ax, ay, az;
       ax.u = a16[buf][pa * 1][sub * 32 + c];
@@ -1241,6 +1244,11 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
         }
       }
     }
+    static const int64_t gy_env = [] {  // M3D_SCORE_GY: grid.y override (tuning sweeps)
+      const char* e = getenv("M3D_SCORE_GY");
+      return e ? (int64_t)atoll(e) : (int64_t)0;
+    }();
+    if (gy_env > 0) sy = std::min<int64_t>(gy_env, tiles);
     const int64_t slice = 0;  // strided tiles
     const float T2 = (float)(cs->s16 * cs->s16 * thr_sq);
     static const float band_on = [] {
