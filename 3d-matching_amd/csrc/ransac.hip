@@ -542,6 +542,9 @@ __device__ __forceinline__ float vmin3a(float a, float b, float c) {
 #ifndef M3D_SCORE_PERM_COUNT
 #define M3D_SCORE_PERM_COUNT 1
 #endif
+#ifndef M3D_SCORE_PERM_OR
+#define M3D_SCORE_PERM_OR 1
+#endif
 #ifndef M3D_SCORE_DMA
 #define M3D_SCORE_DMA 1  // 0: the register-staged tile prefetch (measured 2-3 % slower)
 #endif
@@ -677,10 +680,20 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
         // v_perm selectors 9 / 11 give a byte of 0xFF when S1 / S0 is negative: two sign masks
         // per word, counted by v_bcnt (accumulating) — 8 per outlier, so outl holds 8× the count
         // (2 VALU per 2 values instead of 2 shifts + an add3)
+#if M3D_SCORE_PERM_OR
+        // four sign bytes per v_bcnt: two v_perm fill bytes 0–1 and 2–3, one full-rate OR joins
+        // them (per 4 values 2 perm + 1 or + 1 bcnt instead of 2 perm + 2 bcnt)
+#pragma unroll
+        for (int r = 0; r < 16; r += 4)
+          s += __builtin_popcount(
+              __builtin_amdgcn_perm(__float_as_uint(v[r]), __float_as_uint(v[r + 1]), 0x0C0C0B09u) |
+              __builtin_amdgcn_perm(__float_as_uint(v[r + 2]), __float_as_uint(v[r + 3]), 0x0B090C0Cu));
+#else
 #pragma unroll
         for (int r = 0; r < 16; r += 2)
           s += __builtin_popcount(__builtin_amdgcn_perm(__float_as_uint(v[r]),
                                                         __float_as_uint(v[r + 1]), 0x0C0C0B09u));
+#endif
 #else
 #pragma unroll
         for (int r = 0; r < 16; r += 2)
