@@ -418,48 +418,12 @@ __global__ __launch_bounds__(kGridBlock) void morton_gather_kernel(const float4*
 }
 
 // ------------------------------------------------------------------------------- host side
-// Build temporaries (bounds partials, sort keys/values, hipcub storage) are stream-ordered
-// (hipMallocAsync / hipFreeAsync on the build's stream, from the device's default pool kept
-// cached): a plain hipFree waits for the whole device, and a cold grid build (m3d_icp_create's
-// two grids + the Morton sort) freed ~14 temporaries.  Opt-in while unmeasured
-// (M3D_GRID_ASYNC_TMP=1, tools/ab_grid_tmp.sh); the default keeps hipMalloc / hipFree.
-static bool tmp_async() {
-  static const bool on = [] {
-    const char* e = getenv("M3D_GRID_ASYNC_TMP");
-    if (e == nullptr || atoi(e) != 1) return false;
-    int dev = 0;
-    hipMemPool_t pool = nullptr;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    uint64_t keep = UINT64_MAX;  // keep freed blocks in the pool across synchronisations
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    (void)hipGetLastError();
-    return true;
-  }();
-  return on;
-}
-
-template <typename T>
-static hipError_t tmp_alloc(T** p, size_t bytes, hipStream_t st) {
-  return tmp_async() ? hipMallocAsync(reinterpret_cast<void**>(p), bytes, st)
-                     : hipMalloc(reinterpret_cast<void**>(p), bytes);
-}
-
-static void tmp_free(void* p, hipStream_t st) {
-  if (p == nullptr) return;
-  if (tmp_async())
-    (void)hipFreeAsync(p, st);
-  else
-    (void)hipFree(p);
-}
-
-static hipError_t grid_fail(hipError_t e, hipStream_t st, void* a, void* b, void* c, void* tmp) {
-  tmp_free(a, st);
-  tmp_free(b, st);
-  tmp_free(c, st);
-  tmp_free(tmp, st);
+static hipError_t grid_fail(hipError_t e, void* a, void* b, void* c, void* d, void* tmp) {
+  hipFree(a);
+  hipFree(b);
+  hipFree(c);
+  hipFree(d);
+  hipFree(tmp);
   return e;
 }
 
@@ -472,13 +436,13 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   // per-axis bounds
   const int nb = (int)std::min<int64_t>(1024, (n + kGridBlock - 1) / kGridBlock);
   float* part = nullptr;
-  hipError_t e = tmp_alloc(&part, sizeof(float) * 6 * nb, st);
+  hipError_t e = hipMalloc(&part, sizeof(float) * 6 * nb);
   if (e != hipSuccess) return e;
   minmax3_kernel<<<nb, kGridBlock, 0, st>>>(xyz32, n, part);
   std::vector<float> hp(6 * (size_t)nb);
   e = hipMemcpyAsync(hp.data(), part, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st);
-  tmp_free(part, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipFree(part);
   if (e != hipSuccess) return e;
   float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
   for (int b = 0; b < nb; ++b)
@@ -514,24 +478,19 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   size_t tmp_bytes = 0;
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) < total) ++bits;
-  // vout becomes the grid's cell order (persistent); the rest are build temporaries
-  auto fail = [&](hipError_t err) {
-    hipFree(vout);
-    return grid_fail(err, st, kin, kout, vin, tmp);
-  };
-  if ((e = tmp_alloc(&kin, sizeof(uint32_t) * n, st)) != hipSuccess ||
-      (e = tmp_alloc(&kout, sizeof(uint32_t) * n, st)) != hipSuccess ||
-      (e = tmp_alloc(&vin, sizeof(int32_t) * n, st)) != hipSuccess ||
+  if ((e = hipMalloc(&kin, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&kout, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&vin, sizeof(int32_t) * n)) != hipSuccess ||
       (e = hipMalloc(&vout, sizeof(int32_t) * n)) != hipSuccess)
-    return fail(e);
+    return grid_fail(e, kin, kout, vin, vout, tmp);
   const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
   cell_id_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, n, d, kin, vin);
-  if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+  if ((e = hipGetLastError()) != hipSuccess) return grid_fail(e, kin, kout, vin, vout, tmp);
   e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, bits, st);
-  if (e == hipSuccess) e = tmp_alloc(&tmp, std::max<size_t>(tmp_bytes, 1), st);
+  if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 1));
   if (e == hipSuccess)
     e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, bits, st);
-  if (e != hipSuccess) return fail(e);
+  if (e != hipSuccess) return grid_fail(e, kin, kout, vin, vout, tmp);
   hipFree(g->start);
   hipFree(g->pts);
   hipFree(g->order);
@@ -540,7 +499,7 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   g->order = nullptr;
   if ((e = hipMalloc(&g->start, sizeof(int32_t) * (total + 1))) != hipSuccess ||
       (e = hipMalloc(&g->pts, sizeof(float4) * n)) != hipSuccess)
-    return fail(e);
+    return grid_fail(e, kin, kout, vin, vout, tmp);
   cell_start_kernel<<<(unsigned)((total + 1 + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
       kout, n, total, g->start);
   grid_gather_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, vout, n, g->pts);
@@ -556,16 +515,13 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
     if (e == hipSuccess)
       e = hipMemcpyAsync(&occ, tmp, sizeof(occ), hipMemcpyDeviceToHost, st);
   }
-  tmp_free(kin, st);
-  tmp_free(kout, st);
-  tmp_free(vin, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);  // occ read back
-  tmp_free(tmp, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
   g->n_occ = (int64_t)occ;
   g->order = vout;  // sorted point indices: the cloud's cell order
+  vout = nullptr;
   d.start = g->start;
   d.pts = g->pts;
-  return e;
+  return grid_fail(e, kin, kout, vin, vout, tmp);
 }
 
 void grid_free(Grid* g) {
@@ -600,17 +556,15 @@ hipError_t grid_morton(Grid* g, hipStream_t st) {
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   hipError_t e;
-  if ((e = tmp_alloc(&kin, sizeof(uint32_t) * n, st)) != hipSuccess ||
-      (e = tmp_alloc(&kout, sizeof(uint32_t) * n, st)) != hipSuccess ||
-      (e = tmp_alloc(&vin, sizeof(int32_t) * n, st)) != hipSuccess ||
-      (e = tmp_alloc(&vout, sizeof(int32_t) * n, st)) != hipSuccess) {
-    tmp_free(vout, st);
-    return grid_fail(e, st, kin, kout, vin, tmp);
-  }
+  if ((e = hipMalloc(&kin, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&kout, sizeof(uint32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&vin, sizeof(int32_t) * n)) != hipSuccess ||
+      (e = hipMalloc(&vout, sizeof(int32_t) * n)) != hipSuccess)
+    return grid_fail(e, kin, kout, vin, vout, tmp);
   const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
   morton_key_kernel<<<blocks, kGridBlock, 0, st>>>(g->pts, n, g->dev, sh[0], sh[1], sh[2], kin, vin);
   e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
-  if (e == hipSuccess) e = tmp_alloc(&tmp, std::max<size_t>(tmp_bytes, 1), st);
+  if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 1));
   if (e == hipSuccess)
     e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
   if (e == hipSuccess) e = hipMalloc(&g->mpts, sizeof(float4) * n);
@@ -619,8 +573,6 @@ hipError_t grid_morton(Grid* g, hipStream_t st) {
     morton_gather_kernel<<<blocks, kGridBlock, 0, st>>>(g->pts, vout, n, g->mpts, g->minv);
     e = hipGetLastError();
   }
-  tmp_free(vout, st);
-  e = grid_fail(e, st, kin, kout, vin, tmp);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) {
     hipFree(g->mpts);
@@ -628,7 +580,7 @@ hipError_t grid_morton(Grid* g, hipStream_t st) {
     g->mpts = nullptr;
     g->minv = nullptr;
   }
-  return e;
+  return grid_fail(e, kin, kout, vin, vout, tmp);
 }
 
 // ------------------------------------------------------------------------------- Morton copy
