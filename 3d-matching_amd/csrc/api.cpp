@@ -858,6 +858,17 @@ int ensure_morton_source(m3d_ctx* ctx, const m3d_cloud* c, const Grid* sg, doubl
     return m3d_fail(ctx, M3D_ERR_HIP, std::string("morton source: ") + hipGetErrorString(e));
   }
   c->morton.emplace_back(cell, mc);
+  // bounded cache: callers that query with many different radii (m3d_nn1, the a6 validation) would
+  // otherwise keep one full source copy per cell size for the cloud's lifetime
+  constexpr size_t kMortonKeep = 4;
+  for (size_t k = 0; c->morton.size() > kMortonKeep && k + 1 < c->morton.size();) {
+    if (c->morton[k].second->refs == 0) {
+      m3d_cloud_destroy(c->morton[k].second);
+      c->morton.erase(c->morton.begin() + (ptrdiff_t)k);
+    } else {
+      ++k;
+    }
+  }
   *out = mc;
   *gout = g;
   return M3D_OK;
@@ -956,6 +967,7 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   m3d_icp* s = new m3d_icp();
   s->ctx = ctx;
   s->src = src_m;
+  src_m->refs += 1;  // the Morton copy stays cached while this loop runs on it
   s->user_src = src;
   s->tgt = tgt;
   s->params = *params;
@@ -1002,6 +1014,7 @@ void m3d_icp_destroy(m3d_icp* s) {
   for (hipGraphExec_t g : s->graph)
     if (g != nullptr) hipGraphExecDestroy(g);
   if (s->cap_stream != nullptr) hipStreamDestroy(s->cap_stream);
+  if (s->src != nullptr) s->src->refs -= 1;
   hipFree(s->state);
   hipFree(s->keys);
   hipFree(s->near2);
@@ -1278,7 +1291,7 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
 int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const double* T_host,
             double max_dist, int32_t nn_method, int32_t* idx, double* d2, void* stream) {
   if (!ctx) return M3D_ERR_INVALID;
-  CHECK_ARG(ctx, src && tgt && idx, "invalid arguments");
+  CHECK_ARG(ctx, src && tgt && (idx || src->n == 0), "invalid arguments");
   CHECK_ARG(ctx, max_dist > 0.0, "max_dist must be > 0");
   m3d_icp_params p{1e-6, 1e-6, 0, M3D_EST_POINT_TO_POINT, nn_method, 0};
   m3d_icp* s = nullptr;
@@ -1508,7 +1521,7 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
   const int64_t cap = std::min<int64_t>(
       npass, std::max<int64_t>(64, std::min<int64_t>(8192, ((int64_t)1 << 23) / std::max<int64_t>(ns, 1))));
   const int64_t nbq = validate_blocks(ns);
-  DevTmp<int32_t> dlist;
+  DevTmp<int32_t> dlist, vcorr;
   DevTmp<IcpState> vst;
   DevTmp<double> vpart, vres;
   if (npass > 0) {
@@ -1516,6 +1529,7 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
     if (!rc) rc = dev_alloc(ctx, &vst.p, cap);
     if (!rc) rc = dev_alloc(ctx, &vpart.p, cap * nbq * 2);
     if (!rc) rc = dev_alloc(ctx, &vres.p, cap * 2);
+    if (!rc) rc = dev_alloc(ctx, &vcorr.p, cap);
     if (rc) {
       m3d_icp_destroy(s);
       return rc;
@@ -1525,8 +1539,9 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
   if (npass > 0)
     e = hipMemcpyAsync(dlist.p, list.data(), 4 * npass, hipMemcpyHostToDevice, st);
   int64_t est_k = H, best = -1;
-  double best_fit = 0.0, best_rmse = 0.0;
+  double best_fit = 0.0, best_rmse = 0.0, corres_ratio = 0.0;
   std::vector<double> hs;
+  std::vector<int32_t> hc;
   for (int64_t c0 = 0, bsz = std::min<int64_t>(64, cap); c0 < npass && e == hipSuccess;
        c0 += bsz, bsz = std::min<int64_t>(cap, 2 * bsz)) {
     if (list[c0] >= est_k) break;
@@ -1535,9 +1550,17 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
     if (e == hipSuccess)
       e = launch_validate(s->sgrid, ns, s->src->xyz64, s->tgrid, tgt->xyz64, tgt->n, vst.p, n, vpart.p,
                           vres.p, st);
+    // the exit rule's correspondence inlier counts of the same batch (one small launch; only a
+    // new best's is read)
+    if (e == hipSuccess)
+      e = launch_corres_inlier(src->xyz64, tgt->xyz64, corr, nc, T.p, dlist.p + c0, n,
+                               p->max_correspondence_distance, vcorr.p, st);
     hs.resize(2 * (size_t)n);
+    hc.resize((size_t)n);
     if (e == hipSuccess)
       e = hipMemcpyAsync(hs.data(), vres.p, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(hc.data(), vcorr.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) break;
     for (int64_t k = 0; k < n; ++k) {
@@ -1551,10 +1574,17 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
         best = h;
         best_fit = fit;
         best_rmse = rmse;
-        const double kk = fit < 1.0 ? std::ceil(std::log(1.0 - p->confidence) /
-                                                std::log(1.0 - std::pow(fit, (double)p->ransac_n)))
-                                    : 0.0;
-        if (kk < (double)est_k) est_k = (int64_t)kk;
+        // Open3D 0.19 (Registration.cpp RegistrationRANSACBasedOnCorrespondence): the exit
+        // estimate comes from the new best's CORRESPONDENCE inlier ratio
+        // (EvaluateInlierCorrespondenceRatio), not from its fitness:
+        //   est_k_d = log(1 − confidence) / log(1 − ratio^ransac_n); est_k ← ceil(est_k_d) if smaller.
+        // ratio = 1: log(0) = −inf, est_k_d = −0.0 → 0.  ratio = 0: a division by +0.0 → −inf,
+        // whose int conversion upstream is INT_MIN on x86 → stop (0 here).  NaN: no change.
+        const double ratio = (double)hc[k] / (double)nc;
+        corres_ratio = ratio;
+        const double kd = std::log(1.0 - p->confidence) /
+                          std::log(1.0 - std::pow(ratio, (double)p->ransac_n));
+        if (kd < (double)est_k) est_k = std::isfinite(kd) ? (int64_t)std::ceil(kd) : 0;
       }
     }
   }
@@ -1567,6 +1597,7 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
     out->fitness = best_fit;
     out->inlier_rmse = best_rmse;
     out->best_index = best;
+    out->corres_ratio = corres_ratio;
     if (e == hipSuccess && corr_set_out) {
       e = launch_icp_set_T(s, T.p + 16 * best, st);
       if (e == hipSuccess) e = enqueue_nn(s, 0, st);

@@ -191,12 +191,12 @@ int m3d_icp_shard_steps(m3d_icp* s, m3d_comm* c, int64_t off, int32_t n, void* s
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t ns = s->src->n;
   int rc;
-  if (!s->xready) {  // scratch before the first collective, then every rank agrees
+  if (!s->xready_tgt) {  // scratch before the first collective, then every rank agrees
     rc = alloc_once(ctx, &s->xdk, ns);
     if (!rc) rc = alloc_once(ctx, &s->xcl, ns);
     if (!rc) rc = alloc_once(ctx, &s->xsums, kTermSlots);
     if ((rc = agree(c, rc, st))) return rc;
-    s->xready = true;
+    s->xready_tgt = true;
   }
   const bool split = split_exchange(s);
   // the halves meet on a 4096-slot boundary (whole MFMA query blocks / grid blocks)
@@ -239,10 +239,10 @@ int m3d_icp_source_shard_steps(m3d_icp* s, m3d_comm* c, int32_t n, void* stream)
   if (n < 0) return m3d_fail(ctx, M3D_ERR_INVALID, "n must be >= 0");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc;
-  if (!s->xready) {
+  if (!s->xready_src) {
     rc = alloc_once(ctx, &s->xsums, kTermSlots);
     if ((rc = agree(c, rc, st))) return rc;
-    s->xready = true;
+    s->xready_src = true;
   }
   for (int32_t k = 0; k < n; ++k) {
     if (c->inject == 2) {

@@ -27,6 +27,7 @@
 
 #include "linalg.h"
 #include "m3d_internal.h"
+#include "nnkey.h"
 
 namespace m3d {
 
@@ -258,6 +259,43 @@ __global__ void feat_hyp_kernel(const double* __restrict__ src, const double* __
     }
   }
   pass[h] = ok ? 1 : 0;
+}
+
+// Open3D 0.19 EvaluateInlierCorrespondenceRatio (Registration.cpp): for hypothesis k of a
+// validation batch (T = T_all + 16·list[k]) the number of INPUT correspondences c with
+// |T·p_c − q_c|² < r2 — the source transformed as PointCloud::Transform does and squaredNorm in
+// Eigen's order (nnkey.h q64_of / d2_64, fp64, no contraction), strict <.  Integer counts summed
+// with atomics: exact and order-free.  grid.y = hypothesis of the batch, grid.x strides over nc.
+__global__ __launch_bounds__(256) void corres_inlier_kernel(
+    const double* __restrict__ src, const double* __restrict__ tgt, const int32_t* __restrict__ corr,
+    int64_t nc, const double* __restrict__ T_all, const int32_t* __restrict__ list, double r2,
+    int32_t* __restrict__ count) {
+  const int h = blockIdx.y;
+  double T[12];
+  const double* Tg = T_all + 16 * (int64_t)list[h];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) T[k] = Tg[k];
+  int n = 0;
+  for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < nc; c += (int64_t)gridDim.x * 256) {
+    const int64_t a = corr[2 * c], b = corr[2 * c + 1];
+    double Q[3];
+    q64_of(T, src + 3 * a, Q);
+    n += d2_64(Q, tgt + 3 * b) < r2 ? 1 : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0 && n != 0) atomicAdd(count + h, n);
+}
+
+hipError_t launch_corres_inlier(const double* src, const double* tgt, const int32_t* corr, int64_t nc,
+                                const double* T_all, const int32_t* list, int64_t n, double max_corr,
+                                int32_t* count, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(int32_t) * (size_t)n, st);
+  if (e != hipSuccess || nc <= 0) return e;
+  const unsigned bx = (unsigned)std::min<int64_t>((nc + 255) / 256, 64);
+  corres_inlier_kernel<<<dim3(bx, (unsigned)n), 256, 0, st>>>(src, tgt, corr, nc, T_all, list,
+                                                              max_corr * max_corr, count);
+  return hipGetLastError();
 }
 
 hipError_t launch_feat_hyp(const double* src, const double* tgt, const int32_t* corr, int64_t nc,

@@ -623,7 +623,8 @@ __global__ __launch_bounds__(kGridBlock) void morton_copy_cells_kernel(
 hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Grid* gout,
                        hipStream_t st) {
   const int64_t n = src->n;
-  if (sg->mpts == nullptr || sg->minv == nullptr || sg->n_pts != n) return hipErrorInvalidValue;
+  // an empty cloud has no Morton arrays (grid_morton returns early): the copy is empty too
+  if (sg->n_pts != n || (n > 0 && (sg->mpts == nullptr || sg->minv == nullptr))) return hipErrorInvalidValue;
   out->n = n;
   out->n_pad = src->n_pad;
   for (int k = 0; k < 3; ++k) out->center[k] = src->center[k];

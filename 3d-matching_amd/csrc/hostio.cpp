@@ -4,6 +4,7 @@
 // both compiled code; numpy's text paths (loadtxt / savetxt) cost ~1–3 µs per number.  Parsing
 // uses std::from_chars (correctly rounded, the same doubles numpy's parser returns), formatting
 // std::to_chars (the shortest representation that reads back to the same double).
+#include <immintrin.h>
 #include <charconv>
 #include <cstdint>
 #include <cstdlib>
@@ -369,12 +370,17 @@ int m3d_merge_vertices(const double* xyz, int64_t n, double* uniq, int32_t* inve
 }
 
 // Content keys of the drop-in's cache (m3d.cache "content" policy): the reference's per-call API
-// (ransac.py:195-236 per hypothesis) hands the same arrays over again and again, and an EXACT
-// cache must notice any in-place edit, so every call keys each array by its full content.  At
-// Nc = 1e5 that is ~5.6 MB per call; one thread of xxh3 took ~0.11 ms of a 0.15 ms call.  Here
-// the arrays are cut into fixed 64 KB chunks hashed with XXH64 (Y. Collet's published algorithm)
-// by a persistent pool, then each array's chunk hashes are hashed twice (two seeds) into its
-// 128-bit key: the result does not depend on the thread count.
+// (ransac.py:195-236 per hypothesis) hands the same arrays over again and again, and the cache
+// must notice any in-place edit, so every call keys each array by its full content.  At Nc = 1e5
+// that is ~5.6 MB per call; one thread of xxh3 took ~0.11 ms of a 0.15 ms call.  Here the arrays
+// are cut into 64 KB chunks hashed by a persistent pool with XXH3-128 (Y. Collet's published
+// algorithm, long-input path with the default secret; known-answer tested against the python
+// xxhash package), then each array's chunk digests, its byte length and chunk count are hashed
+// again with XXH3-128 into its 128-bit key; the result does not depend on the thread count.
+// What "128-bit" buys: XXH3-128 is a NON-cryptographic 128-bit hash, so two different arrays of
+// one length share a key with probability ≈ 2⁻¹²⁸ per pair of unrelated contents (round 3 chained
+// 64-bit chunk digests, which bounded the key at 2⁻⁶⁴); it is no defence against a caller who
+// crafts collisions on purpose.  Round 3 used XXH64 per chunk (kept below for its known answers).
 namespace {
 constexpr uint64_t kP1 = 11400714785074694791ull, kP2 = 14029467366897019727ull,
                    kP3 = 1609587929392839161ull, kP4 = 9650029242287828579ull,
@@ -423,14 +429,150 @@ uint64_t xxh64(const uint8_t* p, size_t len, uint64_t seed) {
   return h;
 }
 
+// ---- XXH3-128, inputs of at least 240 bytes (XXH3_hashLong_128b with the default secret, seed 0)
+constexpr uint64_t kQ1 = 0x9E3779B185EBCA87ull, kQ2 = 0xC2B2AE3D27D4EB4Full, kQ3 = 0x165667B19E3779F9ull,
+                   kQ4 = 0x85EBCA77C2B2AE63ull, kQ5 = 0x27D4EB2F165667C5ull;
+constexpr uint32_t kR1 = 0x9E3779B1u, kR2 = 0x85EBCA77u, kR3 = 0xC2B2AE3Du;
+alignas(64) constexpr uint8_t kSecret[192] = {
+    0xb8, 0xfe, 0x6c, 0x39, 0x23, 0xa4, 0x4b, 0xbe, 0x7c, 0x01, 0x81, 0x2c, 0xf7, 0x21, 0xad, 0x1c,
+    0xde, 0xd4, 0x6d, 0xe9, 0x83, 0x90, 0x97, 0xdb, 0x72, 0x40, 0xa4, 0xa4, 0xb7, 0xb3, 0x67, 0x1f,
+    0xcb, 0x79, 0xe6, 0x4e, 0xcc, 0xc0, 0xe5, 0x78, 0x82, 0x5a, 0xd0, 0x7d, 0xcc, 0xff, 0x72, 0x21,
+    0xb8, 0x08, 0x46, 0x74, 0xf7, 0x43, 0x24, 0x8e, 0xe0, 0x35, 0x90, 0xe6, 0x81, 0x3a, 0x26, 0x4c,
+    0x3c, 0x28, 0x52, 0xbb, 0x91, 0xc3, 0x00, 0xcb, 0x88, 0xd0, 0x65, 0x8b, 0x1b, 0x53, 0x2e, 0xa3,
+    0x71, 0x64, 0x48, 0x97, 0xa2, 0x0d, 0xf9, 0x4e, 0x38, 0x19, 0xef, 0x46, 0xa9, 0xde, 0xac, 0xd8,
+    0xa8, 0xfa, 0x76, 0x3f, 0xe3, 0x9c, 0x34, 0x3f, 0xf9, 0xdc, 0xbb, 0xc7, 0xc7, 0x0b, 0x4f, 0x1d,
+    0x8a, 0x51, 0xe0, 0x4b, 0xcd, 0xb4, 0x59, 0x31, 0xc8, 0x9f, 0x7e, 0xc9, 0xd9, 0x78, 0x73, 0x64,
+    0xea, 0xc5, 0xac, 0x83, 0x34, 0xd3, 0xeb, 0xc3, 0xc5, 0x81, 0xa0, 0xff, 0xfa, 0x13, 0x63, 0xeb,
+    0x17, 0x0d, 0xdd, 0x51, 0xb7, 0xf0, 0xda, 0x49, 0xd3, 0x16, 0x55, 0x26, 0x29, 0xd4, 0x68, 0x9e,
+    0x2b, 0x16, 0xbe, 0x58, 0x7d, 0x47, 0xa1, 0xfc, 0x8f, 0xf8, 0xb8, 0xd1, 0x7a, 0xd0, 0x31, 0xce,
+    0x45, 0xcb, 0x3a, 0x8f, 0x95, 0x16, 0x04, 0x28, 0xaf, 0xd7, 0xfb, 0xca, 0xbb, 0x4b, 0x40, 0x7e,
+};
+constexpr size_t kStripe = 64, kSecretSize = sizeof(kSecret), kStripesPerBlock = (kSecretSize - kStripe) / 8,
+                 kBlock = kStripe * kStripesPerBlock;
+constexpr size_t kXxh3Min = 241;  // the long path: inputs above 240 bytes
+
+inline void xxh3_acc512(uint64_t* __restrict acc, const uint8_t* __restrict in, const uint8_t* __restrict key) {
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t v = rd64(in + 8 * i), k = v ^ rd64(key + 8 * i);
+    acc[i ^ 1] += v;
+    acc[i] += (k & 0xFFFFFFFFull) * (k >> 32);
+  }
+}
+inline void xxh3_scramble(uint64_t* acc, const uint8_t* key) {
+  for (int i = 0; i < 8; ++i) {
+    uint64_t a = acc[i];
+    a ^= a >> 47;
+    a ^= rd64(key + 8 * i);
+    acc[i] = a * kR1;
+  }
+}
+inline uint64_t mul128_fold64(uint64_t a, uint64_t b) {
+  const unsigned __int128 m = (unsigned __int128)a * b;
+  return (uint64_t)m ^ (uint64_t)(m >> 64);
+}
+inline uint64_t xxh3_avalanche(uint64_t h) {
+  h ^= h >> 37;
+  h *= 0x165667919E3779F9ull;
+  return h ^ (h >> 32);
+}
+inline uint64_t xxh3_merge(const uint64_t* acc, const uint8_t* key, uint64_t start) {
+  uint64_t r = start;
+  for (int i = 0; i < 4; ++i) r += mul128_fold64(acc[2 * i] ^ rd64(key + 16 * i), acc[2 * i + 1] ^ rd64(key + 16 * i + 8));
+  return xxh3_avalanche(r);
+}
+
+// The stripe loop of whole blocks, vectorised as xxhash's own SSE2 / AVX2 kernels do (the same
+// arithmetic per 64-bit lane: acc[i ^ 1] += v, acc[i] += lo32(v ^ k) · hi32(v ^ k)); the scalar
+// xxh3_acc512 handles the partial block and the last stripe.  AVX2 is chosen at run time.
+__attribute__((target("avx2"))) void xxh3_blocks_avx2(uint64_t* acc, const uint8_t* p, size_t nb) {
+  __m256i a[2] = {_mm256_load_si256(reinterpret_cast<const __m256i*>(acc)),
+                  _mm256_load_si256(reinterpret_cast<const __m256i*>(acc + 4))};
+  const __m256i prime = _mm256_set1_epi32((int)kR1);
+  for (size_t b = 0; b < nb; ++b) {
+    const uint8_t* blk = p + b * kBlock;
+    for (size_t s = 0; s < kStripesPerBlock; ++s) {
+      for (int i = 0; i < 2; ++i) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(blk + s * kStripe + 32 * i));
+        const __m256i k = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(kSecret + 8 * s + 32 * i));
+        const __m256i dk = _mm256_xor_si256(v, k);
+        const __m256i prod = _mm256_mul_epu32(dk, _mm256_shuffle_epi32(dk, _MM_SHUFFLE(0, 3, 0, 1)));
+        a[i] = _mm256_add_epi64(a[i], _mm256_add_epi64(prod, _mm256_shuffle_epi32(v, _MM_SHUFFLE(1, 0, 3, 2))));
+      }
+    }
+    for (int i = 0; i < 2; ++i) {  // scramble: a ^= a >> 47; a ^= key; a *= PRIME32_1
+      const __m256i k = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(kSecret + kSecretSize - kStripe + 32 * i));
+      const __m256i x = _mm256_xor_si256(_mm256_xor_si256(a[i], _mm256_srli_epi64(a[i], 47)), k);
+      const __m256i lo = _mm256_mul_epu32(x, prime);
+      const __m256i hi = _mm256_mul_epu32(_mm256_srli_epi64(x, 32), prime);
+      a[i] = _mm256_add_epi64(lo, _mm256_slli_epi64(hi, 32));
+    }
+  }
+  _mm256_store_si256(reinterpret_cast<__m256i*>(acc), a[0]);
+  _mm256_store_si256(reinterpret_cast<__m256i*>(acc + 4), a[1]);
+}
+
+void xxh3_blocks_sse2(uint64_t* acc, const uint8_t* p, size_t nb) {
+  __m128i a[4];
+  for (int i = 0; i < 4; ++i) a[i] = _mm_load_si128(reinterpret_cast<const __m128i*>(acc + 2 * i));
+  const __m128i prime = _mm_set1_epi32((int)kR1);
+  for (size_t b = 0; b < nb; ++b) {
+    const uint8_t* blk = p + b * kBlock;
+    for (size_t s = 0; s < kStripesPerBlock; ++s) {
+      for (int i = 0; i < 4; ++i) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(blk + s * kStripe + 16 * i));
+        const __m128i k = _mm_loadu_si128(reinterpret_cast<const __m128i*>(kSecret + 8 * s + 16 * i));
+        const __m128i dk = _mm_xor_si128(v, k);
+        const __m128i prod = _mm_mul_epu32(dk, _mm_shuffle_epi32(dk, _MM_SHUFFLE(0, 3, 0, 1)));
+        a[i] = _mm_add_epi64(a[i], _mm_add_epi64(prod, _mm_shuffle_epi32(v, _MM_SHUFFLE(1, 0, 3, 2))));
+      }
+    }
+    for (int i = 0; i < 4; ++i) {
+      const __m128i k = _mm_loadu_si128(reinterpret_cast<const __m128i*>(kSecret + kSecretSize - kStripe + 16 * i));
+      const __m128i x = _mm_xor_si128(_mm_xor_si128(a[i], _mm_srli_epi64(a[i], 47)), k);
+      const __m128i lo = _mm_mul_epu32(x, prime);
+      const __m128i hi = _mm_mul_epu32(_mm_srli_epi64(x, 32), prime);
+      a[i] = _mm_add_epi64(lo, _mm_slli_epi64(hi, 32));
+    }
+  }
+  for (int i = 0; i < 4; ++i) _mm_store_si128(reinterpret_cast<__m128i*>(acc + 2 * i), a[i]);
+}
+
+// out[0] = low 64 bits, out[1] = high 64 bits (xxhash's xxh3_128_intdigest = high << 64 | low)
+void xxh3_128_long(const uint8_t* p, size_t len, uint64_t out[2]) {
+  alignas(64) uint64_t acc[8] = {kR3, kQ1, kQ2, kQ3, kQ4, kR2, kQ5, kR1};
+  const size_t nb = (len - 1) / kBlock;
+  static const bool avx2 = __builtin_cpu_supports("avx2") && getenv("M3D_XXH3_SSE2") == nullptr;
+  if (avx2)
+    xxh3_blocks_avx2(acc, p, nb);
+  else
+    xxh3_blocks_sse2(acc, p, nb);
+  const size_t ns = ((len - 1) - kBlock * nb) / kStripe;
+  for (size_t s = 0; s < ns; ++s) xxh3_acc512(acc, p + nb * kBlock + s * kStripe, kSecret + 8 * s);
+  xxh3_acc512(acc, p + len - kStripe, kSecret + kSecretSize - kStripe - 7);
+  out[0] = xxh3_merge(acc, kSecret + 11, (uint64_t)len * kQ1);
+  out[1] = xxh3_merge(acc, kSecret + kSecretSize - 64 - 11, ~((uint64_t)len * kQ2));
+}
+
 constexpr size_t kHashChunk = (size_t)1 << 16;
 
 struct HashJob {
   const uint8_t* p;
   size_t len;
-  uint64_t seed;
-  uint64_t* out;
+  uint64_t* out;  // 2 words
 };
+
+// a chunk's 128-bit digest: XXH3-128 of the chunk (> 240 bytes: every chunk of an array of at
+// least 256 KB is — the last one absorbs a short tail, see m3d_content_keys), else of the chunk
+// zero-padded to 256 bytes (only whole arrays below 241 bytes; the length is in the array key)
+inline void chunk_digest(const HashJob& j) {
+  if (j.len >= kXxh3Min) {
+    xxh3_128_long(j.p, j.len, j.out);
+  } else {
+    alignas(16) uint8_t pad[256] = {};
+    if (j.len > 0) memcpy(pad, j.p, j.len);
+    xxh3_128_long(pad, sizeof(pad), j.out);
+  }
+}
 
 // Persistent workers (created on first use); a job list is handed out with one atomic counter,
 // the caller works too and waits for the last chunk.
@@ -469,7 +611,7 @@ class HashPool {
       const int64_t k = next_.fetch_add(1);
       if (k >= (int64_t)js->size()) return;
       const HashJob& j = (*js)[(size_t)k];
-      *j.out = xxh64(j.p, j.len, j.seed);
+      chunk_digest(j);
       if (left_.fetch_sub(1) == 1) {
         std::lock_guard<std::mutex> lk(mu_);
         done_cv_.notify_all();
@@ -508,32 +650,53 @@ uint64_t m3d_debug_xxh64(const void* p, size_t len, uint64_t seed) {
   return xxh64(static_cast<const uint8_t*>(p), len, seed);
 }
 
+int m3d_debug_xxh3_128(const void* p, size_t len, uint64_t* out2) {
+  if (out2 == nullptr || (p == nullptr && len > 0) || len < kXxh3Min) return M3D_ERR_INVALID;
+  xxh3_128_long(static_cast<const uint8_t*>(p), len, out2);
+  return M3D_OK;
+}
+
 int m3d_content_keys(const void* const* bufs, const size_t* lens, int32_t n, uint64_t* keys) {
   if (n < 0 || (n > 0 && (bufs == nullptr || lens == nullptr || keys == nullptr))) return M3D_ERR_INVALID;
+  // chunk c of an array = [c·64 KB, (c + 1)·64 KB), except that a last piece shorter than the
+  // XXH3 long-path minimum joins the chunk before it; an empty array has one empty chunk
+  auto nchunks = [](size_t len) -> size_t {
+    if (len <= kHashChunk) return 1;
+    const size_t full = len / kHashChunk, tail = len - full * kHashChunk;
+    return (tail == 0 || tail < kXxh3Min) ? full : full + 1;
+  };
   std::vector<size_t> first((size_t)n + 1, 0);
   for (int32_t i = 0; i < n; ++i) {
     if (lens[i] > 0 && bufs[i] == nullptr) return M3D_ERR_INVALID;
-    first[(size_t)i + 1] = first[(size_t)i] + (lens[i] + kHashChunk - 1) / kHashChunk;
+    first[(size_t)i + 1] = first[(size_t)i] + nchunks(lens[i]);
   }
-  std::vector<uint64_t> ch(first[(size_t)n]);
+  std::vector<uint64_t> ch(2 * first[(size_t)n]);
   std::vector<HashJob> jobs;
-  jobs.reserve(ch.size());
+  jobs.reserve(first[(size_t)n]);
   for (int32_t i = 0; i < n; ++i) {
     const uint8_t* b = static_cast<const uint8_t*>(bufs[i]);
-    for (size_t c = first[(size_t)i], off = 0; off < lens[i]; ++c, off += kHashChunk)
-      jobs.push_back(HashJob{b + off, std::min(kHashChunk, lens[i] - off), (uint64_t)c - first[(size_t)i],
-                             &ch[c]});
+    const size_t nc = first[(size_t)i + 1] - first[(size_t)i];
+    for (size_t c = 0; c < nc; ++c) {
+      const size_t off = c * kHashChunk;
+      const size_t len = (c + 1 == nc) ? lens[i] - off : kHashChunk;
+      jobs.push_back(HashJob{b + off, len, &ch[2 * (first[(size_t)i] + c)]});
+    }
   }
   if (jobs.size() >= 4 && host_threads() > 1) {
     HashPool::get().run(jobs);
   } else {
-    for (const HashJob& j : jobs) *j.out = xxh64(j.p, j.len, j.seed);
+    for (const HashJob& j : jobs) chunk_digest(j);
   }
+  // the array key: XXH3-128 of (chunk digests ‖ byte length ‖ chunk count), zero-padded to at
+  // least 256 bytes (an injective encoding: the digest count follows from the length)
+  std::vector<uint64_t> msg;
   for (int32_t i = 0; i < n; ++i) {
-    const uint8_t* c0 = reinterpret_cast<const uint8_t*>(ch.data() + first[(size_t)i]);
-    const size_t cl = 8 * (first[(size_t)i + 1] - first[(size_t)i]);
-    keys[2 * i] = xxh64(c0, cl, 0x9E3779B97F4A7C15ull ^ (uint64_t)lens[i]);
-    keys[2 * i + 1] = xxh64(c0, cl, 0xC2B2AE3D27D4EB4Full + (uint64_t)lens[i]);
+    const size_t nc = first[(size_t)i + 1] - first[(size_t)i];
+    msg.assign(std::max<size_t>(32, 2 * nc + 2), 0);
+    std::copy(ch.begin() + 2 * first[(size_t)i], ch.begin() + 2 * first[(size_t)i + 1], msg.begin());
+    msg[2 * nc] = (uint64_t)lens[i];
+    msg[2 * nc + 1] = (uint64_t)nc;
+    xxh3_128_long(reinterpret_cast<const uint8_t*>(msg.data()), 8 * msg.size(), keys + 2 * i);
   }
   return M3D_OK;
 }

@@ -693,8 +693,10 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     // Exact path for the flagged (group, sub-tile) pairs, every lane (exact for any lane): direct
     // fp32 d² over the lane's 16 rows, then the lane pair (c, c + 32) merges its two states.
-    // (Deferring the flagged sub-tiles to a per-wave list evaluated after the sweep, off the
-    // barrier path, measured slower: 0.360 vs 0.328 ms per launch at cfg1.)
+    // A group whose queries all start from a real seed defers its flagged sub-tiles to the
+    // per-wave list below (dlist/dtile, resolved after the sweep, off the tile barrier:
+    // M3D_NN_DEFER, −2.2 % per launch at cfg1); unseeded groups and a full list
+    // resolve here, where the threshold refresh still prunes the rest of the sweep.
     hm |= force64;
     if (stats != nullptr && lane == 0) {
       atomicAdd(&stats[0], (unsigned long long)__builtin_popcountll(hm));

@@ -175,6 +175,9 @@ struct m3d_cloud {
   // (parent) cloud of the copy's point k
   mutable std::vector<std::pair<double, m3d_cloud*>> morton;
   int32_t* slot = nullptr;
+  // a Morton copy: live ICP loops running on it (m3d_icp_create / _destroy); the parent keeps at
+  // most kMortonKeep copies and evicts the oldest unreferenced one beyond that (api.cpp)
+  mutable int refs = 0;
 };
 
 struct m3d_icp {
@@ -205,7 +208,10 @@ struct m3d_icp {
   const m3d::Grid* tgrid = nullptr;  // grid NN: the target's grid (owned by the target cloud)
   int64_t ns_total = 0;  // source-sharded multi-GPU: sources over all ranks (fitness denominator)
   // exchange buffers of the library-driven multi-GPU loops (m3d_icp_*shard_steps), lazily
-  bool xready = false;      // exchange buffers allocated and every rank agreed (comm.cpp)
+  // exchange buffers allocated and every rank agreed (comm.cpp), one flag per loop kind: the
+  // target-shard loop needs xdk/xcl/xsums, the source-shard loop only xsums
+  bool xready_tgt = false;
+  bool xready_src = false;
   int64_t* xdk = nullptr;   // ns: d64 keys, MIN-reduced
   int32_t* xcl = nullptr;   // ns: claims, MIN-reduced
   double* xsums = nullptr;  // kTermSlots, SUM-reduced
@@ -370,6 +376,10 @@ hipError_t feature_nn(const double* fq, int64_t nq, const double* fr, int64_t nr
 hipError_t feature_correspondences(const double* fs, int64_t ns, const double* ft, int64_t nt,
                                    int mutual, double ratio, int32_t* corr_out, int64_t* n_out,
                                    hipStream_t st);
+// a6 exit rule: count[k] = #{c : |T_k·p_c − q_c|² < max_corr²}, T_k = T_all + 16·list[k], k < n
+hipError_t launch_corres_inlier(const double* src, const double* tgt, const int32_t* corr, int64_t nc,
+                                const double* T_all, const int32_t* list, int64_t n, double max_corr,
+                                int32_t* count, hipStream_t st);
 hipError_t launch_feat_hyp(const double* src, const double* tgt, const int32_t* corr, int64_t nc,
                            uint64_t seed, int64_t H, double edge, double dist, double* T_out,
                            int32_t* pass, hipStream_t st);

@@ -29,7 +29,7 @@ COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2
 OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -61,7 +61,7 @@ class FeatureRansacParams(C.Structure):
 
 class FeatureRansacResult(C.Structure):
     _fields_ = [("T", dbl * 16), ("fitness", dbl), ("inlier_rmse", dbl), ("best_index", i64),
-                ("validations", i64)]
+                ("validations", i64), ("corres_ratio", dbl)]
 
 
 class IcpResult(C.Structure):
@@ -138,6 +138,7 @@ SIGNATURES = {
     "m3d_merge_vertices": (C.c_int, [C.POINTER(dbl), i64, C.POINTER(dbl), C.POINTER(i32), C.POINTER(i64)]),
     "m3d_content_keys": (C.c_int, [C.POINTER(vp), C.POINTER(C.c_size_t), i32, C.POINTER(u64)]),
     "m3d_debug_xxh64": (u64, [vp, C.c_size_t, u64]),
+    "m3d_debug_xxh3_128": (C.c_int, [vp, C.c_size_t, C.POINTER(u64)]),
     "m3d_debug_kabsch3_host":(C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
     "m3d_debug_ldlt6_host": (C.c_int, [C.POINTER(dbl), C.POINTER(dbl), C.POINTER(dbl)]),
 }

@@ -5,10 +5,13 @@ benchmark_ransac.py:105-113 call compute_step_transformation / evaluate_inlier_r
 of times with the same arrays.  Packing (gather + centring + fp32/fp16 conversion) is O(N)
 device work plus one host sync, so packed objects are cached.  Two key policies:
 
-* "content" (default, exact): a hash of the array CONTENTS: a mutated array gets a new key, never
-  a stale object.  At Nc = 1e5 that is ~5.6 MB per call: arrays of ≥ 256 KB are keyed by the
-  library's parallel hash (csrc/hostio.cpp m3d_content_keys: 64 KB chunks, XXH64, a persistent
-  thread pool; all the arrays of one call in one batch), smaller ones by xxh3-128.
+* "content" (default): a 128-bit hash of the array CONTENTS, so a mutated array gets a new key.
+  Probabilistic, not exact: the hash is non-cryptographic XXH3-128, so two different contents of
+  one array share a key with probability ≈ 2⁻¹²⁸ — a stale object is that unlikely, not
+  impossible (and a caller crafting collisions on purpose is not defended against).  At Nc = 1e5
+  that is ~5.6 MB per call: arrays of ≥ 256 KB are keyed by the library's parallel hash
+  (csrc/hostio.cpp m3d_content_keys: 64 KB chunks, XXH3-128 per chunk and over the chunk digests,
+  a persistent thread pool; all the arrays of one call in one batch), smaller ones by xxh3-128.
 * "identity" (opt-in, ``set_policy("identity")`` or M3D_CACHE=identity): an array's content hash
   is remembered per buffer identity (data pointer, shape, strides, dtype) together with a sampled
   signature (xxh3 of ~4k elements spread over the buffer plus its first and last 256 bytes); the

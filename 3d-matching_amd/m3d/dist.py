@@ -261,6 +261,9 @@ def ransac_sharded(cs, params, comm=None):
         raise err
     if int(failed.item()) != 0:
         raise M3DCommError(f"{int(failed.item())} peer rank(s) failed their local run")
-    count, wid = unpack_best_key(int(key.item()))
+    kv = int(key.item())
+    if kv == 0:  # no rank found a winner: identity and no index, as comm.cpp's native driver
+        return 0, -1, np.eye(4)
+    count, wid = unpack_best_key(kv)
     T, _ = cs.kabsch3(1, seed=params.seed, hyp0=wid)
     return count, wid, T[0].cpu().numpy()

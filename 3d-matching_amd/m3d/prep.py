@@ -122,6 +122,7 @@ class FeatureRansacOutcome:
     best_index: int
     validations: int
     correspondence_set: np.ndarray
+    corres_ratio: float = 0.0  # the best's correspondence inlier ratio (Open3D's exit input)
 
 
 def ransac_on_correspondences(src, tgt, corres, max_correspondence_distance: float, *,
@@ -147,4 +148,4 @@ def ransac_on_correspondences(src, tgt, corres, max_correspondence_distance: flo
     i = np.nonzero(j >= 0)[0]
     return FeatureRansacOutcome(np.array(r.T[:]).reshape(4, 4), r.fitness, r.inlier_rmse,
                                 int(r.best_index), int(r.validations),
-                                np.stack([i, j[i]], axis=1).astype(np.int32))
+                                np.stack([i, j[i]], axis=1).astype(np.int32), float(r.corres_ratio))

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 9
+#define M3D_ABI_VERSION 10
 
 /* return codes */
 #define M3D_OK 0
@@ -387,12 +387,16 @@ typedef struct {
   double inlier_rmse;
   int64_t best_index;  /* hypothesis id of the best, -1 = none */
   int64_t validations; /* hypotheses that passed the checkers and were validated */
+  double corres_ratio; /* the best's correspondence inlier ratio (the exit estimate's input; ABI 10) */
 } m3d_feature_ransac_result;
 
 /* RegistrationRANSACBasedOnCorrespondence (ransac.py:44-58 → Open3D): PointToPoint (no scaling),
  * rows drawn with replacement by the counter sampler, checkers, validation over all source
- * points (1-NN within max_correspondence_distance), IsBetterRANSACThan, early exit
- * k = ceil(log(1-c)/log(1-fitness^3)).  corr [device] nc×2 int32 (source, target) rows.
+ * points (1-NN within max_correspondence_distance), IsBetterRANSACThan, early exit as Open3D
+ * 0.19: after each new best k = ceil(log(1-c)/log(1-ratio^3)) with ratio = the share of the nc
+ * input correspondences within max_correspondence_distance under that best (Registration.cpp
+ * EvaluateInlierCorrespondenceRatio; ABI 10 — ABI ≤ 9 used the fitness).
+ * corr [device] nc×2 int32 (source, target) rows.
  * corr_set_out [device] ns int32 or NULL: the best transform's correspondence per source point
  * (-1 none).  Synchronous. */
 int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt,
@@ -408,6 +412,9 @@ int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16);
 int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6);
 /* XXH64 of [p, p + len) (the chunk hash of m3d_content_keys; known-answer tests). */
 uint64_t m3d_debug_xxh64(const void* p, size_t len, uint64_t seed);
+/* XXH3-128 (default secret, seed 0) of [p, p + len), len >= 241 (the long-input path the content
+ * keys use; known-answer tests against the xxhash package): out2 = (low, high). */
+int m3d_debug_xxh3_128(const void* p, size_t len, uint64_t* out2);
 /* Failure injection for the multi-GPU failure tests: what = 1 fails this rank's next local run of
  * m3d_ransac_run_sharded, 2 its next ICP shard-loop iteration (0 clears). */
 int m3d_debug_comm_inject(m3d_comm* c, int what);
@@ -431,9 +438,11 @@ int m3d_format_ascii_rows(const double* data, int64_t rows, int32_t cols, char* 
  * inverse [host] n int32 (corner → vertex id), *n_unique. */
 int m3d_merge_vertices(const double* xyz, int64_t n, double* uniq, int32_t* inverse,
                        int64_t* n_unique);
-/* Content keys of the drop-in's exact cache (m3d.cache): keys [host] 2·n uint64, the 128-bit key
- * of each buffer [host] bufs[i], lens[i] bytes — its 64 KB chunks hashed (XXH64, chunk index as
- * seed) by a persistent host thread pool, the chunk hashes hashed again with two seeds.  The
+/* Content keys of the drop-in's cache (m3d.cache): keys [host] 2·n uint64 (low, high), the
+ * 128-bit key of each buffer [host] bufs[i], lens[i] bytes — its 64 KB chunks hashed with
+ * XXH3-128 by a persistent host thread pool (a tail under 241 bytes joins the previous chunk),
+ * then XXH3-128 of (chunk digests ‖ length ‖ chunk count) (ABI 10; ABI ≤ 9 chained 64-bit XXH64
+ * chunk digests).  Non-cryptographic: unrelated contents collide with probability ≈ 2⁻¹²⁸.  The
  * same bytes give the same key whatever the thread count. */
 int m3d_content_keys(const void* const* bufs, const size_t* lens, int32_t n, uint64_t* keys);
 

@@ -25,7 +25,10 @@ unpinned**; the GPU path is checked against this restatement:
 * ``ransac_feature``     — ``RegistrationRANSACBasedOnCorrespondence`` restated sequentially:
   ransac_n rows drawn WITH replacement, Umeyama (PointToPoint, no scaling), EdgeLength and
   Distance checkers, validation = 1-NN within max_corr over all source points, best =
-  IsBetterRANSACThan, early exit k = ceil(log(1−c)/log(1−fitness^n)).  Open3D draws rows from a
+  IsBetterRANSACThan, early exit k = ceil(log(1−c)/log(1−ratio^n)) with ratio = the new best's
+  CORRESPONDENCE inlier ratio (``EvaluateInlierCorrespondenceRatio``: the share of the input
+  correspondences within max_corr under T — not the fitness; rounds 1–3 used the fitness here,
+  fixed in round 4).  Open3D draws rows from a
   global RNG under OpenMP (non-deterministic); here the rows are an input (the device's counter
   sampler, restated in ``native_rows``).
 """
@@ -457,14 +460,46 @@ def evaluate(src, tgt, T, max_corr, tree=None):
     return fit, rmse
 
 
+def corres_inlier_ratio(src, tgt, corres, max_corr, T):
+    """Open3D 0.19 EvaluateInlierCorrespondenceRatio (Registration.cpp, static): the share of the
+    INPUT correspondences c with |T·p_c − q_c|² < max_corr² — the source transformed as
+    PointCloud::Transform does (``icp_oracle.transform_points``), squaredNorm as
+    ``icp_oracle.sq_dist``, strict <."""
+    import icp_oracle
+
+    corres = np.asarray(corres, np.int64).reshape(-1, 2)
+    if len(corres) == 0:
+        return 0.0
+    pcd = icp_oracle.transform_points(T, np.asarray(src, np.float64)[corres[:, 0]])
+    d2 = icp_oracle.sq_dist(pcd, np.asarray(tgt, np.float64)[corres[:, 1]])
+    return int(np.count_nonzero(d2 < max_corr * max_corr)) / len(corres)
+
+
+def est_k_update(est_k, ratio, confidence, ransac_n):
+    """Open3D 0.19's exit update after a new best (RegistrationRANSACBasedOnCorrespondence):
+    ``est_k_d = log(1 − confidence) / log(1 − pow(ratio, ransac_n))``, and est_k ← ceil(est_k_d)
+    when est_k_d < est_k.  C semantics: ratio = 1 gives log(0) = −inf, est_k_d = −0.0 → 0 (stop);
+    ratio = 0 gives a division by +0.0 → −inf, whose int cast is INT_MIN on x86 → stop (0 here)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        den = np.log(np.float64(1.0) - np.power(np.float64(ratio), np.float64(ransac_n)))
+        d = np.float64(np.log(np.float64(1.0) - np.float64(confidence))) / den
+    if not d < est_k:  # NaN compares false, as in C
+        return est_k
+    return int(math.ceil(d)) if math.isfinite(d) else 0
+
+
 def ransac_feature(src, tgt, corres, max_corr, rows_fn, max_iteration=30, confidence=0.999,
-                   ransac_n=3, edge_length=0.9, distance=None):
-    """RegistrationRANSACBasedOnCorrespondence, sequential.  rows_fn(h) → ransac_n row ids.
-    Returns dict(transformation, fitness, inlier_rmse, best_index, validations)."""
+                   ransac_n=3, edge_length=0.9, distance=None, exit_rule="open3d"):
+    """RegistrationRANSACBasedOnCorrespondence (Open3D 0.19), sequential.  rows_fn(h) → ransac_n
+    row ids.  The early exit follows upstream: after every new best the estimate est_k comes from
+    the CORRESPONDENCE inlier ratio of that best (``corres_inlier_ratio``), not from its fitness
+    (``exit_rule="fitness"`` keeps the round-1..3 restatement, for the divergence test only).
+    Returns dict(transformation, fitness, inlier_rmse, best_index, validations, corres_ratio)."""
     src = np.asarray(src, np.float64)
     tgt = np.asarray(tgt, np.float64)
     corres = np.asarray(corres, np.int64).reshape(-1, 2)
-    best = dict(transformation=np.eye(4), fitness=0.0, inlier_rmse=0.0, best_index=-1, validations=0)
+    best = dict(transformation=np.eye(4), fitness=0.0, inlier_rmse=0.0, best_index=-1, validations=0,
+                corres_ratio=0.0)
     if ransac_n < 3 or len(corres) < ransac_n or max_corr <= 0:
         return best
     tree = cKDTree(tgt)
@@ -483,6 +518,10 @@ def ransac_feature(src, tgt, corres, max_corr, rows_fn, max_iteration=30, confid
         best["validations"] += 1
         if fit > best["fitness"] or (fit == best["fitness"] and rmse < best["inlier_rmse"]):
             best.update(transformation=T, fitness=fit, inlier_rmse=rmse, best_index=h)
-            k = math.ceil(math.log(1.0 - confidence) / math.log(1.0 - fit ** ransac_n)) if fit < 1 else 0
-            est_k = min(est_k, k)
+            if exit_rule == "fitness":
+                ratio = fit
+            else:
+                ratio = corres_inlier_ratio(src, tgt, corres, max_corr, T)
+                best["corres_ratio"] = ratio
+            est_k = est_k_update(est_k, ratio, confidence, ransac_n)
     return best

@@ -157,6 +157,37 @@ def test_fixed_iterations_and_missing_normals():
         registration_icp(src, tgt, 0.0)
 
 
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_empty_source_icp_and_nn1(nn):
+    """An empty source cloud (round-3 ADVICE: the Morton-slot copy must accept n = 0): nn1 returns
+    empty arrays, ICP returns Open3D's empty result (identity, fitness 0, no correspondences) for
+    both NN methods, and the same cloud objects keep working for a non-empty call afterwards."""
+    tgt, nrm = synth.surface_points(3000, seed=2)
+    empty = Cloud(np.zeros((0, 3)))
+    t = Cloud(tgt, nrm)
+    idx, d2 = nn1(empty, t, np.eye(4), 0.3, nn=nn)
+    assert idx.numel() == 0 and d2.numel() == 0
+    out = icp(empty, t, 0.12, np.eye(4), nn=nn, max_iteration=5)
+    assert out.fitness == 0.0 and out.inlier_rmse == 0.0
+    np.testing.assert_array_equal(out.transformation, np.eye(4))
+    assert len(out.correspondence_set) == 0
+    src, _ = synth.surface_points(500, seed=3)
+    idx, _ = nn1(Cloud(src), t, np.eye(4), 0.3, nn=nn)
+    assert idx.numel() == 500
+
+
+def test_morton_copies_stay_bounded_per_cloud():
+    """nn1 with many different radii on one cloud pair (round-3 ADVICE): the per-cloud Morton
+    source copies are capped (api.cpp kMortonKeep), results stay exact."""
+    tgt, _ = synth.surface_points(4000, seed=4)
+    src, _ = synth.surface_points(3000, seed=5)
+    s, t = Cloud(src), Cloud(tgt)
+    T = synth.random_rigid(6, rot_range=0.02, trans_range=0.05)
+    for r in (0.1, 0.12, 0.15, 0.2, 0.25, 0.3, 0.35, 0.4):
+        idx, d2 = nn1(s, t, T, r, nn="grid")
+        check_nn(src, tgt, T, r, idx.cpu().numpy(), d2.cpu().numpy())
+
+
 def test_no_overlap_gives_identity_and_zero_fitness():
     src, _ = synth.surface_points(2000, seed=1)
     tgt, nrm = synth.surface_points(2000, seed=2)

@@ -8,8 +8,10 @@ Bars (stated):
 * FPFH: within 1e-12 on every point whose neighbourhood is edge-clean (oracle
   spfh_edge_sensitive), ≥ 99.5 % of all rows within 1e-6, every group sums to 100 (or 0);
 * feature correspondences on the device's own FPFH: bit-exact vs the oracle on those features;
-* feature RANSAC: same best hypothesis and validation count, transform within 1e-9, fitness
-  exact and rmse within 1e-12 (the validation NN is the exact fp64 decision, nnkey.h).
+* feature RANSAC: same best hypothesis and validation count (Open3D 0.19's exit rule: the
+  correspondence inlier ratio of each new best), transform within 1e-9, fitness and ratio exact,
+  rmse within 1e-12 (the validation NN is the exact fp64 decision, nnkey.h), and the best's
+  correspondence_set pair for pair.
 """
 import numpy as np
 import pytest
@@ -134,6 +136,30 @@ def test_feature_correspondences_exact(mutual):
     del T
 
 
+def _oracle_pairs(src, tgt, T, max_corr):
+    """GetRegistrationResultAndCorrespondences' correspondence_set for T (exact fp64 1-NN within
+    max_corr, lowest index on ties), sorted by source index."""
+    import icp_oracle
+
+    _, _, corr, _ = icp_oracle.registration_result(icp_oracle.transform_points(T, src), tgt, max_corr)
+    return np.asarray(corr, np.int64)
+
+
+def _assert_same_result(got, ref, src, tgt, max_corr):
+    assert got.validations == ref["validations"]
+    assert got.best_index == ref["best_index"]
+    assert got.fitness == ref["fitness"]
+    assert abs(got.inlier_rmse - ref["inlier_rmse"]) <= 1e-12 * max(1.0, ref["inlier_rmse"])
+    assert got.corres_ratio == ref["corres_ratio"]  # an integer count over nc on both sides
+    np.testing.assert_allclose(got.transformation, ref["transformation"], atol=1e-9)
+    # RegistrationResult.correspondence_set, pair for pair: against the oracle's NN under the
+    # device's own T (the NN decision) and under the oracle's T (within 1e-9 of it)
+    if ref["best_index"] >= 0:
+        pairs = np.asarray(got.correspondence_set, np.int64)
+        np.testing.assert_array_equal(pairs, _oracle_pairs(src, tgt, got.transformation, max_corr))
+        np.testing.assert_array_equal(pairs, _oracle_pairs(src, tgt, ref["transformation"], max_corr))
+
+
 def test_feature_ransac_matches_oracle():
     src, _ = synth.surface_points(4000, seed=8)
     T = synth.random_rigid(3, rot_range=0.5, trans_range=1.0)
@@ -145,20 +171,23 @@ def test_feature_ransac_matches_oracle():
     kw = dict(max_iteration=300, confidence=0.999, edge_length=0.9, distance=0.45)
     got = prep.ransac_on_correspondences(src, tgt, corr, 0.45, seed=11, **kw)
     ref = P.ransac_feature(src, tgt, corr, 0.45, lambda h: P.native_rows(11, h, len(corr)), **kw)
-    assert got.best_index == ref["best_index"]
-    assert got.validations == ref["validations"]
-    np.testing.assert_allclose(got.transformation, ref["transformation"], atol=1e-9)
-    assert abs(got.fitness - ref["fitness"]) < 1e-3
+    _assert_same_result(got, ref, src, tgt, 0.45)
     np.testing.assert_allclose(got.transformation, T, atol=2e-2)
     assert len(got.correspondence_set) == round(got.fitness * len(src))
 
 
-@pytest.mark.parametrize("bad_ratio,iters,seed,edge,nval", [(0.97, 2000, 5, None, 2000), (0.9, 2000, 6, 0.9, 5)])
-def test_feature_ransac_batched_validation_matches_oracle(bad_ratio, iters, seed, edge, nval):
+@pytest.mark.parametrize("bad_ratio,iters,seed,edge,conf,nval",
+                         [(0.5, 2000, 16, None, 1.0, 2000), (0.3, 2000, 6, 0.9, 0.999, 5),
+                          (0.97, 2000, 5, None, 0.999, 1)])
+def test_feature_ransac_batched_validation_matches_oracle(bad_ratio, iters, seed, edge, conf, nval):
     """Batched validation (validate_kernel, batches of 64 → 128 → …) against the sequential
-    oracle.  Case 1: no checkers and a 0.03 radius on a 97 %-outlier set keep every fitness tiny,
-    so the early exit never comes and all 2000 hypotheses are validated in growing batches (ties
-    in fitness decided by rmse); case 2: an early exit inside the first batch."""
+    oracle, Open3D 0.19's exit rule (est_k from the new best's correspondence inlier ratio).
+    Case 1: confidence 1.0 (est_k_d = +inf, "we always consume all the iterations") and a first
+    hypothesis drawn from three inlier rows, so every later best has a ratio > 0: all 2000
+    hypotheses are validated in growing batches, fitness ties decided by rmse.  Case 2: an early
+    exit inside the first batch (ratio ≈ 0.65 → est_k = 17).  Case 3: a 97 %-outlier set whose
+    first best has correspondence ratio 0: log(1 − 0) = 0, the estimate is −inf, and upstream's
+    int conversion of it stops the loop (4 validations)."""
     src, _ = synth.surface_points(3000, seed=seed)
     T = synth.random_rigid(seed + 1, rot_range=0.5, trans_range=1.0)
     tgt = synth.apply(T, src) + np.random.default_rng(seed + 2).normal(scale=0.01, size=src.shape)
@@ -166,15 +195,33 @@ def test_feature_ransac_batched_validation_matches_oracle(bad_ratio, iters, seed
     corr = np.c_[np.arange(3000), np.arange(3000)]
     bad = rng.random(3000) < bad_ratio
     corr[bad, 1] = rng.integers(0, 3000, int(bad.sum()))
-    kw = dict(max_iteration=iters, confidence=0.999, edge_length=edge, distance=None)
+    kw = dict(max_iteration=iters, confidence=conf, edge_length=edge, distance=None)
     got = prep.ransac_on_correspondences(src, tgt, corr, 0.03, seed=seed, **kw)
     ref = P.ransac_feature(src, tgt, corr, 0.03, lambda h: P.native_rows(seed, h, len(corr)), **kw)
     assert ref["validations"] >= nval
-    assert got.validations == ref["validations"]
-    assert got.best_index == ref["best_index"]
-    assert got.fitness == ref["fitness"]
-    assert abs(got.inlier_rmse - ref["inlier_rmse"]) <= 1e-12 * max(1.0, ref["inlier_rmse"])
-    np.testing.assert_allclose(got.transformation, ref["transformation"], atol=1e-9)
+    _assert_same_result(got, ref, src, tgt, 0.03)
+
+
+def test_feature_ransac_exit_uses_corres_ratio_not_fitness():
+    """The round-3 verdict's case: a well-overlapping pair (fitness ≈ 1 at the true pose) with 70 %
+    outlier correspondences.  A fitness-based estimate (rounds 1–3) exits after a handful of
+    validations; Open3D's correspondence-ratio estimate (≈ 0.3 → est_k ≈ 253) keeps going.  The
+    device follows the corrected oracle, validation for validation."""
+    pts, _ = synth.surface_points(1500, seed=7)
+    T = synth.random_rigid(8, rot_range=0.5, trans_range=1.0)
+    tgt = synth.apply(T, pts)
+    rng = np.random.default_rng(9)
+    corr = np.c_[np.arange(1500), np.arange(1500)]
+    bad = rng.random(1500) < 0.7
+    corr[bad, 1] = rng.integers(0, 1500, int(bad.sum()))
+    kw = dict(max_iteration=400, confidence=0.999, edge_length=0.9, distance=0.45)
+    rows = lambda h: P.native_rows(3, h, len(corr))  # noqa: E731
+    ref = P.ransac_feature(pts, tgt, corr, 0.45, rows, **kw)
+    old = P.ransac_feature(pts, tgt, corr, 0.45, rows, exit_rule="fitness", **kw)
+    assert old["validations"] < 10 < ref["validations"]
+    got = prep.ransac_on_correspondences(pts, tgt, corr, 0.45, seed=3, **kw)
+    _assert_same_result(got, ref, pts, tgt, 0.45)
+    assert got.validations != old["validations"]
 
 
 def test_feature_ransac_empty_cases():

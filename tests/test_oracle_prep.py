@@ -118,3 +118,45 @@ def test_native_rows_with_replacement_range():
     flat = np.array(rows).ravel()
     assert flat.min() == 0 and flat.max() == 6
     assert any(len(set(r)) < 3 for r in rows)  # duplicates occur: drawn with replacement
+
+
+def test_est_k_update_c_semantics():
+    """Open3D 0.19's exit update: est_k ← ceil(log(1−c)/log(1−r^n)) when smaller; r = 1 → 0
+    (log(0) = −inf gives −0.0), r = 0 → stop (a division by +0.0 gives −inf), NaN leaves it."""
+    assert P.est_k_update(30, 1.0, 0.999, 3) == 0
+    assert P.est_k_update(30, 0.0, 0.999, 3) == 0
+    assert P.est_k_update(30, float("nan"), 0.999, 3) == 30
+    k = math.ceil(math.log(0.001) / math.log(1 - 0.3 ** 3))
+    assert k == 253 and P.est_k_update(1000, 0.3, 0.999, 3) == 253
+    assert P.est_k_update(30, 0.3, 0.999, 3) == 30     # not below the current est_k
+    assert P.est_k_update(30, 0.9, 0.999, 3) == math.ceil(math.log(0.001) / math.log(1 - 0.729))
+
+
+def test_corres_inlier_ratio_counts_input_correspondences():
+    pts = np.array([[0.0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]])
+    T = np.eye(4)
+    T[0, 3] = 0.1
+    corr = np.array([[0, 0], [1, 1], [2, 3], [3, 3]])
+    # under T: rows 0, 1 and 3 lie 0.1 from their targets; row 2 lies √2-ish away
+    assert P.corres_inlier_ratio(pts, pts, corr, 0.2, T) == 0.75
+    assert P.corres_inlier_ratio(pts, pts, corr, 0.1, T) == 0.0  # strict <: 0.1² is not below
+
+
+def test_ransac_feature_exit_follows_corres_ratio_not_fitness():
+    """A well-overlapping pair (fitness ≈ 1 at the true pose) with 70 % outlier correspondences:
+    the fitness rule exits after a handful of hypotheses, Open3D's correspondence-ratio rule
+    (≈ 0.3 → est_k ≈ 253) keeps validating — the two restatements differ."""
+    pts, _ = synth.surface_points(1500, seed=7)
+    T = synth.random_rigid(8, rot_range=0.5, trans_range=1.0)
+    tgt = synth.apply(T, pts)
+    rng = np.random.default_rng(9)
+    corr = np.c_[np.arange(1500), np.arange(1500)]
+    bad = rng.random(1500) < 0.7
+    corr[bad, 1] = rng.integers(0, 1500, int(bad.sum()))
+    kw = dict(max_iteration=400, edge_length=0.9, distance=0.45)
+    rows = lambda h: P.native_rows(3, h, len(corr))  # noqa: E731
+    new = P.ransac_feature(pts, tgt, corr, 0.45, rows, **kw)
+    old = P.ransac_feature(pts, tgt, corr, 0.45, rows, exit_rule="fitness", **kw)
+    assert new["fitness"] > 0.99 and old["fitness"] > 0.99
+    assert 0.25 < new["corres_ratio"] < 0.35
+    assert old["validations"] < 10 < new["validations"]
