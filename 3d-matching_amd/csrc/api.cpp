@@ -240,7 +240,7 @@ int m3d_profile_enable(m3d_ctx* ctx, int enable) {
 
 int m3d_profile_read(m3d_ctx* ctx, int kernel, double* total_ms, int64_t* launches) {
   if (!ctx) return M3D_ERR_INVALID;
-  CHECK_ARG(ctx, kernel >= 0 && kernel < 4 && total_ms && launches, "invalid arguments");
+  CHECK_ARG(ctx, kernel >= 0 && kernel < 6 && total_ms && launches, "invalid arguments");
   double tot = 0.0;
   const size_t n = ctx->ev_used[kernel];
   for (size_t k = 0; k < n; ++k) {
@@ -1028,6 +1028,8 @@ void m3d_icp_destroy(m3d_icp* s) {
   hipFree(s->corr);
   hipFree(s->partials);
   hipFree(s->sums);
+  hipFree(s->pp);
+  hipFree(s->pcounter);
   delete s;
 }
 
@@ -1147,6 +1149,15 @@ int m3d_icp_prepare_steps(m3d_icp* s, int32_t n) {
 int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   CHECK_ARG(s->ctx, n >= 0, "n must be >= 0");
+  // single-device grid loop: the n steps in ONE persistent launch (icp.hip icp_grid_persist_kernel,
+  // the same bits as the steps below)
+  if (n >= 1 && icp_persist_ok(s)) {
+    hipSetDevice(s->ctx->device);
+    KTimer kt(s->ctx, M3D_KERNEL_LOOP, S(stream));
+    HIPX(s->ctx, launch_icp_persist(s, n, S(stream)));
+    s->keys_clean = false;
+    return M3D_OK;
+  }
   if (n >= 2 && icp_graphs_on() && !s->graph_off && !s->ctx->profiling) {
     const int slot = s->keys_clean ? 1 : 0;
     const bool have = s->graph[slot] != nullptr && s->graph_n[slot] == n;
@@ -1240,8 +1251,14 @@ int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream) {
   if (!s || !out) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;
   IcpState h;
+  int32_t fault = 0;
   HIPX(ctx, hipMemcpyAsync(&h, s->state, sizeof(h), hipMemcpyDeviceToHost, S(stream)));
+  if (s->pcounter != nullptr)
+    HIPX(ctx, hipMemcpyAsync(&fault, s->pcounter + 8, sizeof(fault), hipMemcpyDeviceToHost, S(stream)));
   HIPX(ctx, hipStreamSynchronize(S(stream)));
+  if (fault != 0)
+    return m3d_fail(ctx, M3D_ERR_HIP, "persistent ICP loop: a workgroup waited past its bound for the "
+                                      "others (not all resident); results are invalid");
   for (int k = 0; k < 16; ++k) out->T[k] = h.T[k];
   out->fitness = h.fitness;
   out->inlier_rmse = h.rmse;
@@ -1277,7 +1294,8 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
   int rc = m3d_icp_create(ctx, src, tgt, max_dist, params, &s);
   if (rc) return rc;
   rc = m3d_icp_reset(s, init, stream);
-  for (int k = 0; !rc && k <= params->max_iteration; ++k) rc = m3d_icp_step(s, stream);
+  // max_iteration + 1 evaluations: one persistent launch for the grid loop, else step by step
+  if (!rc) rc = m3d_icp_steps(s, params->max_iteration + 1, stream);
   if (!rc) rc = m3d_icp_result_get(s, out, stream);
   if (!rc && corr_idx && src->n > 0) {
     hipError_t e = launch_scatter_i32(s->corr, s->src->slot, src->n, corr_idx, S(stream));

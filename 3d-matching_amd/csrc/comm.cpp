@@ -68,6 +68,9 @@ int poisoned_error(m3d_comm* c) {
 
 int allreduce(m3d_comm* c, void* buf, int64_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t st) {
   if (count == 0) return M3D_OK;
+  // profiling on: events around the collective on its own stream (M3D_KERNEL_COMM), so a run can
+  // report exchange time beside NN and terms time
+  KTimer kt(c->ctx, M3D_KERNEL_COMM, st);
   const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, dt, op, c->nccl, st);
   if (r != ncclSuccess) return poison(c, comm_fail(c->ctx, r, "ncclAllReduce"));
   return M3D_OK;
@@ -112,7 +115,7 @@ bool split_exchange(const m3d_icp* s) {
     const char* e = getenv("M3D_SHARD_SPLIT");
     return !(e && atoi(e) == 0);
   }();
-  return env && s->src->n >= 2 * 4096 && icp_nn_range_ok(s);
+  return env && !(s->params.flags & M3D_ICP_NO_SPLIT) && s->src->n >= 2 * 4096 && icp_nn_range_ok(s);
 }
 }  // namespace
 

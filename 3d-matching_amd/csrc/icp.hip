@@ -812,6 +812,43 @@ __device__ __forceinline__ double wave_transpose_sum32(const double (&v)[32], in
   return w1 + __shfl_xor(w1, 1, kWave);  // slot lane >> 1
 }
 
+// One source's contribution to the 30 term slots (layout below), in a fixed operation order:
+// every terms pass (terms_block, the persistent grid loop) adds a source through this function,
+// so equal winners give equal bits.  Q = the fp64 transformed source, q / n its winner's point and
+// normal, d2 = the winner's fp64 d², c = the source centre (point-to-point).
+__device__ __forceinline__ void terms_add(double (&acc)[30], const double (&Q)[3], const double (&q)[3],
+                                          const double (&n)[3], double d2, int est, const double (&c)[3]) {
+  const double d[3] = {Q[0] - q[0], Q[1] - q[1], Q[2] - q[2]};
+  acc[28] += 1.0;
+  acc[29] += d2;
+  if (est == M3D_EST_POINT_TO_PLANE) {
+    const double r = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
+    double J[6];
+    cross3(Q, n, J);
+    J[3] = n[0];
+    J[4] = n[1];
+    J[5] = n[2];
+    int k = 0;
+#pragma unroll
+    for (int x = 0; x < 6; ++x)
+#pragma unroll
+      for (int y = x; y < 6; ++y) acc[k++] += J[x] * J[y];
+#pragma unroll
+    for (int x = 0; x < 6; ++x) acc[21 + x] += J[x] * r;
+    acc[27] += r * r;
+  } else {
+    const double pc[3] = {Q[0] - c[0], Q[1] - c[1], Q[2] - c[2]};
+    const double qc[3] = {q[0] - c[0], q[1] - c[1], q[2] - c[2]};
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      acc[x] += pc[x];
+      acc[3 + x] += qc[x];
+#pragma unroll
+      for (int y = 0; y < 3; ++y) acc[6 + 3 * x + y] += pc[x] * qc[y];
+    }
+  }
+}
+
 // Inputs of the terms pass.  Winner of source i:
 //  * claim == nullptr (one device, or a source shard against the whole target): the fp64 winner
 //    decided from the scan keys (nnkey.h winner_fp64; ambiguous queries resolved over the
@@ -956,37 +993,7 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
       a.sq[a.minv[i]] = seed_rec(gj[u], local, a.tgt32 + (local ? gj[u] - a.off : 0), d2[u]);
     }
     if (gj[u] < a.off || gj[u] >= a.off + a.nt_shard) continue;  // none, or another shard's target
-    const double* q = tq[u];
-    const double d[3] = {vs[u][0] - q[0], vs[u][1] - q[1], vs[u][2] - q[2]};
-    acc[28] += 1.0;
-    acc[29] += d2[u];
-    if (a.est == M3D_EST_POINT_TO_PLANE) {
-      const double* n = tn[u];
-      const double r = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
-      double J[6];
-      cross3(vs[u], n, J);
-      J[3] = n[0];
-      J[4] = n[1];
-      J[5] = n[2];
-      int k = 0;
-#pragma unroll
-      for (int x = 0; x < 6; ++x)
-#pragma unroll
-        for (int y = x; y < 6; ++y) acc[k++] += J[x] * J[y];
-#pragma unroll
-      for (int x = 0; x < 6; ++x) acc[21 + x] += J[x] * r;
-      acc[27] += r * r;
-    } else {
-      const double pc[3] = {vs[u][0] - a.c[0], vs[u][1] - a.c[1], vs[u][2] - a.c[2]};
-      const double qc[3] = {q[0] - a.c[0], q[1] - a.c[1], q[2] - a.c[2]};
-#pragma unroll
-      for (int x = 0; x < 3; ++x) {
-        acc[x] += pc[x];
-        acc[3 + x] += qc[x];
-#pragma unroll
-        for (int y = 0; y < 3; ++y) acc[6 + 3 * x + y] += pc[x] * qc[y];
-      }
-    }
+    terms_add(acc, vs[u], tq[u], tn[u], d2[u], a.est, a.c);
   }
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   {
@@ -1284,6 +1291,295 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     if (threadIdx.x == 0) s->ticket = 0;
     if (do_solve) solve_state(red[0], s, sp, in);
   }
+}
+
+// ------------------------------------------------------------------------------- persistent grid loop
+// Round 4: n iterations of the single-device grid-NN ICP loop in ONE launch (m3d_icp_steps; the
+// two-launch loop above stays; m3d_icp_params.flags / M3D_ICP_PERSIST choose).  One workgroup per 512-source tile (the
+// terms pass's block: kTermsBlock threads × 2 sources), all resident (api.cpp checks the grid
+// against the occupancy before choosing this path).  Per iteration a workgroup
+//   (1) scans its 512 queries (kL lanes each, nnkey.h grid_scan) seeded from the previous winner,
+//       whose centred fp32 point it kept in LDS (no corr → target gather);
+//   (2) decides the fp64 winners and adds the terms of its sources exactly as terms_block does
+//       (same thread ↔ source map, same terms_add order, same wave/LDS reduction), writing corr;
+//   (3) publishes its block partial write-through (sc1) into one of two buffers, drains it, and
+//       arrives on a launch-wide counter (agent-scope add); polls the counter (sc1 loads) until
+//       every tile has arrived — MI355X_MICROARCH.md hand-off table, first row;
+//   (4) reduces ALL tile partials in reduce_kernel's fixed group order (sc1 loads) and runs
+//       solve_state on its own LDS copy of the loop state.
+// Every workgroup therefore holds bit-identical sums and state (nobody broadcasts a transform),
+// the same bits as the fused two-launch loop (test_gpu_icp persistent cases).  Partials are
+// double-buffered: a workgroup writes iteration k + 2's partial only after every workgroup has
+// arrived at iteration k + 1, i.e. finished reading iteration k's.  Every spin is bounded: a
+// workgroup that waits too long (a tile not resident) flags `fault` and leaves the loop.
+constexpr int kPTile = 2 * kTermsBlock;  // sources per tile (= per workgroup)
+constexpr uint32_t kPersistMaxSpin = 1u << 22;
+
+struct PersistArgs {
+  const float4* src32;  // the source in Morton slot order (centred fp32)
+  const double* src64;
+  int64_t ns;
+  GridDev g;            // the target grid
+  const double* tgt64;
+  const double* rec64;  // target records (point, normal)
+  const double* nrm64;
+  const float4* tgt32;
+  int64_t nt;
+  int32_t* corr;        // slot order: read once (seeds), written every iteration
+  double* pp;           // 2 × ntiles × kTermSlots
+  uint32_t* counter;    // arrivals, zero at launch
+  int32_t* fault;
+  int32_t n;            // iterations (m3d_icp_step calls) to run
+  int est;
+  double c[3];
+  unsigned long long* prof;  // M3D_PERSIST_PROF=1: per-phase wall-clock ticks of workgroup 0 (else null)
+};
+
+template <int kL, int kR, int kB>
+__global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistArgs a, IcpState* gs,
+                                                                       SolveParams sp) {
+  constexpr int kT = kPTile * kL;
+  __shared__ IcpState S;
+  __shared__ uint64_t k1s[kPTile];
+  __shared__ float n2s[kPTile];
+  __shared__ float4 seedp[kPTile];  // previous winner's centred fp32 point, w = its index (−1 none)
+  __shared__ double red[kTermSlots][kTermsBlock / kWave];
+  __shared__ double gsum[kReduceGroups][kTermSlots];
+  __shared__ int bad;
+  const int tid = threadIdx.x;
+  const int64_t ntiles = gridDim.x;
+  const int64_t base = (int64_t)blockIdx.x * kPTile;
+  for (int k = tid; k < (int)(sizeof(IcpState) / 4); k += kT)
+    reinterpret_cast<uint32_t*>(&S)[k] = reinterpret_cast<const uint32_t*>(gs)[k];
+  if (tid == 0) bad = 0;
+  // scan lanes: query q = tid / kL of the tile; its centred point stays in registers
+  const int q = tid / kL, sub = tid % kL;
+  const int64_t t = base + q;
+  const float4 p = t < a.ns ? a.src32[t] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (sub == 0) {  // seeds of the first iteration: the loop's correspondences on entry (prev)
+    const int32_t j = t < a.ns ? a.corr[t] : -1;
+    float4 v = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+    if (j >= 0) {
+      const float4 w = a.tgt32[j];
+      v = make_float4(w.x, w.y, w.z, __int_as_float(j));
+    }
+    seedp[q] = v;
+  }
+  // terms lanes (waves 0..3): sources base + u·256 + tid, their fp64 points in registers
+  constexpr int kP = 2;
+  double p64[kP][3];
+#pragma unroll
+  for (int u = 0; u < kP; ++u) {
+    const int64_t i = base + u * kTermsBlock + tid;
+    const bool v = tid < kTermsBlock && i < a.ns;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) p64[u][k] = v ? a.src64[3 * i + k] : 0.0;
+  }
+  const int lane = tid & (kWave - 1), wave = tid / kWave;
+  // phase timer (diagnostics only): workgroup 0, thread 0, wall clock after each barrier
+  unsigned long long tph[7] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  const bool prof = a.prof != nullptr && blockIdx.x == 0 && tid == 0;
+  if (prof) tlast = wall_clock64();
+  auto mark = [&](int k) {
+    if (prof) {
+      const unsigned long long t = wall_clock64();
+      tph[k] += t - tlast;
+      tlast = t;
+    }
+  };
+  for (int it = 0; it < a.n; ++it) {
+    __syncthreads();  // S, seedp of this iteration
+    mark(0);
+    if (S.done || bad) break;
+    // (1) scan
+    {
+      const float r2_hi = S.r2_hi, be = S.band_e;
+      const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
+      uint64_t k1 = key0;
+      float k1d = kInf, n2 = kInf;
+      if (t < a.ns) {
+        float qx, qy, qz;
+        xform32(S.Rt32, p, qx, qy, qz);
+        const float4 sd = seedp[q];
+        const int32_t sj = __float_as_int(sd.w);
+        if (sj >= 0) {  // nnkey.h seed_key, single device: the previous winner re-evaluated
+          const float d2 = d2f(qx, qy, qz, sd.x, sd.y, sd.z);
+          if (d2 <= r2_hi) k1 = make_key(d2, (uint32_t)sj);
+        }
+        k1d = key_real_d2(k1);
+        if (a.g.ncells > 0) {
+          const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
+          grid_scan<kL, kR, kB>(a.g, qx, qy, qz, R, r2_hi, 0, sub, k1, k1d, n2);
+        }
+      }
+      grid_merge_lanes<kL>(k1, k1d, n2);
+      if (sub == 0) {
+        k1s[q] = (t < a.ns && k1 != key0) ? k1 : (uint64_t)kKeyNone;
+        n2s[q] = t < a.ns ? n2 : kInf;
+      }
+    }
+    __syncthreads();
+    mark(1);
+    // (2) terms: terms_block's per-thread part for kP = 2, keys from LDS
+    if (tid < kTermsBlock) {
+      double acc[30];
+#pragma unroll
+      for (int k = 0; k < 30; ++k) acc[k] = 0.0;
+      bool valid[kP], fixed[kP];
+      int64_t ii[kP], gj[kP];
+      double vs[kP][3], d2[kP];
+#pragma unroll
+      for (int u = 0; u < kP; ++u) {
+        const int64_t i = base + u * kTermsBlock + tid;
+        valid[u] = i < a.ns;
+        ii[u] = valid[u] ? i : 0;
+        gj[u] = -1;
+        d2[u] = 0.0;
+        fixed[u] = true;
+        q64_of(S.T, p64[u], vs[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kP; ++u) {
+        const int ql = u * kTermsBlock + tid;
+        const uint64_t k1 = valid[u] ? k1s[ql] : (uint64_t)kKeyNone;
+        const float n2 = valid[u] ? n2s[ql] : kInf;
+        const float X = valid[u] && k1 != (uint64_t)kKeyNone ? search_bound(key_d2(k1), S.band_e, S.r2_hi) : -1.0f;
+        const bool amb = X >= 0.0f && n2 <= X;
+        float qx = 0.0f, qy = 0.0f, qz = 0.0f;
+        if (amb) xform32(S.Rt32, a.src32[ii[u]], qx, qy, qz);
+        int64_t bj = -1;
+        double bd = 0.0;
+        resolve_wave(amb, a.g, a.tgt64, 0, qx, qy, qz, X, vs[u], S.r2, bj, bd);
+        if (amb) {
+          gj[u] = bj;
+          d2[u] = bd;
+        } else if (valid[u] && key_real(k1)) {
+          const int64_t c = (int64_t)(uint32_t)k1;
+          if (c < a.nt) {
+            gj[u] = c;
+            fixed[u] = false;
+          }
+        }
+      }
+      double tq[kP][3], tn[kP][3];
+      float4 t32[kP];
+#pragma unroll
+      for (int u = 0; u < kP; ++u) {
+        const bool own = valid[u] && gj[u] >= 0 && gj[u] < a.nt;
+        const int64_t l = own ? gj[u] : 0;
+        if (a.rec64 != nullptr) {
+          const double4 r0 = reinterpret_cast<const double4*>(a.rec64)[2 * l];
+          const double4 r1 = reinterpret_cast<const double4*>(a.rec64)[2 * l + 1];
+          tq[u][0] = r0.x;
+          tq[u][1] = r0.y;
+          tq[u][2] = r0.z;
+          tn[u][0] = r0.w;
+          tn[u][1] = r1.x;
+          tn[u][2] = r1.y;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            tq[u][k] = a.tgt64[3 * l + k];
+            tn[u][k] = a.est == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
+          }
+        }
+        t32[u] = a.tgt32[l];  // the next iteration's seed point
+      }
+#pragma unroll
+      for (int u = 0; u < kP; ++u) {
+        if (!valid[u]) continue;
+        if (!fixed[u]) {
+          const double d = d2_64(vs[u], tq[u]);
+          if (d < S.r2) {
+            d2[u] = d;
+          } else {
+            gj[u] = -1;
+          }
+        }
+        a.corr[ii[u]] = (int32_t)gj[u];
+        seedp[u * kTermsBlock + tid] =
+            gj[u] >= 0 ? make_float4(t32[u].x, t32[u].y, t32[u].z, __int_as_float((int32_t)gj[u]))
+                       : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+        if (gj[u] < 0 || gj[u] >= a.nt) continue;
+        terms_add(acc, vs[u], tq[u], tn[u], d2[u], a.est, a.c);
+      }
+      double v[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) v[k] = k < 30 ? acc[k] : 0.0;
+      const double w = wave_transpose_sum32(v, lane);
+      if ((lane & 1) == 0) red[lane >> 1][wave] = w;
+    }
+    __syncthreads();
+    mark(2);
+    // (3) publish this tile's partial, arrive, wait for every tile
+    double* P = a.pp + (int64_t)(it & 1) * ntiles * kTermSlots;
+    if (tid < kTermSlots) {
+      double v = 0.0;
+      if (tid < 30)
+        for (int w = 0; w < kTermsBlock / kWave; ++w) v += red[tid][w];
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(P + (int64_t)blockIdx.x * kTermSlots + tid),
+                         __double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    mark(3);
+    if (tid == 0) {
+      __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t want = (uint32_t)(ntiles * (it + 1));
+      uint32_t spins = 0;
+      while (__hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kPersistMaxSpin) {
+          bad = 1;
+          *a.fault = 1;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    mark(4);
+    if (bad) break;
+    // (4) every tile's partial, reduce_kernel's order: group g = tiles g, g + 32, …; then the 32
+    // group sums in group order
+    {
+      const int slot = tid & (kTermSlots - 1);
+      for (int g = tid / kTermSlots; g < kReduceGroups; g += kT / kTermSlots) {
+        constexpr int kMaxPer = 8;  // ntiles ≤ 256 (api.cpp)
+        double tv[kMaxPer];
+#pragma unroll
+        for (int r = 0; r < kMaxPer; ++r) {
+          const int64_t b = g + (int64_t)r * kReduceGroups;
+          tv[r] = b < ntiles ? __longlong_as_double(__hip_atomic_load(
+                                   reinterpret_cast<unsigned long long*>(P + b * kTermSlots + slot),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                             : 0.0;
+        }
+        double gv = 0.0;  // out-of-range tiles add +0.0, as terms_solve_kernel's last block does
+#pragma unroll
+        for (int r = 0; r < kMaxPer; ++r) gv += tv[r];
+        gsum[g][slot] = gv;
+      }
+    }
+    __syncthreads();
+    if (tid < kTermSlots) {
+      double tt = 0.0;
+      for (int k = 0; k < kReduceGroups; ++k) tt += gsum[k][tid];
+      gsum[0][tid] = tt;
+    }
+    __syncthreads();
+    mark(5);
+    if (tid < kWave) {
+      SolveIn in;
+      solve_in(&S, in);
+      solve_state(gsum[0], &S, sp, in);
+    }
+  }
+  if (prof)
+    for (int k = 0; k < 7; ++k) atomicAdd(a.prof + k, tph[k]);
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int k = tid; k < (int)(sizeof(IcpState) / 4); k += kT)
+      reinterpret_cast<uint32_t*>(gs)[k] = reinterpret_cast<const uint32_t*>(&S)[k];
 }
 
 // finalize standalone NN (m3d_nn1): the fp64 winner (nnkey.h winner_fp64) and its d64
@@ -1658,6 +1954,112 @@ hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t
     return e == hipSuccess ? launch_icp_solve(s, s->sums, st) : e;
   }
   launch_terms_solve(terms_args(s, 0, nullptr, nullptr, reset_keys), s, s->sums, 1, st);
+  return hipGetLastError();
+}
+
+// The persistent grid loop (icp_grid_persist_kernel): usable when the loop runs the grid NN on
+// one device with 512-source terms tiles, at most 256 tiles (the reduction's unrolled depth), and
+// the whole grid is resident.  Flags M3D_ICP_PERSIST / M3D_ICP_NO_PERSIST, else the env default
+// M3D_ICP_PERSIST = 1 | 0 (off when unset); M3D_PERSIST_LANES = 1 | 2
+// (lanes per query, 512 or 1024 threads per workgroup).
+static int persist_lanes() {
+  static const int v = [] {
+    const char* e = getenv("M3D_PERSIST_LANES");
+    const int k = e ? atoi(e) : 2;
+    return (k == 1 || k == 2) ? k : 2;
+  }();
+  return v;
+}
+
+template <int kL>
+static const void* persist_fn() {
+  return reinterpret_cast<const void*>(&icp_grid_persist_kernel<kL, 2, 2>);
+}
+
+bool icp_persist_ok(const m3d_icp* s) {
+  static const bool dflt = [] {  // M3D_ICP_PERSIST = 1 | 0: the default when the flags say neither
+    const char* e = getenv("M3D_ICP_PERSIST");
+    return e != nullptr && atoi(e) == 1;
+  }();
+  const bool want = (s->params.flags & M3D_ICP_PERSIST) ? true : (s->params.flags & M3D_ICP_NO_PERSIST) ? false : dflt;
+  if (!want || s->params.nn_method != M3D_NN_GRID || s->ns_total > 0 || s->src->n == 0 ||
+      terms_pts() != 2 || s->tgrid == nullptr)
+    return false;
+  const int64_t ntiles = (s->src->n + kPTile - 1) / kPTile;
+  if (ntiles > 8 * kReduceGroups) return false;
+  static int cap = -1;  // resident workgroups of the kernel on this device (per process, device 0 form)
+  if (cap < 0) {
+    int dev = 0, cus = 0, per = 0;
+    const int L = persist_lanes();
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, L == 1 ? persist_fn<1>() : persist_fn<2>(),
+                                                     kPTile * L, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      cap = 0;
+    } else {
+      // one workgroup per CU at most (the hand-off form this kernel uses is measured at one per
+      // CU), and a margin of 8 CUs for anything else resident
+      cap = per >= 1 ? std::max(0, cus - 8) : 0;
+    }
+  }
+  return ntiles <= cap;
+}
+
+hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st) {
+  const int64_t ntiles = (s->src->n + kPTile - 1) / kPTile;
+  if (s->pp == nullptr) {
+    hipError_t e = hipMalloc(&s->pp, sizeof(double) * 2 * kTermSlots * ntiles);
+    if (e == hipSuccess) e = hipMalloc(&s->pcounter, 64);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(s->pcounter, 0, 64, st);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipMemsetAsync(s->pcounter, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  PersistArgs a;
+  a.src32 = s->src->xyz32;
+  a.src64 = s->src->xyz64;
+  a.ns = s->src->n;
+  a.g = s->tgrid->dev;
+  a.tgt64 = s->tgt->xyz64;
+  a.rec64 = s->tgt->rec64;
+  a.nrm64 = s->tgt->nrm64;
+  a.tgt32 = s->tgt->xyz32;
+  a.nt = s->tgt->n;
+  a.corr = s->corr;
+  a.pp = s->pp;
+  a.counter = s->pcounter;
+  a.fault = reinterpret_cast<int32_t*>(s->pcounter) + 8;  // its own 32-B sector of the 64-B block
+  a.n = n;
+  a.est = s->params.estimation;
+  for (int k = 0; k < 3; ++k) a.c[k] = s->src->center[k];
+  static unsigned long long* prof = [] {  // M3D_PERSIST_PROF=1: phase ticks, printed per launch
+    const char* e = getenv("M3D_PERSIST_PROF");
+    unsigned long long* p = nullptr;
+    if (e && atoi(e) == 1 && hipMalloc(&p, 8 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
+    return p;
+  }();
+  a.prof = prof;
+  if (prof != nullptr) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), st);
+  const SolveParams sp = solve_params(s);
+  if (persist_lanes() == 1)
+    icp_grid_persist_kernel<1, 2, 2><<<(unsigned)ntiles, kPTile, 0, st>>>(a, s->state, sp);
+  else
+    icp_grid_persist_kernel<2, 2, 2><<<(unsigned)ntiles, kPTile * 2, 0, st>>>(a, s->state, sp);
+  if (prof != nullptr) {
+    unsigned long long h[8];
+    int khz = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    if (hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
+        hipStreamSynchronize(st) == hipSuccess && khz > 0) {
+      const double us = 1e3 / khz;
+      fprintf(stderr, "[m3d persist] %lld tiles, n=%d, us per iteration: top %.2f scan %.2f terms %.2f "
+              "publish %.2f wait %.2f reduce %.2f (solve in 'top')\n", (long long)ntiles, n,
+              h[0] * us / n, h[1] * us / n, h[2] * us / n, h[3] * us / n, h[4] * us / n, h[5] * us / n);
+    }
+  }
   return hipGetLastError();
 }
 

@@ -118,8 +118,8 @@ struct m3d_ctx {
   std::string err;
   // kernel timing (m3d_profile_*): event pairs per kernel id
   bool profiling = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
-  size_t ev_used[4] = {0, 0, 0, 0};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[6];
+  size_t ev_used[6] = {0, 0, 0, 0, 0, 0};
   // scratch (grown on demand)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -217,6 +217,10 @@ struct m3d_icp {
   double* xsums = nullptr;  // kTermSlots, SUM-reduced
   // m3d_icp_steps replays: an n-step sequence captured into a HIP graph (api.cpp), one slot per
   // keys_clean state on entry; a slot captures a sequence requested a second time
+  // the persistent grid loop (icp.hip icp_grid_persist_kernel): double-buffered tile partials,
+  // the arrival counter (word 0) and the fault flag (word 8) of one 64-B block
+  double* pp = nullptr;
+  uint32_t* pcounter = nullptr;
   hipStream_t cap_stream = nullptr;
   hipGraphExec_t graph[2] = {nullptr, nullptr};
   int32_t graph_n[2] = {-1, -1};
@@ -327,6 +331,9 @@ hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hip
                                int64_t q0 = 0, int64_t q1 = -1);
 hipError_t launch_shard_claim(const m3d_icp* s, const int64_t* dmin, int32_t* claim, hipStream_t st);
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);
+// n grid-loop steps in one persistent launch (icp.hip; icp_persist_ok decides when it applies)
+bool icp_persist_ok(const m3d_icp* s);
+hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st);
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g);
 void grid_free(Grid* g);
 // prev/dprev/tgt32/nt_shard: seed each query with seed_key (nnkey.h); prev == nullptr: no seeds

@@ -78,6 +78,8 @@ int m3d_get_stats(m3d_ctx* ctx, int64_t* out8 /* [host] 8 values */);
 #define M3D_KERNEL_SCORE 1  /* RANSAC fp32 scoring screen       */
 #define M3D_KERNEL_KABSCH 2 /* RANSAC batched 3-point Kabsch    */
 #define M3D_KERNEL_TERMS 3  /* ICP fp64 estimation terms        */
+#define M3D_KERNEL_LOOP 4   /* ICP persistent grid loop: one launch for n steps (ABI 10) */
+#define M3D_KERNEL_COMM 5   /* RCCL all-reduces issued by the library, on their streams (ABI 10) */
 int m3d_profile_enable(m3d_ctx* ctx, int enable);
 /* Synchronises, returns Σ launch durations (ms) and launch count since the last read, resets. */
 int m3d_profile_read(m3d_ctx* ctx, int kernel, double* total_ms, int64_t* launches);
@@ -205,8 +207,16 @@ typedef struct {
   int32_t max_iteration;   /* 30 */
   int32_t estimation;      /* M3D_EST_* */
   int32_t nn_method;       /* M3D_NN_* */
-  int32_t reserved;        /* 0 */
+  int32_t flags;           /* M3D_ICP_* (ABI 10; 0 = defaults) */
 } m3d_icp_params;
+/* m3d_icp_params.flags: the grid loop's steps as ONE persistent launch (M3D_ICP_PERSIST) or as
+ * two launches per step (M3D_ICP_NO_PERSIST); neither: the library default.  The persistent loop
+ * applies to a single device, grid NN, ≤ 248 tiles of 512 sources; both give the same bits. */
+#define M3D_ICP_NO_PERSIST 1
+#define M3D_ICP_PERSIST 4
+/* m3d_icp_params.flags: the target-shard loop exchanges all keys in one MIN instead of two halves
+ * overlapped with the second half's NN (m3d_icp_shard_steps) */
+#define M3D_ICP_NO_SPLIT 2
 
 typedef struct {
   double T[16];

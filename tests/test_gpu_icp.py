@@ -188,6 +188,53 @@ def test_morton_copies_stay_bounded_per_cloud():
         check_nn(src, tgt, T, r, idx.cpu().numpy(), d2.cpu().numpy())
 
 
+@pytest.mark.parametrize("ns,est,crit", [(1, "plane", "fixed"), (511, "plane", "fixed"), (513, "point", "fixed"),
+                                         (20000, "plane", "open3d"), (100_000, "plane", "fixed"),
+                                         (100_000, "point", "open3d"), (126_000, "plane", "fixed"),
+                                         (140_000, "plane", "fixed")])
+def test_persistent_grid_loop_matches_two_launch_loop(ns, est, crit):
+    """The single-device grid loop as ONE persistent launch (icp.hip icp_grid_persist_kernel: every
+    workgroup reduces all tile partials and solves on its own copy of the state) computes the same
+    bits as the two-launch loop (grid scan + fused terms/solve per step): transform, fitness, rmse,
+    iterations, convergence and every correspondence — ragged tile counts, both estimations,
+    fixed iteration counts and Open3D's convergence test (an exit inside the launch), a second
+    launch continuing from the first one's state, and the one-shot m3d_icp_run path."""
+    src, tgt, nrm, _ = synth.icp_pair(max(ns, 2), 100_000, seed=23)
+    src = src[:ns]
+    e = _lib.EST_POINT_TO_PLANE if est == "plane" else _lib.EST_POINT_TO_POINT
+    s, t = Cloud(src), Cloud(tgt, nrm if e == _lib.EST_POINT_TO_PLANE else None)
+    kw = dict(estimation=e, max_iteration=40, nn="grid")
+    if crit == "fixed":
+        kw.update(relative_fitness=-1, relative_rmse=-1)
+    a = IcpLoop(s, t, 0.12, persist=True, **kw)
+    b = IcpLoop(s, t, 0.12, persist=False, **kw)
+
+    def state(lp):
+        r = lp.result()
+        return (r.transformation, r.fitness, r.inlier_rmse, r.iterations, r.converged,
+                lp.correspondences().cpu().numpy())
+
+    for lp in (a, b):
+        lp.reset(np.eye(4))
+        lp.steps(17)
+    x, y = state(a), state(b)
+    np.testing.assert_array_equal(x[0], y[0])
+    assert x[1:5] == y[1:5]
+    np.testing.assert_array_equal(x[5], y[5])
+    for lp in (a, b):  # continue from the state the first launch left
+        lp.steps(30)
+    x, y = state(a), state(b)
+    np.testing.assert_array_equal(x[0], y[0])
+    assert x[1:5] == y[1:5]
+    np.testing.assert_array_equal(x[5], y[5])
+    one = icp(s, t, 0.12, np.eye(4), persist=True, **kw)
+    two = icp(s, t, 0.12, np.eye(4), persist=False, **kw)
+    np.testing.assert_array_equal(one.transformation, two.transformation)
+    assert (one.fitness, one.inlier_rmse, one.iterations, one.converged) == \
+        (two.fitness, two.inlier_rmse, two.iterations, two.converged)
+    np.testing.assert_array_equal(one.correspondence_set, two.correspondence_set)
+
+
 def test_no_overlap_gives_identity_and_zero_fitness():
     src, _ = synth.surface_points(2000, seed=1)
     tgt, nrm = synth.surface_points(2000, seed=2)
@@ -224,7 +271,9 @@ def test_graph_replay_matches_enqueued_steps(nn):
 
     src, tgt, nrm, _ = synth.icp_pair(30000, seed=13)
     s, t = Cloud(src), Cloud(tgt, nrm)
-    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=80, nn=nn)
+    # persist=False: the grid loop's n steps would otherwise run as one persistent launch
+    # (test_persistent_grid_loop_matches_two_launch_loop), not as a captured graph
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=80, nn=nn, persist=False)
     a = IcpLoop(s, t, 0.12, **kw)
     b = IcpLoop(s, t, 0.12, **kw)
 
