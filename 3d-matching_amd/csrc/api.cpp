@@ -1,6 +1,8 @@
 // api.cpp — the C ABI of libm3d.so (include/m3d.h): contexts, packed objects, batching and
 // the host-side drivers of the device loops.  No numerical work happens here except the
 // MT19937 replay of the reference RNG (m3d_replay_triples) and O(1) bookkeeping.
+#include <cfloat>
+#include <chrono>
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -145,6 +147,54 @@ int device_mean3(m3d_ctx* ctx, const double* a, int64_t n, double out[3], hipStr
   return M3D_OK;
 }
 
+// A cloud's centre (mean, unless given), centred fp32 copy, rmax and grid bounds with ONE host
+// sync (ransac.hip cloud_pack_kernel); the same values as device_mean3 + center_pack + the grid
+// build's bounds pass, which took three syncs.  Temporaries from the context's arena.
+int cloud_pack(m3d_ctx* ctx, m3d_cloud* c, int64_t n, bool mean, hipStream_t st) {
+  c->rmax = 0.0;
+  c->has_bounds = false;
+  if (c->n_pad == 0) return M3D_OK;
+  const int sblocks = 128;
+  const int blocks = (int)std::min<int64_t>(1024, (c->n_pad + 255) / 256);
+  const size_t o_c = 0, o_sum = tmp_align(3 * sizeof(double)),
+               o_p7 = o_sum + tmp_align(sizeof(double) * 3 * sblocks);
+  const size_t bytes = o_p7 + tmp_align(sizeof(float) * 7 * blocks);
+  hipError_t e = ctx->tmp.reserve(bytes);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_OOM, "cloud scratch");
+  char* b = ctx->tmp.base;
+  double* cdev = reinterpret_cast<double*>(b + o_c);
+  double* sum_part = reinterpret_cast<double*>(b + o_sum);
+  float* p7 = reinterpret_cast<float*>(b + o_p7);
+  const bool dmean = mean && n > 0;
+  if (dmean) e = launch_sum3(c->xyz64, n, sum_part, sblocks, st);
+  if (e == hipSuccess)
+    e = launch_cloud_pack(c->xyz64, n, c->n_pad, dmean ? sum_part : nullptr, sblocks, cdev, c->center, c->xyz32,
+                          kFar, p7, blocks, st);
+  std::vector<float> h(7 * (size_t)blocks);
+  double hc[3] = {0.0, 0.0, 0.0};
+  if (e == hipSuccess && dmean) e = hipMemcpyAsync(hc, cdev, sizeof(hc), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), p7, sizeof(float) * h.size(), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  if (dmean)
+    for (int k = 0; k < 3; ++k) c->center[k] = hc[k];
+  float m = 0.0f;
+  for (int k = 0; k < 3; ++k) {
+    c->lo[k] = FLT_MAX;
+    c->hi[k] = -FLT_MAX;
+  }
+  for (int bl = 0; bl < blocks; ++bl) {
+    m = std::max(m, h[7 * bl]);
+    for (int k = 0; k < 3; ++k) {
+      c->lo[k] = std::min(c->lo[k], h[7 * bl + 1 + k]);
+      c->hi[k] = std::max(c->hi[k], h[7 * bl + 4 + k]);
+    }
+  }
+  c->rmax = (double)m * (1.0 + 1e-6);
+  c->has_bounds = n > 0;
+  return M3D_OK;
+}
+
 int center_pack(m3d_ctx* ctx, const double* a, int64_t n, int64_t n_pad, const double c[3],
                 float4* out, float pad, double* maxv, hipStream_t st) {
   *maxv = 0.0;
@@ -216,6 +266,7 @@ void m3d_destroy(m3d_ctx* ctx) {
   if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->one_ticket) hipFree(ctx->one_ticket);
   if (ctx->prep) hipFree(ctx->prep);
+  ctx->tmp.release();
   for (auto& v : ctx->ev)
     for (auto& pr : v) {
       hipEventDestroy(pr.first);
@@ -778,11 +829,8 @@ int m3d_cloud_create_framed(m3d_ctx* ctx, const double* xyz, const double* norma
   if (center != nullptr) {
     for (int k = 0; k < 3; ++k) c->center[k] = center[k];
     c->center_given = 1;
-    rc = M3D_OK;
-  } else {
-    rc = device_mean3(ctx, c->xyz64, n, c->center, st);
   }
-  if (!rc) rc = center_pack(ctx, c->xyz64, n, c->n_pad, c->center, c->xyz32, kFar, &c->rmax, st);
+  rc = cloud_pack(ctx, c, n, center == nullptr, st);
   if (!rc) {
     // fp16 screen operand scale: a power of two with |S·x|∞ ≤ 32 (icp.hip pack16_sorted)
     int ex = 0;
@@ -825,7 +873,13 @@ int ensure_grid(m3d_ctx* ctx, const m3d_cloud* c, double cell, hipStream_t st, c
       return M3D_OK;
     }
   Grid* g = new Grid();
-  hipError_t e = grid_build(c->xyz32, c->n, cell, st, g);
+  float lohi[6];
+  for (int k = 0; k < 3; ++k) {
+    lohi[k] = c->lo[k];
+    lohi[3 + k] = c->hi[k];
+  }
+  // asynchronous: the cloud's packing pass gave the bounds, the temporaries come from the arena
+  hipError_t e = grid_build(c->xyz32, c->n, cell, st, g, &ctx->tmp, c->has_bounds ? lohi : nullptr);
   if (e != hipSuccess) {
     grid_free(g);
     delete g;
@@ -847,7 +901,7 @@ int ensure_morton_source(m3d_ctx* ctx, const m3d_cloud* c, const Grid* sg, doubl
       *gout = m.second->grids.front();
       return M3D_OK;
     }
-  hipError_t e = grid_morton(const_cast<Grid*>(sg), nullptr);
+  hipError_t e = grid_morton(const_cast<Grid*>(sg), nullptr, &ctx->tmp);
   m3d_cloud* mc = new m3d_cloud();
   mc->ctx = ctx;
   Grid* g = new Grid();
@@ -926,6 +980,21 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   hipSetDevice(ctx->device);
   const Grid *tg = nullptr, *sg = nullptr;
   const m3d_cloud* src_m = nullptr;
+  // M3D_CREATE_PROF=1 (diagnostics): wall ms of each setup stage, synchronised in between
+  static const bool cprof = [] {
+    const char* e = getenv("M3D_CREATE_PROF");
+    return e && atoi(e) == 1;
+  }();
+  double tprev = 0.0;
+  std::string cstages;
+  auto stage = [&](const char* name) {
+    if (!cprof) return;
+    (void)hipDeviceSynchronize();
+    const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (tprev > 0.0) cstages += std::string(" ") + name + " " + std::to_string(t - tprev);
+    tprev = t;
+  };
+  stage("start");
   {
     // Grid NN: cell ≈ the search radius, a query visits 3 cells per axis.  Brute force: the
     // same grids only ORDER the points (targets and queries in cell order make the MFMA
@@ -938,29 +1007,45 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
     }();
     const double cell = max_dist * 1.001 / cell_div;
     int grc = ensure_grid(ctx, tgt, cell, nullptr, &tg);
+    stage("tgrid");
     if (!grc) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
+    stage("sgrid");
     // Grid NN on a dense target: a seeded query's box is ~1–2 cells per axis, so the candidates
     // it scans grow with the points per cell.  Shrink the target cell by div = ⌊√(m / 3.5)⌋
     // (m = points per occupied cell at cell ≈ r; any cell size gives the same keys, grid.hip):
     // measured (tools/grid_cell_sweep.sh) 1M × 1M (m ≈ 33) 206 → 128 µs per scan at div 3;
     // cfg1 (m ≈ 3.9) and the 1M × 125k shard (m ≈ 4.7) are fastest at div 1.
+    if (!grc && params->nn_method == M3D_NN_GRID && getenv("M3D_GRID_CELL_DIV") == nullptr) {
+      hipError_t e = grid_occupancy(const_cast<Grid*>(tg), &ctx->tmp, nullptr);  // one sync, once per grid
+      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("grid occupancy: ") + hipGetErrorString(e));
+    }
     if (!grc && params->nn_method == M3D_NN_GRID && getenv("M3D_GRID_CELL_DIV") == nullptr &&
         tg->n_occ > 0) {
       const double m = (double)tg->n_pts / (double)tg->n_occ;
       const int div = std::min(4, std::max(1, (int)std::floor(std::sqrt(m / 3.5))));
       if (div > 1) grc = ensure_grid(ctx, tgt, cell / div, nullptr, &tg);
     }
+    stage("tgrid_div");
     // the loop runs on the source in Morton slot order (its grid derived from sg)
     const m3d_cloud* ms = nullptr;
     if (!grc) grc = ensure_morton_source(ctx, src, sg, cell, &ms, &sg);
     if (!grc) src_m = ms;
+    stage("morton");
     if (!grc) {
       hipError_t e = ensure_target_rec(tgt, nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("target records: ") + hipGetErrorString(e));
     }
+    stage("rec");
     if (!grc && params->nn_method == M3D_NN_BRUTE && tg->mf16 == nullptr) {
       hipError_t e = build_mfma_tiles(tgt, const_cast<Grid*>(tg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("mfma tiles: ") + hipGetErrorString(e));
+    }
+    stage("tiles");
+    // the setup above ran asynchronously on the null stream: finish it before the loop object is
+    // used on the caller's streams
+    if (!grc) {
+      hipError_t e = hipStreamSynchronize(nullptr);
+      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("loop setup: ") + hipGetErrorString(e));
     }
     if (grc) return grc;
   }
@@ -983,12 +1068,33 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   }();
   s->qorder = cell_order ? sg->order : nullptr;
   s->sgrid = sg;
-  int rc = dev_alloc(ctx, &s->state, 1);
-  if (!rc) rc = dev_alloc(ctx, &s->keys, std::max<int64_t>(src->n, 1));
-  if (!rc) rc = dev_alloc(ctx, &s->near2, std::max<int64_t>(src->n, 1));
-  if (!rc) rc = dev_alloc(ctx, &s->dprev, std::max<int64_t>(src->n, 1));
-  if (!rc) rc = dev_alloc(ctx, &s->ld64, std::max<int64_t>(src->n, 1));
-  if (!rc) rc = dev_alloc(ctx, &s->lidx, std::max<int64_t>(src->n, 1));
+  // the loop's arrays in ONE allocation (one hipMalloc instead of nine)
+  int rc = M3D_OK;
+  {
+    const size_t n1 = (size_t)std::max<int64_t>(src->n, 1);
+    const size_t sz[8] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
+                          sizeof(double) * (size_t)(s->nblocks * kTermSlots + kTermSlots)};
+    size_t off[8], tot = 0;
+    for (int k = 0; k < 8; ++k) {
+      off[k] = tot;
+      tot += tmp_align(sz[k]);
+    }
+    if (hipMalloc(&s->block, tot) != hipSuccess) {
+      s->block = nullptr;
+      rc = m3d_fail(ctx, M3D_ERR_OOM, "hipMalloc failed (ICP loop arrays)");
+    } else {
+      char* b = static_cast<char*>(s->block);
+      s->state = reinterpret_cast<IcpState*>(b + off[0]);
+      s->keys = reinterpret_cast<int64_t*>(b + off[1]);
+      s->near2 = reinterpret_cast<uint32_t*>(b + off[2]);
+      s->dprev = reinterpret_cast<int64_t*>(b + off[3]);
+      s->ld64 = reinterpret_cast<int64_t*>(b + off[4]);
+      s->lidx = reinterpret_cast<int32_t*>(b + off[5]);
+      s->corr = reinterpret_cast<int32_t*>(b + off[6]);
+      s->partials = reinterpret_cast<double*>(b + off[7]);
+      s->sums = s->partials + s->nblocks * kTermSlots;
+    }
+  }
   // seed records (M3D_GRID_SEEDREC=1): measured slower while the clouds keep the caller's point
   // order — the terms pass's writes to Morton positions scatter (cfg1 grid iteration 38.8 →
   // 41.5 µs, 1M × 125k 137 → 152 µs)
@@ -998,9 +1104,8 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   }();
   if (!rc && seedrec && params->nn_method == M3D_NN_GRID && sg->minv != nullptr)
     rc = dev_alloc(ctx, &s->sq, std::max<int64_t>(src->n, 1));
-  if (!rc) rc = dev_alloc(ctx, &s->corr, std::max<int64_t>(src->n, 1));
-  if (!rc) rc = dev_alloc(ctx, &s->partials, s->nblocks * kTermSlots);
-  if (!rc) rc = dev_alloc(ctx, &s->sums, kTermSlots);
+  stage("loop_alloc");
+  if (cprof) fprintf(stderr, "[m3d create] ms:%s\n", cstages.c_str());
   if (rc) {
     m3d_icp_destroy(s);
     return rc;
@@ -1015,19 +1120,11 @@ void m3d_icp_destroy(m3d_icp* s) {
     if (g != nullptr) hipGraphExecDestroy(g);
   if (s->cap_stream != nullptr) hipStreamDestroy(s->cap_stream);
   if (s->src != nullptr) s->src->refs -= 1;
-  hipFree(s->state);
-  hipFree(s->keys);
-  hipFree(s->near2);
-  hipFree(s->dprev);
-  hipFree(s->ld64);
-  hipFree(s->lidx);
+  hipFree(s->block);  // state, keys, near2, dprev, ld64, lidx, corr, partials, sums
   hipFree(s->sq);
   hipFree(s->xdk);
   hipFree(s->xcl);
   hipFree(s->xsums);
-  hipFree(s->corr);
-  hipFree(s->partials);
-  hipFree(s->sums);
   hipFree(s->pp);
   hipFree(s->pcounter);
   delete s;
@@ -1342,6 +1439,8 @@ int search_grids(m3d_ctx* ctx, const m3d_cloud* c, double radius, int k, hipStre
                  const Grid** g, const Grid** gf, double* hf) {
   int rc = ensure_grid(ctx, c, radius, st, g);
   if (rc) return rc;
+  hipError_t e = grid_occupancy(const_cast<Grid*>(*g), &ctx->tmp, st);  // hybrid_fine_radius reads it
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, std::string("grid occupancy: ") + hipGetErrorString(e));
   *gf = nullptr;
   *hf = hybrid_fine_radius(*g, radius, k);
   if (*hf > 0.0) rc = ensure_grid(ctx, c, *hf, st, gf);

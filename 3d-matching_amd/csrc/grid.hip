@@ -427,29 +427,57 @@ static hipError_t grid_fail(hipError_t e, void* a, void* b, void* c, void* d, vo
   return e;
 }
 
-hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g) {
+// occupied cells from the built grid itself: sorted positions whose cell differs from the
+// previous point's (the cell of a point recomputed from its coordinates as cell_id_kernel does)
+__global__ __launch_bounds__(kGridBlock) void count_occupied_pts_kernel(const float4* __restrict__ pts,
+                                                                        int64_t n, GridDev g,
+                                                                        unsigned long long* __restrict__ occ) {
+  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  auto cell_of = [&](int64_t j) {
+    const float4 v = pts[j];
+    const int cx = grid_coord(v.x, g.o[0], g.inv_h, g.n[0]);
+    const int cy = grid_coord(v.y, g.o[1], g.inv_h, g.n[1]);
+    const int cz = grid_coord(v.z, g.o[2], g.inv_h, g.n[2]);
+    return ((int64_t)cz * g.n[1] + cy) * g.n[0] + cx;
+  };
+  const bool first = k < n && (k == 0 || cell_of(k) != cell_of(k - 1));
+  const unsigned long long b = __ballot(first);
+  if ((threadIdx.x & (kWave - 1)) == 0 && b != 0) atomicAdd(occ, (unsigned long long)__popcll(b));
+}
+
+hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g, TmpArena* ta,
+                      const float* lohi) {
   g->n_pts = n;
   g->cell = cell;
+  g->n_occ = 0;
+  g->occ_known = n == 0;
   GridDev& d = g->dev;
   d.ncells = 0;
   if (n == 0) return hipSuccess;
-  // per-axis bounds
-  const int nb = (int)std::min<int64_t>(1024, (n + kGridBlock - 1) / kGridBlock);
-  float* part = nullptr;
-  hipError_t e = hipMalloc(&part, sizeof(float) * 6 * nb);
-  if (e != hipSuccess) return e;
-  minmax3_kernel<<<nb, kGridBlock, 0, st>>>(xyz32, n, part);
-  std::vector<float> hp(6 * (size_t)nb);
-  e = hipMemcpyAsync(hp.data(), part, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  hipFree(part);
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
   float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (int b = 0; b < nb; ++b)
+  if (lohi != nullptr) {  // the cloud's packing pass already reduced them: no pass, no sync
     for (int k = 0; k < 3; ++k) {
-      lo[k] = std::min(lo[k], hp[6 * b + k]);
-      hi[k] = std::max(hi[k], hp[6 * b + 3 + k]);
+      lo[k] = lohi[k];
+      hi[k] = lohi[3 + k];
     }
+  } else {  // per-axis bounds: one pass + one sync
+    const int nb = (int)std::min<int64_t>(1024, (n + kGridBlock - 1) / kGridBlock);
+    float* part = nullptr;
+    e = hipMalloc(&part, sizeof(float) * 6 * nb);
+    if (e != hipSuccess) return e;
+    minmax3_kernel<<<nb, kGridBlock, 0, st>>>(xyz32, n, part);
+    std::vector<float> hp(6 * (size_t)nb);
+    e = hipMemcpyAsync(hp.data(), part, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipFree(part);
+    if (e != hipSuccess) return e;
+    for (int b = 0; b < nb; ++b)
+      for (int k = 0; k < 3; ++k) {
+        lo[k] = std::min(lo[k], hp[6 * b + k]);
+        hi[k] = std::max(hi[k], hp[6 * b + 3 + k]);
+      }
+  }
   // cell size: requested, grown until the dense grid has at most kMaxCells cells
   double h = cell > 0.0 && std::isfinite(cell) ? cell : 1.0;
   int64_t nn[3], total = 0;
@@ -471,57 +499,82 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   d.inv_h = (float)(1.0 / h);
   d.ncells = total;
   g->cell = h;
-  // (cell, index) pairs → stable radix sort
+  // (cell, index) pairs → stable radix sort; the sorted indices land in g->order
   uint32_t *kin = nullptr, *kout = nullptr;
-  int32_t *vin = nullptr, *vout = nullptr;
+  int32_t* vin = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) < total) ++bits;
-  if ((e = hipMalloc(&kin, sizeof(uint32_t) * n)) != hipSuccess ||
-      (e = hipMalloc(&kout, sizeof(uint32_t) * n)) != hipSuccess ||
-      (e = hipMalloc(&vin, sizeof(int32_t) * n)) != hipSuccess ||
-      (e = hipMalloc(&vout, sizeof(int32_t) * n)) != hipSuccess)
-    return grid_fail(e, kin, kout, vin, vout, tmp);
-  const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
-  cell_id_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, n, d, kin, vin);
-  if ((e = hipGetLastError()) != hipSuccess) return grid_fail(e, kin, kout, vin, vout, tmp);
-  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, bits, st);
-  if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 1));
-  if (e == hipSuccess)
-    e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, bits, st);
-  if (e != hipSuccess) return grid_fail(e, kin, kout, vin, vout, tmp);
   hipFree(g->start);
   hipFree(g->pts);
   hipFree(g->order);
   g->start = nullptr;
   g->pts = nullptr;
   g->order = nullptr;
-  if ((e = hipMalloc(&g->start, sizeof(int32_t) * (total + 1))) != hipSuccess ||
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, g->order, (int)n, 0, bits, st);
+  if (e != hipSuccess) return e;
+  tmp_bytes = std::max<size_t>(tmp_bytes, 1);
+  const size_t a4 = tmp_align(sizeof(uint32_t) * (size_t)n);
+  if (ta != nullptr) {
+    if ((e = ta->reserve(3 * a4 + tmp_align(tmp_bytes))) != hipSuccess) return e;
+    kin = reinterpret_cast<uint32_t*>(ta->base);
+    kout = reinterpret_cast<uint32_t*>(ta->base + a4);
+    vin = reinterpret_cast<int32_t*>(ta->base + 2 * a4);
+    tmp = ta->base + 3 * a4;
+  } else if ((e = hipMalloc(&kin, a4)) != hipSuccess || (e = hipMalloc(&kout, a4)) != hipSuccess ||
+             (e = hipMalloc(&vin, a4)) != hipSuccess || (e = hipMalloc(&tmp, tmp_bytes)) != hipSuccess) {
+    return grid_fail(e, kin, kout, vin, nullptr, tmp);
+  }
+  auto done = [&](hipError_t r) { return ta != nullptr ? r : grid_fail(r, kin, kout, vin, nullptr, tmp); };
+  if ((e = hipMalloc(&g->order, a4)) != hipSuccess ||
+      (e = hipMalloc(&g->start, sizeof(int32_t) * (total + 1))) != hipSuccess ||
       (e = hipMalloc(&g->pts, sizeof(float4) * n)) != hipSuccess)
-    return grid_fail(e, kin, kout, vin, vout, tmp);
+    return done(e);
+  const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
+  cell_id_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, n, d, kin, vin);
+  if ((e = hipGetLastError()) != hipSuccess) return done(e);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, g->order, (int)n, 0, bits, st);
+  if (e != hipSuccess) return done(e);
   cell_start_kernel<<<(unsigned)((total + 1 + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
       kout, n, total, g->start);
-  grid_gather_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, vout, n, g->pts);
-  // occupied-cell count (m3d_icp_create sizes the grid-NN cell from the points per occupied cell);
-  // the radix-sort temp storage (≥ 8 B) holds the counter
-  unsigned long long occ = 0;
+  grid_gather_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, g->order, n, g->pts);
   e = hipGetLastError();
-  if (e == hipSuccess && tmp_bytes >= sizeof(unsigned long long))
-    e = hipMemsetAsync(tmp, 0, sizeof(unsigned long long), st);
-  if (e == hipSuccess && tmp_bytes >= sizeof(unsigned long long)) {
-    count_occupied_kernel<<<blocks, kGridBlock, 0, st>>>(kout, n, reinterpret_cast<unsigned long long*>(tmp));
-    e = hipGetLastError();
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(&occ, tmp, sizeof(occ), hipMemcpyDeviceToHost, st);
-  }
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  g->n_occ = (int64_t)occ;
-  g->order = vout;  // sorted point indices: the cloud's cell order
-  vout = nullptr;
   d.start = g->start;
   d.pts = g->pts;
-  return grid_fail(e, kin, kout, vin, vout, tmp);
+  // without an arena the temporaries are freed here (hipFree waits for the device)
+  return done(e);
+}
+
+hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st) {
+  if (g->occ_known) return hipSuccess;
+  if (g->n_pts == 0 || g->dev.ncells == 0) {
+    g->n_occ = 0;
+    g->occ_known = true;
+    return hipSuccess;
+  }
+  unsigned long long* cnt = nullptr;
+  hipError_t e = hipSuccess;
+  if (ta != nullptr) {
+    if ((e = ta->reserve(256)) != hipSuccess) return e;
+    cnt = reinterpret_cast<unsigned long long*>(ta->base);
+  } else if ((e = hipMalloc(&cnt, sizeof(unsigned long long))) != hipSuccess) {
+    return e;
+  }
+  unsigned long long occ = 0;
+  e = hipMemsetAsync(cnt, 0, sizeof(occ), st);
+  if (e == hipSuccess) {
+    count_occupied_pts_kernel<<<(unsigned)((g->n_pts + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
+        g->pts, g->n_pts, g->dev, cnt);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(&occ, cnt, sizeof(occ), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (ta == nullptr) hipFree(cnt);
+  if (e != hipSuccess) return e;
+  g->n_occ = (int64_t)occ;
+  g->occ_known = true;
+  return hipSuccess;
 }
 
 void grid_free(Grid* g) {
@@ -543,7 +596,7 @@ void grid_free(Grid* g) {
   g->mf_npad = 0;
 }
 
-hipError_t grid_morton(Grid* g, hipStream_t st) {
+hipError_t grid_morton(Grid* g, hipStream_t st, TmpArena* ta) {
   if (g->mpts != nullptr || g->n_pts == 0) return hipSuccess;
   const int64_t n = g->n_pts;
   int sh[3];
@@ -555,32 +608,39 @@ hipError_t grid_morton(Grid* g, hipStream_t st) {
   int32_t *vin = nullptr, *vout = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
-  hipError_t e;
-  if ((e = hipMalloc(&kin, sizeof(uint32_t) * n)) != hipSuccess ||
-      (e = hipMalloc(&kout, sizeof(uint32_t) * n)) != hipSuccess ||
-      (e = hipMalloc(&vin, sizeof(int32_t) * n)) != hipSuccess ||
-      (e = hipMalloc(&vout, sizeof(int32_t) * n)) != hipSuccess)
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
+  if (e != hipSuccess) return e;
+  tmp_bytes = std::max<size_t>(tmp_bytes, 1);
+  const size_t a4 = tmp_align(sizeof(uint32_t) * (size_t)n);
+  if (ta != nullptr) {
+    if ((e = ta->reserve(4 * a4 + tmp_align(tmp_bytes))) != hipSuccess) return e;
+    kin = reinterpret_cast<uint32_t*>(ta->base);
+    kout = reinterpret_cast<uint32_t*>(ta->base + a4);
+    vin = reinterpret_cast<int32_t*>(ta->base + 2 * a4);
+    vout = reinterpret_cast<int32_t*>(ta->base + 3 * a4);
+    tmp = ta->base + 4 * a4;
+  } else if ((e = hipMalloc(&kin, a4)) != hipSuccess || (e = hipMalloc(&kout, a4)) != hipSuccess ||
+             (e = hipMalloc(&vin, a4)) != hipSuccess || (e = hipMalloc(&vout, a4)) != hipSuccess ||
+             (e = hipMalloc(&tmp, tmp_bytes)) != hipSuccess) {
     return grid_fail(e, kin, kout, vin, vout, tmp);
+  }
   const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
   morton_key_kernel<<<blocks, kGridBlock, 0, st>>>(g->pts, n, g->dev, sh[0], sh[1], sh[2], kin, vin);
-  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
-  if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 1));
-  if (e == hipSuccess)
-    e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
   if (e == hipSuccess) e = hipMalloc(&g->mpts, sizeof(float4) * n);
   if (e == hipSuccess) e = hipMalloc(&g->minv, sizeof(int32_t) * n);
   if (e == hipSuccess) {
     morton_gather_kernel<<<blocks, kGridBlock, 0, st>>>(g->pts, vout, n, g->mpts, g->minv);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) {
+    (void)hipStreamSynchronize(st);  // nothing may still write the arrays freed here
     hipFree(g->mpts);
     hipFree(g->minv);
     g->mpts = nullptr;
     g->minv = nullptr;
   }
-  return grid_fail(e, kin, kout, vin, vout, tmp);
+  return ta != nullptr ? e : grid_fail(e, kin, kout, vin, vout, tmp);
 }
 
 // ------------------------------------------------------------------------------- Morton copy
@@ -629,6 +689,11 @@ hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Gri
   out->n_pad = src->n_pad;
   for (int k = 0; k < 3; ++k) out->center[k] = src->center[k];
   out->rmax = src->rmax;
+  for (int k = 0; k < 3; ++k) {
+    out->lo[k] = src->lo[k];
+    out->hi[k] = src->hi[k];
+  }
+  out->has_bounds = src->has_bounds;
   out->s16 = src->s16;
   out->center_given = src->center_given;
   gout->dev = sg->dev;
@@ -668,7 +733,8 @@ hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Gri
     return e;
   gout->dev.start = gout->start;
   gout->dev.pts = gout->pts;
-  return hipStreamSynchronize(st);
+  gout->occ_known = sg->occ_known;
+  return hipSuccess;
 }
 
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, const Grid* g,

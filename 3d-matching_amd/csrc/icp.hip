@@ -25,6 +25,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <vector>
 #include <stdlib.h>
 
 #include "lds_dma.h"
@@ -437,9 +438,7 @@ hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st) {
   g->mf_npad = n_pad;
   pack16_sorted_kernel<<<(unsigned)((n_pad + 255) / 256), 256, 0, st>>>(
       g->pts, c->xyz32, n, n_pad, (float)c->s16, g->mf16, g->mf32);
-  e = hipGetLastError();
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  return e;
+  return hipGetLastError();  // asynchronous (stream order); m3d_icp_create synchronises once
 }
 
 // Self-seeding (single-device fused loop, m3d_icp_step): the fused tail of the previous
@@ -1295,24 +1294,30 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
 
 // ------------------------------------------------------------------------------- persistent grid loop
 // Round 4: n iterations of the single-device grid-NN ICP loop in ONE launch (m3d_icp_steps; the
-// two-launch loop above stays; m3d_icp_params.flags / M3D_ICP_PERSIST choose).  One workgroup per 512-source tile (the
-// terms pass's block: kTermsBlock threads × 2 sources), all resident (api.cpp checks the grid
-// against the occupancy before choosing this path).  Per iteration a workgroup
-//   (1) scans its 512 queries (kL lanes each, nnkey.h grid_scan) seeded from the previous winner,
-//       whose centred fp32 point it kept in LDS (no corr → target gather);
+// two-launch loop above stays; m3d_icp_params.flags / M3D_ICP_PERSIST choose).  One workgroup of
+// 512 threads per 512-source tile (the terms pass's block: kTermsBlock threads × 2 sources), all
+// resident (api.cpp checks the grid against the occupancy before choosing this path).  Per
+// iteration a workgroup
+//   (1) scans its 512 queries, one lane each, seeded from the previous winner, whose centred fp32
+//       point it keeps in LDS.  The targets of a query's cell box are cached in LDS (up to kPCand
+//       points per query, with the box they came from): when the next iteration's box is the same
+//       box — the usual case once the transform has settled — the query re-evaluates exactly the
+//       same target set from LDS without a global load (same set ⇒ same key and runner-up: the
+//       scan state is order-free, nnkey.h near_push);
 //   (2) decides the fp64 winners and adds the terms of its sources exactly as terms_block does
 //       (same thread ↔ source map, same terms_add order, same wave/LDS reduction), writing corr;
 //   (3) publishes its block partial write-through (sc1) into one of two buffers, drains it, and
 //       arrives on a launch-wide counter (agent-scope add); polls the counter (sc1 loads) until
 //       every tile has arrived — MI355X_MICROARCH.md hand-off table, first row;
-//   (4) reduces ALL tile partials in reduce_kernel's fixed group order (sc1 loads) and runs
+//   (4) reduces ALL tile partials in terms_solve_kernel's fixed group order (sc1 loads) and runs
 //       solve_state on its own LDS copy of the loop state.
 // Every workgroup therefore holds bit-identical sums and state (nobody broadcasts a transform),
 // the same bits as the fused two-launch loop (test_gpu_icp persistent cases).  Partials are
 // double-buffered: a workgroup writes iteration k + 2's partial only after every workgroup has
 // arrived at iteration k + 1, i.e. finished reading iteration k's.  Every spin is bounded: a
 // workgroup that waits too long (a tile not resident) flags `fault` and leaves the loop.
-constexpr int kPTile = 2 * kTermsBlock;  // sources per tile (= per workgroup)
+constexpr int kPTile = 2 * kTermsBlock;  // sources per tile (= per workgroup, one lane per query)
+constexpr int kPCand = 15;               // cached targets per query (LDS: 15 × 16 B × 512 = 120 KB)
 constexpr uint32_t kPersistMaxSpin = 1u << 22;
 
 struct PersistArgs {
@@ -1332,19 +1337,21 @@ struct PersistArgs {
   int32_t n;            // iterations (m3d_icp_step calls) to run
   int est;
   double c[3];
-  unsigned long long* prof;  // M3D_PERSIST_PROF=1: per-phase wall-clock ticks of workgroup 0 (else null)
+  unsigned long long* prof;  // M3D_PERSIST_PROF=1: per-phase wall-clock ticks (else null)
 };
 
-template <int kL, int kR, int kB>
-__global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistArgs a, IcpState* gs,
-                                                                       SolveParams sp) {
-  constexpr int kT = kPTile * kL;
+template <int kR, int kB, bool kProf>
+__global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a, IcpState* gs, SolveParams sp) {
+  constexpr int kT = kPTile;
   __shared__ IcpState S;
   __shared__ uint64_t k1s[kPTile];
   __shared__ float n2s[kPTile];
   __shared__ float4 seedp[kPTile];  // previous winner's centred fp32 point, w = its index (−1 none)
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
   __shared__ double gsum[kReduceGroups][kTermSlots];
+  __shared__ int32_t cbox[6][kPTile];       // cached cell box (x0, x1, y0, y1, z0, z1) per query
+  __shared__ int32_t cnum[kPTile];          // its target count (−1: no cache)
+  __shared__ float4 cand[kPCand][kPTile];   // its targets (x, y, z, index bits)
   __shared__ int bad;
   const int tid = threadIdx.x;
   const int64_t ntiles = gridDim.x;
@@ -1352,11 +1359,12 @@ __global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistAr
   for (int k = tid; k < (int)(sizeof(IcpState) / 4); k += kT)
     reinterpret_cast<uint32_t*>(&S)[k] = reinterpret_cast<const uint32_t*>(gs)[k];
   if (tid == 0) bad = 0;
-  // scan lanes: query q = tid / kL of the tile; its centred point stays in registers
-  const int q = tid / kL, sub = tid % kL;
+  cnum[tid] = -1;
+  // scan lane: query q = tid of the tile; its centred point stays in registers
+  const int q = tid;
   const int64_t t = base + q;
   const float4 p = t < a.ns ? a.src32[t] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (sub == 0) {  // seeds of the first iteration: the loop's correspondences on entry (prev)
+  {  // seeds of the first iteration: the loop's correspondences on entry
     const int32_t j = t < a.ns ? a.corr[t] : -1;
     float4 v = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
     if (j >= 0) {
@@ -1376,17 +1384,18 @@ __global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistAr
     for (int k = 0; k < 3; ++k) p64[u][k] = v ? a.src64[3 * i + k] : 0.0;
   }
   const int lane = tid & (kWave - 1), wave = tid / kWave;
-  // phase timer (diagnostics only): workgroup 0, thread 0, wall clock after each barrier
+  // phase timer (diagnostics only): thread 0, wall clock after each barrier
   unsigned long long tph[7] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;
-  const bool prof = a.prof != nullptr && blockIdx.x == 0 && tid == 0;
+  const bool prof = kProf && tid == 0;
   if (prof) tlast = wall_clock64();
   auto mark = [&](int k) {
-    if (prof) {
-      const unsigned long long t = wall_clock64();
-      tph[k] += t - tlast;
-      tlast = t;
+    if (kProf && prof) {
+      const unsigned long long tn_ = wall_clock64();
+      tph[k] += tn_ - tlast;
+      tlast = tn_;
     }
   };
+  unsigned hits = 0;
   for (int it = 0; it < a.n; ++it) {
     __syncthreads();  // S, seedp of this iteration
     mark(0);
@@ -1407,16 +1416,85 @@ __global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistAr
           if (d2 <= r2_hi) k1 = make_key(d2, (uint32_t)sj);
         }
         k1d = key_real_d2(k1);
-        if (a.g.ncells > 0) {
+        const GridDev& g = a.g;
+        if (g.ncells > 0) {
+          // the cell box of q ± R (nnkey.h grid_scan; grid.hip header lemma)
           const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
-          grid_scan<kL, kR, kB>(a.g, qx, qy, qz, R, r2_hi, 0, sub, k1, k1d, n2);
+          const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
+          const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
+          const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
+          const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
+          const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
+          const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
+          const int m0 = cnum[q];
+          const bool hit = m0 >= 0 && cbox[0][q] == x0 && cbox[1][q] == x1 && cbox[2][q] == y0 &&
+                           cbox[3][q] == y1 && cbox[4][q] == z0 && cbox[5][q] == z1;
+          if (hit) {  // the same box: the same targets, from LDS
+            if (kProf) ++hits;
+            for (int c = 0; c < m0; ++c) {
+              const float4 v = cand[c][q];
+              const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
+              if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)__float_as_int(v.w)), d2);
+            }
+          } else {  // grid_scan's row batches from global memory, caching the box's targets
+            const int ny = y1 - y0 + 1;
+            const int rows = ny * (z1 - z0 + 1);
+            int m = 0;  // targets of the box seen so far (> kPCand: no cache)
+            for (int r0 = 0; r0 < rows; r0 += kR) {
+              int32_t ra[kR], rb[kR], ro[kR];
+              int32_t len = 0;
+#pragma unroll
+              for (int k = 0; k < kR; ++k) {
+                const int r = r0 + k;
+                ra[k] = rb[k] = 0;
+                if (r < rows) {
+                  const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
+                  ra[k] = g.start[row + x0];
+                  rb[k] = g.start[row + x1 + 1];
+                }
+              }
+#pragma unroll
+              for (int k = 0; k < kR; ++k) {
+                ro[k] = m;
+                m += rb[k] - ra[k];
+                len = max(len, rb[k] - ra[k]);
+              }
+              for (int32_t b0 = 0; b0 < len; b0 += kB) {
+                float4 v[kR][kB];
+#pragma unroll
+                for (int k = 0; k < kR; ++k)
+#pragma unroll
+                  for (int mm = 0; mm < kB; ++mm) {
+                    const int32_t j = ra[k] + b0 + mm;
+                    if (j < rb[k]) v[k][mm] = g.pts[j];
+                  }
+#pragma unroll
+                for (int k = 0; k < kR; ++k)
+#pragma unroll
+                  for (int mm = 0; mm < kB; ++mm) {
+                    const int32_t j = ra[k] + b0 + mm;
+                    if (j < rb[k]) {
+                      const float d2 = d2f(qx, qy, qz, v[k][mm].x, v[k][mm].y, v[k][mm].z);
+                      if (d2 <= r2_hi)
+                        near_push(k1, k1d, n2, make_key(d2, (uint32_t)__float_as_int(v[k][mm].w)), d2);
+                      const int slot = ro[k] + b0 + mm;
+                      if (slot < kPCand) cand[slot][q] = v[k][mm];
+                    }
+                  }
+              }
+            }
+            cnum[q] = m <= kPCand ? m : -1;
+            cbox[0][q] = x0;
+            cbox[1][q] = x1;
+            cbox[2][q] = y0;
+            cbox[3][q] = y1;
+            cbox[4][q] = z0;
+            cbox[5][q] = z1;
+          }
         }
       }
-      grid_merge_lanes<kL>(k1, k1d, n2);
-      if (sub == 0) {
-        k1s[q] = (t < a.ns && k1 != key0) ? k1 : (uint64_t)kKeyNone;
-        n2s[q] = t < a.ns ? n2 : kInf;
-      }
+      k1s[q] = (t < a.ns && k1 != key0) ? k1 : (uint64_t)kKeyNone;
+      n2s[q] = t < a.ns ? n2 : kInf;
     }
     __syncthreads();
     mark(1);
@@ -1461,6 +1539,7 @@ __global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistAr
           }
         }
       }
+      // the winners' records (point, normal) and fp32 points (the next seeds)
       double tq[kP][3], tn[kP][3];
       float4 t32[kP];
 #pragma unroll
@@ -1483,7 +1562,7 @@ __global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistAr
             tn[u][k] = a.est == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
           }
         }
-        t32[u] = a.tgt32[l];  // the next iteration's seed point
+        t32[u] = a.tgt32[l];
       }
 #pragma unroll
       for (int u = 0; u < kP; ++u) {
@@ -1539,8 +1618,8 @@ __global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistAr
     __syncthreads();
     mark(4);
     if (bad) break;
-    // (4) every tile's partial, reduce_kernel's order: group g = tiles g, g + 32, …; then the 32
-    // group sums in group order
+    // (4) every tile's partial in terms_solve_kernel's order: group g = tiles g, g + 32, … (each
+    // out-of-range tile adds +0.0 as there), then the 32 group sums in group order
     {
       const int slot = tid & (kTermSlots - 1);
       for (int g = tid / kTermSlots; g < kReduceGroups; g += kT / kTermSlots) {
@@ -1554,7 +1633,7 @@ __global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistAr
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                              : 0.0;
         }
-        double gv = 0.0;  // out-of-range tiles add +0.0, as terms_solve_kernel's last block does
+        double gv = 0.0;
 #pragma unroll
         for (int r = 0; r < kMaxPer; ++r) gv += tv[r];
         gsum[g][slot] = gv;
@@ -1574,8 +1653,16 @@ __global__ __launch_bounds__(kPTile * kL) void icp_grid_persist_kernel(PersistAr
       solve_state(gsum[0], &S, sp, in);
     }
   }
-  if (prof)
-    for (int k = 0; k < 7; ++k) atomicAdd(a.prof + k, tph[k]);
+  if (kProf && prof) {  // [0..6] workgroup 0's phases; [8 + 2b], [9 + 2b]: workgroup b's scan, terms; [7] cache hits
+    if (blockIdx.x == 0)
+      for (int k = 0; k < 7; ++k) atomicAdd(a.prof + k, tph[k]);
+    a.prof[8 + 2 * blockIdx.x] = tph[1];
+    a.prof[9 + 2 * blockIdx.x] = tph[2];
+  }
+  if (kProf) {
+    const unsigned long long hb = __reduce_add_sync(~0ull, hits);
+    if (lane == 0) atomicAdd(a.prof + 7, hb);
+  }
   __syncthreads();
   if (blockIdx.x == 0)
     for (int k = tid; k < (int)(sizeof(IcpState) / 4); k += kT)
@@ -1847,8 +1934,7 @@ hipError_t ensure_target_rec(const m3d_cloud* c, hipStream_t st) {
   hipError_t e = hipMalloc(&rec, sizeof(double) * 8 * c->n);
   if (e != hipSuccess) return e;
   pack_rec_kernel<<<(unsigned)((c->n + 255) / 256), 256, 0, st>>>(c->xyz64, c->nrm64, c->n, rec);
-  e = hipGetLastError();
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  e = hipGetLastError();  // asynchronous (stream order); m3d_icp_create synchronises once
   if (e != hipSuccess) {
     hipFree(rec);
     return e;
@@ -1962,18 +2048,8 @@ hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t
 // the whole grid is resident.  Flags M3D_ICP_PERSIST / M3D_ICP_NO_PERSIST, else the env default
 // M3D_ICP_PERSIST = 1 | 0 (off when unset); M3D_PERSIST_LANES = 1 | 2
 // (lanes per query, 512 or 1024 threads per workgroup).
-static int persist_lanes() {
-  static const int v = [] {
-    const char* e = getenv("M3D_PERSIST_LANES");
-    const int k = e ? atoi(e) : 2;
-    return (k == 1 || k == 2) ? k : 2;
-  }();
-  return v;
-}
-
-template <int kL>
 static const void* persist_fn() {
-  return reinterpret_cast<const void*>(&icp_grid_persist_kernel<kL, 2, 2>);
+  return reinterpret_cast<const void*>(&icp_grid_persist_kernel<2, 2, false>);
 }
 
 bool icp_persist_ok(const m3d_icp* s) {
@@ -1990,11 +2066,9 @@ bool icp_persist_ok(const m3d_icp* s) {
   static int cap = -1;  // resident workgroups of the kernel on this device (per process, device 0 form)
   if (cap < 0) {
     int dev = 0, cus = 0, per = 0;
-    const int L = persist_lanes();
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, L == 1 ? persist_fn<1>() : persist_fn<2>(),
-                                                     kPTile * L, 0) != hipSuccess) {
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, persist_fn(), kPTile, 0) != hipSuccess) {
       (void)hipGetLastError();
       cap = 0;
     } else {
@@ -2037,27 +2111,44 @@ hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st) {
   static unsigned long long* prof = [] {  // M3D_PERSIST_PROF=1: phase ticks, printed per launch
     const char* e = getenv("M3D_PERSIST_PROF");
     unsigned long long* p = nullptr;
-    if (e && atoi(e) == 1 && hipMalloc(&p, 8 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
+    if (e && atoi(e) == 1 && hipMalloc(&p, (8 + 2 * 256) * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
     return p;
   }();
   a.prof = prof;
-  if (prof != nullptr) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), st);
+  if (prof != nullptr) (void)hipMemsetAsync(prof, 0, (8 + 2 * 256) * sizeof(unsigned long long), st);
   const SolveParams sp = solve_params(s);
-  if (persist_lanes() == 1)
-    icp_grid_persist_kernel<1, 2, 2><<<(unsigned)ntiles, kPTile, 0, st>>>(a, s->state, sp);
+  if (prof != nullptr)
+    icp_grid_persist_kernel<2, 2, true><<<(unsigned)ntiles, kPTile, 0, st>>>(a, s->state, sp);
   else
-    icp_grid_persist_kernel<2, 2, 2><<<(unsigned)ntiles, kPTile * 2, 0, st>>>(a, s->state, sp);
+    icp_grid_persist_kernel<2, 2, false><<<(unsigned)ntiles, kPTile, 0, st>>>(a, s->state, sp);
   if (prof != nullptr) {
-    unsigned long long h[8];
+    std::vector<unsigned long long> h(8 + 2 * 256);
     int khz = 0, dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-    if (hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
+    if (hipMemcpyAsync(h.data(), prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, st) == hipSuccess &&
         hipStreamSynchronize(st) == hipSuccess && khz > 0) {
       const double us = 1e3 / khz;
       fprintf(stderr, "[m3d persist] %lld tiles, n=%d, us per iteration: top %.2f scan %.2f terms %.2f "
-              "publish %.2f wait %.2f reduce %.2f (solve in 'top')\n", (long long)ntiles, n,
-              h[0] * us / n, h[1] * us / n, h[2] * us / n, h[3] * us / n, h[4] * us / n, h[5] * us / n);
+              "publish %.2f wait %.2f reduce %.2f (solve in 'top'); LDS box hits %.1f%%\n", (long long)ntiles, n,
+              h[0] * us / n, h[1] * us / n, h[2] * us / n, h[3] * us / n, h[4] * us / n, h[5] * us / n,
+              100.0 * h[7] / std::max<double>(1.0, (double)s->src->n * n));
+      std::vector<double> sc, te, tot;
+      for (int64_t b = 0; b < ntiles; ++b) {
+        sc.push_back(h[8 + 2 * b] * us / n);
+        te.push_back(h[9 + 2 * b] * us / n);
+        tot.push_back(sc.back() + te.back());
+      }
+      auto q = [](std::vector<double> v, double f) {
+        std::sort(v.begin(), v.end());
+        return v[(size_t)std::min<double>(v.size() - 1, f * (v.size() - 1))];
+      };
+      int64_t worst = 0;
+      for (int64_t b = 0; b < ntiles; ++b) worst = tot[b] > tot[worst] ? b : worst;
+      fprintf(stderr, "[m3d persist]   per workgroup scan min %.2f med %.2f p90 %.2f max %.2f | terms min %.2f "
+              "med %.2f p90 %.2f max %.2f | worst tile %lld (scan %.2f terms %.2f)\n",
+              q(sc, 0), q(sc, 0.5), q(sc, 0.9), q(sc, 1), q(te, 0), q(te, 0.5), q(te, 0.9), q(te, 1),
+              (long long)worst, sc[worst], te[worst]);
     }
   }
   return hipGetLastError();

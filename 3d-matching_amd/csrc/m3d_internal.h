@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <utility>
 #include <vector>
@@ -98,7 +99,8 @@ struct Grid {
   float4* mpts = nullptr;
   int32_t* minv = nullptr;
   int64_t n_pts = 0;
-  int64_t n_occ = 0;      // occupied cells (0: not counted)
+  int64_t n_occ = 0;      // occupied cells (grid_occupancy; 0: not counted)
+  bool occ_known = false;
   double cell = 0.0;      // cell size used
   double cell_req = 0.0;  // cell size requested
   // brute-force MFMA screen operands in this grid's cell order (icp.hip pack16_sorted), padded
@@ -107,6 +109,37 @@ struct Grid {
   float4* mf32 = nullptr;
   int64_t mf_npad = 0;
 };
+
+// Device scratch for the temporaries of setup work (grid sorts, Morton copies, cloud packing):
+// grown on demand and owned by the context.  Setup work runs in stream order, so consecutive
+// users on one stream reuse it without a host sync; an outgrown buffer is retired (freed with the
+// context), never freed under work still in flight.  Replaces a hipMalloc/hipFree pair per
+// temporary (hipFree waits for the device).
+struct TmpArena {
+  char* base = nullptr;
+  size_t cap = 0;
+  std::vector<void*> retired;
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    const size_t want = std::max(bytes, 2 * cap);
+    void* p = nullptr;
+    const hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) return e;
+    if (base != nullptr) retired.push_back(base);
+    base = static_cast<char*>(p);
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    for (void* p : retired) (void)hipFree(p);
+    retired.clear();
+    if (base != nullptr) (void)hipFree(base);
+    base = nullptr;
+    cap = 0;
+  }
+};
+// 256-B aligned carve-out of a TmpArena reservation
+inline size_t tmp_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
 constexpr int kTermSlots = 32;  // 21 JTJ + 6 JTr + r² + count + Σd² (+2 pad)
 constexpr int64_t kKeyNone = 0x7FFFFFFFFFFFFFFFll;
@@ -137,6 +170,7 @@ struct m3d_ctx {
   // neighbour lists of the synchronous preprocessing calls (api.cpp prep_lists), grown on demand
   void* prep = nullptr;
   size_t prep_bytes = 0;
+  m3d::TmpArena tmp;  // setup temporaries (grids, Morton copies, cloud packing)
 };
 
 struct m3d_corrset {
@@ -163,6 +197,9 @@ struct m3d_cloud {
   float4* xyz32 = nullptr;  // n_pad centred (pad = far away)
   double center[3] = {0, 0, 0};
   double rmax = 0.0;  // max |x_c|∞ (guard-band bound)
+  // per-axis min / max of the centred fp32 points (the grid bounds; from the packing pass)
+  float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+  bool has_bounds = false;
   double s16 = 1.0;  // power-of-two scale of the fp16 MFMA screen operands (|s16·x|∞ ≤ 32)
   int center_given = 0;  // centre supplied by the caller (a frame shared by target shards)
   mutable std::vector<m3d::Grid*> grids;  // uniform grids built on demand, one per cell size
@@ -189,6 +226,7 @@ struct m3d_icp {
   const m3d_cloud* tgt = nullptr;
   m3d_icp_params params{};
   double max_dist = 0.0;
+  void* block = nullptr;           // device: one allocation holding the arrays below (api.cpp)
   m3d::IcpState* state = nullptr;  // device
   int64_t* keys = nullptr;         // ns packed NN keys: k1 = (d2f, index) minimum of the scan
   uint32_t* near2 = nullptr;       // ns: bits of the smallest d2f of any other target evaluated
@@ -258,6 +296,12 @@ hipError_t launch_sum3(const double* a, int64_t n, double* partial /*[blocks*3]*
 hipError_t launch_center_pack(const double* a, int64_t n, int64_t n_pad, const double c[3],
                               float4* out, float pad_value, float* maxnorm_partial, int blocks,
                               int maxinf, hipStream_t st);
+// m3d_cloud_create: sum_part (sum3_kernel partials, sum_blocks of them) → mean into cdev (device),
+// or the given centre c when sum_part is null; centred fp32 copy + 7 floats per block (max |x|∞,
+// lo[3], hi[3])
+hipError_t launch_cloud_pack(const double* a, int64_t n, int64_t n_pad, const double* sum_part,
+                             int sum_blocks, double* cdev, const double c[3], float4* out, float pad_value,
+                             float* part7, int blocks, hipStream_t st);
 struct ScoreMf;
 // a4 batches: kabsch3_kernel also writes the MFMA screen's per-hypothesis operands (hyp16) for
 // the score launch that follows (thr/mode of that launch; no effect when it will not use them)
@@ -334,7 +378,12 @@ hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st
 // n grid-loop steps in one persistent launch (icp.hip; icp_persist_ok decides when it applies)
 bool icp_persist_ok(const m3d_icp* s);
 hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st);
-hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g);
+// grid over xyz32[0, n) with cell ≈ `cell`: asynchronous when `lohi` (per-axis min[3], max[3] of
+// the points) is given, else one sync for the bounds; temporaries from `ta` (null: hipMalloc)
+hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g,
+                      TmpArena* ta = nullptr, const float* lohi = nullptr);
+// g->n_occ, counted on first use (one sync)
+hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st);
 void grid_free(Grid* g);
 // prev/dprev/tgt32/nt_shard: seed each query with seed_key (nnkey.h); prev == nullptr: no seeds
 // qgrid: the query cloud's grid (its Morton-ordered points, grid_morton) — the cooperative kernel
@@ -344,8 +393,9 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           const float4* sq, const int32_t* prev, const int64_t* dprev,
                           const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0 = 0,
                           int64_t q1 = -1);
-hipError_t grid_morton(Grid* g, hipStream_t st);
-// the Morton-slot copy of an ICP source (out, gout freshly allocated structs; see grid.hip)
+hipError_t grid_morton(Grid* g, hipStream_t st, TmpArena* ta = nullptr);
+// the Morton-slot copy of an ICP source (out, gout freshly allocated structs; see grid.hip);
+// asynchronous (stream order)
 hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Grid* gout, hipStream_t st);
 // dst[slot[k]] = v[k], k < n (slot-ordered loop arrays → the caller's source order)
 hipError_t launch_scatter_i32(const int32_t* v, const int32_t* slot, int64_t n, int32_t* dst,

@@ -108,6 +108,69 @@ __global__ __launch_bounds__(256) void center_pack_kernel(const double* __restri
   if (threadIdx.x == 0) maxpart[blockIdx.x] = s[0];
 }
 
+// Cloud packing (m3d_cloud_create): the mean from sum3_kernel's partials reduced on the device in
+// the host's order (partial b = 0, 1, … per axis, then ÷ n: the same double), then the centred
+// fp32 copy with, per block, max |x_c|∞ and the per-axis min / max of the fp32 coordinates (the
+// grid bounds, grid.hip minmax3_kernel's values) — one host sync for the whole cloud.
+__global__ void mean3_final_kernel(const double* __restrict__ part, int blocks, int64_t n,
+                                   double* __restrict__ c) {
+  if (threadIdx.x != 0) return;
+  double o[3] = {0.0, 0.0, 0.0};
+  for (int b = 0; b < blocks; ++b)
+    for (int k = 0; k < 3; ++k) o[k] += part[3 * b + k];
+  for (int k = 0; k < 3; ++k) c[k] = o[k] / (double)n;
+}
+
+__global__ __launch_bounds__(256) void cloud_pack_kernel(const double* __restrict__ a, int64_t n,
+                                                         int64_t n_pad, const double* __restrict__ cdev,
+                                                         double c0, double c1, double c2,
+                                                         float4* __restrict__ out, float pad_value,
+                                                         float* __restrict__ part7) {
+  __shared__ float s[7][256];
+  if (cdev != nullptr) {
+    c0 = cdev[0];
+    c1 = cdev[1];
+    c2 = cdev[2];
+  }
+  float m = 0.0f, lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * 256) {
+    float4 v;
+    if (i < n) {
+      double x = a[3 * i] - c0, y = a[3 * i + 1] - c1, z = a[3 * i + 2] - c2;
+      const float fx = (float)x, fy = (float)y, fz = (float)z;
+      const double w = (double)fx * fx + (double)fy * fy + (double)fz * fz;  // as center_pack_kernel
+      v = make_float4(fx, fy, fz, (float)w);
+      m = fmaxf(m, (float)fmax(fabs(x), fmax(fabs(y), fabs(z))) * (1.0f + 1e-6f));
+      lo[0] = fminf(lo[0], fx);
+      lo[1] = fminf(lo[1], fy);
+      lo[2] = fminf(lo[2], fz);
+      hi[0] = fmaxf(hi[0], fx);
+      hi[1] = fmaxf(hi[1], fy);
+      hi[2] = fmaxf(hi[2], fz);
+    } else {
+      v = make_float4(pad_value, pad_value, pad_value, 3.0f * pad_value * pad_value);
+    }
+    out[i] = v;
+  }
+  s[0][threadIdx.x] = m;
+  for (int k = 0; k < 3; ++k) {
+    s[1 + k][threadIdx.x] = lo[k];
+    s[4 + k][threadIdx.x] = hi[k];
+  }
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      s[0][threadIdx.x] = fmaxf(s[0][threadIdx.x], s[0][threadIdx.x + w]);
+      for (int k = 0; k < 3; ++k) {
+        s[1 + k][threadIdx.x] = fminf(s[1 + k][threadIdx.x], s[1 + k][threadIdx.x + w]);
+        s[4 + k][threadIdx.x] = fmaxf(s[4 + k][threadIdx.x], s[4 + k][threadIdx.x + w]);
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 7) part7[7 * blockIdx.x + threadIdx.x] = s[threadIdx.x][0];
+}
+
 // ------------------------------------------------------------------------------- sampler
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -997,6 +1060,17 @@ hipError_t launch_pack_corr(const double* src, const double* tgt, const int32_t*
 
 hipError_t launch_sum3(const double* a, int64_t n, double* partial, int blocks, hipStream_t st) {
   sum3_kernel<<<blocks, 256, 0, st>>>(a, n, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_cloud_pack(const double* a, int64_t n, int64_t n_pad, const double* sum_part,
+                             int sum_blocks, double* cdev, const double c[3], float4* out, float pad_value,
+                             float* part7, int blocks, hipStream_t st) {
+  if (sum_part != nullptr) {  // mean on the device from sum3 partials (else c is given)
+    mean3_final_kernel<<<1, 64, 0, st>>>(sum_part, sum_blocks, n, cdev);
+  }
+  cloud_pack_kernel<<<blocks, 256, 0, st>>>(a, n, n_pad, sum_part != nullptr ? cdev : nullptr, c[0], c[1], c[2],
+                                            out, pad_value, part7);
   return hipGetLastError();
 }
 

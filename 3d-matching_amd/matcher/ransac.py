@@ -115,22 +115,28 @@ def global_registration(src, tgt, voxel_size: float, iteration: int = 30) -> Reg
     return RegistrationResult(out.transformation, out.fitness, out.inlier_rmse, out.correspondence_set)
 
 
+def inject_noise(corres_np: np.ndarray, n_src: int, n_tgt: int, noise_ratio: float) -> np.ndarray:
+    """ransac.py:89-99's outlier injection on the global legacy numpy RNG: int(N·ratio) random
+    (source, target) rows appended, then the whole set shuffled in place."""
+    if noise_ratio > 0:
+        n_original = len(corres_np)
+        n_noise = int(n_original * noise_ratio)
+        if n_noise > 0:
+            src_indices = np.random.randint(0, n_src, n_noise)
+            tgt_indices = np.random.randint(0, n_tgt, n_noise)
+            noise_corres = np.stack((src_indices, tgt_indices), axis=1)
+            corres_np = np.vstack((corres_np, noise_corres))
+            np.random.shuffle(corres_np)
+    return np.asarray(corres_np, dtype=np.int32)
+
+
 def compute_feature_correspondences(src, tgt, mutual_filter: bool = False,
                                     noise_ratio: float = 0.0) -> np.ndarray:
     """ransac.py:62-101.  Returns an (N,2) int32 array (the Vector2iVector's numpy view)."""
     from m3d import prep
 
     corres_np = prep.feature_correspondences(src.pcd_fpfh, tgt.pcd_fpfh, mutual_filter)
-    if noise_ratio > 0:                                         # ransac.py:89-99
-        n_original = len(corres_np)
-        n_noise = int(n_original * noise_ratio)
-        if n_noise > 0:
-            src_indices = np.random.randint(0, len(_down_points(src)), n_noise)
-            tgt_indices = np.random.randint(0, len(_down_points(tgt)), n_noise)
-            noise_corres = np.stack((src_indices, tgt_indices), axis=1)
-            corres_np = np.vstack((corres_np, noise_corres))
-            np.random.shuffle(corres_np)
-    return np.asarray(corres_np, dtype=np.int32)
+    return inject_noise(corres_np, len(_down_points(src)), len(_down_points(tgt)), noise_ratio)
 
 
 def compute_step_transformation(src, tgt, correspondences) -> RegistrationResult:

@@ -271,7 +271,20 @@ def main():
         tgt_c = (Cloud(tgt_all, nrm_all) if not multi else
                  Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0)))
     src_c = Cloud(src)
-    K_NN, K_TERMS = _lib.KERNEL_NN, _lib.KERNEL_TERMS
+    K_NN, K_TERMS, K_COMM = _lib.KERNEL_NN, _lib.KERNEL_TERMS, _lib.KERNEL_COMM
+
+    def split_times(prof, el_ev, evals):
+        """Per evaluation (one NN + terms + exchange), from the events pass: the NN, terms and
+        RCCL all-reduce times on their own streams (the split target-shard exchange runs half of
+        its keys beside the NN, so the three need not add up to the iteration), max over ranks."""
+        def per(k):
+            return None if k not in prof or prof[k][1] == 0 else max_over_ranks(prof[k][0] / evals)
+        return {"per_evaluation_ms_with_events": max_over_ranks(el_ev) / evals * 1e3,
+                "nn_ms_per_evaluation": per(K_NN), "terms_ms_per_evaluation": per(K_TERMS),
+                "exchange_ms_per_evaluation": per(K_COMM),
+                "allreduces_per_evaluation": None if K_COMM not in prof else prof[K_COMM][1] / evals,
+                "exchange_note": ("library RCCL all-reduces timed by events on their streams"
+                                  if comm_name == "libm3d-rccl" else "exchange not issued by the library")}
 
     def bench_icp(nn):
         loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters, nn=nn)
@@ -348,11 +361,12 @@ def main():
             for _ in range(args.warmup):
                 run()
             torch.cuda.synchronize()
-            e1, _, prof = timed(run, args.steps, (K_NN, K_TERMS))
+            e1, e1_ev, prof = timed(run, args.steps, (K_NN, K_TERMS, K_COMM))
             rs1 = lp.result()
             sec = {"value": iters * args.steps / e1, "ms_per_step": e1 / args.steps * 1e3,
                    "nn_avg_launch_ms": max_over_ranks(prof[K_NN][0] / max(prof[K_NN][1], 1)),
                    "fitness": rs1.fitness, "max_abs_err_vs_T_true": float(np.abs(rs1.transformation - T1).max())}
+            sec.update(split_times(prof, e1_ev, args.steps * (iters + 1)))
             if nn == "brute":
                 cfg1_strong.update(sec)
             else:
@@ -391,7 +405,7 @@ def main():
             run = icp_runner(lp, it3, mode3, o3)
             run()
             torch.cuda.synchronize()
-            e3, e3_ev, prof = timed(run, args.cfg3_steps, (K_NN, K_TERMS))
+            e3, e3_ev, prof = timed(run, args.cfg3_steps, (K_NN, K_TERMS, K_COMM))
             (m, n), (tm, tn) = prof[K_NN], prof[K_TERMS]
             avg = max_over_ranks(m / max(n, 1))
             r3 = lp.result()
@@ -399,6 +413,20 @@ def main():
                    "ms_per_iteration_with_kernel_events": e3_ev / (it3 * args.cfg3_steps) * 1e3,
                    "nn_avg_launch_ms": avg, "terms_avg_launch_ms": tm / max(tn, 1),
                    "fitness": r3.fitness, "max_abs_err_vs_T_true": float(np.abs(r3.transformation - T3).max())}
+            if multi:
+                sec.update(split_times(prof, e3_ev, args.cfg3_steps * (it3 + 1)))
+                # the same loop with the keys exchanged in one piece (no overlap with the NN)
+                del lp
+                lp = IcpLoop(s3c, t3c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=it3, nn=nn,
+                             split=False)
+                run = icp_runner(lp, it3, mode3, o3)
+                run()
+                torch.cuda.synchronize()
+                e3n, e3n_ev, profn = timed(run, args.cfg3_steps, (K_NN, K_TERMS, K_COMM))
+                sec["split_off"] = {"value": it3 * args.cfg3_steps / e3n,
+                                    "ms_per_iteration": e3n / (it3 * args.cfg3_steps) * 1e3,
+                                    "same_result": bool(np.array_equal(lp.result().transformation, r3.transformation)),
+                                    **split_times(profn, e3n_ev, args.cfg3_steps * (it3 + 1))}
             if nn == "brute":
                 sec["roofline"] = nn_roofline(n3, c3, avg, n, tm / max(tn, 1))
                 sec["roofline"]["note"] = "per rank: " + NN_NOTE
@@ -476,11 +504,58 @@ def main():
             for _ in range(3):
                 ransac_strong_run()
             torch.cuda.synchronize()
-            rs_el, _, _ = timed(ransac_strong_run, args.ransac_steps, ())
+            rs_el, rs_ev, rs_prof = timed(ransac_strong_run, args.ransac_steps, (K_SC, K_COMM))
             kc, kid = D.unpack_best_key(int(key.item()))
             ransac_strong = {"value": H * args.ransac_steps / rs_el, "ms_per_run": rs_el / args.ransac_steps * 1e3,
+                             "score_ms_per_run": max_over_ranks(rs_prof[K_SC][0] / args.ransac_steps),
+                             "exchange_ms_per_run": (max_over_ranks(rs_prof[K_COMM][0] / args.ransac_steps)
+                                                     if rs_prof[K_COMM][1] else None),
+                             "ms_per_run_with_events": rs_ev / args.ransac_steps * 1e3,
                              "hyps_per_run": H, "hyps_on_rank": c2, "best_id": kid, "best_count": kc,
                              "workload": f"cfg2 fixed batch: {H} hypotheses split over {world} GPUs, MAX key"}
+        # cfg2's secondary workload (the GUI default _visualize_matcher.py:168):
+        # noise_ratio 2.0 on the same pair (ransac.py:89-99 after np.random.seed(3): Nc = 3e5, the
+        # set tests/golden/ransac_cfg2_full.npz pins), 1e5 hypotheses, the GUI's comparator
+        # (evaluate_inlier_ratio_fast, Σd² < (1.5·v)²), seed 42, no early stop
+        from matcher.ransac import inject_noise
+
+        np.random.seed(3)
+        corr3 = inject_noise(np.asarray(corr), len(rs_src), len(rs_tgt), 2.0)
+        cs3 = CorrSet(rs_src, rs_tgt, corr3)
+        p3 = RansacParams(max_iter=H, seed=42, thr=thr * thr, mode=_lib.SCORE_SQUARED, early_stop=False,
+                          hyp0=rank * H)
+        res3 = torch.zeros(RESULT_WORDS, dtype=torch.int64, device=dev)
+
+        def ransac3_run():
+            cs3.run_async(p3, res3)
+            if multi:
+                if comm_name == "libm3d-rccl":
+                    cs3.best_allreduce(comm, res3, rank * H, key)
+                else:
+                    key.copy_(res3[19:20] * (1 << 32) + (0xFFFFFFFF - (rank * H + res3[17:18])))
+                    comm.max_(key)
+
+        for _ in range(3):
+            ransac3_run()
+        torch.cuda.synchronize()
+        rel3, rel3_ev, prof3 = timed(ransac3_run, args.ransac_steps, (K_SC, K_KB))
+        out3 = RansacOutcome.from_device(res3, len(corr3))
+        sc3_avg = max_over_ranks(prof3[K_SC][0] / max(prof3[K_SC][1], 1))
+        pairs3 = len(corr3) * H / max(prof3[K_SC][1] // args.ransac_steps, 1)
+        sc3_algo = SCORE_FLOP_PER_PAIR * pairs3 / (sc3_avg * 1e-3) / 1e12
+        ransac_nc3e5 = {
+            "metric": "RANSAC hypotheses/sec (cfg2 secondary: noise_ratio 2.0, Nc=3e5, a1+a3, no early stop)",
+            "value": world * H * args.ransac_steps / rel3, "unit": "hyp/s",
+            "ms_per_run": rel3 / args.ransac_steps * 1e3, "nc": len(corr3), "hyps_per_gpu": H,
+            "best_fitness": out3.fitness, "best_index": out3.best_index,
+            "roofline": {"bound": "mfma", "kernel": "score_mfma_kernel", "achieved": sc3_algo,
+                         "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s", "frac": sc3_algo / MFMA_F16_PEAK_TF,
+                         "avg_launch_ms": sc3_avg, "pairs_per_launch": pairs3,
+                         "flop_per_pair": SCORE_FLOP_PER_PAIR,
+                         "mfma_issue_frac": SCORE_MFMA_FLOP_PER_PAIR * pairs3 / (sc3_avg * 1e-3) / 1e12
+                         / MFMA_F16_PEAK_TF},
+        }
+        del cs3
         ransac = {
             "metric": "RANSAC hypotheses/sec (cfg2: Nc=1e5, a1+a2, no early stop)",
             "value": world * H * args.ransac_steps / rel, "unit": "hyp/s",
@@ -498,6 +573,7 @@ def main():
                                  "run on the matrix pipe, DESIGN.md 3.2a)"},
             "kabsch_avg_launch_ms": kb_ms / max(kb_n, 1),
             "strong": ransac_strong,
+            "nc3e5": ransac_nc3e5,
         }
 
     # ------------------------------------------------------------------ drop-in per-call path

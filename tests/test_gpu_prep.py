@@ -209,7 +209,9 @@ def test_feature_ransac_exit_uses_corres_ratio_not_fitness():
     device follows the corrected oracle, validation for validation."""
     pts, _ = synth.surface_points(1500, seed=7)
     T = synth.random_rigid(8, rot_range=0.5, trans_range=1.0)
-    tgt = synth.apply(T, pts)
+    # 0.01 noise: rmse values are then real distances, not rounding noise (an exact copy makes
+    # every good hypothesis's rmse ~1e-15, and "lower rmse wins" compares rounding orders)
+    tgt = synth.apply(T, pts) + np.random.default_rng(10).normal(scale=0.01, size=pts.shape)
     rng = np.random.default_rng(9)
     corr = np.c_[np.arange(1500), np.arange(1500)]
     bad = rng.random(1500) < 0.7

@@ -148,7 +148,9 @@ def test_ransac_feature_exit_follows_corres_ratio_not_fitness():
     (≈ 0.3 → est_k ≈ 253) keeps validating — the two restatements differ."""
     pts, _ = synth.surface_points(1500, seed=7)
     T = synth.random_rigid(8, rot_range=0.5, trans_range=1.0)
-    tgt = synth.apply(T, pts)
+    # 0.01 noise: rmse values are then real distances, not rounding noise (an exact copy makes
+    # every good hypothesis's rmse ~1e-15, and "lower rmse wins" compares rounding orders)
+    tgt = synth.apply(T, pts) + np.random.default_rng(10).normal(scale=0.01, size=pts.shape)
     rng = np.random.default_rng(9)
     corr = np.c_[np.arange(1500), np.arange(1500)]
     bad = rng.random(1500) < 0.7
@@ -157,6 +159,6 @@ def test_ransac_feature_exit_follows_corres_ratio_not_fitness():
     rows = lambda h: P.native_rows(3, h, len(corr))  # noqa: E731
     new = P.ransac_feature(pts, tgt, corr, 0.45, rows, **kw)
     old = P.ransac_feature(pts, tgt, corr, 0.45, rows, exit_rule="fitness", **kw)
-    assert new["fitness"] > 0.99 and old["fitness"] > 0.99
+    assert new["fitness"] > 0.98 and old["fitness"] > 0.98
     assert 0.25 < new["corres_ratio"] < 0.35
     assert old["validations"] < 10 < new["validations"]
