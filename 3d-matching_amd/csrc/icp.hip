@@ -25,6 +25,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <string>
 #include <vector>
 #include <stdlib.h>
 
@@ -1299,11 +1300,11 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
 // resident (api.cpp checks the grid against the occupancy before choosing this path).  Per
 // iteration a workgroup
 //   (1) scans its 512 queries, one lane each, seeded from the previous winner, whose centred fp32
-//       point it keeps in LDS.  The targets of a query's cell box are cached in LDS (up to kPCand
-//       points per query, with the box they came from): when the next iteration's box is the same
-//       box — the usual case once the transform has settled — the query re-evaluates exactly the
-//       same target set from LDS without a global load (same set ⇒ same key and runner-up: the
-//       scan state is order-free, nnkey.h near_push);
+//       point it keeps in LDS.  The sorted-array ranges of a query's cell-box rows are cached in
+//       LDS (up to kPRows rows, with the box they came from): when the next iteration's box is the
+//       same box — the usual case once the transform has settled — the query loads exactly the
+//       same targets straight away, skipping the dependent row-start loads (same set ⇒ same key
+//       and runner-up: the scan state is order-free, nnkey.h near_push);
 //   (2) decides the fp64 winners and adds the terms of its sources exactly as terms_block does
 //       (same thread ↔ source map, same terms_add order, same wave/LDS reduction), writing corr;
 //   (3) publishes its block partial write-through (sc1) into one of two buffers, drains it, and
@@ -1317,7 +1318,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
 // arrived at iteration k + 1, i.e. finished reading iteration k's.  Every spin is bounded: a
 // workgroup that waits too long (a tile not resident) flags `fault` and leaves the loop.
 constexpr int kPTile = 2 * kTermsBlock;  // sources per tile (= per workgroup, one lane per query)
-constexpr int kPCand = 15;               // cached targets per query (LDS: 15 × 16 B × 512 = 120 KB)
+constexpr int kPRows = 9;                // cached row ranges per query (a seeded box: ≤ 3 × 3 rows)
 constexpr uint32_t kPersistMaxSpin = 1u << 22;
 
 struct PersistArgs {
@@ -1340,18 +1341,54 @@ struct PersistArgs {
   unsigned long long* prof;  // M3D_PERSIST_PROF=1: per-phase wall-clock ticks (else null)
 };
 
+// One query's scan over a list of cell-box rows [a, b) in the target grid's sorted array, kR rows
+// × kB points per load batch (nnkey.h grid_scan's loop with the row ranges given).
+template <int kR, int kB>
+__device__ __forceinline__ void scan_ranges(const GridDev& g, const int2* __restrict__ rr, int nrows,
+                                            int r_begin, int32_t p_begin, float qx, float qy, float qz,
+                                            float r2_hi, uint64_t& k1, float& k1d, float& n2) {
+  for (int r0 = r_begin; r0 < nrows; r0 += kR) {
+    int32_t ra[kR], rb[kR], len = 0;
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+      const int2 ab = r0 + k < nrows ? rr[r0 + k] : make_int2(0, 0);
+      ra[k] = ab.x;
+      rb[k] = ab.y;
+      len = max(len, rb[k] - ra[k]);
+    }
+    for (int32_t b0 = r0 == r_begin ? p_begin : 0; b0 < len; b0 += kB) {
+      float4 v[kR][kB];
+#pragma unroll
+      for (int k = 0; k < kR; ++k)
+#pragma unroll
+        for (int m = 0; m < kB; ++m) {
+          const int32_t j = ra[k] + b0 + m;
+          if (j < rb[k]) v[k][m] = g.pts[j];
+        }
+#pragma unroll
+      for (int k = 0; k < kR; ++k)
+#pragma unroll
+        for (int m = 0; m < kB; ++m) {
+          const int32_t j = ra[k] + b0 + m;
+          if (j < rb[k]) {
+            const float d2 = d2f(qx, qy, qz, v[k][m].x, v[k][m].y, v[k][m].z);
+            if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)__float_as_int(v[k][m].w)), d2);
+          }
+        }
+    }
+  }
+}
+
 template <int kR, int kB, bool kProf>
-__global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a, IcpState* gs, SolveParams sp) {
-  constexpr int kT = kPTile;
+__global__ __launch_bounds__(kTermsBlock) void icp_grid_persist_kernel(PersistArgs a, IcpState* gs, SolveParams sp) {
+  constexpr int kT = kTermsBlock;  // 4 waves, one per SIMD: the whole register file per wave
+  constexpr int kP = 2;            // sources per thread: u·256 + tid of the tile (terms_block's map)
   __shared__ IcpState S;
-  __shared__ uint64_t k1s[kPTile];
-  __shared__ float n2s[kPTile];
-  __shared__ float4 seedp[kPTile];  // previous winner's centred fp32 point, w = its index (−1 none)
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
   __shared__ double gsum[kReduceGroups][kTermSlots];
-  __shared__ int32_t cbox[6][kPTile];       // cached cell box (x0, x1, y0, y1, z0, z1) per query
-  __shared__ int32_t cnum[kPTile];          // its target count (−1: no cache)
-  __shared__ float4 cand[kPCand][kPTile];   // its targets (x, y, z, index bits)
+  __shared__ int32_t cbox[6][kPTile];   // cached cell box (x0, x1, y0, y1, z0, z1) per query
+  __shared__ int32_t cnum[kPTile];      // its row count (−1: no cache)
+  __shared__ int2 crow[kPTile][kPRows]; // its rows' [a, b) in the target grid's sorted array
   __shared__ int bad;
   const int tid = threadIdx.x;
   const int64_t ntiles = gridDim.x;
@@ -1359,33 +1396,30 @@ __global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a,
   for (int k = tid; k < (int)(sizeof(IcpState) / 4); k += kT)
     reinterpret_cast<uint32_t*>(&S)[k] = reinterpret_cast<const uint32_t*>(gs)[k];
   if (tid == 0) bad = 0;
-  cnum[tid] = -1;
-  // scan lane: query q = tid of the tile; its centred point stays in registers
-  const int q = tid;
-  const int64_t t = base + q;
-  const float4 p = t < a.ns ? a.src32[t] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  {  // seeds of the first iteration: the loop's correspondences on entry
-    const int32_t j = t < a.ns ? a.corr[t] : -1;
-    float4 v = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
-    if (j >= 0) {
-      const float4 w = a.tgt32[j];
-      v = make_float4(w.x, w.y, w.z, __int_as_float(j));
-    }
-    seedp[q] = v;
-  }
-  // terms lanes (waves 0..3): sources base + u·256 + tid, their fp64 points in registers
-  constexpr int kP = 2;
+  const GridDev& g = a.g;
+  // per source: centred fp32 point, fp64 point, the seed (previous winner's fp32 point + index)
+  float4 p[kP], seed[kP];
   double p64[kP][3];
+  bool valid[kP];
+  int64_t ii[kP];
 #pragma unroll
   for (int u = 0; u < kP; ++u) {
     const int64_t i = base + u * kTermsBlock + tid;
-    const bool v = tid < kTermsBlock && i < a.ns;
+    valid[u] = i < a.ns;
+    ii[u] = valid[u] ? i : 0;
+    p[u] = valid[u] ? a.src32[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) p64[u][k] = v ? a.src64[3 * i + k] : 0.0;
+    for (int k = 0; k < 3; ++k) p64[u][k] = valid[u] ? a.src64[3 * i + k] : 0.0;
+    const int32_t j = valid[u] ? a.corr[i] : -1;  // the loop's correspondences on entry
+    seed[u] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+    if (j >= 0) {
+      const float4 w = a.tgt32[j];
+      seed[u] = make_float4(w.x, w.y, w.z, __int_as_float(j));
+    }
+    cnum[u * kTermsBlock + tid] = -1;
   }
   const int lane = tid & (kWave - 1), wave = tid / kWave;
-  // phase timer (diagnostics only): thread 0, wall clock after each barrier
-  unsigned long long tph[7] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  unsigned long long tph[7] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;  // phase timer (diagnostics)
   const bool prof = kProf && tid == 0;
   if (prof) tlast = wall_clock64();
   auto mark = [&](int k) {
@@ -1395,122 +1429,139 @@ __global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a,
       tlast = tn_;
     }
   };
-  unsigned hits = 0;
   for (int it = 0; it < a.n; ++it) {
-    __syncthreads();  // S, seedp of this iteration
+    __syncthreads();  // S of this iteration
     mark(0);
     if (S.done || bad) break;
-    // (1) scan
+    // (1) scan both queries of this thread
+    const float r2_hi = S.r2_hi, be = S.band_e;
+    const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
+    uint64_t k1[kP];
+    float k1d[kP], n2[kP], qx[kP], qy[kP], qz[kP];
+    int bx[kP][6], m0[kP];
+    bool hit[kP];
+#pragma unroll
+    for (int u = 0; u < kP; ++u) {
+      k1[u] = key0;
+      k1d[u] = n2[u] = kInf;
+      hit[u] = false;
+      m0[u] = 0;
+      xform32(S.Rt32, p[u], qx[u], qy[u], qz[u]);
+      const int32_t sj = __float_as_int(seed[u].w);
+      if (valid[u] && sj >= 0) {  // nnkey.h seed_key, single device: the previous winner re-evaluated
+        const float d2 = d2f(qx[u], qy[u], qz[u], seed[u].x, seed[u].y, seed[u].z);
+        if (d2 <= r2_hi) k1[u] = make_key(d2, (uint32_t)sj);
+      }
+      k1d[u] = key_real_d2(k1[u]);
+      const float R = sqrtf(search_bound(key_d2(k1[u]), be, r2_hi)) * 1.001f;
+      bx[u][0] = grid_coord(qx[u] - R, g.o[0], g.inv_h, g.n[0]);
+      bx[u][1] = grid_coord(qx[u] + R, g.o[0], g.inv_h, g.n[0]);
+      bx[u][2] = grid_coord(qy[u] - R, g.o[1], g.inv_h, g.n[1]);
+      bx[u][3] = grid_coord(qy[u] + R, g.o[1], g.inv_h, g.n[1]);
+      bx[u][4] = grid_coord(qz[u] - R, g.o[2], g.inv_h, g.n[2]);
+      bx[u][5] = grid_coord(qz[u] + R, g.o[2], g.inv_h, g.n[2]);
+      const int ql = u * kTermsBlock + tid;
+      const int mc = cnum[ql];
+      hit[u] = valid[u] && g.ncells > 0 && mc >= 0 && cbox[0][ql] == bx[u][0] && cbox[1][ql] == bx[u][1] &&
+               cbox[2][ql] == bx[u][2] && cbox[3][ql] == bx[u][3] && cbox[4][ql] == bx[u][4] &&
+               cbox[5][ql] == bx[u][5];
+      m0[u] = hit[u] ? mc : 0;
+    }
+    if (kProf && it < 64) {  // one atomic per wave
+      const unsigned long long nh = (unsigned long long)__popcll(__ballot(hit[0])) + __popcll(__ballot(hit[1]));
+      if (lane == 0 && nh) atomicAdd(a.prof + 520 + it, nh);
+    }
+    // hits: the first kR rows × kB points of BOTH queries in one batch of loads (one round trip
+    // for a typical seeded box), then any remainder per query
     {
-      const float r2_hi = S.r2_hi, be = S.band_e;
-      const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
-      uint64_t k1 = key0;
-      float k1d = kInf, n2 = kInf;
-      if (t < a.ns) {
-        float qx, qy, qz;
-        xform32(S.Rt32, p, qx, qy, qz);
-        const float4 sd = seedp[q];
-        const int32_t sj = __float_as_int(sd.w);
-        if (sj >= 0) {  // nnkey.h seed_key, single device: the previous winner re-evaluated
-          const float d2 = d2f(qx, qy, qz, sd.x, sd.y, sd.z);
-          if (d2 <= r2_hi) k1 = make_key(d2, (uint32_t)sj);
+      float4 v[kP][kR][kB];
+      int32_t ra[kP][kR], rb[kP][kR];
+#pragma unroll
+      for (int u = 0; u < kP; ++u)
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          const int2 ab = hit[u] && k < m0[u] ? crow[u * kTermsBlock + tid][k] : make_int2(0, 0);
+          ra[u][k] = ab.x;
+          rb[u][k] = ab.y;
         }
-        k1d = key_real_d2(k1);
-        const GridDev& g = a.g;
-        if (g.ncells > 0) {
-          // the cell box of q ± R (nnkey.h grid_scan; grid.hip header lemma)
-          const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
-          const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
-          const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
-          const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
-          const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
-          const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
-          const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
-          const int m0 = cnum[q];
-          const bool hit = m0 >= 0 && cbox[0][q] == x0 && cbox[1][q] == x1 && cbox[2][q] == y0 &&
-                           cbox[3][q] == y1 && cbox[4][q] == z0 && cbox[5][q] == z1;
-          if (hit) {  // the same box: the same targets, from LDS
-            if (kProf) ++hits;
-            for (int c = 0; c < m0; ++c) {
-              const float4 v = cand[c][q];
-              const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
-              if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)__float_as_int(v.w)), d2);
+#pragma unroll
+      for (int u = 0; u < kP; ++u)
+#pragma unroll
+        for (int k = 0; k < kR; ++k)
+#pragma unroll
+          for (int m = 0; m < kB; ++m)
+            if (ra[u][k] + m < rb[u][k]) v[u][k][m] = g.pts[ra[u][k] + m];
+#pragma unroll
+      for (int u = 0; u < kP; ++u)
+#pragma unroll
+        for (int k = 0; k < kR; ++k)
+#pragma unroll
+          for (int m = 0; m < kB; ++m)
+            if (ra[u][k] + m < rb[u][k]) {
+              const float d2 = d2f(qx[u], qy[u], qz[u], v[u][k][m].x, v[u][k][m].y, v[u][k][m].z);
+              if (d2 <= r2_hi)
+                near_push(k1[u], k1d[u], n2[u], make_key(d2, (uint32_t)__float_as_int(v[u][k][m].w)), d2);
             }
-          } else {  // grid_scan's row batches from global memory, caching the box's targets
-            const int ny = y1 - y0 + 1;
-            const int rows = ny * (z1 - z0 + 1);
-            int m = 0;  // targets of the box seen so far (> kPCand: no cache)
-            for (int r0 = 0; r0 < rows; r0 += kR) {
-              int32_t ra[kR], rb[kR], ro[kR];
-              int32_t len = 0;
 #pragma unroll
-              for (int k = 0; k < kR; ++k) {
-                const int r = r0 + k;
-                ra[k] = rb[k] = 0;
-                if (r < rows) {
-                  const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
-                  ra[k] = g.start[row + x0];
-                  rb[k] = g.start[row + x1 + 1];
-                }
-              }
+      for (int u = 0; u < kP; ++u) {
+        if (!hit[u]) continue;
+        const int2* rr = crow[u * kTermsBlock + tid];
+        int32_t more = 0;  // points beyond kB in the first kR rows
 #pragma unroll
-              for (int k = 0; k < kR; ++k) {
-                ro[k] = m;
-                m += rb[k] - ra[k];
-                len = max(len, rb[k] - ra[k]);
-              }
-              for (int32_t b0 = 0; b0 < len; b0 += kB) {
-                float4 v[kR][kB];
+        for (int k = 0; k < kR; ++k) more = max(more, rb[u][k] - ra[u][k] - kB);
+        if (more > 0) scan_ranges<kR, kB>(g, rr, min(m0[u], kR), 0, kB, qx[u], qy[u], qz[u], r2_hi, k1[u], k1d[u], n2[u]);
+        if (m0[u] > kR) scan_ranges<kR, kB>(g, rr, m0[u], kR, 0, qx[u], qy[u], qz[u], r2_hi, k1[u], k1d[u], n2[u]);
+      }
+    }
+    // misses: the box's row starts from the grid, the ranges cached (≤ kPRows rows)
 #pragma unroll
-                for (int k = 0; k < kR; ++k)
+    for (int u = 0; u < kP; ++u) {
+      if (hit[u] || !valid[u] || g.ncells == 0) continue;
+      const int ql = u * kTermsBlock + tid;
+      const int ny = bx[u][3] - bx[u][2] + 1;
+      const int rows = ny * (bx[u][5] - bx[u][4] + 1);
+      int2* rr = crow[ql];
+      for (int r0 = 0; r0 < rows; r0 += kPRows) {
+        int2 ab[kPRows];
 #pragma unroll
-                  for (int mm = 0; mm < kB; ++mm) {
-                    const int32_t j = ra[k] + b0 + mm;
-                    if (j < rb[k]) v[k][mm] = g.pts[j];
-                  }
+        for (int k = 0; k < kPRows; ++k) {
+          const int r = r0 + k;
+          ab[k] = make_int2(0, 0);
+          if (r < rows) {
+            const int64_t row = ((int64_t)(bx[u][4] + r / ny) * g.n[1] + (bx[u][2] + r % ny)) * g.n[0];
+            ab[k] = make_int2(g.start[row + bx[u][0]], g.start[row + bx[u][1] + 1]);
+          }
+        }
+        if (rows <= kPRows) {  // cache the box (one batch of starts covers it)
 #pragma unroll
-                for (int k = 0; k < kR; ++k)
-#pragma unroll
-                  for (int mm = 0; mm < kB; ++mm) {
-                    const int32_t j = ra[k] + b0 + mm;
-                    if (j < rb[k]) {
-                      const float d2 = d2f(qx, qy, qz, v[k][mm].x, v[k][mm].y, v[k][mm].z);
-                      if (d2 <= r2_hi)
-                        near_push(k1, k1d, n2, make_key(d2, (uint32_t)__float_as_int(v[k][mm].w)), d2);
-                      const int slot = ro[k] + b0 + mm;
-                      if (slot < kPCand) cand[slot][q] = v[k][mm];
-                    }
-                  }
-              }
-            }
-            cnum[q] = m <= kPCand ? m : -1;
-            cbox[0][q] = x0;
-            cbox[1][q] = x1;
-            cbox[2][q] = y0;
-            cbox[3][q] = y1;
-            cbox[4][q] = z0;
-            cbox[5][q] = z1;
+          for (int k = 0; k < kPRows; ++k)
+            if (k < rows) rr[k] = ab[k];
+          scan_ranges<kR, kB>(g, rr, rows, 0, 0, qx[u], qy[u], qz[u], r2_hi, k1[u], k1d[u], n2[u]);
+        } else {
+          for (int k = 0; k < kPRows && r0 + k < rows; ++k) {
+            int2 one[1] = {ab[k]};
+            scan_ranges<1, kB>(g, one, 1, 0, 0, qx[u], qy[u], qz[u], r2_hi, k1[u], k1d[u], n2[u]);
           }
         }
       }
-      k1s[q] = (t < a.ns && k1 != key0) ? k1 : (uint64_t)kKeyNone;
-      n2s[q] = t < a.ns ? n2 : kInf;
+      cnum[ql] = rows <= kPRows ? rows : -1;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) cbox[k][ql] = bx[u][k];
     }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kP; ++u)
+      if (!valid[u] || k1[u] == key0) k1[u] = (uint64_t)kKeyNone;
     mark(1);
-    // (2) terms: terms_block's per-thread part for kP = 2, keys from LDS
-    if (tid < kTermsBlock) {
+    // (2) terms: terms_block's per-thread part for kP = 2, on the scan results in registers
+    {
       double acc[30];
 #pragma unroll
       for (int k = 0; k < 30; ++k) acc[k] = 0.0;
-      bool valid[kP], fixed[kP];
-      int64_t ii[kP], gj[kP];
+      bool fixed[kP];
+      int64_t gj[kP];
       double vs[kP][3], d2[kP];
 #pragma unroll
       for (int u = 0; u < kP; ++u) {
-        const int64_t i = base + u * kTermsBlock + tid;
-        valid[u] = i < a.ns;
-        ii[u] = valid[u] ? i : 0;
         gj[u] = -1;
         d2[u] = 0.0;
         fixed[u] = true;
@@ -1518,28 +1569,22 @@ __global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a,
       }
 #pragma unroll
       for (int u = 0; u < kP; ++u) {
-        const int ql = u * kTermsBlock + tid;
-        const uint64_t k1 = valid[u] ? k1s[ql] : (uint64_t)kKeyNone;
-        const float n2 = valid[u] ? n2s[ql] : kInf;
-        const float X = valid[u] && k1 != (uint64_t)kKeyNone ? search_bound(key_d2(k1), S.band_e, S.r2_hi) : -1.0f;
-        const bool amb = X >= 0.0f && n2 <= X;
-        float qx = 0.0f, qy = 0.0f, qz = 0.0f;
-        if (amb) xform32(S.Rt32, a.src32[ii[u]], qx, qy, qz);
+        const float X = valid[u] && k1[u] != (uint64_t)kKeyNone ? search_bound(key_d2(k1[u]), S.band_e, S.r2_hi) : -1.0f;
+        const bool amb = X >= 0.0f && (valid[u] ? n2[u] : kInf) <= X;
         int64_t bj = -1;
         double bd = 0.0;
-        resolve_wave(amb, a.g, a.tgt64, 0, qx, qy, qz, X, vs[u], S.r2, bj, bd);
+        resolve_wave(amb, g, a.tgt64, 0, qx[u], qy[u], qz[u], X, vs[u], S.r2, bj, bd);
         if (amb) {
           gj[u] = bj;
           d2[u] = bd;
-        } else if (valid[u] && key_real(k1)) {
-          const int64_t c = (int64_t)(uint32_t)k1;
+        } else if (valid[u] && key_real(k1[u])) {
+          const int64_t c = (int64_t)(uint32_t)k1[u];
           if (c < a.nt) {
             gj[u] = c;
             fixed[u] = false;
           }
         }
       }
-      // the winners' records (point, normal) and fp32 points (the next seeds)
       double tq[kP][3], tn[kP][3];
       float4 t32[kP];
 #pragma unroll
@@ -1562,7 +1607,7 @@ __global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a,
             tn[u][k] = a.est == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
           }
         }
-        t32[u] = a.tgt32[l];
+        t32[u] = a.tgt32[l];  // the next iteration's seed point
       }
 #pragma unroll
       for (int u = 0; u < kP; ++u) {
@@ -1576,9 +1621,8 @@ __global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a,
           }
         }
         a.corr[ii[u]] = (int32_t)gj[u];
-        seedp[u * kTermsBlock + tid] =
-            gj[u] >= 0 ? make_float4(t32[u].x, t32[u].y, t32[u].z, __int_as_float((int32_t)gj[u]))
-                       : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+        seed[u] = gj[u] >= 0 ? make_float4(t32[u].x, t32[u].y, t32[u].z, __int_as_float((int32_t)gj[u]))
+                             : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
         if (gj[u] < 0 || gj[u] >= a.nt) continue;
         terms_add(acc, vs[u], tq[u], tn[u], d2[u], a.est, a.c);
       }
@@ -1622,12 +1666,12 @@ __global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a,
     // out-of-range tile adds +0.0 as there), then the 32 group sums in group order
     {
       const int slot = tid & (kTermSlots - 1);
-      for (int g = tid / kTermSlots; g < kReduceGroups; g += kT / kTermSlots) {
+      for (int gg = tid / kTermSlots; gg < kReduceGroups; gg += kT / kTermSlots) {
         constexpr int kMaxPer = 8;  // ntiles ≤ 256 (api.cpp)
         double tv[kMaxPer];
 #pragma unroll
         for (int r = 0; r < kMaxPer; ++r) {
-          const int64_t b = g + (int64_t)r * kReduceGroups;
+          const int64_t b = gg + (int64_t)r * kReduceGroups;
           tv[r] = b < ntiles ? __longlong_as_double(__hip_atomic_load(
                                    reinterpret_cast<unsigned long long*>(P + b * kTermSlots + slot),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
@@ -1636,7 +1680,7 @@ __global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a,
         double gv = 0.0;
 #pragma unroll
         for (int r = 0; r < kMaxPer; ++r) gv += tv[r];
-        gsum[g][slot] = gv;
+        gsum[gg][slot] = gv;
       }
     }
     __syncthreads();
@@ -1653,15 +1697,11 @@ __global__ __launch_bounds__(kPTile) void icp_grid_persist_kernel(PersistArgs a,
       solve_state(gsum[0], &S, sp, in);
     }
   }
-  if (kProf && prof) {  // [0..6] workgroup 0's phases; [8 + 2b], [9 + 2b]: workgroup b's scan, terms; [7] cache hits
+  if (kProf && prof) {  // [0..6] workgroup 0's phases; [8 + 2b], [9 + 2b]: workgroup b's scan, terms
     if (blockIdx.x == 0)
       for (int k = 0; k < 7; ++k) atomicAdd(a.prof + k, tph[k]);
     a.prof[8 + 2 * blockIdx.x] = tph[1];
     a.prof[9 + 2 * blockIdx.x] = tph[2];
-  }
-  if (kProf) {
-    const unsigned long long hb = __reduce_add_sync(~0ull, hits);
-    if (lane == 0) atomicAdd(a.prof + 7, hb);
   }
   __syncthreads();
   if (blockIdx.x == 0)
@@ -2048,8 +2088,34 @@ hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t
 // the whole grid is resident.  Flags M3D_ICP_PERSIST / M3D_ICP_NO_PERSIST, else the env default
 // M3D_ICP_PERSIST = 1 | 0 (off when unset); M3D_PERSIST_LANES = 1 | 2
 // (lanes per query, 512 or 1024 threads per workgroup).
+// rows × points per lane and load batch (M3D_PERSIST_RB = 22 | 24 | 28 | 44, tuning)
+static int persist_rb() {
+  static const int v = [] {
+    const char* e = getenv("M3D_PERSIST_RB");
+    const int k = e ? atoi(e) : 24;
+    return (k == 22 || k == 24 || k == 28 || k == 44) ? k : 24;
+  }();
+  return v;
+}
+
+template <bool kProf>
+static void persist_launch(int rb, unsigned grid, const PersistArgs& a, IcpState* st_, const SolveParams& sp,
+                           hipStream_t st) {
+  switch (rb) {
+    case 22: icp_grid_persist_kernel<2, 2, kProf><<<grid, kTermsBlock, 0, st>>>(a, st_, sp); break;
+    case 28: icp_grid_persist_kernel<2, 8, kProf><<<grid, kTermsBlock, 0, st>>>(a, st_, sp); break;
+    case 44: icp_grid_persist_kernel<4, 4, kProf><<<grid, kTermsBlock, 0, st>>>(a, st_, sp); break;
+    default: icp_grid_persist_kernel<2, 4, kProf><<<grid, kTermsBlock, 0, st>>>(a, st_, sp); break;
+  }
+}
+
 static const void* persist_fn() {
-  return reinterpret_cast<const void*>(&icp_grid_persist_kernel<2, 2, false>);
+  switch (persist_rb()) {
+    case 22: return reinterpret_cast<const void*>(&icp_grid_persist_kernel<2, 2, false>);
+    case 28: return reinterpret_cast<const void*>(&icp_grid_persist_kernel<2, 8, false>);
+    case 44: return reinterpret_cast<const void*>(&icp_grid_persist_kernel<4, 4, false>);
+    default: return reinterpret_cast<const void*>(&icp_grid_persist_kernel<2, 4, false>);
+  }
 }
 
 bool icp_persist_ok(const m3d_icp* s) {
@@ -2068,7 +2134,7 @@ bool icp_persist_ok(const m3d_icp* s) {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, persist_fn(), kPTile, 0) != hipSuccess) {
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, persist_fn(), kTermsBlock, 0) != hipSuccess) {
       (void)hipGetLastError();
       cap = 0;
     } else {
@@ -2111,18 +2177,18 @@ hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st) {
   static unsigned long long* prof = [] {  // M3D_PERSIST_PROF=1: phase ticks, printed per launch
     const char* e = getenv("M3D_PERSIST_PROF");
     unsigned long long* p = nullptr;
-    if (e && atoi(e) == 1 && hipMalloc(&p, (8 + 2 * 256) * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
+    if (e && atoi(e) == 1 && hipMalloc(&p, (520 + 64) * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
     return p;
   }();
   a.prof = prof;
-  if (prof != nullptr) (void)hipMemsetAsync(prof, 0, (8 + 2 * 256) * sizeof(unsigned long long), st);
+  if (prof != nullptr) (void)hipMemsetAsync(prof, 0, (520 + 64) * sizeof(unsigned long long), st);
   const SolveParams sp = solve_params(s);
   if (prof != nullptr)
-    icp_grid_persist_kernel<2, 2, true><<<(unsigned)ntiles, kPTile, 0, st>>>(a, s->state, sp);
+    persist_launch<true>(persist_rb(), (unsigned)ntiles, a, s->state, sp, st);
   else
-    icp_grid_persist_kernel<2, 2, false><<<(unsigned)ntiles, kPTile, 0, st>>>(a, s->state, sp);
+    persist_launch<false>(persist_rb(), (unsigned)ntiles, a, s->state, sp, st);
   if (prof != nullptr) {
-    std::vector<unsigned long long> h(8 + 2 * 256);
+    std::vector<unsigned long long> h(520 + 64);
     int khz = 0, dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
@@ -2130,9 +2196,8 @@ hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st) {
         hipStreamSynchronize(st) == hipSuccess && khz > 0) {
       const double us = 1e3 / khz;
       fprintf(stderr, "[m3d persist] %lld tiles, n=%d, us per iteration: top %.2f scan %.2f terms %.2f "
-              "publish %.2f wait %.2f reduce %.2f (solve in 'top'); LDS box hits %.1f%%\n", (long long)ntiles, n,
-              h[0] * us / n, h[1] * us / n, h[2] * us / n, h[3] * us / n, h[4] * us / n, h[5] * us / n,
-              100.0 * h[7] / std::max<double>(1.0, (double)s->src->n * n));
+              "publish %.2f wait %.2f reduce %.2f (solve in 'top')\n", (long long)ntiles, n,
+              h[0] * us / n, h[1] * us / n, h[2] * us / n, h[3] * us / n, h[4] * us / n, h[5] * us / n);
       std::vector<double> sc, te, tot;
       for (int64_t b = 0; b < ntiles; ++b) {
         sc.push_back(h[8 + 2 * b] * us / n);
@@ -2149,6 +2214,13 @@ hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st) {
               "med %.2f p90 %.2f max %.2f | worst tile %lld (scan %.2f terms %.2f)\n",
               q(sc, 0), q(sc, 0.5), q(sc, 0.9), q(sc, 1), q(te, 0), q(te, 0.5), q(te, 0.9), q(te, 1),
               (long long)worst, sc[worst], te[worst]);
+      std::string hs;
+      for (int k = 0; k < std::min(n, 64); ++k) {
+        char b[16];
+        snprintf(b, sizeof(b), " %.1f", 100.0 * h[520 + k] / std::max<double>(1.0, (double)s->src->n));
+        hs += b;
+      }
+      fprintf(stderr, "[m3d persist]   box hits per iteration (%%):%s\n", hs.c_str());
     }
   }
   return hipGetLastError();

@@ -271,7 +271,7 @@ def main():
         tgt_c = (Cloud(tgt_all, nrm_all) if not multi else
                  Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0)))
     src_c = Cloud(src)
-    K_NN, K_TERMS, K_COMM = _lib.KERNEL_NN, _lib.KERNEL_TERMS, _lib.KERNEL_COMM
+    K_NN, K_TERMS, K_COMM, K_LOOP = _lib.KERNEL_NN, _lib.KERNEL_TERMS, _lib.KERNEL_COMM, _lib.KERNEL_LOOP
 
     def split_times(prof, el_ev, evals):
         """Per evaluation (one NN + terms + exchange), from the events pass: the NN, terms and
@@ -286,16 +286,20 @@ def main():
                 "exchange_note": ("library RCCL all-reduces timed by events on their streams"
                                   if comm_name == "libm3d-rccl" else "exchange not issued by the library")}
 
-    def bench_icp(nn):
-        loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters, nn=nn)
+    def bench_icp(nn, persist=None):
+        loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters, nn=nn,
+                       persist=persist)
         if mode1 == "source":
             loop.set_source_total(ns * world)
         run = icp_runner(loop, iters, mode1, off, ns * world)
         for _ in range(args.warmup):
             run()
         torch.cuda.synchronize()
-        el, el_ev, prof = timed(run, args.steps, (K_NN, K_TERMS))
+        el, el_ev, prof = timed(run, args.steps, (K_NN, K_TERMS, K_LOOP))
         (nn_ms, nn_n), (t_ms, t_n) = prof[K_NN], prof[K_TERMS]
+        if persist:  # one persistent launch per step: per-evaluation time of that launch
+            lp_ms, lp_n = prof[K_LOOP]
+            return el, el_ev, max_over_ranks(lp_ms / max(lp_n, 1) / (iters + 1)), lp_n, None, loop.result()
         return el, el_ev, max_over_ranks(nn_ms / max(nn_n, 1)), nn_n, t_ms / max(t_n, 1), loop.result()
 
     el, el_ev, nn_avg_ms, nn_n, terms_avg_ms, res = bench_icp("brute")
@@ -321,7 +325,22 @@ def main():
         IcpLoop(src_c, tgt_c, r, max_iteration=0, nn="grid")  # builds both clouds' grids once
         torch.cuda.synchronize()
         build_ms = (time.perf_counter() - tg0) * 1e3
-        gel, gel_ev, g_ms, g_n, g_terms_ms, gres = bench_icp("grid")
+        gel, gel_ev, g_ms, g_n, g_terms_ms, gres = bench_icp("grid", persist=False)
+        # the same loop as ONE persistent launch per step (icp.hip icp_grid_persist_kernel; the
+        # same bits), single device only
+        persist = None
+        if not multi:
+            pel, pel_ev, p_ms, p_n, _, pres = bench_icp("grid", persist=True)
+            p_bytes = 28 * ns + 16 * nt + 84 * ns  # the scan's bytes + the terms' 84 B per source
+            persist = {"value": iters * args.steps / pel, "ms_per_step": pel / args.steps * 1e3,
+                       "same_result_as_two_launch": bool(np.array_equal(pres.transformation, gres.transformation)
+                                                          and pres.fitness == gres.fitness),
+                       "per_evaluation_ms": p_ms,
+                       "roofline": {"bound": "hbm", "kernel": "icp_grid_persist_kernel",
+                                    "achieved": p_bytes / (p_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                    "unit": "GB/s", "frac": p_bytes / (p_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    "bytes_per_evaluation": p_bytes,
+                                    "note": "algorithmic bytes of one scan + terms pass per evaluation"}}
         g_bytes = 28 * ns + 16 * nt
         g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
         icp_grid = {
@@ -335,6 +354,7 @@ def main():
                          "traffic": pmc_traffic("grid_nn")[0], "avg_launch_ms": g_ms,
                          "launches": g_n, "bytes_per_launch": g_bytes,
                          "terms_avg_launch_ms": g_terms_ms},
+            "persistent": persist,
         }
 
     # ------------------------------------------------------------------ cfg1 strong scaling
