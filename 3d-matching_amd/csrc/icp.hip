@@ -1133,7 +1133,11 @@ __device__ __forceinline__ void solve_in(const IcpState* s, SolveIn& in) {
   for (int k = 0; k < 12; ++k) in.rt[k] = s->Rt32[k];
 }
 
-__device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp, const SolveIn& in) {
+// clk (diagnostics, null in production): wall clock at entry, after the LDLT, after the update
+// matrix, after T ← ΔT·T, at the end (the persistent loop's M3D_PERSIST_PROF)
+__device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp, const SolveIn& in,
+                            unsigned long long* clk = nullptr) {
+  if (clk != nullptr) clk[0] = wall_clock64();
   double sm[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) sm[k] = sums[k];
@@ -1185,7 +1189,9 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
         }
       for (int a = 0; a < 6; ++a) b[a] = -sm[21 + a];
       ldlt6_solve(A, b, x);
+      if (clk != nullptr) clk[1] = wall_clock64();
       vec6_to_matrix_wave(x, upd);
+      if (clk != nullptr) clk[2] = wall_clock64();
     } else {
       const double n = count;
       double mp[3], mq[3], Hm[9], R[9];
@@ -1208,10 +1214,12 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   if (!finite)
     for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
   matmul4(upd, T, T);
+  if (clk != nullptr) clk[3] = wall_clock64();
 #pragma unroll
   for (int k = 0; k < 16; ++k) s->T[k] = T[k];
   s->iters = iters + 1;
   refresh_rt32_from(s, T, r2, sp.f);
+  if (clk != nullptr) clk[4] = wall_clock64();
 }
 
 __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
@@ -1694,7 +1702,14 @@ __global__ __launch_bounds__(kTermsBlock) void icp_grid_persist_kernel(PersistAr
     if (tid < kWave) {
       SolveIn in;
       solve_in(&S, in);
-      solve_state(gsum[0], &S, sp, in);
+      unsigned long long clk[5] = {0, 0, 0, 0, 0};
+      solve_state(gsum[0], &S, sp, in, kProf ? clk : nullptr);
+      if (kProf && prof && clk[4] != 0) {
+        atomicAdd(a.prof + 600, clk[1] - clk[0]);
+        atomicAdd(a.prof + 601, clk[2] - clk[1]);
+        atomicAdd(a.prof + 602, clk[3] - clk[2]);
+        atomicAdd(a.prof + 603, clk[4] - clk[3]);
+      }
     }
   }
   if (kProf && prof) {  // [0..6] workgroup 0's phases; [8 + 2b], [9 + 2b]: workgroup b's scan, terms
@@ -2177,18 +2192,18 @@ hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st) {
   static unsigned long long* prof = [] {  // M3D_PERSIST_PROF=1: phase ticks, printed per launch
     const char* e = getenv("M3D_PERSIST_PROF");
     unsigned long long* p = nullptr;
-    if (e && atoi(e) == 1 && hipMalloc(&p, (520 + 64) * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
+    if (e && atoi(e) == 1 && hipMalloc(&p, 640 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
     return p;
   }();
   a.prof = prof;
-  if (prof != nullptr) (void)hipMemsetAsync(prof, 0, (520 + 64) * sizeof(unsigned long long), st);
+  if (prof != nullptr) (void)hipMemsetAsync(prof, 0, 640 * sizeof(unsigned long long), st);
   const SolveParams sp = solve_params(s);
   if (prof != nullptr)
     persist_launch<true>(persist_rb(), (unsigned)ntiles, a, s->state, sp, st);
   else
     persist_launch<false>(persist_rb(), (unsigned)ntiles, a, s->state, sp, st);
   if (prof != nullptr) {
-    std::vector<unsigned long long> h(520 + 64);
+    std::vector<unsigned long long> h(640);
     int khz = 0, dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
@@ -2221,6 +2236,8 @@ hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st) {
         hs += b;
       }
       fprintf(stderr, "[m3d persist]   box hits per iteration (%%):%s\n", hs.c_str());
+      fprintf(stderr, "[m3d persist]   solve (all workgroups' wave 0, us per solve): ldlt+entry %.2f update %.2f matmul %.2f refresh %.2f\n",
+              h[600] * us / (n * ntiles), h[601] * us / (n * ntiles), h[602] * us / (n * ntiles), h[603] * us / (n * ntiles));
     }
   }
   return hipGetLastError();
