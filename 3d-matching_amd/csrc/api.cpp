@@ -218,6 +218,108 @@ int center_pack(m3d_ctx* ctx, const double* a, int64_t n, int64_t n_pad, const d
 
 int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
+// Host arrays → device.  Default: pageable hipMemcpyAsync straight into the cloud's buffers (the
+// runtime stages them itself).  M3D_UPLOAD=stage (measured slower, kept for A/B): the host pool's
+// threads copy M3D_UPLOAD_CHUNK-byte chunks (default 1 MB) into the context's pinned staging
+// memory while the caller issues each chunk's DMA as soon as that chunk and all before it are
+// staged (hostio.cpp host_pipeline); uploads larger than the staging cap go in rounds (each round
+// waits for the previous one's DMAs before it refills the buffer).  M3D_UPLOAD=register: the host
+// arrays are page-locked in place (hipHostRegister) for the copy.
+int upload_host(m3d_ctx* ctx, int narr, void* const* dst, const void* const* src, const size_t* bytes,
+                hipStream_t st) {
+  static const int mode = [] {
+    const char* e = getenv("M3D_UPLOAD");
+    if (e && strcmp(e, "stage") == 0) return 1;
+    if (e && strcmp(e, "register") == 0) return 2;
+    return 0;
+  }();
+  static const size_t kChunk = [] {
+    const char* e = getenv("M3D_UPLOAD_CHUNK");
+    const long v = e ? atol(e) : 0;
+    return v >= 4096 ? (size_t)v : ((size_t)1 << 20);
+  }();
+  size_t total = 0;
+  for (int i = 0; i < narr; ++i) total += bytes[i];
+  if (total == 0) return M3D_OK;
+  if (mode == 0) {
+    for (int i = 0; i < narr; ++i)
+      if (bytes[i] > 0) HIPX(ctx, hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyHostToDevice, st));
+    return M3D_OK;
+  }
+  if (mode == 2) {
+    hipError_t e = hipSuccess;
+    int nreg = 0;
+    for (int i = 0; i < narr && e == hipSuccess; ++i) {
+      if (bytes[i] == 0) continue;
+      e = hipHostRegister(const_cast<void*>(src[i]), bytes[i], hipHostRegisterDefault);
+      if (e != hipSuccess) break;
+      nreg = i + 1;
+      e = hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyHostToDevice, st);
+    }
+    const hipError_t es = hipStreamSynchronize(st);
+    for (int i = 0; i < nreg; ++i)
+      if (bytes[i] > 0) (void)hipHostUnregister(const_cast<void*>(src[i]));
+    if (e == hipSuccess) e = es;
+    if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+    return M3D_OK;
+  }
+  constexpr size_t kCap = (size_t)64 << 20;
+  const size_t want = std::min(kCap, (size_t)round_up((int64_t)total, (int64_t)1 << 22));
+  if (ctx->stage_ev == nullptr) HIPX(ctx, hipEventCreateWithFlags(&ctx->stage_ev, hipEventDisableTiming));
+  if (ctx->stage_cap < want) {
+    if (ctx->stage_pending) HIPX(ctx, hipEventSynchronize(ctx->stage_ev));
+    ctx->stage_pending = false;
+    if (ctx->stage != nullptr) hipHostFree(ctx->stage);
+    ctx->stage = nullptr;
+    ctx->stage_cap = 0;
+    if (hipHostMalloc(&ctx->stage, want, hipHostMallocDefault) != hipSuccess) {
+      ctx->stage = nullptr;
+      return m3d_fail(ctx, M3D_ERR_OOM, "pinned staging memory");
+    }
+    ctx->stage_cap = want;
+  }
+  struct Piece {
+    char* d;
+    const char* s;
+    size_t len, soff;
+  };
+  std::vector<Piece> pieces;
+  size_t done_bytes = 0;
+  int i = 0;
+  size_t off = 0;
+  while (done_bytes < total) {
+    // one round: up to stage_cap bytes of the concatenated arrays, cut into chunks
+    pieces.clear();
+    size_t soff = 0;
+    while (i < narr && soff < ctx->stage_cap) {
+      if (off >= bytes[i]) {
+        ++i;
+        off = 0;
+        continue;
+      }
+      const size_t len = std::min({kChunk, bytes[i] - off, ctx->stage_cap - soff});
+      pieces.push_back(Piece{static_cast<char*>(dst[i]) + off, static_cast<const char*>(src[i]) + off, len, soff});
+      off += len;
+      soff += len;
+    }
+    if (ctx->stage_pending) HIPX(ctx, hipEventSynchronize(ctx->stage_ev));
+    char* stage = static_cast<char*>(ctx->stage);
+    hipError_t err = hipSuccess;
+    host_pipeline(
+        (int64_t)pieces.size(),
+        [&](int64_t k) { memcpy(stage + pieces[(size_t)k].soff, pieces[(size_t)k].s, pieces[(size_t)k].len); },
+        [&](int64_t k) {
+          const Piece& pc = pieces[(size_t)k];
+          if (err == hipSuccess) err = hipMemcpyAsync(pc.d, stage + pc.soff, pc.len, hipMemcpyHostToDevice, st);
+        });
+    if (err == hipSuccess) err = hipEventRecord(ctx->stage_ev, st);
+    if (err != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(err));
+    ctx->stage_pending = true;
+    done_bytes += soff;
+  }
+  return M3D_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -266,7 +368,10 @@ void m3d_destroy(m3d_ctx* ctx) {
   if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->one_ticket) hipFree(ctx->one_ticket);
   if (ctx->prep) hipFree(ctx->prep);
+  if (ctx->stage) hipHostFree(ctx->stage);
+  if (ctx->stage_ev) hipEventDestroy(ctx->stage_ev);
   ctx->tmp.release();
+  ctx->run.release();
   for (auto& v : ctx->ev)
     for (auto& pr : v) {
       hipEventDestroy(pr.first);
@@ -795,8 +900,24 @@ int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int
   return m3d_cloud_create_framed(ctx, xyz, normals, n, nullptr, stream, out);
 }
 
+namespace {
+int cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n, const double* center,
+                 bool host, void* stream, m3d_cloud** out);
+}
+
 int m3d_cloud_create_framed(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
                             const double* center, void* stream, m3d_cloud** out) {
+  return cloud_create(ctx, xyz, normals, n, center, false, stream, out);
+}
+
+int m3d_cloud_create_host(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                          const double* center, void* stream, m3d_cloud** out) {
+  return cloud_create(ctx, xyz, normals, n, center, true, stream, out);
+}
+
+namespace {
+int cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n, const double* center,
+                 bool host, void* stream, m3d_cloud** out) {
   if (!ctx) return M3D_ERR_INVALID;
   CHECK_ARG(ctx, out != nullptr, "null output");
   CHECK_ARG(ctx, n >= 0 && n < (int64_t)1 << 31, "point count out of range");
@@ -817,7 +938,16 @@ int m3d_cloud_create_framed(m3d_ctx* ctx, const double* xyz, const double* norma
     m3d_cloud_destroy(c);
     return rc;
   }
-  if (n > 0) {
+  if (n > 0 && host) {
+    void* const dst[2] = {c->xyz64, c->nrm64};
+    const void* const srcs[2] = {xyz, normals};
+    const size_t bytes[2] = {sizeof(double) * 3 * (size_t)n, normals ? sizeof(double) * 3 * (size_t)n : 0};
+    rc = upload_host(ctx, 2, dst, srcs, bytes, st);
+    if (rc) {
+      m3d_cloud_destroy(c);
+      return rc;
+    }
+  } else if (n > 0) {
     hipError_t e = hipMemcpyAsync(c->xyz64, xyz, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess && normals)
       e = hipMemcpyAsync(c->nrm64, normals, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st);
@@ -844,6 +974,7 @@ int m3d_cloud_create_framed(m3d_ctx* ctx, const double* xyz, const double* norma
   *out = c;
   return M3D_OK;
 }
+}  // namespace
 
 void m3d_cloud_destroy(m3d_cloud* c) {
   if (!c) return;
@@ -963,8 +1094,23 @@ int icp_shard_nn_range(m3d_icp* s, int64_t off, int64_t q0, int64_t q1, int64_t*
 }  // namespace m3d
 }  // extern "C++"
 
+namespace {
+int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
+               const m3d_icp_params* params, m3d_icp** out, bool run_arena);
+}
+
 int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
                    const m3d_icp_params* params, m3d_icp** out) {
+  return icp_create(ctx, src, tgt, max_dist, params, out, false);
+}
+
+namespace {
+// run_arena: the loop's arrays come from the context's run arena (kept between calls) instead of
+// their own allocation — for the synchronous one-shot entry points (m3d_icp_run, m3d_nn1), whose
+// loop object dies inside the call: no hipMalloc / hipFree (≈0.2 ms, the free waits for the
+// device and unmaps) per call
+int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
+               const m3d_icp_params* params, m3d_icp** out, bool run_arena) {
   if (!ctx) return M3D_ERR_INVALID;
   CHECK_ARG(ctx, src && tgt && params && out, "invalid arguments");
   CHECK_ARG(ctx, max_dist > 0.0, "Invalid max_correspondence_distance.");
@@ -1010,6 +1156,18 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
     stage("tgrid");
     if (!grc) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
     stage("sgrid");
+    // the loop runs on the source in Morton slot order (its grid derived from sg)
+    const m3d_cloud* ms = nullptr;
+    if (!grc) grc = ensure_morton_source(ctx, src, sg, cell, &ms, &sg);
+    if (!grc) src_m = ms;
+    stage("morton");
+    if (!grc) {
+      hipError_t e = ensure_target_rec(tgt, nullptr);
+      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("target records: ") + hipGetErrorString(e));
+    }
+    stage("rec");
+    // (after the source grid, Morton copy and target records are enqueued: the occupancy's one
+    // sync then also covers them instead of stalling the queue in between)
     // Grid NN on a dense target: a seeded query's box is ~1–2 cells per axis, so the candidates
     // it scans grow with the points per cell.  Shrink the target cell by div = ⌊√(m / 3.5)⌋
     // (m = points per occupied cell at cell ≈ r; any cell size gives the same keys, grid.hip):
@@ -1026,16 +1184,6 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
       if (div > 1) grc = ensure_grid(ctx, tgt, cell / div, nullptr, &tg);
     }
     stage("tgrid_div");
-    // the loop runs on the source in Morton slot order (its grid derived from sg)
-    const m3d_cloud* ms = nullptr;
-    if (!grc) grc = ensure_morton_source(ctx, src, sg, cell, &ms, &sg);
-    if (!grc) src_m = ms;
-    stage("morton");
-    if (!grc) {
-      hipError_t e = ensure_target_rec(tgt, nullptr);
-      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("target records: ") + hipGetErrorString(e));
-    }
-    stage("rec");
     if (!grc && params->nn_method == M3D_NN_BRUTE && tg->mf16 == nullptr) {
       hipError_t e = build_mfma_tiles(tgt, const_cast<Grid*>(tg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("mfma tiles: ") + hipGetErrorString(e));
@@ -1079,11 +1227,17 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
       off[k] = tot;
       tot += tmp_align(sz[k]);
     }
-    if (hipMalloc(&s->block, tot) != hipSuccess) {
-      s->block = nullptr;
-      rc = m3d_fail(ctx, M3D_ERR_OOM, "hipMalloc failed (ICP loop arrays)");
+    char* b = nullptr;
+    if (run_arena) {
+      if (ctx->run.reserve(tot) == hipSuccess) b = ctx->run.base;
+    } else if (hipMalloc(&s->block, tot) == hipSuccess) {
+      b = static_cast<char*>(s->block);
     } else {
-      char* b = static_cast<char*>(s->block);
+      s->block = nullptr;
+    }
+    if (b == nullptr) {
+      rc = m3d_fail(ctx, M3D_ERR_OOM, "device allocation failed (ICP loop arrays)");
+    } else {
       s->state = reinterpret_cast<IcpState*>(b + off[0]);
       s->keys = reinterpret_cast<int64_t*>(b + off[1]);
       s->near2 = reinterpret_cast<uint32_t*>(b + off[2]);
@@ -1113,6 +1267,7 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
   *out = s;
   return M3D_OK;
 }
+}  // namespace
 
 void m3d_icp_destroy(m3d_icp* s) {
   if (!s) return;
@@ -1365,6 +1520,34 @@ int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream) {
   return M3D_OK;
 }
 
+int m3d_corr_pairs(m3d_ctx* ctx, const int32_t* corr_idx, int64_t n, int32_t* pairs_out, int64_t* count,
+                   void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, count != nullptr && n >= 0 && n < (int64_t)1 << 31, "invalid arguments");
+  CHECK_ARG(ctx, n == 0 || (corr_idx != nullptr && pairs_out != nullptr), "null array");
+  *count = 0;
+  if (n == 0) return M3D_OK;
+  hipSetDevice(ctx->device);
+  hipStream_t st = S(stream);
+  const int64_t nb = (n + 1023) / 1024;
+  const size_t o_p = tmp_align(sizeof(int32_t) * (size_t)(nb + 1));
+  if (ctx->tmp.reserve(o_p + sizeof(int32_t) * 2 * (size_t)n) != hipSuccess)
+    return m3d_fail(ctx, M3D_ERR_OOM, "correspondence pairs scratch");
+  int32_t* cnt = reinterpret_cast<int32_t*>(ctx->tmp.base);
+  int32_t* pairs = reinterpret_cast<int32_t*>(ctx->tmp.base + o_p);
+  int32_t m = 0;
+  hipError_t e = launch_corr_pairs(corr_idx, n, cnt, pairs, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(&m, cnt + nb, sizeof(m), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && m > 0) {
+    e = hipMemcpyAsync(pairs_out, pairs, sizeof(int32_t) * 2 * (size_t)m, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
+  if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  *count = m;
+  return M3D_OK;
+}
+
 const int32_t* m3d_icp_corr(const m3d_icp* s) { return s ? s->corr : nullptr; }
 
 int m3d_icp_copy_corr(const m3d_icp* s, int32_t* dst, void* stream) {
@@ -1387,19 +1570,63 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
                 int32_t* corr_idx, void* stream) {
   if (!ctx) return M3D_ERR_INVALID;
   CHECK_ARG(ctx, out != nullptr, "null output");
+  // M3D_RUN_PROF=1 (diagnostics): wall ms of each stage, synchronised in between
+  static const bool rprof = [] {
+    const char* e = getenv("M3D_RUN_PROF");
+    return e && atoi(e) == 1;
+  }();
+  double tprev = 0.0;
+  std::string rstages;
+  auto stage = [&](const char* name) {
+    if (!rprof) return;
+    (void)hipDeviceSynchronize();
+    const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (name != nullptr) rstages += std::string(" ") + name + " " + std::to_string(t - tprev);
+    tprev = t;
+  };
+  stage(nullptr);
   m3d_icp* s = nullptr;
-  int rc = m3d_icp_create(ctx, src, tgt, max_dist, params, &s);
+  int rc = icp_create(ctx, src, tgt, max_dist, params, &s, true);
   if (rc) return rc;
+  stage("create");
   rc = m3d_icp_reset(s, init, stream);
-  // max_iteration + 1 evaluations: one persistent launch for the grid loop, else step by step
-  if (!rc) rc = m3d_icp_steps(s, params->max_iteration + 1, stream);
+  // max_iteration + 1 evaluations: one persistent launch for the grid loop, else enqueued in
+  // growing chunks (4, 8, 16, …) with a look at the state's `done` between chunks — a converged
+  // loop (often after a handful of evaluations) then does not enqueue the remaining ~2 launches
+  // per evaluation that would only read `done` and return.  The evaluations that run are the
+  // same; only the early-exit launches are skipped.
+  if (!rc) {
+    const int32_t total = params->max_iteration + 1;
+    if (icp_persist_ok(s)) {
+      rc = m3d_icp_steps(s, total, stream);
+    } else {
+      int32_t left = total, chunk = 4;
+      while (!rc && left > 0) {
+        const int32_t k = std::min(chunk, left);
+        rc = m3d_icp_steps(s, k, stream);
+        left -= k;
+        chunk *= 2;
+        if (rc || left == 0) break;
+        int32_t done = 0;
+        hipError_t e = hipMemcpyAsync(&done, &s->state->done, sizeof(done), hipMemcpyDeviceToHost, S(stream));
+        if (e == hipSuccess) e = hipStreamSynchronize(S(stream));
+        if (e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+        if (done) break;
+      }
+    }
+  }
+  stage("steps");
   if (!rc) rc = m3d_icp_result_get(s, out, stream);
+  stage("result");
   if (!rc && corr_idx && src->n > 0) {
     hipError_t e = launch_scatter_i32(s->corr, s->src->slot, src->n, corr_idx, S(stream));
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));
     if (e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   }
+  stage("corr");
   m3d_icp_destroy(s);
+  stage("destroy");
+  if (rprof) fprintf(stderr, "[m3d run] ms:%s evaluations %d\n", rstages.c_str(), out->iterations + 1);
   return rc;
 }
 
@@ -1410,7 +1637,7 @@ int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const doub
   CHECK_ARG(ctx, max_dist > 0.0, "max_dist must be > 0");
   m3d_icp_params p{1e-6, 1e-6, 0, M3D_EST_POINT_TO_POINT, nn_method, 0};
   m3d_icp* s = nullptr;
-  int rc = m3d_icp_create(ctx, src, tgt, max_dist, &p, &s);
+  int rc = icp_create(ctx, src, tgt, max_dist, &p, &s, true);
   if (rc) return rc;
   hipStream_t st = S(stream);
   rc = m3d_icp_reset(s, T_host, stream);

@@ -14,6 +14,8 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <functional>
+#include <memory>
 #include <limits>
 #include <mutex>
 #include <thread>
@@ -574,62 +576,80 @@ inline void chunk_digest(const HashJob& j) {
   }
 }
 
-// Persistent workers (created on first use); a job list is handed out with one atomic counter,
-// the caller works too and waits for the last chunk.
-class HashPool {
+// Persistent workers (created on first use): a batch of n items is handed out with one atomic
+// counter; the caller works too and waits for the last item.  In-order form (host_pipeline): the
+// caller also receives each item's completion in index order (e.g. to issue the DMA of a staged
+// chunk as soon as it and every chunk before it are ready).
+class WorkPool {
  public:
-  static HashPool& get() {
-    static HashPool* pool = new HashPool();  // never destroyed: workers outlive static teardown
+  static WorkPool& get() {
+    static WorkPool* pool = new WorkPool();  // never destroyed: workers outlive static teardown
     return *pool;
   }
-  void run(const std::vector<HashJob>& jobs) {
+  void run(int64_t n, const std::function<void(int64_t)>& fn, const std::function<void(int64_t)>* in_order) {
     std::lock_guard<std::mutex> one(run_mu_);  // one batch at a time
+    std::unique_ptr<std::atomic<uint8_t>[]> done(new std::atomic<uint8_t>[(size_t)std::max<int64_t>(n, 1)]);
+    for (int64_t k = 0; k < n; ++k) done[k].store(0, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> lk(mu_);
-      jobs_ = &jobs;
+      fn_ = &fn;
+      n_ = n;
+      done_ = done.get();
       next_.store(0);
-      left_.store((int64_t)jobs.size());
+      left_.store(n);
       ++gen_;
     }
     cv_.notify_all();
-    work(&jobs);
+    if (in_order == nullptr) {
+      work();
+    } else {
+      for (int64_t k = 0; k < n;) {
+        if (done[k].load(std::memory_order_acquire)) {
+          (*in_order)(k++);
+          continue;
+        }
+        if (!take_one()) std::this_thread::yield();
+      }
+    }
     std::unique_lock<std::mutex> lk(mu_);
-    // every chunk done AND every worker that joined this batch out of work(): the job list is
-    // the caller's and dies with this call
+    // every item done AND every worker that joined this batch out of work(): the function and
+    // the flags are the caller's and die with this call
     done_cv_.wait(lk, [&] { return left_.load() == 0 && active_ == 0; });
-    jobs_ = nullptr;
+    fn_ = nullptr;
+    done_ = nullptr;
   }
 
  private:
-  HashPool() {
+  WorkPool() {
     const int n = std::max(0, std::min(host_threads(), 8) - 1);
     for (int t = 0; t < n; ++t)
       std::thread([this] { loop(); }).detach();
   }
-  void work(const std::vector<HashJob>* js) {
-    for (;;) {
-      const int64_t k = next_.fetch_add(1);
-      if (k >= (int64_t)js->size()) return;
-      const HashJob& j = (*js)[(size_t)k];
-      chunk_digest(j);
-      if (left_.fetch_sub(1) == 1) {
-        std::lock_guard<std::mutex> lk(mu_);
-        done_cv_.notify_all();
-      }
+  bool take_one() {
+    const int64_t k = next_.fetch_add(1);
+    if (k >= n_) return false;
+    (*fn_)(k);
+    done_[k].store(1, std::memory_order_release);
+    if (left_.fetch_sub(1) == 1) {
+      std::lock_guard<std::mutex> lk(mu_);
+      done_cv_.notify_all();
+    }
+    return true;
+  }
+  void work() {
+    while (take_one()) {
     }
   }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
-      const std::vector<HashJob>* js;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen && jobs_ != nullptr; });
+        cv_.wait(lk, [&] { return gen_ != seen && fn_ != nullptr; });
         seen = gen_;
-        js = jobs_;
         ++active_;
       }
-      work(js);
+      work();
       {
         std::lock_guard<std::mutex> lk(mu_);
         --active_;
@@ -639,12 +659,30 @@ class HashPool {
   }
   std::mutex run_mu_, mu_;
   std::condition_variable cv_, done_cv_;
-  const std::vector<HashJob>* jobs_ = nullptr;
+  const std::function<void(int64_t)>* fn_ = nullptr;
+  std::atomic<uint8_t>* done_ = nullptr;
+  int64_t n_ = 0;
   std::atomic<int64_t> next_{0}, left_{0};
   uint64_t gen_ = 0;
   int active_ = 0;  // workers inside work() for the current batch (guarded by mu_)
 };
 }  // namespace
+
+extern "C++" {
+namespace m3d {
+void host_pipeline(int64_t n, const std::function<void(int64_t)>& fn, const std::function<void(int64_t)>& in_order) {
+  if (n <= 0) return;
+  if (host_threads() > 1 && n > 1) {
+    WorkPool::get().run(n, fn, &in_order);
+    return;
+  }
+  for (int64_t k = 0; k < n; ++k) {
+    fn(k);
+    in_order(k);
+  }
+}
+}  // namespace m3d
+}  // extern "C++"
 
 uint64_t m3d_debug_xxh64(const void* p, size_t len, uint64_t seed) {
   return xxh64(static_cast<const uint8_t*>(p), len, seed);
@@ -683,7 +721,8 @@ int m3d_content_keys(const void* const* bufs, const size_t* lens, int32_t n, uin
     }
   }
   if (jobs.size() >= 4 && host_threads() > 1) {
-    HashPool::get().run(jobs);
+    const std::function<void(int64_t)> fn = [&](int64_t k) { chunk_digest(jobs[(size_t)k]); };
+    WorkPool::get().run((int64_t)jobs.size(), fn, nullptr);
   } else {
     for (const HashJob& j : jobs) chunk_digest(j);
   }

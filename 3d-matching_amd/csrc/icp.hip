@@ -1757,6 +1757,90 @@ __global__ void scatter_i32_kernel(const int32_t* __restrict__ v, const int32_t*
   if (k < n) dst[slot[k]] = v[k];
 }
 
+// ------------------------------------------------------------------------------- pairs
+// The correspondence set (Open3D RegistrationResult.correspondence_set): (i, v[i]) for every i
+// with v[i] ≥ 0, in increasing i.  An order-preserving compaction in three launches over chunks
+// of 1024 entries (256 threads × 4, entry base + u·256 + t): per-chunk counts, one block's
+// exclusive scan of the counts, placement (per-wave ballots, LDS prefix over the chunk's 16
+// (u, wave) groups in index order).
+constexpr int kPairChunk = 1024;
+
+__global__ __launch_bounds__(256) void pair_count_kernel(const int32_t* __restrict__ v, int64_t n,
+                                                         int32_t* __restrict__ cnt) {
+  __shared__ int part[4];
+  const int64_t base = (int64_t)blockIdx.x * kPairChunk;
+  int c = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = base + u * 256 + threadIdx.x;
+    c += __popcll(__ballot(i < n && v[i] >= 0));
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) part[threadIdx.x / kWave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// one block: cnt[0..nb) → exclusive offsets in place, the total in cnt[nb]
+__global__ __launch_bounds__(1024) void pair_scan_kernel(int32_t* __restrict__ cnt, int64_t nb) {
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry_s;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
+    const int64_t b = b0 + threadIdx.x;
+    const int32_t x = b < nb ? cnt[b] : 0;
+    int32_t incl = x;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int32_t y = __shfl_up(incl, o, kWave);
+      if (lane >= o) incl += y;
+    }
+    if (lane == kWave - 1) wsum[w] = incl;
+    __syncthreads();
+    int32_t before = carry_s;
+    for (int k = 0; k < w; ++k) before += wsum[k];
+    if (b < nb) cnt[b] = before + incl - x;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry_s = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cnt[nb] = carry_s;
+}
+
+__global__ __launch_bounds__(256) void pair_place_kernel(const int32_t* __restrict__ v, int64_t n,
+                                                         const int32_t* __restrict__ off,
+                                                         int32_t* __restrict__ pairs) {
+  __shared__ int grp[16];  // popcount of group (u, wave), index order u·4 + wave
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int64_t base = (int64_t)blockIdx.x * kPairChunk;
+  bool hit[4];
+  int32_t val[4];
+  uint64_t m[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = base + u * 256 + threadIdx.x;
+    val[u] = i < n ? v[i] : -1;
+    hit[u] = val[u] >= 0;
+    m[u] = __ballot(hit[u]);
+    if (lane == 0) grp[u * 4 + w] = __popcll(m[u]);
+  }
+  __syncthreads();
+  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int32_t o = off[blockIdx.x];  // entries of the chunk's rows before row u
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    int32_t before = o;
+    for (int k = 0; k < w; ++k) before += grp[u * 4 + k];
+    if (hit[u]) {
+      const int32_t k = before + __popcll(m[u] & below);
+      pairs[2 * (int64_t)k] = (int32_t)(base + u * 256 + threadIdx.x);
+      pairs[2 * (int64_t)k + 1] = val[u];
+    }
+    for (int k = 0; k < 4; ++k) o += grp[u * 4 + k];
+  }
+}
+
 __global__ void keys_to_idx_kernel(const int64_t* __restrict__ keys, int64_t n,
                                    int32_t* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -2257,6 +2341,15 @@ hipError_t launch_scatter_i32(const int32_t* v, const int32_t* slot, int64_t n, 
   if (n == 0) return hipSuccess;
   if (slot == nullptr) return hipMemcpyAsync(dst, v, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st);
   scatter_i32_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(v, slot, n, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_corr_pairs(const int32_t* v, int64_t n, int32_t* cnt, int32_t* pairs, hipStream_t st) {
+  if (n <= 0) return hipMemsetAsync(cnt, 0, sizeof(int32_t), st);
+  const int64_t nb = (n + kPairChunk - 1) / kPairChunk;
+  pair_count_kernel<<<(unsigned)nb, 256, 0, st>>>(v, n, cnt);
+  pair_scan_kernel<<<1, 1024, 0, st>>>(cnt, nb);
+  pair_place_kernel<<<(unsigned)nb, 256, 0, st>>>(v, n, cnt, pairs);
   return hipGetLastError();
 }
 

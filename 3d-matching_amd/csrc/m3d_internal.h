@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <string>
 #include <utility>
+#include <functional>
 #include <vector>
 
 #include "../../include/m3d.h"
@@ -138,6 +139,9 @@ struct TmpArena {
     cap = 0;
   }
 };
+// hostio.cpp's worker pool: fn(0 .. n-1) over the pool's threads and the caller; in_order(k) runs
+// on the caller's thread once items 0..k are all done, in index order
+void host_pipeline(int64_t n, const std::function<void(int64_t)>& fn, const std::function<void(int64_t)>& in_order);
 // 256-B aligned carve-out of a TmpArena reservation
 inline size_t tmp_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
@@ -171,6 +175,13 @@ struct m3d_ctx {
   void* prep = nullptr;
   size_t prep_bytes = 0;
   m3d::TmpArena tmp;  // setup temporaries (grids, Morton copies, cloud packing)
+  m3d::TmpArena run;  // loop arrays of the synchronous one-shot ICP / NN calls (api.cpp icp_create)
+  // pinned staging memory of the host-array uploads (api.cpp upload_host); stage_ev follows the
+  // last DMA out of it
+  void* stage = nullptr;
+  size_t stage_cap = 0;
+  hipEvent_t stage_ev = nullptr;
+  bool stage_pending = false;
 };
 
 struct m3d_corrset {
@@ -398,6 +409,9 @@ hipError_t grid_morton(Grid* g, hipStream_t st, TmpArena* ta = nullptr);
 // asynchronous (stream order)
 hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Grid* gout, hipStream_t st);
 // dst[slot[k]] = v[k], k < n (slot-ordered loop arrays → the caller's source order)
+// correspondence pairs (i, v[i]) for v[i] >= 0 in increasing i; cnt: (n + 1023) / 1024 + 1 ints of
+// scratch, the total in cnt[(n + 1023) / 1024] (cnt[0] when n == 0)
+hipError_t launch_corr_pairs(const int32_t* v, int64_t n, int32_t* cnt, int32_t* pairs, hipStream_t st);
 hipError_t launch_scatter_i32(const int32_t* v, const int32_t* slot, int64_t n, int32_t* dst,
                               hipStream_t st);
 hipError_t launch_keys_to_idx(const int64_t* keys, int64_t n, int32_t* idx, hipStream_t st);

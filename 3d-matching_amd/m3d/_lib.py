@@ -30,7 +30,7 @@ COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2
 OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -94,6 +94,7 @@ SIGNATURES = {
                                      C.POINTER(i32)]),
     "m3d_cloud_create": (C.c_int, [vp, vp, vp, i64, vp, C.POINTER(vp)]),
     "m3d_cloud_create_framed": (C.c_int, [vp, vp, vp, i64, C.POINTER(C.c_double), vp, C.POINTER(vp)]),
+    "m3d_cloud_create_host": (C.c_int, [vp, vp, vp, i64, C.POINTER(C.c_double), vp, C.POINTER(vp)]),
     "m3d_cloud_destroy": (None, [vp]),
     "m3d_cloud_size": (i64, [vp]),
     "m3d_nn1": (C.c_int, [vp, vp, vp, C.POINTER(dbl), dbl, i32, vp, vp, vp]),
@@ -114,6 +115,7 @@ SIGNATURES = {
     "m3d_icp_set_source_total": (C.c_int, [vp, i64]),
     "m3d_icp_corr": (vp, [vp]),
     "m3d_icp_copy_corr": (C.c_int, [vp, vp, vp]),
+    "m3d_corr_pairs": (C.c_int, [vp, vp, i64, vp, C.POINTER(i64), vp]),
     "m3d_icp_copy_slots": (C.c_int, [vp, vp, vp]),
     "m3d_voxel_down_sample": (C.c_int, [vp, vp, vp, i64, dbl, vp, vp, C.POINTER(i64), vp]),
     "m3d_hybrid_search": (C.c_int, [vp, vp, dbl, i32, vp, vp, vp, vp]),

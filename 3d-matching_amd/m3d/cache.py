@@ -191,9 +191,19 @@ def corrset_gathered(p_src, p_tgt) -> CorrSet:
 
 
 def cloud(points, normals=None) -> Cloud:
-    points = np.asarray(points, np.float64)
-    normals = None if normals is None else np.asarray(normals, np.float64)
-    return _get(("cl", array_key(points), array_key(normals)), lambda: Cloud(points, normals))
+    return clouds([(points, normals)])[0]
+
+
+def clouds(pairs) -> list:
+    """cloud() of several (points, normals-or-None) pairs, the content keys of every array in ONE
+    batch (one wake-up of the library's hash pool instead of one per array)."""
+    arrs = [(np.asarray(p, np.float64), None if n is None else np.asarray(n, np.float64)) for p, n in pairs]
+    if _POLICY == "content":
+        flat = _content_keys([a for pn in arrs for a in pn])
+        keys = [(flat[2 * k], flat[2 * k + 1]) for k in range(len(arrs))]
+    else:
+        keys = [(array_key(p), array_key(n)) for p, n in arrs]
+    return [_get(("cl",) + k, lambda p=p, n=n: Cloud(p, n)) for k, (p, n) in zip(keys, arrs)]
 
 
 def clear():

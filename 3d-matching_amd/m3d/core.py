@@ -346,18 +346,33 @@ class Cloud:
     (m3d_cloud_create_framed)."""
 
     def __init__(self, points, normals=None, ctx: Context | None = None, center=None):
+        """points / normals: torch cuda tensors (device arrays: m3d_cloud_create[_framed]) or
+        host arrays (numpy / sequences: m3d_cloud_create_host, the library's staged upload)."""
         self.ctx = ctx or context()
-        p = to_device(points)
-        nrm = None if normals is None else to_device(normals)
+        torch = _torch()
+        on_dev = isinstance(points, torch.Tensor) and points.is_cuda
+        if on_dev:
+            p = to_device(points)
+            nrm = None if normals is None else to_device(normals)
+        else:
+            require_device()
+            p = np.ascontiguousarray(np.asarray(points, np.float64).reshape(-1, 3))
+            nrm = None if normals is None else np.ascontiguousarray(
+                np.asarray(normals.cpu() if isinstance(normals, torch.Tensor) else normals,
+                           np.float64).reshape(-1, 3))
         if nrm is not None and nrm.shape != p.shape:
             raise ValueError("normals must match points")
         self.n = p.shape[0]
         h = C.c_void_p()
-        if center is None:
+        c3 = None if center is None else (C.c_double * 3)(*[float(x) for x in np.asarray(center, np.float64).reshape(3)])
+        if not on_dev:
+            rc = self.ctx.lib.m3d_cloud_create_host(self.ctx.h, p.ctypes.data if self.n else None,
+                                                    nrm.ctypes.data if nrm is not None else None, self.n, c3,
+                                                    stream_handle(), C.byref(h))
+        elif center is None:
             rc = self.ctx.lib.m3d_cloud_create(self.ctx.h, ptr(p), ptr(nrm), self.n, stream_handle(),
                                                C.byref(h))
         else:
-            c3 = (C.c_double * 3)(*[float(x) for x in np.asarray(center, np.float64).reshape(3)])
             rc = self.ctx.lib.m3d_cloud_create_framed(self.ctx.h, ptr(p), ptr(nrm), self.n, c3,
                                                       stream_handle(), C.byref(h))
         self.ctx.check(rc, "cloud_create")
@@ -411,6 +426,17 @@ class IcpOutcome:
     correspondence_set: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.int32))
 
 
+def corr_pairs(ctx: Context, corr, n: int) -> np.ndarray:
+    """RegistrationResult.correspondence_set of a per-source index array (cuda int32, -1 none):
+    the (i, corr[i]) pairs with corr[i] >= 0 in increasing i, compacted on the device
+    (m3d_corr_pairs) — only the pairs cross to the host."""
+    out = np.empty((max(n, 1), 2), np.int32)
+    m = C.c_int64(0)
+    ctx.check(ctx.lib.m3d_corr_pairs(ctx.h, ptr(corr) if n > 0 else None, int(n), out.ctypes.data, C.byref(m),
+                                     stream_handle()), "corr_pairs")
+    return out[: m.value]
+
+
 def icp(src: Cloud, tgt: Cloud, max_dist: float, init=None, estimation=_lib.EST_POINT_TO_PLANE,
         relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30, with_correspondences=True,
         nn: str = "grid", persist=None):
@@ -424,11 +450,7 @@ def icp(src: Cloud, tgt: Cloud, max_dist: float, init=None, estimation=_lib.EST_
     init16 = _T16(np.eye(4) if init is None else init)
     src.ctx.check(src.ctx.lib.m3d_icp_run(src.ctx.h, src.h, tgt.h, init16, float(max_dist), C.byref(p),
                                           C.byref(res), ptr(corr), stream_handle()), "icp_run")
-    cs = np.zeros((0, 2), np.int32)
-    if with_correspondences and src.n > 0:
-        j = corr[: src.n].cpu().numpy()
-        i = np.nonzero(j >= 0)[0]
-        cs = np.stack([i, j[i]], axis=1).astype(np.int32)
+    cs = corr_pairs(src.ctx, corr, src.n) if with_correspondences else np.zeros((0, 2), np.int32)
     return IcpOutcome(np.array(res.T[:]).reshape(4, 4), res.fitness, res.inlier_rmse,
                       res.num_correspondences, res.iterations, bool(res.converged), cs)
 

@@ -23,7 +23,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from .core import Cloud, _torch, context, ptr, stream_handle, to_device
+from .core import Cloud, _torch, context, corr_pairs, ptr, stream_handle, to_device
 
 
 def voxel_down_sample(points, voxel_size: float, normals=None):
@@ -144,8 +144,6 @@ def ransac_on_correspondences(src, tgt, corres, max_correspondence_distance: flo
     ctx.check(ctx.lib.m3d_ransac_on_correspondences(ctx.h, sc.h, tc.h, ptr(corr), corr.shape[0], C.byref(p),
                                                     C.byref(r), ptr(cs), stream_handle()),
               "ransac_on_correspondences")
-    j = cs[: sc.n].cpu().numpy()
-    i = np.nonzero(j >= 0)[0]
     return FeatureRansacOutcome(np.array(r.T[:]).reshape(4, 4), r.fitness, r.inlier_rmse,
-                                int(r.best_index), int(r.validations),
-                                np.stack([i, j[i]], axis=1).astype(np.int32), float(r.corres_ratio))
+                                int(r.best_index), int(r.validations), corr_pairs(ctx, cs, sc.n),
+                                float(r.corres_ratio))

@@ -42,8 +42,7 @@ def registration_icp(source, target, max_correspondence_distance, init=None,
     if est == _lib.EST_POINT_TO_PLANE and tn is None:
         raise ValueError("TransformationEstimationPointToPlane and TransformationEstimationColoredICP "
                          "require pre-computed normal vectors for target PointCloud.")
-    src = _cache.cloud(sp)
-    tgt = _cache.cloud(tp, tn if est == _lib.EST_POINT_TO_PLANE else None)
+    src, tgt = _cache.clouds([(sp, None), (tp, tn if est == _lib.EST_POINT_TO_PLANE else None)])
     out = _icp(src, tgt, max_correspondence_distance, init=np.eye(4) if init is None else init,
                estimation=est, relative_fitness=relative_fitness, relative_rmse=relative_rmse,
                max_iteration=max_iteration)

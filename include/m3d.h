@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 10
+#define M3D_ABI_VERSION 11
 
 /* return codes */
 #define M3D_OK 0
@@ -187,6 +187,13 @@ int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int
  * bound instead of the radius (nnkey.h seed_key) — same result, far fewer screen hits. */
 int m3d_cloud_create_framed(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
                             const double* center, void* stream, m3d_cloud** out);
+/* The same from HOST arrays (ABI 11): xyz [host] n×3 f64, normals [host] n×3 f64 or NULL, center
+ * [host] 3 f64 or NULL (the cloud's mean).  The library's host threads copy the arrays in 256 KB
+ * chunks into the context's pinned staging memory and each chunk's DMA is issued as soon as it is
+ * staged (copies and DMAs overlap) — instead of a caller's single-threaded pageable upload plus a
+ * device-to-device copy.  The same cloud, bit for bit.  Synchronous. */
+int m3d_cloud_create_host(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                          const double* center, void* stream, m3d_cloud** out);
 void m3d_cloud_destroy(m3d_cloud* c);
 int64_t m3d_cloud_size(const m3d_cloud* c);
 
@@ -336,6 +343,14 @@ int m3d_comm_poisoned(const m3d_comm* c);
 
 /* Read the loop state (synchronises the stream). */
 int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream);
+/* The correspondence set of a per-source index array (RegistrationResult.correspondence_set,
+ * icp.py:42 / ransac.py:42-59; ABI 11): pairs_out [host] with room for 2·n int32 receives
+ * (i, corr_idx[i]) for every i with corr_idx[i] >= 0, in increasing i; *count [host] = the number
+ * of pairs.  corr_idx [device] n int32 (m3d_icp_run's corr_idx, m3d_icp_copy_corr's dst, the
+ * feature RANSAC's corr_set_out).  Compacted on the device; only the pairs cross to the host.
+ * Synchronous. */
+int m3d_corr_pairs(m3d_ctx* ctx, const int32_t* corr_idx, int64_t n, int32_t* pairs_out, int64_t* count,
+                   void* stream);
 /* Device pointer to the current correspondence index array (ns int32, -1 = none) in SOURCE SLOT
  * order (see m3d_icp_copy_slots); m3d_icp_copy_corr gives it in source order. */
 const int32_t* m3d_icp_corr(const m3d_icp* s);

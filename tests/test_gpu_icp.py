@@ -262,6 +262,76 @@ def test_step_loop_matches_run():
 
 
 @pytest.mark.parametrize("nn", ["brute", "grid"])
+@pytest.mark.parametrize("max_iteration", [0, 1, 3, 7, 30])
+def test_run_chunks_match_stepped_loop(nn, max_iteration):
+    """m3d_icp_run enqueues its evaluations in chunks of 4, 8, 16, … and stops enqueueing once the
+    state says done: converging (Open3D criteria) and non-converging runs give the loop's bits,
+    iteration count and correspondence set."""
+    import torch
+
+    src, tgt, nrm, _ = synth.icp_pair(20000, seed=12)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    for crit in ((1e-6, 1e-6), (-1.0, -1.0)):
+        full = icp(s, t, 0.12, np.eye(4), relative_fitness=crit[0], relative_rmse=crit[1],
+                   max_iteration=max_iteration, nn=nn, persist=False)
+        loop = IcpLoop(s, t, 0.12, relative_fitness=crit[0], relative_rmse=crit[1],
+                       max_iteration=max_iteration, nn=nn, persist=False)
+        loop.reset(np.eye(4))
+        for _ in range(max_iteration + 1):
+            loop.step()
+        r = loop.result()
+        np.testing.assert_array_equal(r.transformation, full.transformation)
+        assert (r.fitness, r.iterations, r.converged) == (full.fitness, full.iterations, full.converged)
+        jj = loop.correspondences().cpu().numpy()
+        i = np.flatnonzero(jj >= 0)
+        np.testing.assert_array_equal(full.correspondence_set, np.stack([i, jj[i]], 1))
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, 100_000, 3_000_000])
+def test_host_cloud_equals_device_cloud(n):
+    """m3d_cloud_create_host (the staged upload: 256 KB chunks, rounds past the 64 MB staging cap
+    at 3M points with normals) builds the cloud m3d_cloud_create builds from device arrays: the
+    same NN (indices and d²) and, with normals, the same ICP bits."""
+    import torch
+
+    rng = np.random.default_rng(n)
+    pts = rng.normal(size=(n, 3)) * 3.0
+    nrm = rng.normal(size=(n, 3))
+    q = pts[: min(n, 20000)] + rng.normal(size=(min(n, 20000), 3)) * 0.01
+    a_t, a_n = Cloud(pts, nrm), Cloud(torch.from_numpy(pts).cuda(), torch.from_numpy(nrm).cuda())
+    assert a_t.n == a_n.n == n
+    s = Cloud(q)
+    T = synth.random_rigid(5, rot_range=0.001, trans_range=0.001)
+    i1, d1 = nn1(s, a_t, T, 0.05, nn="grid")
+    i2, d2 = nn1(s, a_n, T, 0.05, nn="grid")
+    np.testing.assert_array_equal(i1.cpu().numpy(), i2.cpu().numpy())
+    np.testing.assert_array_equal(d1.cpu().numpy(), d2.cpu().numpy())
+    if n >= 5:
+        r1 = icp(s, a_t, 0.05, np.eye(4), max_iteration=3)
+        r2 = icp(s, a_n, 0.05, np.eye(4), max_iteration=3)
+        np.testing.assert_array_equal(r1.transformation, r2.transformation)
+        np.testing.assert_array_equal(r1.correspondence_set, r2.correspondence_set)
+
+
+@pytest.mark.parametrize("n", [0, 1, 1023, 1024, 1025, 4096, 100_000, 3_000_001])
+def test_corr_pairs_compaction(n):
+    """m3d_corr_pairs: the (i, v[i]) pairs for v[i] >= 0 in increasing i, against numpy, at chunk
+    edges, with none / all / a random half valid."""
+    import torch
+
+    from m3d.core import context, corr_pairs
+
+    rng = np.random.default_rng(n)
+    ctx = context()
+    for frac in (0.0, 1.0, 0.5):
+        v = np.where(rng.random(n) < frac, rng.integers(0, 1 << 30, n), -1).astype(np.int32)
+        got = corr_pairs(ctx, torch.from_numpy(v).cuda(), n)
+        i = np.flatnonzero(v >= 0)
+        assert got.dtype == np.int32 and got.shape == (len(i), 2)
+        np.testing.assert_array_equal(got, np.stack([i, v[i]], 1).astype(np.int32))
+
+
+@pytest.mark.parametrize("nn", ["brute", "grid"])
 def test_graph_replay_matches_enqueued_steps(nn):
     """m3d_icp_steps captures an n-step sequence into a HIP graph the second time it is requested
     (one graph per keys-clean state on entry) and replays it; it must compute what the steps

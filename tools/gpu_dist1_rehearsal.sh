@@ -22,5 +22,11 @@ print(sys.argv[1], "comm", d["config"]["comm"], "| cfg1 %.1f it/s err %.2e" % (d
       "| strong %.1f grid %s" % (s["value"], s.get("grid_value")),
       "| ransac %.3g strong %.3g best %s" % (r["value"], r["strong"]["value"], r["strong"].get("best_count")),
       "| cfg3 %.1f grid %.1f" % (c3["value"], c3["grid"]["value"]))
+keys = ("per_evaluation_ms_with_events", "nn_ms_per_evaluation", "terms_ms_per_evaluation",
+        "exchange_ms_per_evaluation", "allreduces_per_evaluation")
+for name, sec in (("cfg1_strong", s), ("cfg3", c3), ("cfg3.grid", c3["grid"]),
+                  ("cfg3.split_off", c3.get("split_off") or {}), ("cfg3.grid.split_off", c3["grid"].get("split_off") or {})):
+    print("  %-20s" % name, " ".join("%s=%s" % (k.replace("_per_evaluation", ""), None if sec.get(k) is None else round(sec[k], 4)) for k in keys))
+print("  ransac.strong score_ms %s exchange_ms %s" % (r["strong"].get("score_ms_per_run"), r["strong"].get("exchange_ms_per_run")))
 PY
 done
