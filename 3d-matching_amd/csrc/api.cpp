@@ -1032,12 +1032,14 @@ int ensure_morton_source(m3d_ctx* ctx, const m3d_cloud* c, const Grid* sg, doubl
       *gout = m.second->grids.front();
       return M3D_OK;
     }
-  hipError_t e = grid_morton(const_cast<Grid*>(sg), nullptr, &ctx->tmp);
+  // sg == nullptr: straight from the points (grid.hip morton_source, the same slots without the
+  // source's cell grid); else derived from the source grid (morton_copy)
+  hipError_t e = sg != nullptr ? grid_morton(const_cast<Grid*>(sg), nullptr, &ctx->tmp) : hipSuccess;
   m3d_cloud* mc = new m3d_cloud();
   mc->ctx = ctx;
   Grid* g = new Grid();
   mc->grids.push_back(g);
-  if (e == hipSuccess) e = morton_copy(c, sg, mc, g, nullptr);
+  if (e == hipSuccess) e = sg != nullptr ? morton_copy(c, sg, mc, g, nullptr) : morton_source(c, cell, mc, g, &ctx->tmp, nullptr);
   if (e != hipSuccess) {
     m3d_cloud_destroy(mc);
     return m3d_fail(ctx, M3D_ERR_HIP, std::string("morton source: ") + hipGetErrorString(e));
@@ -1154,9 +1156,17 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
     const double cell = max_dist * 1.001 / cell_div;
     int grc = ensure_grid(ctx, tgt, cell, nullptr, &tg);
     stage("tgrid");
-    if (!grc) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
+    // the source's own cell grid only for the A/B switches that read it (M3D_NN_QORDER=cell
+    // orders brute-force queries by its cells; M3D_MORTON_DIRECT=0 derives the Morton slots from
+    // it as in round 3); by default the Morton slots come straight from the points
+    static const bool src_grid = [] {
+      const char* q = getenv("M3D_NN_QORDER");
+      const char* m = getenv("M3D_MORTON_DIRECT");
+      return (q && strcmp(q, "cell") == 0) || (m && atoi(m) == 0);
+    }();
+    if (!grc && src_grid) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
     stage("sgrid");
-    // the loop runs on the source in Morton slot order (its grid derived from sg)
+    // the loop runs on the source in Morton slot order (sg: the copy's query grid afterwards)
     const m3d_cloud* ms = nullptr;
     if (!grc) grc = ensure_morton_source(ctx, src, sg, cell, &ms, &sg);
     if (!grc) src_m = ms;
@@ -1214,7 +1224,7 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
     const char* e = getenv("M3D_NN_QORDER");
     return e && strcmp(e, "cell") == 0;
   }();
-  s->qorder = cell_order ? sg->order : nullptr;
+  s->qorder = cell_order ? sg->order : nullptr;  // (cell_order builds the source grid, above)
   s->sgrid = sg;
   // the loop's arrays in ONE allocation (one hipMalloc instead of nine)
   int rc = M3D_OK;

@@ -445,6 +445,31 @@ __global__ __launch_bounds__(kGridBlock) void count_occupied_pts_kernel(const fl
   if ((threadIdx.x & (kWave - 1)) == 0 && b != 0) atomicAdd(occ, (unsigned long long)__popcll(b));
 }
 
+// The dense cell array over [lo, hi] for a requested cell size: origin, cells per axis, 1/h; the
+// cell grows until the grid has at most kMaxCells cells.  Returns the cell size h.
+static double grid_params(const float lo[3], const float hi[3], double cell, GridDev& d) {
+  double h = cell > 0.0 && std::isfinite(cell) ? cell : 1.0;
+  int64_t nn[3], total = 0;
+  for (;;) {
+    total = 1;
+    for (int k = 0; k < 3; ++k) {
+      const double ext = std::isfinite((double)hi[k] - lo[k]) ? (double)hi[k] - lo[k] : 0.0;
+      nn[k] = (int64_t)std::floor(ext / h) + 1;
+      total *= nn[k];
+      if (total > kMaxCells) break;
+    }
+    if (total <= kMaxCells) break;
+    h *= 1.26;
+  }
+  for (int k = 0; k < 3; ++k) {
+    d.o[k] = lo[k];
+    d.n[k] = (int)nn[k];
+  }
+  d.inv_h = (float)(1.0 / h);
+  d.ncells = total;
+  return h;
+}
+
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g, TmpArena* ta,
                       const float* lohi) {
   g->n_pts = n;
@@ -478,26 +503,8 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
         hi[k] = std::max(hi[k], hp[6 * b + 3 + k]);
       }
   }
-  // cell size: requested, grown until the dense grid has at most kMaxCells cells
-  double h = cell > 0.0 && std::isfinite(cell) ? cell : 1.0;
-  int64_t nn[3], total = 0;
-  for (;;) {
-    total = 1;
-    for (int k = 0; k < 3; ++k) {
-      const double ext = std::isfinite((double)hi[k] - lo[k]) ? (double)hi[k] - lo[k] : 0.0;
-      nn[k] = (int64_t)std::floor(ext / h) + 1;
-      total *= nn[k];
-      if (total > kMaxCells) break;
-    }
-    if (total <= kMaxCells) break;
-    h *= 1.26;
-  }
-  for (int k = 0; k < 3; ++k) {
-    d.o[k] = lo[k];
-    d.n[k] = (int)nn[k];
-  }
-  d.inv_h = (float)(1.0 / h);
-  d.ncells = total;
+  const double h = grid_params(lo, hi, cell, d);
+  const int64_t total = d.ncells;
   g->cell = h;
   // (cell, index) pairs → stable radix sort; the sorted indices land in g->order
   uint32_t *kin = nullptr, *kout = nullptr;
@@ -734,6 +741,122 @@ hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Gri
   gout->dev.start = gout->start;
   gout->dev.pts = gout->pts;
   gout->occ_known = sg->occ_known;
+  return hipSuccess;
+}
+
+// The same copy straight from the source's points (m3d_icp_create's default since round 4): the
+// Morton key of each point's cell under the grid parameters grid_build would choose (the cloud's
+// bounds, cell size), one stable radix sort of (key, index) from index order, one copy pass —
+// instead of a cell sort, a Morton sort of the cell-ordered points and a copy.  Without
+// coarsening (≤ 1024 cells per axis) equal keys mean equal cells, so both orders are (Morton key,
+// index): the same slots.  The copy's grid keeps only what the loop reads of a query grid (its
+// Morton points and slot map, grid parameters); its cell arrays are not built (ncells = 0, and
+// cell_req = −1 so no cell-size request ever matches it).
+__global__ __launch_bounds__(kGridBlock) void morton_key_src_kernel(const float4* __restrict__ pts, int64_t n,
+                                                                    GridDev g, int sx, int sy, int sz,
+                                                                    uint32_t* __restrict__ key,
+                                                                    int32_t* __restrict__ val) {
+  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (k >= n) return;
+  const float4 v = pts[k];
+  const uint32_t cx = (uint32_t)grid_coord(v.x, g.o[0], g.inv_h, g.n[0]) >> sx;
+  const uint32_t cy = (uint32_t)grid_coord(v.y, g.o[1], g.inv_h, g.n[1]) >> sy;
+  const uint32_t cz = (uint32_t)grid_coord(v.z, g.o[2], g.inv_h, g.n[2]) >> sz;
+  key[k] = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
+  val[k] = (int32_t)k;
+}
+
+__global__ __launch_bounds__(kGridBlock) void morton_src_copy_kernel(
+    const double* __restrict__ xyz64, const double* __restrict__ nrm64, const float4* __restrict__ xyz32,
+    const int32_t* __restrict__ perm, int64_t n, double* __restrict__ oxyz64, double* __restrict__ onrm64,
+    float4* __restrict__ oxyz32, int32_t* __restrict__ slot, float4* __restrict__ ompts,
+    int32_t* __restrict__ ominv) {
+  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
+  if (k >= n) return;
+  const int64_t j = perm[k];
+  slot[k] = (int32_t)j;
+  for (int a = 0; a < 3; ++a) oxyz64[3 * k + a] = xyz64[3 * j + a];
+  if (onrm64 != nullptr)
+    for (int a = 0; a < 3; ++a) onrm64[3 * k + a] = nrm64[3 * j + a];
+  const float4 v = xyz32[j];
+  oxyz32[k] = v;
+  ompts[k] = make_float4(v.x, v.y, v.z, __int_as_float((int32_t)k));
+  ominv[k] = (int32_t)k;
+}
+
+hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid* gout, TmpArena* ta,
+                         hipStream_t st) {
+  const int64_t n = src->n;
+  out->n = n;
+  out->n_pad = src->n_pad;
+  for (int k = 0; k < 3; ++k) out->center[k] = src->center[k];
+  out->rmax = src->rmax;
+  for (int k = 0; k < 3; ++k) {
+    out->lo[k] = src->lo[k];
+    out->hi[k] = src->hi[k];
+  }
+  out->has_bounds = src->has_bounds;
+  out->s16 = src->s16;
+  out->center_given = src->center_given;
+  gout->n_pts = n;
+  gout->n_occ = 0;
+  gout->occ_known = false;
+  gout->cell_req = -1.0;
+  GridDev d;
+  d.ncells = 0;
+  float lo[3] = {0.0f, 0.0f, 0.0f}, hi[3] = {0.0f, 0.0f, 0.0f};
+  if (src->has_bounds)
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = src->lo[k];
+      hi[k] = src->hi[k];
+    }
+  gout->cell = grid_params(lo, hi, cell, d);
+  gout->dev = d;
+  gout->dev.ncells = 0;  // no cell arrays
+  gout->dev.start = nullptr;
+  gout->dev.pts = nullptr;
+  const size_t n1 = (size_t)std::max<int64_t>(n, 1);
+  hipError_t e;
+  if ((e = hipMalloc(&out->xyz64, sizeof(double) * 3 * n1)) != hipSuccess ||
+      (src->nrm64 != nullptr && (e = hipMalloc(&out->nrm64, sizeof(double) * 3 * n1)) != hipSuccess) ||
+      (e = hipMalloc(&out->xyz32, sizeof(float4) * (size_t)std::max<int64_t>(src->n_pad, 1))) != hipSuccess ||
+      (e = hipMalloc(&out->slot, sizeof(int32_t) * n1)) != hipSuccess ||
+      (e = hipMalloc(&gout->mpts, sizeof(float4) * n1)) != hipSuccess ||
+      (e = hipMalloc(&gout->minv, sizeof(int32_t) * n1)) != hipSuccess)
+    return e;
+  if (n == 0) return hipSuccess;
+  int sh[3];
+  for (int k = 0; k < 3; ++k) {
+    sh[k] = 0;
+    while ((d.n[k] >> sh[k]) > 1024) ++sh[k];
+  }
+  uint32_t *kin = nullptr, *kout = nullptr;
+  int32_t *vin = nullptr, *vout = nullptr;
+  size_t tmp_bytes = 0;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st)) !=
+      hipSuccess)
+    return e;
+  tmp_bytes = std::max<size_t>(tmp_bytes, 1);
+  const size_t a4 = tmp_align(sizeof(uint32_t) * (size_t)n);
+  if ((e = ta->reserve(4 * a4 + tmp_align(tmp_bytes))) != hipSuccess) return e;
+  kin = reinterpret_cast<uint32_t*>(ta->base);
+  kout = reinterpret_cast<uint32_t*>(ta->base + a4);
+  vin = reinterpret_cast<int32_t*>(ta->base + 2 * a4);
+  vout = reinterpret_cast<int32_t*>(ta->base + 3 * a4);
+  void* tmp = ta->base + 4 * a4;
+  const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
+  morton_key_src_kernel<<<blocks, kGridBlock, 0, st>>>(src->xyz32, n, d, sh[0], sh[1], sh[2], kin, vin);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st)) !=
+      hipSuccess)
+    return e;
+  morton_src_copy_kernel<<<blocks, kGridBlock, 0, st>>>(src->xyz64, src->nrm64, src->xyz32, vout, n, out->xyz64,
+                                                        out->nrm64, out->xyz32, out->slot, gout->mpts, gout->minv);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (src->n_pad > n &&
+      (e = hipMemcpyAsync(out->xyz32 + n, src->xyz32 + n, sizeof(float4) * (size_t)(src->n_pad - n),
+                          hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    return e;
   return hipSuccess;
 }
 

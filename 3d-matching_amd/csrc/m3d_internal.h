@@ -408,6 +408,9 @@ hipError_t grid_morton(Grid* g, hipStream_t st, TmpArena* ta = nullptr);
 // the Morton-slot copy of an ICP source (out, gout freshly allocated structs; see grid.hip);
 // asynchronous (stream order)
 hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Grid* gout, hipStream_t st);
+// the same copy straight from the source's points (no source grid): grid.hip morton_source
+hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid* gout, TmpArena* ta,
+                         hipStream_t st);
 // dst[slot[k]] = v[k], k < n (slot-ordered loop arrays → the caller's source order)
 // correspondence pairs (i, v[i]) for v[i] >= 0 in increasing i; cnt: (n + 1023) / 1024 + 1 ints of
 // scratch, the total in cnt[(n + 1023) / 1024] (cnt[0] when n == 0)
