@@ -931,9 +931,14 @@ int cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t
   c->ctx = ctx;
   c->n = n;
   c->n_pad = round_up(std::max<int64_t>(n, 1), kCloudPad);
-  int rc = dev_alloc(ctx, &c->xyz64, 3 * n);
-  if (!rc && normals) rc = dev_alloc(ctx, &c->nrm64, 3 * n);
-  if (!rc) rc = dev_alloc(ctx, &c->xyz32, c->n_pad);
+  int rc = M3D_OK;
+  {
+    Carve cv;  // the three point arrays in one allocation
+    if (n > 0) cv.add(&c->xyz64, 3 * (size_t)n);
+    if (n > 0 && normals) cv.add(&c->nrm64, 3 * (size_t)n);
+    cv.add(&c->xyz32, (size_t)c->n_pad);
+    if (cv.alloc(&c->block, &c->block_bytes) != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_OOM, "hipMalloc failed (cloud)");
+  }
   if (rc) {
     m3d_cloud_destroy(c);
     return rc;
@@ -983,6 +988,10 @@ void m3d_cloud_destroy(m3d_cloud* c) {
     delete g;
   }
   for (auto& m : c->morton) m3d_cloud_destroy(m.second);
+  for (void** p : {reinterpret_cast<void**>(&c->slot), reinterpret_cast<void**>(&c->xyz64),
+                   reinterpret_cast<void**>(&c->nrm64), reinterpret_cast<void**>(&c->xyz32)})
+    if (in_block(*p, c->block, c->block_bytes)) *p = nullptr;
+  hipFree(c->block);
   hipFree(c->slot);
   hipFree(c->xyz64);
   hipFree(c->nrm64);

@@ -513,9 +513,15 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   size_t tmp_bytes = 0;
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) < total) ++bits;
-  hipFree(g->start);
-  hipFree(g->pts);
-  hipFree(g->order);
+  if (g->block != nullptr) {  // a rebuild: the previous cell arrays (one block)
+    hipFree(g->block);
+    g->block = nullptr;
+    g->block_bytes = 0;
+  } else {
+    hipFree(g->start);
+    hipFree(g->pts);
+    hipFree(g->order);
+  }
   g->start = nullptr;
   g->pts = nullptr;
   g->order = nullptr;
@@ -534,10 +540,13 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
     return grid_fail(e, kin, kout, vin, nullptr, tmp);
   }
   auto done = [&](hipError_t r) { return ta != nullptr ? r : grid_fail(r, kin, kout, vin, nullptr, tmp); };
-  if ((e = hipMalloc(&g->order, a4)) != hipSuccess ||
-      (e = hipMalloc(&g->start, sizeof(int32_t) * (total + 1))) != hipSuccess ||
-      (e = hipMalloc(&g->pts, sizeof(float4) * n)) != hipSuccess)
-    return done(e);
+  {
+    Carve cv;
+    cv.add(&g->order, (size_t)n);
+    cv.add(&g->start, (size_t)total + 1);
+    cv.add(&g->pts, (size_t)n);
+    if ((e = cv.alloc(&g->block, &g->block_bytes)) != hipSuccess) return done(e);
+  }
   const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
   cell_id_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, n, d, kin, vin);
   if ((e = hipGetLastError()) != hipSuccess) return done(e);
@@ -586,6 +595,13 @@ hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st) {
 
 void grid_free(Grid* g) {
   if (!g) return;
+  for (void** p : {reinterpret_cast<void**>(&g->start), reinterpret_cast<void**>(&g->pts),
+                   reinterpret_cast<void**>(&g->order), reinterpret_cast<void**>(&g->mpts),
+                   reinterpret_cast<void**>(&g->minv)})
+    if (in_block(*p, g->block, g->block_bytes)) *p = nullptr;
+  hipFree(g->block);
+  g->block = nullptr;
+  g->block_bytes = 0;
   hipFree(g->start);
   hipFree(g->pts);
   hipFree(g->order);
@@ -817,13 +833,18 @@ hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid
   gout->dev.pts = nullptr;
   const size_t n1 = (size_t)std::max<int64_t>(n, 1);
   hipError_t e;
-  if ((e = hipMalloc(&out->xyz64, sizeof(double) * 3 * n1)) != hipSuccess ||
-      (src->nrm64 != nullptr && (e = hipMalloc(&out->nrm64, sizeof(double) * 3 * n1)) != hipSuccess) ||
-      (e = hipMalloc(&out->xyz32, sizeof(float4) * (size_t)std::max<int64_t>(src->n_pad, 1))) != hipSuccess ||
-      (e = hipMalloc(&out->slot, sizeof(int32_t) * n1)) != hipSuccess ||
-      (e = hipMalloc(&gout->mpts, sizeof(float4) * n1)) != hipSuccess ||
-      (e = hipMalloc(&gout->minv, sizeof(int32_t) * n1)) != hipSuccess)
-    return e;
+  {
+    Carve cc, cg;
+    cc.add(&out->xyz64, 3 * n1);
+    if (src->nrm64 != nullptr) cc.add(&out->nrm64, 3 * n1);
+    cc.add(&out->xyz32, (size_t)std::max<int64_t>(src->n_pad, 1));
+    cc.add(&out->slot, n1);
+    cg.add(&gout->mpts, n1);
+    cg.add(&gout->minv, n1);
+    if ((e = cc.alloc(&out->block, &out->block_bytes)) != hipSuccess ||
+        (e = cg.alloc(&gout->block, &gout->block_bytes)) != hipSuccess)
+      return e;
+  }
   if (n == 0) return hipSuccess;
   int sh[3];
   for (int k = 0; k < 3; ++k) {

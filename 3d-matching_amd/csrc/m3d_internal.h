@@ -109,6 +109,9 @@ struct Grid {
   uint4* mf16 = nullptr;
   float4* mf32 = nullptr;
   int64_t mf_npad = 0;
+  // one allocation holding several of the arrays above (Carve; grid_free frees it, not them)
+  void* block = nullptr;
+  size_t block_bytes = 0;
 };
 
 // Device scratch for the temporaries of setup work (grid sorts, Morton copies, cloud packing):
@@ -144,6 +147,35 @@ struct TmpArena {
 void host_pipeline(int64_t n, const std::function<void(int64_t)>& fn, const std::function<void(int64_t)>& in_order);
 // 256-B aligned carve-out of a TmpArena reservation
 inline size_t tmp_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// Several device arrays in ONE allocation (256-B aligned pieces): the setup paths make one
+// hipMalloc per object instead of one per array, and the owner one hipFree.
+struct Carve {
+  std::vector<std::pair<void**, size_t>> parts;
+  template <class T>
+  void add(T** p, size_t count) {
+    parts.emplace_back(reinterpret_cast<void**>(p), tmp_align(sizeof(T) * std::max<size_t>(count, 1)));
+  }
+  hipError_t alloc(void** block, size_t* bytes) {
+    size_t tot = 0;
+    for (auto& q : parts) tot += q.second;
+    void* b = nullptr;
+    const hipError_t e = hipMalloc(&b, std::max<size_t>(tot, 1));
+    *block = e == hipSuccess ? b : nullptr;
+    *bytes = e == hipSuccess ? tot : 0;
+    if (e != hipSuccess) return e;
+    size_t o = 0;
+    for (auto& q : parts) {
+      *q.first = static_cast<char*>(b) + o;
+      o += q.second;
+    }
+    return hipSuccess;
+  }
+};
+// whether p lies inside [block, block + bytes) (the arrays a Carve block holds)
+inline bool in_block(const void* p, const void* block, size_t bytes) {
+  return block != nullptr && p >= block && static_cast<const char*>(p) < static_cast<const char*>(block) + bytes;
+}
 
 constexpr int kTermSlots = 32;  // 21 JTJ + 6 JTr + r² + count + Σd² (+2 pad)
 constexpr int64_t kKeyNone = 0x7FFFFFFFFFFFFFFFll;
@@ -226,6 +258,9 @@ struct m3d_cloud {
   // a Morton copy: live ICP loops running on it (m3d_icp_create / _destroy); the parent keeps at
   // most kMortonKeep copies and evicts the oldest unreferenced one beyond that (api.cpp)
   mutable int refs = 0;
+  // one allocation holding the point arrays (Carve; m3d_cloud_destroy frees it, not them)
+  void* block = nullptr;
+  size_t block_bytes = 0;
 };
 
 struct m3d_icp {
