@@ -516,6 +516,7 @@ void m3d_corrset_destroy(m3d_corrset* cs) {
   hipFree(cs->p32);
   hipFree(cs->q32);
   hipFree(cs->ca16);
+  hipFree(cs->cull_block);  // cas16, rowmap, cca16, tstat
   delete cs;
 }
 
@@ -707,22 +708,53 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
     if (p->early_stop) B = std::min<int64_t>(B, 16384);
   }
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(max_iter, 1)));
+  const double thr_sq = thr_sq_of(p->thr, p->mode);
+  // tile culling of the MFMA screen (ransac.hip, round 4; opt-in M3D_SCORE_CULL=1): the corrset's
+  // sorted rows and tile bounds are built on its first culled run (one sync)
+  const bool cull = nc > 0 && score_cull_on(cs, thr_sq);
+  if (cull) HIPX(ctx, ensure_cull(cs, st));
   Arena a(ctx, S(stream));
   size_t o[kScoreSlots];
   score_layout(a, B, o);
   size_t o_T = a.take(sizeof(double) * 16 * B);
   size_t o_c = a.take(sizeof(int32_t) * B);
+  size_t oc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t hpB = score_mf_hpad(B);
+  const size_t csort = cull ? cull_sort_bytes(hpB) : 0;
+  if (cull) {
+    oc[0] = a.take(sizeof(uint32_t) * hpB);
+    oc[1] = a.take(sizeof(uint32_t) * hpB);
+    oc[2] = a.take(sizeof(int32_t) * hpB);
+    oc[3] = a.take(sizeof(int32_t) * hpB);
+    oc[4] = a.take(sizeof(float) * hpB);
+    oc[5] = a.take(sizeof(float) * hpB);
+    oc[6] = a.take(sizeof(float) * hpB);
+    oc[7] = a.take(sizeof(uint32_t) * (size_t)(hpB / 32) * (size_t)(cs->nsub_pad / 32));
+    oc[8] = a.take(csort);
+  }
   int rc = a.commit();
   if (rc) return rc;
   ScoreScratch s = score_bind(a, o);
   double* Tb = a.at<double>(o_T);
   int32_t* cb = a.at<int32_t>(o_c);
+  ScoreCull cc;
+  if (cull) {
+    cc.key = a.at<uint32_t>(oc[0]);
+    cc.key2 = a.at<uint32_t>(oc[1]);
+    cc.val = a.at<int32_t>(oc[2]);
+    cc.perm = a.at<int32_t>(oc[3]);
+    cc.a = a.at<float>(oc[4]);
+    cc.apos = a.at<float>(oc[5]);
+    cc.edpos = a.at<float>(oc[6]);
+    cc.skip = a.at<uint32_t>(oc[7]);
+    cc.sort_tmp = a.at<char>(oc[8]);
+    cc.sort_bytes = csort;
+  }
   // counts of the hypotheses after an early stop are never scored: they read 0
   if (counts_out != nullptr && max_iter > 0)
     HIPX(ctx, hipMemsetAsync(counts_out, 0, sizeof(int32_t) * max_iter, st));
   HIPX(ctx, launch_ransac_init(ctx->rstate, ctx->stats, max_iter == 0 ? 1 : 0, st));
   const int32_t* done = &ctx->rstate->done;
-  const double thr_sq = thr_sq_of(p->thr, p->mode);
   static const bool fuse_on = [] {  // M3D_RANSAC_FUSE=0: separate hyp16 launch (A/B)
     const char* e = getenv("M3D_RANSAC_FUSE");
     return !(e && atoi(e) == 0);
@@ -736,13 +768,17 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
       KTimer kt(ctx, M3D_KERNEL_KABSCH, st);
       const ScoreFuse fz{&s.mf, p->thr, p->mode};
       e = launch_kabsch3(cs, tri, p->seed, p->hyp0 + b0, n, thr_sq, Tb, nullptr, s.hypf, done,
-                         ZeroArgs{cnt}, st, (nc > 0 && fuse_on) ? &fz : nullptr);
+                         ZeroArgs{cnt}, st, (nc > 0 && fuse_on && !cull) ? &fz : nullptr);
     }
     if (e == hipSuccess) {
-      if (nc > 0)
+      if (cull) {
+        KTimer kt(ctx, M3D_KERNEL_SCORE, st);
+        e = launch_score_culled(cs, Tb, n, p->thr, p->mode, cnt, ctx->stats, done, s.mf, cc, st);
+      } else if (nc > 0) {
         e = score_enqueue(ctx, cs, Tb, n, p->thr, p->mode, cnt, s, done, st, fuse_on);
-      else
+      } else {
         e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * n, st);
+      }
     }
     if (e == hipSuccess)
       e = launch_select(cnt, b0, n, std::max<int64_t>(nc, 1), max_iter, p->early_stop,

@@ -230,6 +230,17 @@ struct m3d_corrset {
   // splits of S·p_c / S·q_c (plane 0: the p part, planes 1-3: the q_x / q_y / q_z parts)
   uint4* ca16 = nullptr;
   double s16 = 0.0;  // the power-of-two scale S (0: MFMA scoring unavailable)
+  // Tile culling of the a4 batches (round 4, ransac.hip ensure_cull; built on the first culled
+  // run, in stream order): the rows in the Morton order of (p_c, q_c), their MFMA operands, and
+  // per 32-row tile the centre's operands and the bounds (S·ρ, S·e) of
+  // | |d_i| − |d_c| | ≤ ‖R − R0‖_F·ρ + e (R0: the Kabsch rotation of the whole set)
+  mutable void* cull_block = nullptr;
+  mutable uint4* cas16 = nullptr;    // 4 planes × nc_pad, sorted rows
+  mutable int32_t* rowmap = nullptr; // nc_pad: sorted row → original row
+  mutable uint4* cca16 = nullptr;    // 4 planes × nsub_pad: tile centres
+  mutable float2* tstat = nullptr;   // nsub_pad: (S·ρ, S·e); e = +inf: never decided
+  mutable double R0h[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // R0 (host copy, passed by value)
+  mutable int64_t nsub = 0, nsub_pad = 0;
 };
 
 struct m3d_cloud {
@@ -381,6 +392,25 @@ int64_t score_mf_hpad(int64_t H);
 hipError_t launch_corr16(m3d_corrset* cs, hipStream_t st);  // cs->ca16, cs->s16
 hipError_t launch_score_prep(const m3d_corrset* cs, const double* T64, int64_t H, double thr,
                              int mode, const ScoreMf& mf, hipStream_t st);
+// a4 batch scoring with tile culling (ransac.hip): scratch of one batch of h_pad hypotheses
+struct ScoreCull {
+  uint32_t* key = nullptr;    // h_pad sort keys (‖R − R0‖_F bits)
+  uint32_t* key2 = nullptr;   // h_pad
+  int32_t* val = nullptr;     // h_pad
+  int32_t* perm = nullptr;    // h_pad: position → hypothesis
+  float* a = nullptr;         // h_pad: ‖R − R0‖_F (rounded up) by hypothesis
+  float* apos = nullptr;      // h_pad: by position
+  float* edpos = nullptr;     // h_pad: the screen's per-component error bound E_d by position
+  uint32_t* skip = nullptr;   // (h_pad / 32) × (nsub_pad / 32) bits: (group, tile) decided
+  void* sort_tmp = nullptr;
+  size_t sort_bytes = 0;
+};
+size_t cull_sort_bytes(int64_t h_pad);
+bool score_cull_on(const m3d_corrset* cs, double thr_sq);
+hipError_t ensure_cull(const m3d_corrset* cs, hipStream_t st);
+hipError_t launch_score_culled(const m3d_corrset* cs, const double* T64, int64_t H, double thr, int mode,
+                               int32_t* counts, int64_t* stats, const int32_t* done, const ScoreMf& mf,
+                               const ScoreCull& cc, hipStream_t st);
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
                         const double* T64, double thr, int mode, int64_t* stats,
                         const int32_t* done, const ScoreMf& mf, hipStream_t st);

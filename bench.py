@@ -575,6 +575,49 @@ def main():
                          "mfma_issue_frac": SCORE_MFMA_FLOP_PER_PAIR * pairs3 / (sc3_avg * 1e-3) / 1e12
                          / MFMA_F16_PEAK_TF},
         }
+        # the tile-culled screen (ransac.hip cull_classify_kernel; library opt-in M3D_SCORE_CULL=1,
+        # DESIGN.md §3.2d) on both cfg2 workloads, beside the plain screen above: same winner, the
+        # share of (32-hypothesis group, 32-row tile) blocks it skipped (one extra run with the
+        # classifier's counters on), and its rate on the pairs it actually screened
+        culled = None
+        if not multi:
+            culled = {}
+            for key, cset, pp, base in (("nc1e5", cs, params, (rel, out)), ("nc3e5", cs3, p3, (rel3, out3))):
+                os.environ["M3D_SCORE_CULL"] = "1"
+                rb = torch.zeros(RESULT_WORDS, dtype=torch.int64, device=dev)
+                try:
+                    for _ in range(3):
+                        cset.run_async(pp, rb)
+                    torch.cuda.synchronize()
+                    relc, _, profc = timed(lambda: cset.run_async(pp, rb), args.ransac_steps, (K_SC,))
+                    oc = RansacOutcome.from_device(rb, cset.nc)
+                    os.environ["M3D_CULL_STATS"] = "1"
+                    s0 = ctx.stats()
+                    cset.run_async(pp, rb)
+                    torch.cuda.synchronize()
+                    s1 = ctx.stats()
+                finally:
+                    os.environ.pop("M3D_SCORE_CULL", None)
+                    os.environ.pop("M3D_CULL_STATS", None)
+                skip = float((s1[4] - s0[4]) / max(s1[5] - s0[5], 1))
+                sc_ms = profc[K_SC][0] / max(profc[K_SC][1], 1)
+                scr_pairs = cset.nc * H * (1.0 - skip)  # per run (one launch sequence per batch)
+                culled[key] = {
+                    "value": H * args.ransac_steps / relc, "unit": "hyp/s",
+                    "ms_per_run": relc / args.ransac_steps * 1e3,
+                    "plain_ms_per_run": base[0] / args.ransac_steps * 1e3,
+                    "same_winner_as_plain": bool(oc.best_index == base[1].best_index
+                                                 and oc.best_count == base[1].best_count),
+                    "blocks_skipped_frac": skip,
+                    "roofline": {"bound": "mfma", "kernel": "cull_classify_kernel + score_mfma_kernel<2, true>",
+                                 "achieved": SCORE_FLOP_PER_PAIR * scr_pairs / (sc_ms * 1e-3 * profc[K_SC][1] / args.ransac_steps) / 1e12,
+                                 "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s",
+                                 "basis": "27 flop per (hypothesis, correspondence) pair actually screened",
+                                 "pairs_screened_per_run": scr_pairs,
+                                 "score_ms_per_launch": sc_ms},
+                    "note": "opt-in (M3D_SCORE_CULL=1): not the library default, measured no faster end to end",
+                }
+                culled[key]["roofline"]["frac"] = culled[key]["roofline"]["achieved"] / MFMA_F16_PEAK_TF
         del cs3
         ransac = {
             "metric": "RANSAC hypotheses/sec (cfg2: Nc=1e5, a1+a2, no early stop)",
@@ -594,6 +637,7 @@ def main():
             "kabsch_avg_launch_ms": kb_ms / max(kb_n, 1),
             "strong": ransac_strong,
             "nc3e5": ransac_nc3e5,
+            "culled": culled,
         }
 
     # ------------------------------------------------------------------ drop-in per-call path
