@@ -1744,31 +1744,37 @@ __global__ __launch_bounds__(512) void cull_classify_kernel(
     const s_floatx16 dx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax.h, bx, zacc, 0, 0, 0);
     const s_floatx16 dy = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay.h, by, zacc, 0, 0, 0);
     const s_floatx16 dz = __builtin_amdgcn_mfma_f32_32x32x16_f16(az.h, bz, zacc, 0, 0, 0);
-    uint32_t sk = 0;  // bit = tile of the block decided for all 32 hypotheses of the group
-    uint64_t inm[16];
+    // branch-free: the decisions as lane bits (no short-circuit control flow), the all-32
+    // tests on the wave masks in scalar registers
+    uint32_t dec = 0, inb = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
       const float2 ts = sst[q * kCullSub + row];
       const float X = fmaf(dx[r], dx[r], fmaf(dy[r], dy[r], dz[r] * dz[r]));  // S²|d̃_c|²
       const float w = fmaf(a, ts.x, ts.y);                                   // S·(a·ρ + e)
-      const float bo = kout + w, bi = kin - w;
-      const bool o = X >= bo * bo * c_out;
-      const bool i_ = bi > 0.0f && X * c_out < bi * bi * c_in;
-      const uint64_t bd = __ballot(o || i_);
-      inm[r] = __ballot(i_);
+      const float bo = kout + w, bi = fmaxf(kin - w, 0.0f);  // bi ≤ 0: never inside (X ≥ 0)
+      const uint32_t o = X >= bo * bo * c_out ? 1u : 0u;
+      const uint32_t i_ = X * c_out < bi * bi * c_in ? 1u : 0u;
+      dec |= (o | i_) << r;
+      inb |= i_ << r;
+    }
+    uint32_t sk = 0;  // bit = tile of the block decided for all 32 hypotheses of the group
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint64_t bd = __ballot((dec >> r) & 1u);
       const int row0 = (r & 3) + 8 * (r >> 2);
-      if ((uint32_t)bd == 0xFFFFFFFFu) sk |= 1u << row0;
-      if ((uint32_t)(bd >> 32) == 0xFFFFFFFFu) sk |= 1u << (row0 + 4);
+      sk |= ((uint32_t)bd == 0xFFFFFFFFu ? 1u : 0u) << row0;
+      sk |= ((uint32_t)(bd >> 32) == 0xFFFFFFFFu ? 1u : 0u) << (row0 + 4);
     }
     if (lane == 0) skip[grp * nwords + blockIdx.y * kCullSB + q] = sk;
     nskip += __builtin_popcount(sk);
     nblk += kCullSub;
+    // this lane's tiles (rows row0 + 4h) that were skipped AND decided inlier for its hypothesis
+    uint32_t mine = 0;  // bit r: tile row(r, h) skipped
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (((sk >> row) & 1u) && ((inm[r] >> lane) & 1ull)) inl += kCullSub;
-    }
+    for (int r = 0; r < 16; ++r) mine |= ((sk >> ((r & 3) + 8 * (r >> 2) + 4 * h)) & 1u) << r;
+    inl += kCullSub * __builtin_popcount(mine & inb);
   }
   inl += __shfl_xor(inl, 32);
   const int64_t hyp = perm[pos];
