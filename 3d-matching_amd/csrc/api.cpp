@@ -1652,6 +1652,7 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
   // same; only the early-exit launches are skipped.
   if (!rc) {
     const int32_t total = params->max_iteration + 1;
+    s->graph_off = true;  // a one-shot loop: no HIP graph capture (two equal chunks would trigger one)
     if (icp_persist_ok(s)) {
       rc = m3d_icp_steps(s, total, stream);
     } else {
