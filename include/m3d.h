@@ -69,7 +69,9 @@ int m3d_device_count(int* count);
 int m3d_create(int device, m3d_ctx** out);
 void m3d_destroy(m3d_ctx* ctx);
 const char* m3d_last_error(const m3d_ctx* ctx);
-/* Device-side hit counters (cumulative): [0] pairs rechecked by chunk, [1] by full hypothesis. */
+/* Device-side hit counters (cumulative): [0] pairs rechecked by chunk, [1] by full hypothesis;
+ * [4] / [5] (group, tile) blocks skipped / classified by the a4 batches' tile culling (counted only
+ * with M3D_CULL_STATS=1; the culling itself is opt-in, M3D_SCORE_CULL=1 — exact, same counts). */
 int m3d_get_stats(m3d_ctx* ctx, int64_t* out8 /* [host] 8 values */);
 
 /* Kernel timing with HIP events recorded on the launch stream immediately before and after each
