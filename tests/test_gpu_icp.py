@@ -640,3 +640,37 @@ print(json.dumps(out))
         res[fused] = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["0"] == res["1"]
     assert res["1"]["brute"] == res["1"]["grid"]
+
+
+@pytest.mark.parametrize("mode", ["stage", "register"])
+def test_host_upload_modes_give_the_same_cloud(mode):
+    """The alternative host uploads of m3d_cloud_create_host (M3D_UPLOAD=stage: pinned staging
+    filled by the host pool, 1 MB chunks and rounds past the 64 MB cap; register: page-locked in
+    place) build the cloud the default pageable copy builds — the same NN bits (one subprocess each:
+    the mode is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    code = r'''
+import sys
+sys.path[:0] = [sys.argv[1]]
+import numpy as np, torch
+from m3d.core import Cloud, nn1
+rng = np.random.default_rng(9)
+for n in (1, 70_000, 3_000_000):
+    pts = rng.normal(size=(n, 3)) * 3.0
+    nrm = rng.normal(size=(n, 3))
+    a = Cloud(pts, nrm)
+    b = Cloud(torch.from_numpy(pts).cuda(), torch.from_numpy(nrm).cuda())
+    q = Cloud(pts[: min(n, 5000)] + 0.01)
+    i1, d1 = nn1(q, a, np.eye(4), 0.05, nn="grid")
+    i2, d2 = nn1(q, b, np.eye(4), 0.05, nn="grid")
+    assert np.array_equal(i1.cpu().numpy(), i2.cpu().numpy()) and np.array_equal(d1.cpu().numpy(), d2.cpu().numpy()), n
+print("ok")
+'''
+    env = dict(os.environ, M3D_UPLOAD=mode)
+    pkg = str(Path(__file__).resolve().parents[1] / "3d-matching_amd")
+    r = subprocess.run([sys.executable, "-c", code, pkg], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
