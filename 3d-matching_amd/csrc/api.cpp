@@ -1119,7 +1119,8 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = 
   if (s->params.nn_method == M3D_NN_GRID) {
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->sgrid, s->tgrid, off, s->state, s->keys,
-                          s->near2, s->sq, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st, q0, q1);
+                          s->near2, s->sq, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st, q0, q1,
+                          s->hlist, s->hcnt, s->cand_cap);
   }
   if (!seeded) {
     hipError_t e = launch_icp_keyinit(s, off, st, q0, q1);
@@ -1173,6 +1174,7 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
   hipSetDevice(ctx->device);
   const Grid *tg = nullptr, *sg = nullptr;
   const m3d_cloud* src_m = nullptr;
+  int64_t coarse_max_occ = 0;  // most target points in one cell at cell ≈ r (grid NN)
   // M3D_CREATE_PROF=1 (diagnostics): wall ms of each setup stage, synchronised in between
   static const bool cprof = [] {
     const char* e = getenv("M3D_CREATE_PROF");
@@ -1234,6 +1236,7 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
     }
     if (!grc && params->nn_method == M3D_NN_GRID && getenv("M3D_GRID_CELL_DIV") == nullptr &&
         tg->n_occ > 0) {
+      coarse_max_occ = tg->max_occ;
       const double m = (double)tg->n_pts / (double)tg->n_occ;
       const int div = std::min(4, std::max(1, (int)std::floor(std::sqrt(m / 3.5))));
       if (div > 1) grc = ensure_grid(ctx, tgt, cell / div, nullptr, &tg);
@@ -1271,14 +1274,29 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
   }();
   s->qorder = cell_order ? sg->order : nullptr;  // (cell_order builds the source grid, above)
   s->sgrid = sg;
+  // Dense target cells (a cell at ≈ r holding ≥ kHeavyCell points — e.g. the vertex fan at a
+  // UV-sphere pole, ~30× the mean density): queries with more than kHeavyCand candidates are
+  // deferred to grid_nn_heavy_kernel (one block per query) so that the few waves of such queries
+  // do not set the launch time (cfg4: up to 250 µs per evaluation).  M3D_GRID_HEAVY=0: never,
+  // =N: always, with cap N (tests).  Off on evenly dense clouds (cfg1's largest cell ≈ 20).
+  constexpr int64_t kHeavyCell = 256;
+  constexpr int32_t kHeavyCand = 256;
+  static const int heavy_env = [] {
+    const char* e = getenv("M3D_GRID_HEAVY");
+    return e ? std::max(0, atoi(e)) : -1;
+  }();
+  if (params->nn_method == M3D_NN_GRID)
+    s->cand_cap = heavy_env > 0 ? heavy_env : (heavy_env < 0 && coarse_max_occ >= kHeavyCell ? kHeavyCand : 0);
   // the loop's arrays in ONE allocation (one hipMalloc instead of nine)
   int rc = M3D_OK;
   {
     const size_t n1 = (size_t)std::max<int64_t>(src->n, 1);
-    const size_t sz[8] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
-                          sizeof(double) * (size_t)(s->nblocks * kTermSlots + kTermSlots)};
-    size_t off[8], tot = 0;
-    for (int k = 0; k < 8; ++k) {
+    const size_t nh = s->cand_cap > 0 ? n1 : 0;
+    const size_t sz[10] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
+                           sizeof(double) * (size_t)(s->nblocks * kTermSlots + kTermSlots), 4 * nh,
+                           sizeof(uint32_t)};
+    size_t off[10], tot = 0;
+    for (int k = 0; k < 10; ++k) {
       off[k] = tot;
       tot += tmp_align(sz[k]);
     }
@@ -1302,6 +1320,10 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
       s->corr = reinterpret_cast<int32_t*>(b + off[6]);
       s->partials = reinterpret_cast<double*>(b + off[7]);
       s->sums = s->partials + s->nblocks * kTermSlots;
+      if (nh > 0) {
+        s->hlist = reinterpret_cast<int32_t*>(b + off[8]);
+        s->hcnt = reinterpret_cast<uint32_t*>(b + off[9]);
+      }
     }
   }
   // seed records (M3D_GRID_SEEDREC=1): measured slower while the clouds keep the caller's point

@@ -206,15 +206,16 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __res
 // one dependent load per point.  Blocks are remapped XCD-contiguously (blocks b and b + 8 share
 // an XCD's L2: each XCD gets one contiguous slice of the Morton order, so its L2 holds one
 // region's targets and cell starts instead of every region's).
-template <int kL, int kR, int kB>
+template <int kL, int kR, int kB, bool kDefer = false>
 __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const float4* __restrict__ qpts, int64_t ns, GridDev g, int64_t off,
     const IcpState* __restrict__ s, int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
     const float4* __restrict__ sq, const int32_t* __restrict__ prev,
     const int64_t* __restrict__ dprev, const float4* __restrict__ tgt32, int64_t nt_shard,
-    int64_t nblocks, unsigned long long* __restrict__ stats, int64_t q0) {
+    int64_t nblocks, unsigned long long* __restrict__ stats, int64_t q0, int32_t* __restrict__ hlist,
+    uint32_t* __restrict__ hcnt, int cand_cap) {
   // stats (M3D_GRID_STATS=1, diagnostics only, else null): [0] queries, [1] cell rows,
-  // [2] candidate points, [3] queries with a seed
+  // [2] candidate points, [3] queries with a seed, [4] most candidates of one query
   if (s->done) return;
   const int64_t per = (nblocks + 7) / 8;
   const int64_t blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
@@ -240,12 +241,18 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     if (g.ncells > 0) {
       const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
       int rows = 0, cand = 0;
-      grid_scan<kL, kR, kB>(g, qx, qy, qz, R, r2_hi, off, sub, k1, k1d, n2, &rows, &cand);
+      grid_scan<kL, kR, kB>(g, qx, qy, qz, R, r2_hi, off, sub, k1, k1d, n2, &rows, &cand,
+                            kDefer ? cand_cap : 0x7FFFFFFF);
+      if (kDefer && cand > cand_cap) {  // a dense box: grid_nn_heavy_kernel scans it with a whole block
+        if (sub == 0) hlist[atomicAdd(hcnt, 1u)] = (int32_t)t;
+        i = -1;
+      }
       if (stats != nullptr && sub == 0) {
         atomicAdd(&stats[0], 1ull);
         atomicAdd(&stats[1], (unsigned long long)rows);
         atomicAdd(&stats[2], (unsigned long long)cand);
         if (seed != kKeyNone) atomicAdd(&stats[3], 1ull);
+        atomicMax(&stats[4], (unsigned long long)cand);
       }
     }
   }
@@ -253,6 +260,68 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
   if (i >= 0 && sub == 0) {
     keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
     near2[i] = __float_as_uint(n2);
+  }
+}
+
+// Deferred queries of grid_nn_batched_kernel (more than cand_cap candidates in their box: the
+// cells of a dense cluster, where kL lanes would walk hundreds of points each and one wave would
+// hold the whole launch): one block per query, its 4 waves over the box's rows and each wave's
+// 64 lanes over a row's points.  Same seed, same box, same pushes as the per-query scan, merged
+// by the same near_merge: the same (k1, near2) bits.
+__global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
+    const float4* __restrict__ qpts, GridDev g, int64_t off, const IcpState* __restrict__ s,
+    int64_t* __restrict__ keys, uint32_t* __restrict__ near2, const float4* __restrict__ sq,
+    const int32_t* __restrict__ prev, const int64_t* __restrict__ dprev,
+    const float4* __restrict__ tgt32, int64_t nt_shard, const int32_t* __restrict__ hlist,
+    const uint32_t* __restrict__ hcnt) {
+  constexpr int kWaves = kGridBlock / kWave;
+  __shared__ uint64_t wk[kWaves];
+  __shared__ float wn[kWaves];
+  if (s->done) return;
+  const uint32_t nh = *hcnt;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const float r2_hi = s->r2_hi, be = s->band_e;
+  const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
+  for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
+    const int64_t t = hlist[h];
+    const float4 p = qpts[t];
+    const int64_t i = (int64_t)__float_as_int(p.w);
+    float qx, qy, qz;
+    xform32(s->Rt32, p, qx, qy, qz);
+    const int64_t seed = sq != nullptr ? seed_from_rec(s, sq[t], p, qx, qy, qz)
+                                       : seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
+    uint64_t k1 = seed != kKeyNone ? (uint64_t)seed : key0;
+    float k1d = key_real_d2(k1), n2 = kInf;
+    const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
+    const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
+    const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
+    const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
+    const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
+    const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
+    const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
+    const int ny = y1 - y0 + 1;
+    const int rows = ny * (z1 - z0 + 1);
+    for (int r = wave; r < rows; r += kWaves) {
+      const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
+      const int32_t b = g.start[row + x1 + 1];
+      for (int32_t j = g.start[row + x0] + lane; j < b; j += kWave) {
+        const float4 v = g.pts[j];
+        const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
+        if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(v.w))), d2);
+      }
+    }
+    grid_merge_lanes<kWave>(k1, k1d, n2);
+    if (lane == 0) {
+      wk[wave] = k1;
+      wn[wave] = n2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < kWaves; ++w) near_merge(k1, k1d, n2, wk[w], wn[w]);
+      keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
+      near2[i] = __float_as_uint(n2);
+    }
+    __syncthreads();
   }
 }
 
@@ -428,7 +497,8 @@ static hipError_t grid_fail(hipError_t e, void* a, void* b, void* c, void* d, vo
 }
 
 // occupied cells from the built grid itself: sorted positions whose cell differs from the
-// previous point's (the cell of a point recomputed from its coordinates as cell_id_kernel does)
+// previous point's (the cell of a point recomputed from its coordinates as cell_id_kernel does);
+// occ[1] = the most points in one cell (the first point of each cell reads its cell's range)
 __global__ __launch_bounds__(kGridBlock) void count_occupied_pts_kernel(const float4* __restrict__ pts,
                                                                         int64_t n, GridDev g,
                                                                         unsigned long long* __restrict__ occ) {
@@ -440,9 +510,16 @@ __global__ __launch_bounds__(kGridBlock) void count_occupied_pts_kernel(const fl
     const int cz = grid_coord(v.z, g.o[2], g.inv_h, g.n[2]);
     return ((int64_t)cz * g.n[1] + cy) * g.n[0] + cx;
   };
-  const bool first = k < n && (k == 0 || cell_of(k) != cell_of(k - 1));
+  const int64_t c = k < n ? cell_of(k) : 0;
+  const bool first = k < n && (k == 0 || c != cell_of(k - 1));
+  int run = first ? g.start[c + 1] - g.start[c] : 0;
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) run = max(run, __shfl_xor(run, o));
   const unsigned long long b = __ballot(first);
-  if ((threadIdx.x & (kWave - 1)) == 0 && b != 0) atomicAdd(occ, (unsigned long long)__popcll(b));
+  if ((threadIdx.x & (kWave - 1)) == 0 && b != 0) {
+    atomicAdd(occ, (unsigned long long)__popcll(b));
+    atomicMax(occ + 1, (unsigned long long)run);
+  }
 }
 
 // The dense cell array over [lo, hi] for a requested cell size: origin, cells per axis, 1/h; the
@@ -574,21 +651,22 @@ hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st) {
   if (ta != nullptr) {
     if ((e = ta->reserve(256)) != hipSuccess) return e;
     cnt = reinterpret_cast<unsigned long long*>(ta->base);
-  } else if ((e = hipMalloc(&cnt, sizeof(unsigned long long))) != hipSuccess) {
+  } else if ((e = hipMalloc(&cnt, 2 * sizeof(unsigned long long))) != hipSuccess) {
     return e;
   }
-  unsigned long long occ = 0;
+  unsigned long long occ[2] = {0, 0};
   e = hipMemsetAsync(cnt, 0, sizeof(occ), st);
   if (e == hipSuccess) {
     count_occupied_pts_kernel<<<(unsigned)((g->n_pts + kGridBlock - 1) / kGridBlock), kGridBlock, 0, st>>>(
         g->pts, g->n_pts, g->dev, cnt);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipMemcpyAsync(&occ, cnt, sizeof(occ), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(occ, cnt, sizeof(occ), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (ta == nullptr) hipFree(cnt);
   if (e != hipSuccess) return e;
-  g->n_occ = (int64_t)occ;
+  g->n_occ = (int64_t)occ[0];
+  g->max_occ = (int64_t)occ[1];
   g->occ_known = true;
   return hipSuccess;
 }
@@ -885,7 +963,7 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
                           const float4* sq, const int32_t* prev, const int64_t* dprev,
                           const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0,
-                          int64_t q1) {
+                          int64_t q1, int32_t* hlist, uint32_t* hcnt, int32_t cand_cap) {
   const int64_t ns_all = ns;
   if (q1 >= 0) ns = q1;
   if (ns <= q0) return hipSuccess;
@@ -911,23 +989,38 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
     static unsigned long long* gstats = [] {
       const char* e = getenv("M3D_GRID_STATS");
       unsigned long long* p = nullptr;
-      if (e && atoi(e) == 1 && hipMalloc(&p, 4 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
+      if (e && atoi(e) == 1 && hipMalloc(&p, 5 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
       return p;
     }();
-    if (gstats != nullptr) (void)hipMemsetAsync(gstats, 0, 4 * sizeof(unsigned long long), st);
+    if (gstats != nullptr) (void)hipMemsetAsync(gstats, 0, 5 * sizeof(unsigned long long), st);
     const int64_t nb = ((ns - q0) * L + kGridBlock - 1) / kGridBlock;
     const unsigned launch = (unsigned)((nb + 7) / 8 * 8);
-#define M3D_GB(LV, RV, BV) grid_nn_batched_kernel<LV, RV, BV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0)
+    // deferral (dense target cells, api.cpp icp_create) in the default shapes: 2 or 4 lanes, RB 22
+    const bool defer = hlist != nullptr && hcnt != nullptr && cand_cap > 0 && g->dev.ncells > 0 &&
+                       (L == 2 || L == 4) && RB == 22;
+    const int cap = defer ? cand_cap : 0x7FFFFFFF;
+    if (defer) {
+      hipError_t e = hipMemsetAsync(hcnt, 0, sizeof(uint32_t), st);
+      if (e != hipSuccess) return e;
+    }
+#define M3D_GB(LV, RV, BV) grid_nn_batched_kernel<LV, RV, BV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0, hlist, hcnt, cap)
 #define M3D_GBL(RV, BV) if (L == 1) M3D_GB(1, RV, BV); else if (L == 2) M3D_GB(2, RV, BV); else if (L == 4) M3D_GB(4, RV, BV); else if (L == 8) M3D_GB(8, RV, BV); else M3D_GB(16, RV, BV)
-    if (RB == 22) { M3D_GBL(2, 2); } else if (RB == 41) { M3D_GBL(4, 1); } else if (RB == 42) { M3D_GBL(4, 2); } else { M3D_GBL(2, 4); }
+    if (defer && L == 4) grid_nn_batched_kernel<4, 2, 2, true><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0, hlist, hcnt, cap);
+    else if (defer) grid_nn_batched_kernel<2, 2, 2, true><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0, hlist, hcnt, cap);
+    else if (RB == 22) { M3D_GBL(2, 2); } else if (RB == 41) { M3D_GBL(4, 1); } else if (RB == 42) { M3D_GBL(4, 2); } else { M3D_GBL(2, 4); }
 #undef M3D_GBL
 #undef M3D_GB
+    if (defer) {  // a fixed grid striding over the deferred queries (their count stays on the device)
+      const unsigned hb = (unsigned)std::min<int64_t>(512, ns - q0);
+      grid_nn_heavy_kernel<<<hb, kGridBlock, 0, st>>>(qgrid->mpts, g->dev, off, s, keys, near2, sq, prev,
+                                                      dprev, tgt32, nt_shard, hlist, hcnt);
+    }
     if (gstats != nullptr) {
-      unsigned long long h[4] = {0, 0, 0, 0};
+      unsigned long long h[5] = {0, 0, 0, 0, 0};
       if (hipMemcpyAsync(h, gstats, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
           hipStreamSynchronize(st) == hipSuccess && h[0] > 0)
-        fprintf(stderr, "[m3d grid stats] %llu queries (%.1f%% seeded): %.2f cell rows, %.1f candidates per query\n",
-                h[0], 100.0 * h[3] / h[0], (double)h[1] / h[0], (double)h[2] / h[0]);
+        fprintf(stderr, "[m3d grid stats] %llu queries (%.1f%% seeded): %.2f cell rows, %.1f candidates per query, max %llu\n",
+                h[0], 100.0 * h[3] / h[0], (double)h[1] / h[0], (double)h[2] / h[0], h[4]);
     }
     return hipGetLastError();
   }

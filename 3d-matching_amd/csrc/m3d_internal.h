@@ -101,6 +101,7 @@ struct Grid {
   int32_t* minv = nullptr;
   int64_t n_pts = 0;
   int64_t n_occ = 0;      // occupied cells (grid_occupancy; 0: not counted)
+  int64_t max_occ = 0;    // most points in one cell (grid_occupancy)
   bool occ_known = false;
   double cell = 0.0;      // cell size used
   double cell_req = 0.0;  // cell size requested
@@ -293,6 +294,11 @@ struct m3d_icp {
   // grid NN: each source's seed record in the source's Morton order (nnkey.h SeedRec), written by
   // the terms pass with the correspondence, read by the grid scan beside the query point
   float4* sq = nullptr;
+  // grid NN on a target with dense cells (grid.hip grid_nn_heavy_kernel): the queries deferred
+  // by the per-query scan (ns slots) and their count; cand_cap = 0: no deferral
+  int32_t* hlist = nullptr;
+  uint32_t* hcnt = nullptr;
+  int32_t cand_cap = 0;
   bool keys_clean = false;         // host view: every key is kKeyNone (fused tail reset them)
   int32_t* corr = nullptr;         // ns current correspondence (-1 none)
   double* partials = nullptr;      // nblocks × kTermSlots
@@ -468,7 +474,8 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
                           const float4* sq, const int32_t* prev, const int64_t* dprev,
                           const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0 = 0,
-                          int64_t q1 = -1);
+                          int64_t q1 = -1, int32_t* hlist = nullptr, uint32_t* hcnt = nullptr,
+                          int32_t cand_cap = 0);
 hipError_t grid_morton(Grid* g, hipStream_t st, TmpArena* ta = nullptr);
 // the Morton-slot copy of an ICP source (out, gout freshly allocated structs; see grid.hip);
 // asynchronous (stream order)

@@ -114,16 +114,18 @@ __device__ __forceinline__ int grid_coord(float x, float o, float inv_h, int n) 
   return (int)f;
 }
 
-// Grid scan of one query by kL cooperating lanes (grid.hip grid_nn_batched_kernel, icp.hip
-// grid_icp_kernel): every lane of the query sees every cell row of the box q ± R and takes the
-// row's points sub, sub + kL, …; the start offsets of kR rows are loaded together, then kR × kB
-// point loads per lane go out at once.  Each lane pushes the targets with d2f ≤ r2_hi into its
-// (k1, k1d, near2) state; grid_merge_lanes combines the kL states.
+// Grid scan of one query by kL cooperating lanes (grid.hip grid_nn_batched_kernel): every lane
+// of the query sees every cell row of the box q ± R and takes the row's points sub, sub + kL, …;
+// the start offsets of kR rows are loaded together, then kR × kB point loads per lane go out at
+// once.  Each lane pushes the targets with d2f ≤ r2_hi into its (k1, k1d, near2) state;
+// grid_merge_lanes combines the kL states.  A query whose rows hold more than cand_cap points
+// stops at the batch that crosses it (*ncand > cand_cap: the caller defers it, see
+// grid.hip grid_nn_heavy_kernel).
 template <int kL, int kR, int kB>
 __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, float qz, float R,
                                           float r2_hi, int64_t off, int sub, uint64_t& k1,
                                           float& k1d, float& n2, int* nrows = nullptr,
-                                          int* ncand = nullptr) {
+                                          int* ncand = nullptr, int cand_cap = 0x7FFFFFFF) {
   const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
   const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
   const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
@@ -149,6 +151,7 @@ __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, 
       len = max(len, b[k] - a[k]);
       cand += b[k] - a[k];
     }
+    if (cand > cand_cap) break;  // deferred (same rows on every lane of the query)
     for (int32_t base = sub; base < len; base += kL * kB) {
       float4 v[kR][kB];
 #pragma unroll

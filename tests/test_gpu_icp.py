@@ -50,7 +50,11 @@ def _grid_cases():
     # a few far outliers make the fp16-scaled queries overflow: the MFMA kernel's exact scan
     outl = sph[::3].copy()
     outl[::500] += 2e4
+    # a vertex fan: 3000 targets within 0.004 of one surface point (≥ 256 in one cell at r: the
+    # loop defers the queries near it to grid_nn_heavy_kernel)
+    fan = np.vstack([sph, sph[7] + rng.normal(scale=0.002, size=(3000, 3))])
     return {
+        "dense_cluster": (np.vstack([sph[::3] * 1.001, sph[7] + rng.normal(scale=0.03, size=(2000, 3))]), fan, 0.12),
         "sphere": (sph[::3] * 1.002, sph, 0.12),
         "sphere_big_r": (sph[::7], sph, 50.0),  # radius larger than the cloud
         "sphere_tiny_r": (sph[::5] + 1e-4, sph, 1e-3),
@@ -674,3 +678,53 @@ print("ok")
     pkg = str(Path(__file__).resolve().parents[1] / "3d-matching_amd")
     r = subprocess.run([sys.executable, "-c", code, pkg], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def test_deferred_dense_queries_give_the_same_bits():
+    """grid_nn_heavy_kernel (one block per query with more than the candidate cap) returns the
+    per-query scan's keys: M3D_GRID_HEAVY=8 defers nearly every query, =0 none; both give the
+    brute-force loop's bits on a pair with a dense vertex fan (where the default defers some)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    code = r'''
+import json, sys
+import numpy as np
+sys.path[:0] = [sys.argv[1]]
+import torch
+from m3d import synth
+from m3d.core import Cloud, IcpLoop, nn1
+src, tgt, nrm, _ = synth.icp_pair(60000, 50000, seed=43)
+rng = np.random.default_rng(5)
+fan = tgt[11] + rng.normal(scale=0.002, size=(4000, 3))
+tgt = np.vstack([tgt, fan]); nrm = np.vstack([nrm, np.repeat(nrm[11:12], 4000, 0)])
+src = np.vstack([src, tgt[11] + rng.normal(scale=0.05, size=(3000, 3))])
+s, t = Cloud(src), Cloud(tgt, nrm)
+out = {}
+for nn in ("brute", "grid"):
+    lp = IcpLoop(s, t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=8, nn=nn)
+    lp.reset(synth.random_rigid(3, rot_range=0.03, trans_range=0.05))
+    lp.steps(9)
+    r = lp.result()
+    c = lp.correspondences().cpu().numpy()
+    out[nn] = [r.transformation.tolist(), r.fitness, r.inlier_rmse, r.iterations, int(c.sum()), int((c >= 0).sum())]
+i, d = nn1(Cloud(src), t, np.eye(4), 0.12, nn="grid")
+out["nn1"] = [int(i.sum().item()), float(d.sum().item())]
+print(json.dumps(out))
+'''
+    pkg = str(Path(__file__).resolve().parents[1] / "3d-matching_amd")
+    res = {}
+    for mode in ("0", "8", None):
+        env = dict(os.environ)
+        env.pop("M3D_GRID_HEAVY", None)
+        if mode is not None:
+            env["M3D_GRID_HEAVY"] = mode
+        r = subprocess.run([sys.executable, "-c", code, pkg], env=env, capture_output=True, text=True,
+                           timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[mode] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["0"] == res["8"] == res[None]
+    assert res[None]["brute"] == res[None]["grid"]
