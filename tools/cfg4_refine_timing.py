@@ -43,7 +43,9 @@ def main():
         print(f"points {len(sp)} / {len(tp)}, dtypes {sp.dtype} {tp.dtype} {tn.dtype}, "
               f"contiguous {sp.flags.c_contiguous} {tp.flags.c_contiguous} {tn.flags.c_contiguous}", flush=True)
         rows = []
+        sc = tc = out = None
         for _ in range(a.reps + 1):
+            del sc, tc, out  # the previous clouds' hipFree outside the timed stages
             cache.clear()
             torch.cuda.synchronize()
             t = [time.perf_counter()]
