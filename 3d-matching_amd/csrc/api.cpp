@@ -1120,7 +1120,7 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = 
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->sgrid, s->tgrid, off, s->state, s->keys,
                           s->near2, s->sq, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st, q0, q1,
-                          s->hlist, s->hcnt, s->cand_cap);
+                          s->hlist, s->hcnt, s->cand_cap, s->src->xyz64, s->tgt->xyz64);
   }
   if (!seeded) {
     hipError_t e = launch_icp_keyinit(s, off, st, q0, q1);
@@ -1294,7 +1294,7 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
     const size_t nh = s->cand_cap > 0 ? n1 : 0;
     const size_t sz[10] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
                            sizeof(double) * (size_t)(s->nblocks * kTermSlots + kTermSlots), 4 * nh,
-                           sizeof(uint32_t)};
+                           2 * sizeof(uint32_t)};
     size_t off[10], tot = 0;
     for (int k = 0; k < 10; ++k) {
       off[k] = tot;
@@ -1320,9 +1320,11 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
       s->corr = reinterpret_cast<int32_t*>(b + off[6]);
       s->partials = reinterpret_cast<double*>(b + off[7]);
       s->sums = s->partials + s->nblocks * kTermSlots;
-      if (nh > 0) {
+      if (nh > 0) {  // count + ticket start at zero; grid_nn_heavy_kernel re-zeroes them
         s->hlist = reinterpret_cast<int32_t*>(b + off[8]);
         s->hcnt = reinterpret_cast<uint32_t*>(b + off[9]);
+        if (hipMemset(s->hcnt, 0, 2 * sizeof(uint32_t)) != hipSuccess)
+          rc = m3d_fail(ctx, M3D_ERR_HIP, "loop arrays: deferral counter");
       }
     }
   }

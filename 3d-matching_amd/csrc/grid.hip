@@ -244,7 +244,13 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
       grid_scan<kL, kR, kB>(g, qx, qy, qz, R, r2_hi, off, sub, k1, k1d, n2, &rows, &cand,
                             kDefer ? cand_cap : 0x7FFFFFFF);
       if (kDefer && cand > cand_cap) {  // a dense box: grid_nn_heavy_kernel scans it with a whole block
-        if (sub == 0) hlist[atomicAdd(hcnt, 1u)] = (int32_t)t;
+        if (sub == 0) {
+          const uint32_t slot = atomicAdd(hcnt, 1u);
+#ifdef M3D_DEBUG_GUARDS
+          if ((int64_t)slot >= ns) printf("[guard] defer slot %u >= ns %lld (t %lld)\n", slot, (long long)ns, (long long)t); else
+#endif
+          hlist[slot] = (int32_t)t;
+        }
         i = -1;
       }
       if (stats != nullptr && sub == 0) {
@@ -260,6 +266,16 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
   if (i >= 0 && sub == 0) {
     keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
     near2[i] = __float_as_uint(n2);
+    // deferral mode: an ambiguous query (the terms pass's test, nnkey.h winner_fp64) is decided in
+    // fp64 by grid_nn_heavy_kernel too — a dense cluster makes whole waves ambiguous, and the
+    // terms pass resolves a wave's queries one after another
+    if (kDefer && k1 != key0 && n2 <= search_bound(key_d2(k1), be, r2_hi)) {
+      const uint32_t slot = atomicAdd(hcnt, 1u);
+#ifdef M3D_DEBUG_GUARDS
+      if ((int64_t)slot >= ns) printf("[guard] amb slot %u >= ns %lld (t %lld)\n", slot, (long long)ns, (long long)t); else
+#endif
+      hlist[slot] = (int32_t)t;
+    }
   }
 }
 
@@ -273,19 +289,40 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
     int64_t* __restrict__ keys, uint32_t* __restrict__ near2, const float4* __restrict__ sq,
     const int32_t* __restrict__ prev, const int64_t* __restrict__ dprev,
     const float4* __restrict__ tgt32, int64_t nt_shard, const int32_t* __restrict__ hlist,
-    const uint32_t* __restrict__ hcnt) {
+    uint32_t* __restrict__ hcnt, const double* __restrict__ src64,
+    const double* __restrict__ tgt64, int64_t nq) {
   constexpr int kWaves = kGridBlock / kWave;
   __shared__ uint64_t wk[kWaves];
   __shared__ float wn[kWaves];
+  __shared__ double wd[kWaves];
+  __shared__ int64_t wj[kWaves];
   if (s->done) return;
-  const uint32_t nh = *hcnt;
+  uint32_t nh = __hip_atomic_load(hcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef M3D_DEBUG_GUARDS
+  if ((int64_t)nh > nq) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) printf("[guard] heavy count %u > %lld\n", nh, (long long)nq);
+    nh = 0;
+  }
+#endif
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const float r2_hi = s->r2_hi, be = s->band_e;
   const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
   for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
     const int64_t t = hlist[h];
+#ifdef M3D_DEBUG_GUARDS
+    if (t < 0 || t >= nq) {
+      if (threadIdx.x == 0) printf("[guard] heavy h %u of %u: t %lld outside [0, %lld)\n", h, nh, (long long)t, (long long)nq);
+      continue;
+    }
+#endif
     const float4 p = qpts[t];
     const int64_t i = (int64_t)__float_as_int(p.w);
+#ifdef M3D_DEBUG_GUARDS
+    if (i < 0 || i >= nq) {
+      if (threadIdx.x == 0) printf("[guard] heavy t %lld: i %lld outside [0, %lld)\n", (long long)t, (long long)i, (long long)nq);
+      continue;
+    }
+#endif
     float qx, qy, qz;
     xform32(s->Rt32, p, qx, qy, qz);
     const int64_t seed = sq != nullptr ? seed_from_rec(s, sq[t], p, qx, qy, qz)
@@ -316,12 +353,86 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
       wn[wave] = n2;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int w = 1; w < kWaves; ++w) near_merge(k1, k1d, n2, wk[w], wn[w]);
-      keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
-      near2[i] = __float_as_uint(n2);
+    for (int w = 0; w < kWaves; ++w)  // every thread merges the same states in the same order
+      if (w != wave) near_merge(k1, k1d, n2, wk[w], wn[w]);
+    // the terms pass's ambiguity test (nnkey.h winner_fp64); an ambiguous query is decided here by
+    // the whole block as resolve_wave does: every target of the q ± 1.001·√X box with d2f ≤ X
+    // re-evaluated in fp64, the lexicographic (d64, index) minimum among d64 < r2 — written as the
+    // key with near2 = none, which the terms pass then takes as it is (its fp64 re-check of k1's
+    // target gives the same d64)
+    const float X = k1 != key0 ? search_bound(key_d2(k1), be, r2_hi) : -1.0f;
+    if (!(X >= 0.0f && n2 <= X)) {
+      if (threadIdx.x == 0) {
+        keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
+        near2[i] = __float_as_uint(n2);
+      }
+    } else {
+      double Q[3];
+      q64_of(s->T, src64 + 3 * i, Q);
+      double dl = kInf;
+      int64_t jl = INT64_MAX;
+      const float RX = sqrtf(X) * 1.001f;
+      const int a0 = grid_coord(qx - RX, g.o[0], g.inv_h, g.n[0]);
+      const int a1 = grid_coord(qx + RX, g.o[0], g.inv_h, g.n[0]);
+      const int b0 = grid_coord(qy - RX, g.o[1], g.inv_h, g.n[1]);
+      const int b1 = grid_coord(qy + RX, g.o[1], g.inv_h, g.n[1]);
+      const int c0 = grid_coord(qz - RX, g.o[2], g.inv_h, g.n[2]);
+      const int c1 = grid_coord(qz + RX, g.o[2], g.inv_h, g.n[2]);
+      const int nby = b1 - b0 + 1;
+      const int xrows = nby * (c1 - c0 + 1);
+      for (int r = wave; r < xrows; r += kWaves) {
+        const int64_t row = ((int64_t)(c0 + r / nby) * g.n[1] + (b0 + r % nby)) * g.n[0];
+        const int32_t b = g.start[row + a1 + 1];
+        for (int32_t j = g.start[row + a0] + lane; j < b; j += kWave) {
+          const float4 v = g.pts[j];
+          if (!(d2f(qx, qy, qz, v.x, v.y, v.z) <= X)) continue;
+          const int64_t lj = (int64_t)__float_as_int(v.w);
+#ifdef M3D_DEBUG_GUARDS
+          if (lj < 0 || lj >= nt_shard) { printf("[guard] heavy resolve lj %lld nt %lld j %d\n", (long long)lj, (long long)nt_shard, j); continue; }
+#endif
+          const double* tp = tgt64 + 3 * lj;
+          const double dx = Q[0] - tp[0], dy = Q[1] - tp[1], dz = Q[2] - tp[2];
+          const double d = (dx * dx + dy * dy) + dz * dz;
+          const int64_t gj = off + lj;
+          if (d < s->r2 && (d < dl || (d == dl && gj < jl))) {
+            dl = d;
+            jl = gj;
+          }
+        }
+      }
+#pragma unroll
+      for (int o = kWave / 2; o > 0; o >>= 1) {
+        const double od = __shfl_xor(dl, o);
+        const int64_t oj = __shfl_xor(jl, o);
+        if (od < dl || (od == dl && oj < jl)) {
+          dl = od;
+          jl = oj;
+        }
+      }
+      if (lane == 0) {
+        wd[wave] = dl;
+        wj[wave] = jl;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int w = 1; w < kWaves; ++w)
+          if (wd[w] < dl || (wd[w] == dl && wj[w] < jl)) {
+            dl = wd[w];
+            jl = wj[w];
+          }
+        keys[i] = jl == INT64_MAX ? kKeyNone : (int64_t)make_key(__double2float_ru(dl), (uint32_t)jl);
+        near2[i] = kNearNone;
+      }
     }
     __syncthreads();
+  }
+  // the list is consumed: the last block to finish zeroes the count (and this ticket) for the
+  // next launch — in the kernel, ordered with the launches around it (a host-enqueued 4-byte
+  // memset was measured not to be: back-to-back steps saw the previous step's count)
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(hcnt + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+    __hip_atomic_store(hcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(hcnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -963,7 +1074,8 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
                           const float4* sq, const int32_t* prev, const int64_t* dprev,
                           const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0,
-                          int64_t q1, int32_t* hlist, uint32_t* hcnt, int32_t cand_cap) {
+                          int64_t q1, int32_t* hlist, uint32_t* hcnt, int32_t cand_cap,
+                          const double* src64, const double* tgt64) {
   const int64_t ns_all = ns;
   if (q1 >= 0) ns = q1;
   if (ns <= q0) return hipSuccess;
@@ -997,12 +1109,8 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
     const unsigned launch = (unsigned)((nb + 7) / 8 * 8);
     // deferral (dense target cells, api.cpp icp_create) in the default shapes: 2 or 4 lanes, RB 22
     const bool defer = hlist != nullptr && hcnt != nullptr && cand_cap > 0 && g->dev.ncells > 0 &&
-                       (L == 2 || L == 4) && RB == 22;
+                       src64 != nullptr && tgt64 != nullptr && (L == 2 || L == 4) && RB == 22;
     const int cap = defer ? cand_cap : 0x7FFFFFFF;
-    if (defer) {
-      hipError_t e = hipMemsetAsync(hcnt, 0, sizeof(uint32_t), st);
-      if (e != hipSuccess) return e;
-    }
 #define M3D_GB(LV, RV, BV) grid_nn_batched_kernel<LV, RV, BV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0, hlist, hcnt, cap)
 #define M3D_GBL(RV, BV) if (L == 1) M3D_GB(1, RV, BV); else if (L == 2) M3D_GB(2, RV, BV); else if (L == 4) M3D_GB(4, RV, BV); else if (L == 8) M3D_GB(8, RV, BV); else M3D_GB(16, RV, BV)
     if (defer && L == 4) grid_nn_batched_kernel<4, 2, 2, true><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0, hlist, hcnt, cap);
@@ -1013,7 +1121,7 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
     if (defer) {  // a fixed grid striding over the deferred queries (their count stays on the device)
       const unsigned hb = (unsigned)std::min<int64_t>(512, ns - q0);
       grid_nn_heavy_kernel<<<hb, kGridBlock, 0, st>>>(qgrid->mpts, g->dev, off, s, keys, near2, sq, prev,
-                                                      dprev, tgt32, nt_shard, hlist, hcnt);
+                                                      dprev, tgt32, nt_shard, hlist, hcnt, src64, tgt64, ns);
     }
     if (gstats != nullptr) {
       unsigned long long h[5] = {0, 0, 0, 0, 0};

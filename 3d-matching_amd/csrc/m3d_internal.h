@@ -295,7 +295,8 @@ struct m3d_icp {
   // the terms pass with the correspondence, read by the grid scan beside the query point
   float4* sq = nullptr;
   // grid NN on a target with dense cells (grid.hip grid_nn_heavy_kernel): the queries deferred
-  // by the per-query scan (ns slots) and their count; cand_cap = 0: no deferral
+  // by the per-query scan (ns slots), their count and the kernel's block ticket; cand_cap = 0: no
+  // deferral
   int32_t* hlist = nullptr;
   uint32_t* hcnt = nullptr;
   int32_t cand_cap = 0;
@@ -475,7 +476,8 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           const float4* sq, const int32_t* prev, const int64_t* dprev,
                           const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0 = 0,
                           int64_t q1 = -1, int32_t* hlist = nullptr, uint32_t* hcnt = nullptr,
-                          int32_t cand_cap = 0);
+                          int32_t cand_cap = 0, const double* src64 = nullptr,
+                          const double* tgt64 = nullptr);
 hipError_t grid_morton(Grid* g, hipStream_t st, TmpArena* ta = nullptr);
 // the Morton-slot copy of an ICP source (out, gout freshly allocated structs; see grid.hip);
 // asynchronous (stream order)

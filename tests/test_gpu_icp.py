@@ -681,9 +681,11 @@ print("ok")
 
 
 def test_deferred_dense_queries_give_the_same_bits():
-    """grid_nn_heavy_kernel (one block per query with more than the candidate cap) returns the
-    per-query scan's keys: M3D_GRID_HEAVY=8 defers nearly every query, =0 none; both give the
-    brute-force loop's bits on a pair with a dense vertex fan (where the default defers some)."""
+    """grid_nn_heavy_kernel (one block per query with more than the candidate cap, and every
+    ambiguous query decided in fp64) gives the per-query scan + terms pass's bits:
+    M3D_GRID_HEAVY=8 defers nearly every query, =0 none; both give the brute-force loop's bits on
+    a pair with a dense vertex fan (where the default defers some), over 41 steps enqueued back to
+    back (the list's count is re-zeroed by the kernel, never by the host)."""
     import json
     import os
     import subprocess
@@ -705,9 +707,10 @@ src = np.vstack([src, tgt[11] + rng.normal(scale=0.05, size=(3000, 3))])
 s, t = Cloud(src), Cloud(tgt, nrm)
 out = {}
 for nn in ("brute", "grid"):
-    lp = IcpLoop(s, t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=8, nn=nn)
+    lp = IcpLoop(s, t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=40, nn=nn, persist=False)
     lp.reset(synth.random_rigid(3, rot_range=0.03, trans_range=0.05))
-    lp.steps(9)
+    for _ in range(41):  # back to back, no host sync: each launch must start from an empty list
+        lp.step()
     r = lp.result()
     c = lp.correspondences().cpu().numpy()
     out[nn] = [r.transformation.tolist(), r.fitness, r.inlier_rmse, r.iterations, int(c.sum()), int((c >= 0).sum())]
