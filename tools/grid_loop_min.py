@@ -16,10 +16,17 @@ def main():
     src, tgt, nrm, _ = synth.icp_pair(100_000, 100_000, seed=0)
     lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
                  max_iteration=50, nn="grid", persist=False)
+    import time
+    ts = []
     for _ in range(6):
         lp.reset(np.eye(4))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         lp.steps(50)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3 / 50)
+    print(f"grid loop us per iteration: median {np.median(ts[1:]) * 1e3:.2f} (all {[round(t * 1e3, 1) for t in ts]})",
+          flush=True)
 
 
 if __name__ == "__main__":
