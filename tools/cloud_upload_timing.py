@@ -13,6 +13,8 @@ sys.path[:0] = [os.path.join(HERE, "..", "3d-matching_amd")]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--ns", type=int, default=180002)
+    ap.add_argument("--nt", type=int, default=217802)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -20,8 +22,8 @@ def main():
     from m3d.core import Cloud
 
     rng = np.random.default_rng(0)
-    sp = rng.normal(size=(180002, 3))
-    tp, tn = rng.normal(size=(217802, 3)), rng.normal(size=(217802, 3))
+    sp = rng.normal(size=(a.ns, 3))
+    tp, tn = rng.normal(size=(a.nt, 3)), rng.normal(size=(a.nt, 3))
 
     def med(fn):
         ts = []
@@ -41,6 +43,9 @@ def main():
         "m3d host tgt+nrm": med(lambda: Cloud(tp, tn)),
         "m3d host both": med(lambda: (Cloud(sp), Cloud(tp, tn))),
         "m3d device both": med(lambda: (Cloud(dev[0]), Cloud(dev[1], dev[2]))),
+        "m3d device src": med(lambda: Cloud(dev[0])),
+        "torch empty 2 blocks (alloc)": med(lambda: (torch.empty(a.ns * 7, dtype=torch.float64, device="cuda"),
+                                                    torch.empty(a.nt * 10, dtype=torch.float64, device="cuda"))),
         "torch pageable H2D (3 arrays)": med(lambda: [torch.from_numpy(x).cuda() for x in (sp, tp, tn)]),
         "torch pinned H2D (3 arrays)": med(lambda: [x.cuda(non_blocking=True) for x in pin]),
         "torch pageable H2D src only": med(lambda: torch.from_numpy(sp).cuda()),
