@@ -9,6 +9,8 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "linalg.h"
@@ -59,6 +61,97 @@ KTimer::~KTimer() {
 #define HIPX(ctx, expr) M3D_HIP_CHECK(ctx, expr)
 
 static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+namespace m3d {
+namespace {
+struct CachedBlock {
+  void* p;
+  size_t bytes;
+  int dev;
+  bool safe;  // a hipDeviceSynchronize on its device has run since the release
+};
+std::mutex g_bc_mu;
+std::vector<CachedBlock> g_bc;  // released, oldest first
+std::unordered_map<void*, std::pair<size_t, int>> g_bc_live;  // from block_alloc: size, device
+size_t g_bc_bytes = 0;
+constexpr size_t kBcMaxBytes = (size_t)2 << 30;
+constexpr size_t kBcMaxCount = 64;
+bool bc_on() {
+  static const bool on = [] {
+    const char* e = getenv("M3D_BLOCK_CACHE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+void bc_trim_locked(size_t max_bytes, size_t max_count) {
+  while (!g_bc.empty() && (g_bc_bytes > max_bytes || g_bc.size() > max_count)) {
+    (void)hipFree(g_bc.front().p);
+    g_bc_bytes -= g_bc.front().bytes;
+    g_bc.erase(g_bc.begin());
+  }
+}
+}  // namespace
+
+hipError_t block_alloc(void** out, size_t bytes) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (bc_on()) {
+    std::lock_guard<std::mutex> lk(g_bc_mu);
+    int best = -1;
+    for (int k = 0; k < (int)g_bc.size(); ++k) {
+      const CachedBlock& b = g_bc[(size_t)k];
+      if (b.dev == dev && b.bytes >= bytes && b.bytes <= 2 * bytes && (best < 0 || b.bytes < g_bc[(size_t)best].bytes))
+        best = k;
+    }
+    if (best >= 0) {
+      if (!g_bc[(size_t)best].safe) {
+        const hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) return e;
+        for (CachedBlock& b : g_bc)
+          if (b.dev == dev) b.safe = true;
+      }
+      const CachedBlock b = g_bc[(size_t)best];
+      g_bc.erase(g_bc.begin() + best);
+      g_bc_bytes -= b.bytes;
+      g_bc_live[b.p] = {b.bytes, dev};
+      *out = b.p;
+      return hipSuccess;
+    }
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess && bc_on()) {  // out of memory: give the cached blocks back and retry
+    std::lock_guard<std::mutex> lk(g_bc_mu);
+    (void)hipDeviceSynchronize();
+    bc_trim_locked(0, 0);
+    (void)hipGetLastError();
+    e = hipMalloc(&p, bytes);
+  }
+  if (e != hipSuccess) return e;
+  if (bc_on()) {
+    std::lock_guard<std::mutex> lk(g_bc_mu);
+    g_bc_live[p] = {bytes, dev};
+  }
+  *out = p;
+  return hipSuccess;
+}
+
+void block_release(void* p) {
+  if (p == nullptr) return;
+  if (bc_on()) {
+    std::lock_guard<std::mutex> lk(g_bc_mu);
+    auto it = g_bc_live.find(p);
+    if (it != g_bc_live.end()) {
+      g_bc.push_back(CachedBlock{p, it->second.first, it->second.second, false});
+      g_bc_bytes += it->second.first;
+      g_bc_live.erase(it);
+      bc_trim_locked(kBcMaxBytes, kBcMaxCount);
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
+}  // namespace m3d
 
 namespace {
 
@@ -516,7 +609,7 @@ void m3d_corrset_destroy(m3d_corrset* cs) {
   hipFree(cs->p32);
   hipFree(cs->q32);
   hipFree(cs->ca16);
-  hipFree(cs->cull_block);  // cas16, rowmap, cca16, tstat
+  block_release(cs->cull_block);  // cas16, rowmap, cca16, tstat
   delete cs;
 }
 
@@ -1027,12 +1120,12 @@ void m3d_cloud_destroy(m3d_cloud* c) {
   for (void** p : {reinterpret_cast<void**>(&c->slot), reinterpret_cast<void**>(&c->xyz64),
                    reinterpret_cast<void**>(&c->nrm64), reinterpret_cast<void**>(&c->xyz32)})
     if (in_block(*p, c->block, c->block_bytes)) *p = nullptr;
-  hipFree(c->block);
+  block_release(c->block);
   hipFree(c->slot);
   hipFree(c->xyz64);
   hipFree(c->nrm64);
   hipFree(c->xyz32);
-  hipFree(c->rec64);
+  block_release(c->rec64);
   delete c;
 }
 

@@ -702,7 +702,7 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) < total) ++bits;
   if (g->block != nullptr) {  // a rebuild: the previous cell arrays (one block)
-    hipFree(g->block);
+    block_release(g->block);
     g->block = nullptr;
     g->block_bytes = 0;
   } else {
@@ -788,7 +788,7 @@ void grid_free(Grid* g) {
                    reinterpret_cast<void**>(&g->order), reinterpret_cast<void**>(&g->mpts),
                    reinterpret_cast<void**>(&g->minv)})
     if (in_block(*p, g->block, g->block_bytes)) *p = nullptr;
-  hipFree(g->block);
+  block_release(g->block);
   g->block = nullptr;
   g->block_bytes = 0;
   hipFree(g->start);
@@ -798,8 +798,8 @@ void grid_free(Grid* g) {
   hipFree(g->minv);
   g->mpts = nullptr;
   g->minv = nullptr;
-  hipFree(g->mf16);
-  hipFree(g->mf32);
+  block_release(g->mf16);
+  block_release(g->mf32);
   g->start = nullptr;
   g->pts = nullptr;
   g->order = nullptr;

@@ -151,6 +151,16 @@ inline size_t tmp_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // Several device arrays in ONE allocation (256-B aligned pieces): the setup paths make one
 // hipMalloc per object instead of one per array, and the owner one hipFree.
+// Device block cache (api.cpp): the blocks of clouds, grids, Morton copies, target records and
+// MFMA tiles go back to a process-wide cache when their object dies, and a later allocation of
+// a size in [need, 2·need] takes one — after one hipDeviceSynchronize, so that no work enqueued
+// before the release can still use it.  hipFree of a 2–5 MB block costs ≈ 160 µs on the box
+// (unmapping; tools/ubench_alloc.hip), which a caller registering many pairs paid on every call
+// that evicted older clouds from the drop-in cache (tools/multipair_timing.py).  Bounded (64
+// blocks, 2 GiB; the oldest are freed first); M3D_BLOCK_CACHE=0 frees at once.
+hipError_t block_alloc(void** p, size_t bytes);
+void block_release(void* p);
+
 struct Carve {
   std::vector<std::pair<void**, size_t>> parts;
   template <class T>
@@ -161,7 +171,7 @@ struct Carve {
     size_t tot = 0;
     for (auto& q : parts) tot += q.second;
     void* b = nullptr;
-    const hipError_t e = hipMalloc(&b, std::max<size_t>(tot, 1));
+    const hipError_t e = block_alloc(&b, std::max<size_t>(tot, 1));
     *block = e == hipSuccess ? b : nullptr;
     *bytes = e == hipSuccess ? tot : 0;
     if (e != hipSuccess) return e;

@@ -1852,7 +1852,7 @@ hipError_t ensure_cull(const m3d_corrset* cs, hipStream_t st) {
     cv.add(&cca16, 4 * (size_t)nsub_pad);
     cv.add(&tstat, (size_t)nsub_pad);
     if ((e = cv.alloc(&blk, &bbytes)) != hipSuccess) {
-      hipFree(tb);
+      block_release(tb);
       return e;
     }
   }
@@ -1888,9 +1888,9 @@ hipError_t ensure_cull(const m3d_corrset* cs, hipStream_t st) {
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  hipFree(tb);
+  block_release(tb);
   if (e != hipSuccess) {
-    hipFree(blk);
+    block_release(blk);
     return e;
   }
   cs->cull_block = blk;
