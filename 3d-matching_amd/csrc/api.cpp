@@ -249,8 +249,9 @@ int cloud_pack(m3d_ctx* ctx, m3d_cloud* c, int64_t n, bool mean, hipStream_t st)
   if (c->n_pad == 0) return M3D_OK;
   const int sblocks = 128;
   const int blocks = (int)std::min<int64_t>(1024, (c->n_pad + 255) / 256);
-  const size_t o_c = 0, o_sum = tmp_align(3 * sizeof(double)),
-               o_p7 = o_sum + tmp_align(sizeof(double) * 3 * sblocks);
+  // [block sums | centre | block (rmax, lo, hi)]: the centre and the bounds partials adjacent, so
+  // that ONE device-to-host copy brings both back
+  const size_t o_sum = 0, o_c = tmp_align(sizeof(double) * 3 * sblocks), o_p7 = o_c + tmp_align(3 * sizeof(double));
   const size_t bytes = o_p7 + tmp_align(sizeof(float) * 7 * blocks);
   hipError_t e = ctx->tmp.reserve(bytes);
   if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_OOM, "cloud scratch");
@@ -263,14 +264,14 @@ int cloud_pack(m3d_ctx* ctx, m3d_cloud* c, int64_t n, bool mean, hipStream_t st)
   if (e == hipSuccess)
     e = launch_cloud_pack(c->xyz64, n, c->n_pad, dmean ? sum_part : nullptr, sblocks, cdev, c->center, c->xyz32,
                           kFar, p7, blocks, st);
-  std::vector<float> h(7 * (size_t)blocks);
-  double hc[3] = {0.0, 0.0, 0.0};
-  if (e == hipSuccess && dmean) e = hipMemcpyAsync(hc, cdev, sizeof(hc), hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), p7, sizeof(float) * h.size(), hipMemcpyDeviceToHost, st);
+  const size_t span = o_p7 - o_c + sizeof(float) * 7 * (size_t)blocks;
+  std::vector<double> hb((span + sizeof(double) - 1) / sizeof(double));
+  if (e == hipSuccess) e = hipMemcpyAsync(hb.data(), b + o_c, span, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+  const float* h = reinterpret_cast<const float*>(reinterpret_cast<const char*>(hb.data()) + (o_p7 - o_c));
   if (dmean)
-    for (int k = 0; k < 3; ++k) c->center[k] = hc[k];
+    for (int k = 0; k < 3; ++k) c->center[k] = hb[(size_t)k];
   float m = 0.0f;
   for (int k = 0; k < 3; ++k) {
     c->lo[k] = FLT_MAX;
