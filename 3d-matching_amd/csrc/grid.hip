@@ -279,11 +279,13 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
   }
 }
 
-// Deferred queries of grid_nn_batched_kernel (more than cand_cap candidates in their box: the
-// cells of a dense cluster, where kL lanes would walk hundreds of points each and one wave would
-// hold the whole launch): one block per query, its 4 waves over the box's rows and each wave's
-// 64 lanes over a row's points.  Same seed, same box, same pushes as the per-query scan, merged
-// by the same near_merge: the same (k1, near2) bits.
+// Deferred queries of grid_nn_batched_kernel<..., true>: those with more than cand_cap candidates
+// in their box (the cells of a dense cluster, where kL lanes would walk hundreds of points each
+// and one wave would hold the whole launch) and the ambiguous ones (runner-up within the band).
+// One block per query, its 4 waves over the box's rows and each wave's 64 lanes over a row's
+// points: same seed, same box, same pushes as the per-query scan, merged by the same near_merge
+// — the same (k1, near2) bits; an ambiguous query is then decided in fp64 here (below).  The
+// list's count is re-zeroed by the last block (hcnt[1] = block ticket).
 __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
     const float4* __restrict__ qpts, GridDev g, int64_t off, const IcpState* __restrict__ s,
     int64_t* __restrict__ keys, uint32_t* __restrict__ near2, const float4* __restrict__ sq,
