@@ -95,7 +95,75 @@ def parse():
                     help="N>1 collectives: libm3d's RCCL communicator, or torch.distributed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU baseline leg")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="bring up the ranks and the process group only, print the line with the "
+                         "rank count and exit (no GPU work: the launcher's CPU test)")
     return ap.parse_args()
+
+
+def visible_gpu_count() -> int:
+    """GPUs this job may use, counted in a throwaway child so that the launcher itself never
+    initialises the GPU (it starts the ranks afterwards)."""
+    import subprocess
+
+    try:
+        out = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                             capture_output=True, text=True, timeout=600)
+        return int(out.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported: the caller refuses to launch
+        print(f"[bench] could not count GPUs: {e}", file=sys.stderr)
+        return 0
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) without WORLD_SIZE: start N ranks, one per GPU, under
+    torch.distributed.run as a CHILD process (this process has not touched the GPU and never
+    execs), and return its exit code.  Refuses, without printing a line, when fewer than N GPUs
+    are visible — an N = 1 line for --gpus N is never printed.  M3D_BENCH_SAME_DEVICE=1 (every
+    rank on cuda:0, the functional rehearsal) skips the count."""
+    import socket
+    import subprocess
+
+    n = args.gpus
+    if os.environ.get("M3D_BENCH_SAME_DEVICE") != "1":
+        have = visible_gpu_count()
+        if have < n:
+            print(f"[bench] --gpus {n} needs {n} visible GPUs, this job sees {have}: refusing "
+                  "(one rank per GPU; RCCL cannot place two ranks on one device)", file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(args, world, rank):
+    """--launch-check: the process group over gloo (no GPU), a SUM of ones to count the ranks
+    that actually joined, and rank 0's line."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+        one = torch.ones(1, dtype=torch.int64)
+        dist.all_reduce(one)
+        joined, pg_world = int(one.item()), dist.get_world_size()
+    else:
+        joined, pg_world = 1, 1
+    if pg_world != args.gpus or joined != args.gpus:
+        print(f"[bench] rank {rank}: process group has {pg_world} ranks ({joined} joined), --gpus {args.gpus}",
+              file=sys.stderr)
+        return 3
+    if rank == 0:
+        print(json.dumps({"metric": "launch check", "value": None, "n_gpus": pg_world,
+                          "ranks_joined": joined, "launch_check": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 def pmc_traffic(kernel_substr: str, shape: str = ""):
@@ -146,13 +214,25 @@ def nn_roofline(ns, nt, avg_ms, launches, terms_ms):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("[bench] --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))  # before anything here touches the GPU
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to print a mislabelled line",
+              file=sys.stderr)
+        sys.exit(2)
+    if args.launch_check:
+        sys.exit(launch_check(args, world, rank))
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # M3D_BENCH_DIST=1 (under torch.distributed.run): take the N > 1 code path even at world 1 —
     # the nccl process group, the libm3d RCCL communicator beside it and the sharded protocols —
     # a rehearsal of the driver's multi-GPU runs on a one-GPU box (tools/gpu_dist1_rehearsal.sh)
@@ -189,6 +269,18 @@ def main():
                       file=sys.stderr)
         if comm is None:
             comm, comm_name = D.TorchComm(), f"torch.distributed-{dist.get_backend()}"
+    # the rank count the line reports is the one the collectives actually reach: a SUM of ones
+    # through the same communicator the hot path uses (RCCL inside libm3d, or torch.distributed)
+    comm_ranks = 1
+    if multi:
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"[bench] process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+        one = torch.ones(1, dtype=torch.int64, device=dev)
+        comm.sum_(one)
+        torch.cuda.synchronize()
+        comm_ranks = int(one.item())
+        if comm_ranks != world:
+            raise SystemExit(f"[bench] {comm_name} reached {comm_ranks} ranks, world {world}")
 
     def barrier():
         if multi:
@@ -680,7 +772,7 @@ def main():
         "data": "synthetic (m3d.synth: asymmetric closed surface, extent ~10, analytic normals)",
         "config": {"workload": head["workload"], "ns": ns, "nt_per_gpu": nt, "icp_iterations_per_step": iters,
                    "max_corr": r, "parallelism": "single" if not multi else f"{mode1}-shard x{world}",
-                   "comm": comm_name},
+                   "comm": comm_name, "comm_ranks": comm_ranks},
         "roofline": head["roofline"],
         "ms_per_step_with_kernel_events": cfg1["ms_per_step_with_kernel_events"],
         "cfg1": {k: v for k, v in cfg1.items() if k != "roofline"} if args.config == "cfg3" else None,
