@@ -312,105 +312,13 @@ int center_pack(m3d_ctx* ctx, const double* a, int64_t n, int64_t n_pad, const d
 
 int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
-// Host arrays → device.  Default: pageable hipMemcpyAsync straight into the cloud's buffers (the
-// runtime stages them itself).  M3D_UPLOAD=stage (measured slower, kept for A/B): the host pool's
-// threads copy M3D_UPLOAD_CHUNK-byte chunks (default 1 MB) into the context's pinned staging
-// memory while the caller issues each chunk's DMA as soon as that chunk and all before it are
-// staged (hostio.cpp host_pipeline); uploads larger than the staging cap go in rounds (each round
-// waits for the previous one's DMAs before it refills the buffer).  M3D_UPLOAD=register: the host
-// arrays are page-locked in place (hipHostRegister) for the copy.
+// Host arrays → device: pageable hipMemcpyAsync straight into the cloud's buffers (the runtime
+// stages them itself).  Measured against pinned staging through the host pool and against
+// hipHostRegister of the caller's arrays (round 3): both were slower at cfg1 sizes.
 int upload_host(m3d_ctx* ctx, int narr, void* const* dst, const void* const* src, const size_t* bytes,
                 hipStream_t st) {
-  static const int mode = [] {
-    const char* e = getenv("M3D_UPLOAD");
-    if (e && strcmp(e, "stage") == 0) return 1;
-    if (e && strcmp(e, "register") == 0) return 2;
-    return 0;
-  }();
-  static const size_t kChunk = [] {
-    const char* e = getenv("M3D_UPLOAD_CHUNK");
-    const long v = e ? atol(e) : 0;
-    return v >= 4096 ? (size_t)v : ((size_t)1 << 20);
-  }();
-  size_t total = 0;
-  for (int i = 0; i < narr; ++i) total += bytes[i];
-  if (total == 0) return M3D_OK;
-  if (mode == 0) {
-    for (int i = 0; i < narr; ++i)
-      if (bytes[i] > 0) HIPX(ctx, hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyHostToDevice, st));
-    return M3D_OK;
-  }
-  if (mode == 2) {
-    hipError_t e = hipSuccess;
-    int nreg = 0;
-    for (int i = 0; i < narr && e == hipSuccess; ++i) {
-      if (bytes[i] == 0) continue;
-      e = hipHostRegister(const_cast<void*>(src[i]), bytes[i], hipHostRegisterDefault);
-      if (e != hipSuccess) break;
-      nreg = i + 1;
-      e = hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyHostToDevice, st);
-    }
-    const hipError_t es = hipStreamSynchronize(st);
-    for (int i = 0; i < nreg; ++i)
-      if (bytes[i] > 0) (void)hipHostUnregister(const_cast<void*>(src[i]));
-    if (e == hipSuccess) e = es;
-    if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
-    return M3D_OK;
-  }
-  constexpr size_t kCap = (size_t)64 << 20;
-  const size_t want = std::min(kCap, (size_t)round_up((int64_t)total, (int64_t)1 << 22));
-  if (ctx->stage_ev == nullptr) HIPX(ctx, hipEventCreateWithFlags(&ctx->stage_ev, hipEventDisableTiming));
-  if (ctx->stage_cap < want) {
-    if (ctx->stage_pending) HIPX(ctx, hipEventSynchronize(ctx->stage_ev));
-    ctx->stage_pending = false;
-    if (ctx->stage != nullptr) hipHostFree(ctx->stage);
-    ctx->stage = nullptr;
-    ctx->stage_cap = 0;
-    if (hipHostMalloc(&ctx->stage, want, hipHostMallocDefault) != hipSuccess) {
-      ctx->stage = nullptr;
-      return m3d_fail(ctx, M3D_ERR_OOM, "pinned staging memory");
-    }
-    ctx->stage_cap = want;
-  }
-  struct Piece {
-    char* d;
-    const char* s;
-    size_t len, soff;
-  };
-  std::vector<Piece> pieces;
-  size_t done_bytes = 0;
-  int i = 0;
-  size_t off = 0;
-  while (done_bytes < total) {
-    // one round: up to stage_cap bytes of the concatenated arrays, cut into chunks
-    pieces.clear();
-    size_t soff = 0;
-    while (i < narr && soff < ctx->stage_cap) {
-      if (off >= bytes[i]) {
-        ++i;
-        off = 0;
-        continue;
-      }
-      const size_t len = std::min({kChunk, bytes[i] - off, ctx->stage_cap - soff});
-      pieces.push_back(Piece{static_cast<char*>(dst[i]) + off, static_cast<const char*>(src[i]) + off, len, soff});
-      off += len;
-      soff += len;
-    }
-    if (ctx->stage_pending) HIPX(ctx, hipEventSynchronize(ctx->stage_ev));
-    char* stage = static_cast<char*>(ctx->stage);
-    hipError_t err = hipSuccess;
-    host_pipeline(
-        (int64_t)pieces.size(),
-        [&](int64_t k) { memcpy(stage + pieces[(size_t)k].soff, pieces[(size_t)k].s, pieces[(size_t)k].len); },
-        [&](int64_t k) {
-          const Piece& pc = pieces[(size_t)k];
-          if (err == hipSuccess) err = hipMemcpyAsync(pc.d, stage + pc.soff, pc.len, hipMemcpyHostToDevice, st);
-        });
-    if (err == hipSuccess) err = hipEventRecord(ctx->stage_ev, st);
-    if (err != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(err));
-    ctx->stage_pending = true;
-    done_bytes += soff;
-  }
+  for (int i = 0; i < narr; ++i)
+    if (bytes[i] > 0) HIPX(ctx, hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyHostToDevice, st));
   return M3D_OK;
 }
 
@@ -462,8 +370,6 @@ void m3d_destroy(m3d_ctx* ctx) {
   if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->one_ticket) hipFree(ctx->one_ticket);
   if (ctx->prep) hipFree(ctx->prep);
-  if (ctx->stage) hipHostFree(ctx->stage);
-  if (ctx->stage_ev) hipEventDestroy(ctx->stage_ev);
   ctx->tmp.release();
   ctx->run.release();
   for (auto& v : ctx->ev)
@@ -610,7 +516,6 @@ void m3d_corrset_destroy(m3d_corrset* cs) {
   hipFree(cs->p32);
   hipFree(cs->q32);
   hipFree(cs->ca16);
-  block_release(cs->cull_block);  // cas16, rowmap, cca16, tstat
   delete cs;
 }
 
@@ -803,56 +708,21 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
   }
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(max_iter, 1)));
   const double thr_sq = thr_sq_of(p->thr, p->mode);
-  // tile culling of the MFMA screen (ransac.hip, round 4; opt-in M3D_SCORE_CULL=1): the corrset's
-  // sorted rows and tile bounds are built on its first culled run (one sync)
-  const bool cull = nc > 0 && score_cull_on(cs, thr_sq);
-  if (cull) HIPX(ctx, ensure_cull(cs, st));
   Arena a(ctx, S(stream));
   size_t o[kScoreSlots];
   score_layout(a, B, o);
   size_t o_T = a.take(sizeof(double) * 16 * B);
   size_t o_c = a.take(sizeof(int32_t) * B);
-  size_t oc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const int64_t hpB = score_mf_hpad(B);
-  const size_t csort = cull ? cull_sort_bytes(hpB) : 0;
-  if (cull) {
-    oc[0] = a.take(sizeof(uint32_t) * hpB);
-    oc[1] = a.take(sizeof(uint32_t) * hpB);
-    oc[2] = a.take(sizeof(int32_t) * hpB);
-    oc[3] = a.take(sizeof(int32_t) * hpB);
-    oc[4] = a.take(sizeof(float) * hpB);
-    oc[5] = a.take(sizeof(float) * hpB);
-    oc[6] = a.take(sizeof(float) * hpB);
-    oc[7] = a.take(sizeof(uint32_t) * (size_t)(hpB / 32) * (size_t)(cs->nsub_pad / 32));
-    oc[8] = a.take(csort);
-  }
   int rc = a.commit();
   if (rc) return rc;
   ScoreScratch s = score_bind(a, o);
   double* Tb = a.at<double>(o_T);
   int32_t* cb = a.at<int32_t>(o_c);
-  ScoreCull cc;
-  if (cull) {
-    cc.key = a.at<uint32_t>(oc[0]);
-    cc.key2 = a.at<uint32_t>(oc[1]);
-    cc.val = a.at<int32_t>(oc[2]);
-    cc.perm = a.at<int32_t>(oc[3]);
-    cc.a = a.at<float>(oc[4]);
-    cc.apos = a.at<float>(oc[5]);
-    cc.edpos = a.at<float>(oc[6]);
-    cc.skip = a.at<uint32_t>(oc[7]);
-    cc.sort_tmp = a.at<char>(oc[8]);
-    cc.sort_bytes = csort;
-  }
   // counts of the hypotheses after an early stop are never scored: they read 0
   if (counts_out != nullptr && max_iter > 0)
     HIPX(ctx, hipMemsetAsync(counts_out, 0, sizeof(int32_t) * max_iter, st));
   HIPX(ctx, launch_ransac_init(ctx->rstate, ctx->stats, max_iter == 0 ? 1 : 0, st));
   const int32_t* done = &ctx->rstate->done;
-  static const bool fuse_on = [] {  // M3D_RANSAC_FUSE=0: separate hyp16 launch (A/B)
-    const char* e = getenv("M3D_RANSAC_FUSE");
-    return !(e && atoi(e) == 0);
-  }();
   for (int64_t b0 = 0; b0 < max_iter; b0 += B) {
     const int64_t n = std::min(B, max_iter - b0);
     const int32_t* tri = triples ? triples + 3 * b0 : nullptr;
@@ -862,14 +732,11 @@ int m3d_ransac_run_async(m3d_ctx* ctx, const m3d_corrset* cs, const m3d_ransac_p
       KTimer kt(ctx, M3D_KERNEL_KABSCH, st);
       const ScoreFuse fz{&s.mf, p->thr, p->mode};
       e = launch_kabsch3(cs, tri, p->seed, p->hyp0 + b0, n, thr_sq, Tb, nullptr, s.hypf, done,
-                         ZeroArgs{cnt}, st, (nc > 0 && fuse_on && !cull) ? &fz : nullptr);
+                         ZeroArgs{cnt}, st, nc > 0 ? &fz : nullptr);
     }
     if (e == hipSuccess) {
-      if (cull) {
-        KTimer kt(ctx, M3D_KERNEL_SCORE, st);
-        e = launch_score_culled(cs, Tb, n, p->thr, p->mode, cnt, ctx->stats, done, s.mf, cc, st);
-      } else if (nc > 0) {
-        e = score_enqueue(ctx, cs, Tb, n, p->thr, p->mode, cnt, s, done, st, fuse_on);
+      if (nc > 0) {
+        e = score_enqueue(ctx, cs, Tb, n, p->thr, p->mode, cnt, s, done, st, true);
       } else {
         e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * n, st);
       }
@@ -1161,24 +1028,22 @@ int ensure_grid(m3d_ctx* ctx, const m3d_cloud* c, double cell, hipStream_t st, c
   return M3D_OK;
 }
 
-// The ICP source in Morton slot order for cell size `cell` (grid.hip morton_copy), built once and
+// The ICP source in Morton slot order for cell size `cell` (grid.hip morton_source), built once and
 // cached on the caller's cloud; sg = the caller's grid at that cell size.
-int ensure_morton_source(m3d_ctx* ctx, const m3d_cloud* c, const Grid* sg, double cell,
-                         const m3d_cloud** out, const Grid** gout) {
+int ensure_morton_source(m3d_ctx* ctx, const m3d_cloud* c, double cell, const m3d_cloud** out,
+                         const Grid** gout) {
   for (auto& m : c->morton)
     if (m.first == cell && m.second->n == c->n) {
       *out = m.second;
       *gout = m.second->grids.front();
       return M3D_OK;
     }
-  // sg == nullptr: straight from the points (grid.hip morton_source, the same slots without the
-  // source's cell grid); else derived from the source grid (morton_copy)
-  hipError_t e = sg != nullptr ? grid_morton(const_cast<Grid*>(sg), nullptr, &ctx->tmp) : hipSuccess;
+  // straight from the points (grid.hip morton_source: the slots without the source's cell grid)
   m3d_cloud* mc = new m3d_cloud();
   mc->ctx = ctx;
   Grid* g = new Grid();
   mc->grids.push_back(g);
-  if (e == hipSuccess) e = sg != nullptr ? morton_copy(c, sg, mc, g, nullptr) : morton_source(c, cell, mc, g, &ctx->tmp, nullptr);
+  hipError_t e = morton_source(c, cell, mc, g, &ctx->tmp, nullptr);
   if (e != hipSuccess) {
     m3d_cloud_destroy(mc);
     return m3d_fail(ctx, M3D_ERR_HIP, std::string("morton source: ") + hipGetErrorString(e));
@@ -1213,7 +1078,7 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = 
   if (s->params.nn_method == M3D_NN_GRID) {
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->sgrid, s->tgrid, off, s->state, s->keys,
-                          s->near2, s->sq, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st, q0, q1,
+                          s->near2, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st, q0, q1,
                           s->hlist, s->hcnt, s->cand_cap, s->src->xyz64, s->tgt->xyz64);
   }
   if (!seeded) {
@@ -1269,54 +1134,21 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
   const Grid *tg = nullptr, *sg = nullptr;
   const m3d_cloud* src_m = nullptr;
   int64_t coarse_max_occ = 0;  // most target points in one cell at cell ≈ r (grid NN)
-  // M3D_CREATE_PROF=1 (diagnostics): wall ms of each setup stage, synchronised in between
-  static const bool cprof = [] {
-    const char* e = getenv("M3D_CREATE_PROF");
-    return e && atoi(e) == 1;
-  }();
-  double tprev = 0.0;
-  std::string cstages;
-  auto stage = [&](const char* name) {
-    if (!cprof) return;
-    (void)hipDeviceSynchronize();
-    const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-    if (tprev > 0.0) cstages += std::string(" ") + name + " " + std::to_string(t - tprev);
-    tprev = t;
-  };
-  stage("start");
   {
     // Grid NN: cell ≈ the search radius, a query visits 3 cells per axis.  Brute force: the
     // same grids only ORDER the points (targets and queries in cell order make the MFMA
     // screen's 32-target sub-tiles and 64-query waves spatially compact); every pair is still
     // screened.
-    static const double cell_div = [] {  // M3D_GRID_CELL_DIV (experiment): cell = radius / div
-      const char* e = getenv("M3D_GRID_CELL_DIV");
-      const double v = e ? atof(e) : 1.0;
-      return v >= 1.0 ? v : 1.0;
-    }();
-    const double cell = max_dist * 1.001 / cell_div;
+    const double cell = max_dist * 1.001;
     int grc = ensure_grid(ctx, tgt, cell, nullptr, &tg);
-    stage("tgrid");
-    // the source's own cell grid only for the A/B switches that read it (M3D_NN_QORDER=cell
-    // orders brute-force queries by its cells; M3D_MORTON_DIRECT=0 derives the Morton slots from
-    // it as in round 3); by default the Morton slots come straight from the points
-    static const bool src_grid = [] {
-      const char* q = getenv("M3D_NN_QORDER");
-      const char* m = getenv("M3D_MORTON_DIRECT");
-      return (q && strcmp(q, "cell") == 0) || (m && atoi(m) == 0);
-    }();
-    if (!grc && src_grid) grc = ensure_grid(ctx, src, cell, nullptr, &sg);
-    stage("sgrid");
-    // the loop runs on the source in Morton slot order (sg: the copy's query grid afterwards)
+    // the loop runs on the source in Morton slot order (sg: the copy's query grid)
     const m3d_cloud* ms = nullptr;
-    if (!grc) grc = ensure_morton_source(ctx, src, sg, cell, &ms, &sg);
+    if (!grc) grc = ensure_morton_source(ctx, src, cell, &ms, &sg);
     if (!grc) src_m = ms;
-    stage("morton");
     if (!grc) {
       hipError_t e = ensure_target_rec(tgt, nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("target records: ") + hipGetErrorString(e));
     }
-    stage("rec");
     // (after the source grid, Morton copy and target records are enqueued: the occupancy's one
     // sync then also covers them instead of stalling the queue in between)
     // Grid NN on a dense target: a seeded query's box is ~1–2 cells per axis, so the candidates
@@ -1324,23 +1156,20 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
     // (m = points per occupied cell at cell ≈ r; any cell size gives the same keys, grid.hip):
     // measured (tools/grid_cell_sweep.sh) 1M × 1M (m ≈ 33) 206 → 128 µs per scan at div 3;
     // cfg1 (m ≈ 3.9) and the 1M × 125k shard (m ≈ 4.7) are fastest at div 1.
-    if (!grc && params->nn_method == M3D_NN_GRID && getenv("M3D_GRID_CELL_DIV") == nullptr) {
+    if (!grc && params->nn_method == M3D_NN_GRID) {
       hipError_t e = grid_occupancy(const_cast<Grid*>(tg), &ctx->tmp, nullptr);  // one sync, once per grid
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("grid occupancy: ") + hipGetErrorString(e));
     }
-    if (!grc && params->nn_method == M3D_NN_GRID && getenv("M3D_GRID_CELL_DIV") == nullptr &&
-        tg->n_occ > 0) {
+    if (!grc && params->nn_method == M3D_NN_GRID && tg->n_occ > 0) {
       coarse_max_occ = tg->max_occ;
       const double m = (double)tg->n_pts / (double)tg->n_occ;
       const int div = std::min(4, std::max(1, (int)std::floor(std::sqrt(m / 3.5))));
       if (div > 1) grc = ensure_grid(ctx, tgt, cell / div, nullptr, &tg);
     }
-    stage("tgrid_div");
     if (!grc && params->nn_method == M3D_NN_BRUTE && tg->mf16 == nullptr) {
       hipError_t e = build_mfma_tiles(tgt, const_cast<Grid*>(tg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("mfma tiles: ") + hipGetErrorString(e));
     }
-    stage("tiles");
     // the setup above ran asynchronously on the null stream: finish it before the loop object is
     // used on the caller's streams
     if (!grc) {
@@ -1360,13 +1189,7 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
   s->nblocks = terms_blocks(src->n);
   s->tgrid = tg;
   // brute-force query order: the Morton slots themselves (compact 64-query waves, contiguous
-  // slot ranges for the split exchange of the target-shard loop); M3D_NN_QORDER=cell: the source
-  // grid's row-major cell order (round 2)
-  static const bool cell_order = [] {
-    const char* e = getenv("M3D_NN_QORDER");
-    return e && strcmp(e, "cell") == 0;
-  }();
-  s->qorder = cell_order ? sg->order : nullptr;  // (cell_order builds the source grid, above)
+  // slot ranges for the split exchange of the target-shard loop)
   s->sgrid = sg;
   // Dense target cells (a cell at ≈ r holding ≥ kHeavyCell points — e.g. the vertex fan at a
   // UV-sphere pole, ~30× the mean density): queries with more than kHeavyCand candidates are
@@ -1422,17 +1245,6 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
       }
     }
   }
-  // seed records (M3D_GRID_SEEDREC=1): measured slower while the clouds keep the caller's point
-  // order — the terms pass's writes to Morton positions scatter (cfg1 grid iteration 38.8 →
-  // 41.5 µs, 1M × 125k 137 → 152 µs)
-  static const bool seedrec = [] {
-    const char* e = getenv("M3D_GRID_SEEDREC");
-    return e && atoi(e) == 1;
-  }();
-  if (!rc && seedrec && params->nn_method == M3D_NN_GRID && sg->minv != nullptr)
-    rc = dev_alloc(ctx, &s->sq, std::max<int64_t>(src->n, 1));
-  stage("loop_alloc");
-  if (cprof) fprintf(stderr, "[m3d create] ms:%s\n", cstages.c_str());
   if (rc) {
     m3d_icp_destroy(s);
     return rc;
@@ -1449,12 +1261,9 @@ void m3d_icp_destroy(m3d_icp* s) {
   if (s->cap_stream != nullptr) hipStreamDestroy(s->cap_stream);
   if (s->src != nullptr) s->src->refs -= 1;
   hipFree(s->block);  // state, keys, near2, dprev, ld64, lidx, corr, partials, sums
-  hipFree(s->sq);
   hipFree(s->xdk);
   hipFree(s->xcl);
   hipFree(s->xsums);
-  hipFree(s->pp);
-  hipFree(s->pcounter);
   delete s;
 }
 
@@ -1468,8 +1277,6 @@ int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
   HIPX(ctx, hipMemsetAsync(s->corr, 0xFF, sizeof(int32_t) * std::max<int64_t>(s->src->n, 1), st));
   // all-ones bits = a NaN distance: no bound seed until a target-shard exchange wrote dprev
   HIPX(ctx, hipMemsetAsync(s->dprev, 0xFF, sizeof(int64_t) * std::max<int64_t>(s->src->n, 1), st));
-  if (s->sq != nullptr)  // all-ones index: no seed (nnkey.h seed_rec)
-    HIPX(ctx, hipMemsetAsync(s->sq, 0xFF, sizeof(float4) * std::max<int64_t>(s->src->n, 1), st));
   HIPX(ctx, launch_icp_reset(s, T, st));
   s->keys_clean = false;
   return M3D_OK;
@@ -1574,15 +1381,6 @@ int m3d_icp_prepare_steps(m3d_icp* s, int32_t n) {
 int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   CHECK_ARG(s->ctx, n >= 0, "n must be >= 0");
-  // single-device grid loop: the n steps in ONE persistent launch (icp.hip icp_grid_persist_kernel,
-  // the same bits as the steps below)
-  if (n >= 1 && icp_persist_ok(s)) {
-    hipSetDevice(s->ctx->device);
-    KTimer kt(s->ctx, M3D_KERNEL_LOOP, S(stream));
-    HIPX(s->ctx, launch_icp_persist(s, n, S(stream)));
-    s->keys_clean = false;
-    return M3D_OK;
-  }
   if (n >= 2 && icp_graphs_on() && !s->graph_off && !s->ctx->profiling) {
     const int slot = s->keys_clean ? 1 : 0;
     const bool have = s->graph[slot] != nullptr && s->graph_n[slot] == n;
@@ -1676,14 +1474,8 @@ int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream) {
   if (!s || !out) return M3D_ERR_INVALID;
   m3d_ctx* ctx = s->ctx;
   IcpState h;
-  int32_t fault = 0;
   HIPX(ctx, hipMemcpyAsync(&h, s->state, sizeof(h), hipMemcpyDeviceToHost, S(stream)));
-  if (s->pcounter != nullptr)
-    HIPX(ctx, hipMemcpyAsync(&fault, s->pcounter + 8, sizeof(fault), hipMemcpyDeviceToHost, S(stream)));
   HIPX(ctx, hipStreamSynchronize(S(stream)));
-  if (fault != 0)
-    return m3d_fail(ctx, M3D_ERR_HIP, "persistent ICP loop: a workgroup waited past its bound for the "
-                                      "others (not all resident); results are invalid");
   for (int k = 0; k < 16; ++k) out->T[k] = h.T[k];
   out->fitness = h.fitness;
   out->inlier_rmse = h.rmse;
@@ -1743,27 +1535,11 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
                 int32_t* corr_idx, void* stream) {
   if (!ctx) return M3D_ERR_INVALID;
   CHECK_ARG(ctx, out != nullptr, "null output");
-  // M3D_RUN_PROF=1 (diagnostics): wall ms of each stage, synchronised in between
-  static const bool rprof = [] {
-    const char* e = getenv("M3D_RUN_PROF");
-    return e && atoi(e) == 1;
-  }();
-  double tprev = 0.0;
-  std::string rstages;
-  auto stage = [&](const char* name) {
-    if (!rprof) return;
-    (void)hipDeviceSynchronize();
-    const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-    if (name != nullptr) rstages += std::string(" ") + name + " " + std::to_string(t - tprev);
-    tprev = t;
-  };
-  stage(nullptr);
   m3d_icp* s = nullptr;
   int rc = icp_create(ctx, src, tgt, max_dist, params, &s, true);
   if (rc) return rc;
-  stage("create");
   rc = m3d_icp_reset(s, init, stream);
-  // max_iteration + 1 evaluations: one persistent launch for the grid loop, else enqueued in
+  // max_iteration + 1 evaluations, enqueued in
   // growing chunks (4, 8, 16, …) with a look at the state's `done` between chunks — a converged
   // loop (often after a handful of evaluations) then does not enqueue the remaining ~2 launches
   // per evaluation that would only read `done` and return.  The evaluations that run are the
@@ -1771,36 +1547,27 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
   if (!rc) {
     const int32_t total = params->max_iteration + 1;
     s->graph_off = true;  // a one-shot loop: no HIP graph capture (two equal chunks would trigger one)
-    if (icp_persist_ok(s)) {
-      rc = m3d_icp_steps(s, total, stream);
-    } else {
-      int32_t left = total, chunk = 4;
-      while (!rc && left > 0) {
-        const int32_t k = std::min(chunk, left);
-        rc = m3d_icp_steps(s, k, stream);
-        left -= k;
-        chunk *= 2;
-        if (rc || left == 0) break;
-        int32_t done = 0;
-        hipError_t e = hipMemcpyAsync(&done, &s->state->done, sizeof(done), hipMemcpyDeviceToHost, S(stream));
-        if (e == hipSuccess) e = hipStreamSynchronize(S(stream));
-        if (e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
-        if (done) break;
-      }
+    int32_t left = total, chunk = 4;
+    while (!rc && left > 0) {
+      const int32_t k = std::min(chunk, left);
+      rc = m3d_icp_steps(s, k, stream);
+      left -= k;
+      chunk *= 2;
+      if (rc || left == 0) break;
+      int32_t done = 0;
+      hipError_t e = hipMemcpyAsync(&done, &s->state->done, sizeof(done), hipMemcpyDeviceToHost, S(stream));
+      if (e == hipSuccess) e = hipStreamSynchronize(S(stream));
+      if (e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
+      if (done) break;
     }
   }
-  stage("steps");
   if (!rc) rc = m3d_icp_result_get(s, out, stream);
-  stage("result");
   if (!rc && corr_idx && src->n > 0) {
     hipError_t e = launch_scatter_i32(s->corr, s->src->slot, src->n, corr_idx, S(stream));
     if (e == hipSuccess) e = hipStreamSynchronize(S(stream));
     if (e != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
   }
-  stage("corr");
   m3d_icp_destroy(s);
-  stage("destroy");
-  if (rprof) fprintf(stderr, "[m3d run] ms:%s evaluations %d\n", rstages.c_str(), out->iterations + 1);
   return rc;
 }
 

@@ -109,13 +109,9 @@ int agree(m3d_comm* c, int local_rc, hipStream_t st) {
 }
 
 // Target-shard loop: split the sources into two slot halves so that the first half's d64 MIN
-// runs on the exchange stream while the second half's NN runs (M3D_SHARD_SPLIT=0: one piece).
+// runs on the exchange stream while the second half's NN runs (M3D_ICP_NO_SPLIT: one piece).
 bool split_exchange(const m3d_icp* s) {
-  static const bool env = [] {
-    const char* e = getenv("M3D_SHARD_SPLIT");
-    return !(e && atoi(e) == 0);
-  }();
-  return env && !(s->params.flags & M3D_ICP_NO_SPLIT) && s->src->n >= 2 * 4096 && icp_nn_range_ok(s);
+  return !(s->params.flags & M3D_ICP_NO_SPLIT) && s->src->n >= 2 * 4096 && icp_nn_range_ok(s);
 }
 }  // namespace
 

@@ -119,86 +119,10 @@ __global__ __launch_bounds__(kGridBlock) void grid_gather_kernel(const float4* _
 
 // ------------------------------------------------------------------------------- query
 
-// kGridLanes lanes cooperate on one query: the query's cell rows (contiguous runs of the sorted
-// array) are dealt round-robin to the lanes, each lane keeps its packed (bits(d²) << 32 | index)
-// minimum and the runner-up distance near2 (nnkey.h near_push), and the lanes combine with
-// shuffles.  A key compare is exactly the lexicographic (d², index) compare of the brute-force
-// scan (d² ≥ +0, so the float bits order as the values; NaN bits order above every finite bound
-// and are never selected).  Several lanes per query keep more loads in flight than one lane
-// per query: the scan is latency-bound, not bandwidth.
-constexpr int kGridLanesDefault = 4;  // M3D_GRID_LANES = 1|2|4|8|16 overrides (tuning)
-
-template <int kGridLanes>
-__global__ __launch_bounds__(kGridBlock) void grid_nn_kernel(const float4* __restrict__ src32,
-                                                             int64_t ns,
-                                                             const int32_t* __restrict__ order,
-                                                             GridDev g, int64_t off,
-                                                             const IcpState* __restrict__ s,
-                                                             int64_t* __restrict__ keys,
-                                                             uint32_t* __restrict__ near2,
-                                                             const int32_t* __restrict__ prev,
-                                                             const int64_t* __restrict__ dprev,
-                                                             const float4* __restrict__ tgt32,
-                                                             int64_t nt_shard) {
-  // The query starts from seed_key (its previous correspondence re-evaluated, or a bound): the
-  // cell box then only has to cover the seed's search bound (search_bound: the fp64 band around
-  // it, capped at r2_hi) instead of r2_hi (same lemma as above with r2_hi replaced by that
-  // bound); k1 is still the lexicographic minimum over all targets with d² ≤ r2_hi, and near2
-  // covers every other target within the band of k1 (nnkey.h header).
-  if (s->done) return;
-  const int64_t t = ((int64_t)blockIdx.x * kGridBlock + threadIdx.x) / kGridLanes;
-  const int sub = threadIdx.x & (kGridLanes - 1);
-  const float r2_hi = s->r2_hi, be = s->band_e;
-  const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
-  uint64_t k1 = key0;
-  float k1d = kInf, n2 = kInf;
-  int64_t i = 0;
-  if (t < ns) {
-    i = order != nullptr ? (int64_t)order[t] : t;
-    const float4 p = src32[i];
-    float qx, qy, qz;
-    xform32(s->Rt32, p, qx, qy, qz);
-    const int64_t seed = seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
-    if (seed != kKeyNone) k1 = (uint64_t)seed;
-    k1d = key_real_d2(k1);
-    if (g.ncells > 0) {
-      const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
-      const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
-      const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
-      const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
-      const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
-      const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
-      const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
-      const int ny = y1 - y0 + 1;
-      const int rows = ny * (z1 - z0 + 1);
-      for (int r = sub; r < rows; r += kGridLanes) {
-        const int cz = z0 + r / ny, cy = y0 + r % ny;
-        const int64_t row = ((int64_t)cz * g.n[1] + cy) * g.n[0];
-        const int32_t j0 = g.start[row + x0], j1 = g.start[row + x1 + 1];
-        for (int32_t j = j0; j < j1; ++j) {
-          const float4 v = g.pts[j];
-          const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
-          if (d2 <= r2_hi)
-            near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(v.w))), d2);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int o = kGridLanes / 2; o > 0; o >>= 1) {
-    const uint64_t b1 = ((uint64_t)(uint32_t)__shfl_xor((int)(k1 >> 32), o, kGridLanes) << 32) |
-                        (uint32_t)__shfl_xor((int)(uint32_t)k1, o, kGridLanes);
-    const float bn2 = __shfl_xor(n2, o, kGridLanes);
-    near_merge(k1, k1d, n2, b1, bn2);
-  }
-  if (t < ns && sub == 0) {
-    keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
-    near2[i] = __float_as_uint(n2);
-  }
-}
-
-// ------------------------------------------------------------------------------- batched
-// Per-query form over the Morton query order: kL lanes per query, the queries straight from the
+// ------------------------------------------------------------------------------- query
+// kL lanes per query over the Morton query order (the scan state of nnkey.h per lane: packed
+// (bits(d²) << 32 | index) minimum and runner-up near2, lanes combined by shuffles; a key compare
+// is the lexicographic (d², index) compare of the brute-force scan), the queries straight from the
 // Morton-sorted points (no order[] indirection).  Every lane of a query sees every cell row of
 // its box and takes the row's points sub, sub + kL, …: the start offsets of kR rows are loaded
 // together, then kR × kB point loads per lane go out at once, so a typical seeded query (≤ kR
@@ -210,12 +134,9 @@ template <int kL, int kR, int kB, bool kDefer = false>
 __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const float4* __restrict__ qpts, int64_t ns, GridDev g, int64_t off,
     const IcpState* __restrict__ s, int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
-    const float4* __restrict__ sq, const int32_t* __restrict__ prev,
-    const int64_t* __restrict__ dprev, const float4* __restrict__ tgt32, int64_t nt_shard,
-    int64_t nblocks, unsigned long long* __restrict__ stats, int64_t q0, int32_t* __restrict__ hlist,
-    uint32_t* __restrict__ hcnt, int cand_cap) {
-  // stats (M3D_GRID_STATS=1, diagnostics only, else null): [0] queries, [1] cell rows,
-  // [2] candidate points, [3] queries with a seed, [4] most candidates of one query
+    const int32_t* __restrict__ prev, const int64_t* __restrict__ dprev,
+    const float4* __restrict__ tgt32, int64_t nt_shard, int64_t nblocks, int64_t q0,
+    int32_t* __restrict__ hlist, uint32_t* __restrict__ hcnt, int cand_cap) {
   if (s->done) return;
   const int64_t per = (nblocks + 7) / 8;
   const int64_t blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
@@ -232,10 +153,8 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     i = (int64_t)__float_as_int(p.w);
     float qx, qy, qz;
     xform32(s->Rt32, p, qx, qy, qz);
-    // seed: the record the terms pass left in query order (no prev[] → target gather), or
-    // the correspondence array when no record buffer is kept
-    const int64_t seed = sq != nullptr ? seed_from_rec(s, sq[t], p, qx, qy, qz)
-                                       : seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
+    // seed: the previous correspondence re-evaluated (nnkey.h seed_key), or a bound
+    const int64_t seed = seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
     if (seed != kKeyNone) k1 = (uint64_t)seed;
     k1d = key_real_d2(k1);
     if (g.ncells > 0) {
@@ -252,13 +171,6 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
           hlist[slot] = (int32_t)t;
         }
         i = -1;
-      }
-      if (stats != nullptr && sub == 0) {
-        atomicAdd(&stats[0], 1ull);
-        atomicAdd(&stats[1], (unsigned long long)rows);
-        atomicAdd(&stats[2], (unsigned long long)cand);
-        if (seed != kKeyNone) atomicAdd(&stats[3], 1ull);
-        atomicMax(&stats[4], (unsigned long long)cand);
       }
     }
   }
@@ -288,8 +200,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
 // list's count is re-zeroed by the last block (hcnt[1] = block ticket).
 __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
     const float4* __restrict__ qpts, GridDev g, int64_t off, const IcpState* __restrict__ s,
-    int64_t* __restrict__ keys, uint32_t* __restrict__ near2, const float4* __restrict__ sq,
-    const int32_t* __restrict__ prev, const int64_t* __restrict__ dprev,
+    int64_t* __restrict__ keys, uint32_t* __restrict__ near2, const int32_t* __restrict__ prev, const int64_t* __restrict__ dprev,
     const float4* __restrict__ tgt32, int64_t nt_shard, const int32_t* __restrict__ hlist,
     uint32_t* __restrict__ hcnt, const double* __restrict__ src64,
     const double* __restrict__ tgt64, int64_t nq) {
@@ -327,8 +238,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
 #endif
     float qx, qy, qz;
     xform32(s->Rt32, p, qx, qy, qz);
-    const int64_t seed = sq != nullptr ? seed_from_rec(s, sq[t], p, qx, qy, qz)
-                                       : seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
+    const int64_t seed = seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
     uint64_t k1 = seed != kKeyNone ? (uint64_t)seed : key0;
     float k1d = key_real_d2(k1), n2 = kInf;
     const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
@@ -563,42 +473,6 @@ hipError_t launch_validate(const Grid* qgrid, int64_t ns, const double* src64, c
   return hipGetLastError();
 }
 
-// Morton (Z-curve) order of a cloud's points by their cells (10 bits per axis; finer grids are
-// coarsened — only locality matters, any order gives the same keys).
-__device__ __forceinline__ uint32_t spread3(uint32_t v) {
-  v &= 0x3FF;
-  v = (v | (v << 16)) & 0x030000FF;
-  v = (v | (v << 8)) & 0x0300F00F;
-  v = (v | (v << 4)) & 0x030C30C3;
-  v = (v | (v << 2)) & 0x09249249;
-  return v;
-}
-
-__global__ __launch_bounds__(kGridBlock) void morton_key_kernel(const float4* __restrict__ pts, int64_t n,
-                                                                GridDev g, int sx, int sy, int sz,
-                                                                uint32_t* __restrict__ key,
-                                                                int32_t* __restrict__ val) {
-  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
-  if (k >= n) return;
-  const float4 v = pts[k];
-  const uint32_t cx = (uint32_t)grid_coord(v.x, g.o[0], g.inv_h, g.n[0]) >> sx;
-  const uint32_t cy = (uint32_t)grid_coord(v.y, g.o[1], g.inv_h, g.n[1]) >> sy;
-  const uint32_t cz = (uint32_t)grid_coord(v.z, g.o[2], g.inv_h, g.n[2]) >> sz;
-  key[k] = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
-  val[k] = (int32_t)k;
-}
-
-__global__ __launch_bounds__(kGridBlock) void morton_gather_kernel(const float4* __restrict__ pts,
-                                                                   const int32_t* __restrict__ perm,
-                                                                   int64_t n, float4* __restrict__ out,
-                                                                   int32_t* __restrict__ minv) {
-  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
-  if (k >= n) return;
-  const float4 v = pts[perm[k]];
-  out[k] = v;
-  minv[__float_as_int(v.w)] = (int32_t)k;
-}
-
 // ------------------------------------------------------------------------------- host side
 static hipError_t grid_fail(hipError_t e, void* a, void* b, void* c, void* d, void* tmp) {
   hipFree(a);
@@ -810,155 +684,26 @@ void grid_free(Grid* g) {
   g->mf_npad = 0;
 }
 
-hipError_t grid_morton(Grid* g, hipStream_t st, TmpArena* ta) {
-  if (g->mpts != nullptr || g->n_pts == 0) return hipSuccess;
-  const int64_t n = g->n_pts;
-  int sh[3];
-  for (int k = 0; k < 3; ++k) {
-    sh[k] = 0;
-    while ((g->dev.n[k] >> sh[k]) > 1024) ++sh[k];
-  }
-  uint32_t *kin = nullptr, *kout = nullptr;
-  int32_t *vin = nullptr, *vout = nullptr;
-  void* tmp = nullptr;
-  size_t tmp_bytes = 0;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
-  if (e != hipSuccess) return e;
-  tmp_bytes = std::max<size_t>(tmp_bytes, 1);
-  const size_t a4 = tmp_align(sizeof(uint32_t) * (size_t)n);
-  if (ta != nullptr) {
-    if ((e = ta->reserve(4 * a4 + tmp_align(tmp_bytes))) != hipSuccess) return e;
-    kin = reinterpret_cast<uint32_t*>(ta->base);
-    kout = reinterpret_cast<uint32_t*>(ta->base + a4);
-    vin = reinterpret_cast<int32_t*>(ta->base + 2 * a4);
-    vout = reinterpret_cast<int32_t*>(ta->base + 3 * a4);
-    tmp = ta->base + 4 * a4;
-  } else if ((e = hipMalloc(&kin, a4)) != hipSuccess || (e = hipMalloc(&kout, a4)) != hipSuccess ||
-             (e = hipMalloc(&vin, a4)) != hipSuccess || (e = hipMalloc(&vout, a4)) != hipSuccess ||
-             (e = hipMalloc(&tmp, tmp_bytes)) != hipSuccess) {
-    return grid_fail(e, kin, kout, vin, vout, tmp);
-  }
-  const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
-  morton_key_kernel<<<blocks, kGridBlock, 0, st>>>(g->pts, n, g->dev, sh[0], sh[1], sh[2], kin, vin);
-  e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 30, st);
-  if (e == hipSuccess) e = hipMalloc(&g->mpts, sizeof(float4) * n);
-  if (e == hipSuccess) e = hipMalloc(&g->minv, sizeof(int32_t) * n);
-  if (e == hipSuccess) {
-    morton_gather_kernel<<<blocks, kGridBlock, 0, st>>>(g->pts, vout, n, g->mpts, g->minv);
-    e = hipGetLastError();
-  }
-  if (e != hipSuccess) {
-    (void)hipStreamSynchronize(st);  // nothing may still write the arrays freed here
-    hipFree(g->mpts);
-    hipFree(g->minv);
-    g->mpts = nullptr;
-    g->minv = nullptr;
-  }
-  return ta != nullptr ? e : grid_fail(e, kin, kout, vin, vout, tmp);
-}
-
 // ------------------------------------------------------------------------------- Morton copy
-// The ICP loop's source in the Morton order of its grid (m3d_icp_create): slot k holds source
-// point mpts[k].w.  Every per-source array of the loop (keys, runner-ups, correspondences, seeds,
-// exchange buffers) is then indexed by slot, so the grid scan's key writes and seed reads and the
-// terms pass's source loads are coalesced and its winner gathers spatially coherent; the ABI
-// translates back to source order (m3d_icp_copy_corr).  The copy's grid is derived from the
-// source's, not rebuilt: the same cells and starts; within a cell the Morton sort kept index order,
-// so a cell's points are consecutive ascending slots and the cell-ordered arrays only change their
-// index bits (minv: source index → slot).
-__global__ __launch_bounds__(kGridBlock) void morton_copy_points_kernel(
-    const double* __restrict__ xyz64, const double* __restrict__ nrm64,
-    const float4* __restrict__ xyz32, const float4* __restrict__ mpts, int64_t n,
-    double* __restrict__ oxyz64, double* __restrict__ onrm64, float4* __restrict__ oxyz32,
-    int32_t* __restrict__ slot, float4* __restrict__ ompts, int32_t* __restrict__ ominv) {
-  const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
-  if (k >= n) return;
-  const float4 m = mpts[k];
-  const int64_t j = __float_as_int(m.w);
-  slot[k] = (int32_t)j;
-  for (int a = 0; a < 3; ++a) oxyz64[3 * k + a] = xyz64[3 * j + a];
-  if (onrm64 != nullptr)
-    for (int a = 0; a < 3; ++a) onrm64[3 * k + a] = nrm64[3 * j + a];
-  oxyz32[k] = xyz32[j];
-  ompts[k] = make_float4(m.x, m.y, m.z, __int_as_float((int32_t)k));
-  ominv[k] = (int32_t)k;
+// The ICP loop's source in the Morton (Z-curve) order of its cells (m3d_icp_create): slot k holds
+// source point slot[k].  Every per-source array of the loop (keys, runner-ups, correspondences,
+// exchange buffers) is indexed by slot, so the grid scan's key writes and seed reads and the terms
+// pass's source loads are coalesced and its winner gathers spatially coherent; the ABI translates
+// back to source order (m3d_icp_copy_corr).  The Morton key of each point's cell under the grid
+// parameters grid_build would choose (the cloud's bounds, cell size; 10 bits per axis, finer grids
+// coarsened — only locality matters, any order gives the same keys), one stable radix sort of
+// (key, index) from index order, one copy pass.  The copy's grid keeps only what the loop reads of
+// a query grid (its Morton points and slot map, grid parameters); its cell arrays are not built
+// (ncells = 0, and cell_req = −1 so no cell-size request ever matches it).
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {
+  v &= 0x3FF;
+  v = (v | (v << 16)) & 0x030000FF;
+  v = (v | (v << 8)) & 0x0300F00F;
+  v = (v | (v << 4)) & 0x030C30C3;
+  v = (v | (v << 2)) & 0x09249249;
+  return v;
 }
 
-__global__ __launch_bounds__(kGridBlock) void morton_copy_cells_kernel(
-    const float4* __restrict__ pts, const int32_t* __restrict__ order, const int32_t* __restrict__ minv,
-    int64_t n, float4* __restrict__ opts, int32_t* __restrict__ oorder) {
-  const int64_t j = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
-  if (j >= n) return;
-  const float4 v = pts[j];
-  opts[j] = make_float4(v.x, v.y, v.z, __int_as_float(minv[__float_as_int(v.w)]));
-  oorder[j] = minv[order[j]];
-}
-
-hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Grid* gout,
-                       hipStream_t st) {
-  const int64_t n = src->n;
-  // an empty cloud has no Morton arrays (grid_morton returns early): the copy is empty too
-  if (sg->n_pts != n || (n > 0 && (sg->mpts == nullptr || sg->minv == nullptr))) return hipErrorInvalidValue;
-  out->n = n;
-  out->n_pad = src->n_pad;
-  for (int k = 0; k < 3; ++k) out->center[k] = src->center[k];
-  out->rmax = src->rmax;
-  for (int k = 0; k < 3; ++k) {
-    out->lo[k] = src->lo[k];
-    out->hi[k] = src->hi[k];
-  }
-  out->has_bounds = src->has_bounds;
-  out->s16 = src->s16;
-  out->center_given = src->center_given;
-  gout->dev = sg->dev;
-  gout->n_pts = n;
-  gout->n_occ = sg->n_occ;
-  gout->cell = sg->cell;
-  gout->cell_req = sg->cell_req;
-  const size_t n1 = (size_t)std::max<int64_t>(n, 1);
-  const int64_t ncells = sg->dev.ncells;
-  hipError_t e;
-  if ((e = hipMalloc(&out->xyz64, sizeof(double) * 3 * n1)) != hipSuccess ||
-      (src->nrm64 != nullptr && (e = hipMalloc(&out->nrm64, sizeof(double) * 3 * n1)) != hipSuccess) ||
-      (e = hipMalloc(&out->xyz32, sizeof(float4) * (size_t)std::max<int64_t>(src->n_pad, 1))) != hipSuccess ||
-      (e = hipMalloc(&out->slot, sizeof(int32_t) * n1)) != hipSuccess ||
-      (e = hipMalloc(&gout->mpts, sizeof(float4) * n1)) != hipSuccess ||
-      (e = hipMalloc(&gout->minv, sizeof(int32_t) * n1)) != hipSuccess)
-    return e;
-  if (n == 0) return hipSuccess;
-  if ((e = hipMalloc(&gout->start, sizeof(int32_t) * (size_t)(ncells + 1))) != hipSuccess ||
-      (e = hipMalloc(&gout->pts, sizeof(float4) * n1)) != hipSuccess ||
-      (e = hipMalloc(&gout->order, sizeof(int32_t) * n1)) != hipSuccess)
-    return e;
-  const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
-  morton_copy_points_kernel<<<blocks, kGridBlock, 0, st>>>(src->xyz64, src->nrm64, src->xyz32, sg->mpts,
-                                                           n, out->xyz64, out->nrm64, out->xyz32,
-                                                           out->slot, gout->mpts, gout->minv);
-  morton_copy_cells_kernel<<<blocks, kGridBlock, 0, st>>>(sg->pts, sg->order, sg->minv, n, gout->pts,
-                                                          gout->order);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  // the pads of the centred fp32 copy (far points) and the cell starts are the source's
-  if (src->n_pad > n &&
-      (e = hipMemcpyAsync(out->xyz32 + n, src->xyz32 + n, sizeof(float4) * (size_t)(src->n_pad - n),
-                          hipMemcpyDeviceToDevice, st)) != hipSuccess)
-    return e;
-  if (ncells > 0 && (e = hipMemcpyAsync(gout->start, sg->start, sizeof(int32_t) * (size_t)(ncells + 1),
-                                        hipMemcpyDeviceToDevice, st)) != hipSuccess)
-    return e;
-  gout->dev.start = gout->start;
-  gout->dev.pts = gout->pts;
-  gout->occ_known = sg->occ_known;
-  return hipSuccess;
-}
-
-// The same copy straight from the source's points (m3d_icp_create's default since round 4): the
-// Morton key of each point's cell under the grid parameters grid_build would choose (the cloud's
-// bounds, cell size), one stable radix sort of (key, index) from index order, one copy pass —
-// instead of a cell sort, a Morton sort of the cell-ordered points and a copy.  Without
-// coarsening (≤ 1024 cells per axis) equal keys mean equal cells, so both orders are (Morton key,
-// index): the same slots.  The copy's grid keeps only what the loop reads of a query grid (its
-// Morton points and slot map, grid parameters); its cell arrays are not built (ncells = 0, and
-// cell_req = −1 so no cell-size request ever matches it).
 __global__ __launch_bounds__(kGridBlock) void morton_key_src_kernel(const float4* __restrict__ pts, int64_t n,
                                                                     GridDev g, int sx, int sy, int sz,
                                                                     uint32_t* __restrict__ key,
@@ -1074,79 +819,37 @@ hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid
 
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, const Grid* g,
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
-                          const float4* sq, const int32_t* prev, const int64_t* dprev,
-                          const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0,
-                          int64_t q1, int32_t* hlist, uint32_t* hcnt, int32_t cand_cap,
-                          const double* src64, const double* tgt64) {
-  const int64_t ns_all = ns;
+                          const int32_t* prev, const int64_t* dprev, const float4* tgt32, int64_t nt_shard,
+                          hipStream_t st, int64_t q0, int64_t q1, int32_t* hlist, uint32_t* hcnt,
+                          int32_t cand_cap, const double* src64, const double* tgt64) {
   if (q1 >= 0) ns = q1;
   if (ns <= q0) return hipSuccess;
-  static const bool batched = [] {  // M3D_GRID_BATCHED=0: the per-query kernel above (A/B)
-    const char* e = getenv("M3D_GRID_BATCHED");
-    return !(e && atoi(e) == 0);
-  }();
-  // lanes per query: M3D_GRID_LANES, else by size — 4 while the queries fill about one occupancy
-  // round (cfg1: 15.1 µs vs 18.3 at 2), 2 beyond (1M × 125k 71.6 → 60.1 µs, 1M × 1M 117.7 →
-  // 112.1 µs: twice the queries in flight per wave)
-  static const int L_env = [] {
-    const char* e = getenv("M3D_GRID_LANES");
-    const int v = e ? atoi(e) : 0;
-    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
-  }();
-  const int L = L_env ? L_env : ((ns - q0) > 300000 ? 2 : kGridLanesDefault);
-  static const int RB = [] {  // M3D_GRID_RB = kR·10 + kB (tuning): 22, 41, 42, 24
-    const char* e = getenv("M3D_GRID_RB");
-    const int v = e ? atoi(e) : 22;
-    return (v == 42 || v == 41 || v == 22 || v == 24) ? v : 22;
-  }();
-  if (batched && qgrid != nullptr && qgrid->mpts != nullptr) {
-    static unsigned long long* gstats = [] {
-      const char* e = getenv("M3D_GRID_STATS");
-      unsigned long long* p = nullptr;
-      if (e && atoi(e) == 1 && hipMalloc(&p, 5 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
-      return p;
-    }();
-    if (gstats != nullptr) (void)hipMemsetAsync(gstats, 0, 5 * sizeof(unsigned long long), st);
-    const int64_t nb = ((ns - q0) * L + kGridBlock - 1) / kGridBlock;
-    const unsigned launch = (unsigned)((nb + 7) / 8 * 8);
-    // deferral (dense target cells, api.cpp icp_create) in the default shapes: 2 or 4 lanes, RB 22
-    const bool defer = hlist != nullptr && hcnt != nullptr && cand_cap > 0 && g->dev.ncells > 0 &&
-                       src64 != nullptr && tgt64 != nullptr && (L == 2 || L == 4) && RB == 22;
-    const int cap = defer ? cand_cap : 0x7FFFFFFF;
-#define M3D_GB(LV, RV, BV) grid_nn_batched_kernel<LV, RV, BV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0, hlist, hcnt, cap)
-#define M3D_GBL(RV, BV) if (L == 1) M3D_GB(1, RV, BV); else if (L == 2) M3D_GB(2, RV, BV); else if (L == 4) M3D_GB(4, RV, BV); else if (L == 8) M3D_GB(8, RV, BV); else M3D_GB(16, RV, BV)
-    if (defer && L == 4) grid_nn_batched_kernel<4, 2, 2, true><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0, hlist, hcnt, cap);
-    else if (defer) grid_nn_batched_kernel<2, 2, 2, true><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, near2, sq, prev, dprev, tgt32, nt_shard, nb, gstats, q0, hlist, hcnt, cap);
-    else if (RB == 22) { M3D_GBL(2, 2); } else if (RB == 41) { M3D_GBL(4, 1); } else if (RB == 42) { M3D_GBL(4, 2); } else { M3D_GBL(2, 4); }
-#undef M3D_GBL
-#undef M3D_GB
-    if (defer) {  // a fixed grid striding over the deferred queries (their count stays on the device)
-      const unsigned hb = (unsigned)std::min<int64_t>(512, ns - q0);
-      grid_nn_heavy_kernel<<<hb, kGridBlock, 0, st>>>(qgrid->mpts, g->dev, off, s, keys, near2, sq, prev,
-                                                      dprev, tgt32, nt_shard, hlist, hcnt, src64, tgt64, ns);
-    }
-    if (gstats != nullptr) {
-      unsigned long long h[5] = {0, 0, 0, 0, 0};
-      if (hipMemcpyAsync(h, gstats, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
-          hipStreamSynchronize(st) == hipSuccess && h[0] > 0)
-        fprintf(stderr, "[m3d grid stats] %llu queries (%.1f%% seeded): %.2f cell rows, %.1f candidates per query, max %llu\n",
-                h[0], 100.0 * h[3] / h[0], (double)h[1] / h[0], (double)h[2] / h[0], h[4]);
-    }
-    return hipGetLastError();
+  if (qgrid == nullptr || qgrid->mpts == nullptr) return hipErrorInvalidValue;  // Morton query order
+  // lanes per query by size: 4 while the queries fill about one occupancy round (cfg1: 15.1 µs vs
+  // 18.3 at 2), 2 beyond (1M × 125k 71.6 → 60.1 µs, 1M × 1M 117.7 → 112.1 µs: twice the queries in
+  // flight per wave); 2 rows × 2 points per lane and load batch
+  const int L = (ns - q0) > 300000 ? 2 : 4;
+  const int64_t nb = ((ns - q0) * L + kGridBlock - 1) / kGridBlock;
+  const unsigned launch = (unsigned)((nb + 7) / 8 * 8);
+  // deferral of dense-cell and ambiguous queries to grid_nn_heavy_kernel (api.cpp icp_create)
+  const bool defer = hlist != nullptr && hcnt != nullptr && cand_cap > 0 && g->dev.ncells > 0 &&
+                     src64 != nullptr && tgt64 != nullptr;
+  const int cap = defer ? cand_cap : 0x7FFFFFFF;
+#define M3D_GB(LV, DV)                                                                              \
+  grid_nn_batched_kernel<LV, 2, 2, DV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, \
+                                                                     near2, prev, dprev, tgt32, nt_shard, nb, \
+                                                                     q0, hlist, hcnt, cap)
+  if (defer) {
+    if (L == 4) M3D_GB(4, true); else M3D_GB(2, true);
+  } else {
+    if (L == 4) M3D_GB(4, false); else M3D_GB(2, false);
   }
-  if (q0 != 0 || ns != ns_all) return hipErrorInvalidValue;  // per-query form: every source
-  const int32_t* order = qgrid != nullptr ? qgrid->order : nullptr;
-  const unsigned blocks = (unsigned)((ns * L + kGridBlock - 1) / kGridBlock);
-  if (L == 1)
-    grid_nn_kernel<1><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
-  else if (L == 2)
-    grid_nn_kernel<2><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
-  else if (L == 4)
-    grid_nn_kernel<4><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
-  else if (L == 8)
-    grid_nn_kernel<8><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
-  else
-    grid_nn_kernel<16><<<blocks, kGridBlock, 0, st>>>(src32, ns, order, g->dev, off, s, keys, near2, prev, dprev, tgt32, nt_shard);
+#undef M3D_GB
+  if (defer) {  // a fixed grid striding over the deferred queries (their count stays on the device)
+    const unsigned hb = (unsigned)std::min<int64_t>(512, ns - q0);
+    grid_nn_heavy_kernel<<<hb, kGridBlock, 0, st>>>(qgrid->mpts, g->dev, off, s, keys, near2, prev, dprev,
+                                                    tgt32, nt_shard, hlist, hcnt, src64, tgt64, ns);
+  }
   return hipGetLastError();
 }
 

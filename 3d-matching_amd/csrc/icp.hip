@@ -36,21 +36,14 @@
 
 namespace m3d {
 
-constexpr int kNNQDefault = 4;  // queries per lane (M3D_NN_Q=1|2|4 overrides, tuning)
+constexpr int kNNQ = 4;       // queries per lane (nn_kernel)
 constexpr int kNNTile = 16;   // screen sub-tile (one branch per sub-tile)
 constexpr int kNNLds = 512;   // targets per LDS tile (8 KB, double-buffered)
 constexpr int kNNBlock = 256;
 constexpr int kTermsBlock = 256;
 constexpr int kTermsPtsDefault = 2;  // sources per terms thread (M3D_TERMS_PTS = 1|2|4, tuning):
                                      // 2× fewer block partials for the last block to reduce
-static int terms_pts() {
-  static const int v = [] {
-    const char* e = getenv("M3D_TERMS_PTS");
-    const int k = e ? atoi(e) : kTermsPtsDefault;
-    return (k == 1 || k == 2 || k == 4) ? k : kTermsPtsDefault;
-  }();
-  return v;
-}
+static int terms_pts() { return kTermsPtsDefault; }
 constexpr double kU = 5.9604644775390625e-08;
 constexpr double kU64 = 1.1102230246251565e-16;
 
@@ -213,9 +206,8 @@ __global__ __launch_bounds__(256) void keyinit_kernel(const float4* __restrict__
 }
 
 // ------------------------------------------------------------------------------- NN scan
-// fp32 VALU form of the brute-force scan (fallback: no MFMA tiles, M3D_NN_MFMA=0).  Per query
+// fp32 VALU form of the brute-force scan (fallback: a target without MFMA tiles).  Per query
 // the scan state (k1, near2) of nnkey.h; the screen bound is search_bound(k1).
-template <int kNNQ>
 __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__ src32, int64_t ns,
                                                       const float4* __restrict__ tgt,
                                                       int64_t nt_pad, int64_t slice_len,
@@ -341,17 +333,13 @@ __global__ __launch_bounds__(kNNBlock) void nn_kernel(const float4* __restrict__
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int kMGDefault = 2;  // 32-query groups per wave (M3D_NN_MG = 1|2|4 overrides, tuning)
+constexpr int kMG = 2;        // 32-query groups per wave
 constexpr int kMTile = 256;   // targets per half tile (8 sub-tiles of 32)
-#ifndef M3D_NN_DMA
-#define M3D_NN_DMA 1  // 0: the register-staged tile prefetch
-#endif
-constexpr int kTHDefault = 4;  // half tiles per LDS tile (M3D_NN_TH = 1 | 2 | 4)
+constexpr int kTH = 4;        // half tiles per LDS tile
 constexpr int kMTilePad = 1024; // MFMA operand arrays are padded to a multiple of every tile size
 constexpr int kMBlock = 512;  // 8 waves × kMG × 32 = 512 queries per block: every target tile
                               // staged in LDS serves 512 queries (L2→LDS traffic per pair halved)
-template <int kMG>
-constexpr int mqueries() { return (kMBlock / 64) * kMG * 32; }
+constexpr int kMQueries = (kMBlock / 64) * kMG * 32;  // queries per block
 
 __device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
   hi = (_Float16)x;
@@ -469,18 +457,16 @@ __device__ __forceinline__ bool publish_k1(const SeedArgs& sa, uint64_t k1, uint
 // Exact fallback of nn_mfma_kernel when the scaled operands do not fit fp16 (mfma_ok == 0, a
 // far-off transform): the same scan state over the block's slice by a plain scan, one thread
 // per query.  Keeps the fp32 VALU kernel off the launch path.
-template <int kMG>
-__device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns,
-                              const int32_t* __restrict__ order, const float4* __restrict__ tgt32,
+__device__ void nn_slice_scan(const float4* __restrict__ src32, int64_t ns, const float4* __restrict__ tgt32,
                               int64_t jb, int64_t je, int64_t off, const IcpState* __restrict__ s,
                               int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
                               const SeedArgs& sa, int64_t q0) {
   const float* Rt = s->Rt32;
   const float r2_hi = s->r2_hi;
-  for (int qs = threadIdx.x; qs < mqueries<kMG>(); qs += kMBlock) {
-    const int64_t slot = q0 + (int64_t)blockIdx.x * mqueries<kMG>() + qs;
+  for (int qs = threadIdx.x; qs < kMQueries; qs += kMBlock) {
+    const int64_t slot = q0 + (int64_t)blockIdx.x * kMQueries + qs;
     if (slot >= ns) return;
-    const int64_t i = order != nullptr ? (int64_t)order[slot] : slot;
+    const int64_t i = slot;
     float qx, qy, qz;
     const float4 p = src32[i];
     xform32(Rt, p, qx, qy, qz);
@@ -522,29 +508,23 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-template <int kMG, int kTH>
 __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) void nn_mfma_kernel(const float4* __restrict__ src32,
                                                           int64_t ns,
-                                                          const int32_t* __restrict__ order,
                                                           const uint4* __restrict__ tgt16,
                                                           const float4* __restrict__ tgt32,
-                                                          int64_t nt_pad, int64_t slice_len,
-                                                          int64_t off,
+                                                          int64_t nt_pad, int64_t off,
                                                           const IcpState* __restrict__ s,
                                                           int64_t* __restrict__ keys,
                                                           uint32_t* __restrict__ near2,
-                                                          uint64_t exp_mask,
-                                                          unsigned long long* __restrict__ stats,
-                                                          int strided, SeedArgs sa, int64_t q0,
-                                                          int defer) {
-  // exp_mask: all ones; M3D_NN_EXP=1 zeroes it to time the sweep without the exact path
-  // (profiling experiment only: the keys are then wrong).  stats (M3D_NN_STATS=1, diagnostics
-  // only, else null): [0] flagged (group, sub-tile) steps, [1] all steps.
+                                                          SeedArgs sa, int64_t q0) {
   if (s->done) return;
-  if (!s->mfma_ok) {
-    const int64_t jb = (int64_t)blockIdx.y * slice_len;
-    nn_slice_scan<kMG>(src32, ns, order, tgt32, jb, min(nt_pad, jb + slice_len), off, s, keys,
-                       near2, sa, q0);
+  // grid.y block y takes every gridDim.y-th target tile (strided: a query block's few candidate
+  // tiles, adjacent in cell order, spread over gridDim.y blocks instead of landing in one)
+  const int64_t tstep = (int64_t)gridDim.y * kTH * kMTile;
+  const int64_t jb = (int64_t)blockIdx.y * kTH * kMTile;
+  if (!s->mfma_ok) {  // the same tiles by a plain scan
+    for (int64_t t0 = jb; t0 < nt_pad; t0 += tstep)
+      nn_slice_scan(src32, ns, tgt32, t0, min(nt_pad, t0 + kTH * kMTile), off, s, keys, near2, sa, q0);
     return;
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -562,8 +542,8 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
   for (int g = 0; g < kMG; ++g) {
     // queries: positions [q0, ns) of the visit order (order, or the slots themselves)
-    const int64_t slot = q0 + (int64_t)blockIdx.x * mqueries<kMG>() + (wave * kMG + g) * 32 + c;
-    const int64_t i = slot < ns ? (order != nullptr ? (int64_t)order[slot] : slot) : -1;
+    const int64_t slot = q0 + (int64_t)blockIdx.x * kMQueries + (wave * kMG + g) * 32 + c;
+    const int64_t i = slot < ns ? slot : -1;
     qi[g] = i;
     n2[g] = kInf;
     float X = -1.0f;  // inactive: negative threshold, never hits
@@ -601,11 +581,9 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
   // but can wait in a per-wave list (tile offset, flagged bits) until after the sweep.  The
   // candidates evaluated are the same sub-tiles' rows, so the key is the same.
   uint32_t dfr = 0;
-  if (defer) {
 #pragma unroll
-    for (int g = 0; g < kMG; ++g)
-      if (!((force >> (g * 8)) & 1u) && __all(qi[g] < 0 || key_real(k1[g]))) dfr |= 1u << g;
-  }
+  for (int g = 0; g < kMG; ++g)
+    if (!((force >> (g * 8)) & 1u) && __all(qi[g] < 0 || key_real(k1[g]))) dfr |= 1u << g;
   // Tiles of kTH × 256 targets, [buffer][lane half][target]: a half-wave's 32 ds_read_b128 hit
   // 32 consecutive 16-B slots.  Thread t stages kTH elements (e = t + u·512: plane e / kTT, target
   // e % kTT; mf16 is stored as two planes, so the loads are coalesced).  The sweep runs the tile
@@ -627,10 +605,7 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
     if ((dfr >> g) & 1u) dmask |= kGMask << (g * kSub);
   dmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(dmask >> 32)) << 32) |
           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dmask);  // wave-uniform: SGPRs
-  // contiguous slice of slice_len targets per grid.y, or (strided) every gridDim.y-th tile
-  const int64_t tstep = strided ? (int64_t)gridDim.y * kTT : (int64_t)kTT;
-  const int64_t jb = strided ? (int64_t)blockIdx.y * kTT : (int64_t)blockIdx.y * slice_len;
-  const int64_t je = strided ? nt_pad : min(nt_pad, jb + slice_len);
+  const int64_t je = nt_pad;
 #pragma unroll
   for (int u = 0; u < kTH; ++u) {
     const int e = threadIdx.x + u * kMBlock;
@@ -644,7 +619,6 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
   int buf = 0;
   for (int64_t j0 = jb; j0 < je; j0 += tstep) {
     const bool has_next = j0 + tstep < je;
-#if M3D_NN_DMA
     // the next tile global → LDS by DMA while this one is swept (lds_dma.h): no prefetch
     // registers (a wave's 64 elements are one plane's 64 consecutive targets)
     if (has_next) {
@@ -654,16 +628,6 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
         lds_dma16(tgt16 + (e / kTT) * nt_pad + j0 + tstep + e % kTT, &t16[buf ^ 1][e / kTT][(e % kTT) & ~63]);
       }
     }
-#else
-    uint4 pre[kTH];
-    if (has_next) {
-#pragma unroll
-      for (int u = 0; u < kTH; ++u) {
-        const int e = threadIdx.x + u * kMBlock;
-        pre[u] = tgt16[(e / kTT) * nt_pad + j0 + tstep + e % kTT];
-      }
-    }
-#endif
     // Sweep: MFMA + sign-OR test for the tile's sub-tiles, branch-free; a sub-tile that hits
     // anywhere in the wave sets a bit of the wave-uniform mask (SALU).  Software-pipelined: the
     // MFMA of step t+1 is issued before step t's tree, so a wave never waits on its own MFMA.
@@ -695,15 +659,11 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
     // fp32 d² over the lane's 16 rows, then the lane pair (c, c + 32) merges its two states.
     // A group whose queries all start from a real seed defers its flagged sub-tiles to the
     // per-wave list below (dlist/dtile, resolved after the sweep, off the tile barrier:
-    // M3D_NN_DEFER, −2.2 % per launch at cfg1); unseeded groups and a full list
-    // resolve here, where the threshold refresh still prunes the rest of the sweep.
+    // −2.2 % per launch at cfg1); unseeded groups and a full list resolve here,
+    // where the threshold refresh still prunes the rest of the sweep.
     hm |= force64;
-    if (stats != nullptr && lane == 0) {
-      atomicAdd(&stats[0], (unsigned long long)__builtin_popcountll(hm));
-      atomicAdd(&stats[1], (unsigned long long)(kSub * kMG));
-    }
     {
-      const uint64_t hd = hm & dmask & exp_mask;
+      const uint64_t hd = hm & dmask;
       if (hd != 0 && dn < kDefer) {
         if (lane == 0) {
           dlist[wave][dn] = hd;
@@ -715,7 +675,7 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
 #pragma unroll
     for (int g = 0; g < kMG; ++g) {
-      uint64_t mg = (hm >> (g * kSub)) & kGMask & exp_mask;
+      uint64_t mg = (hm >> (g * kSub)) & kGMask;
       if (mg == 0) continue;
       while (mg != 0) {
         const int sub = __builtin_ctzll(mg);
@@ -731,17 +691,7 @@ __global__ __launch_bounds__(kMBlock) __attribute__((amdgpu_waves_per_eu(4))) vo
       thr_operand(bt, X < 0.0f ? -1.0f : ((X - qq[g]) + eps) * S2, fg);
       if (h == 1) bq[g] = bt;  // the threshold only ever tightens: force stays as it was
     }
-#if M3D_NN_DMA
     lds_dma_wait();
-#else
-    if (has_next) {
-#pragma unroll
-      for (int u = 0; u < kTH; ++u) {
-        const int e = threadIdx.x + u * kMBlock;
-        t16[buf ^ 1][e / kTT][e % kTT] = pre[u];
-      }
-    }
-#endif
     __syncthreads();
     buf ^= 1;
   }
@@ -813,7 +763,7 @@ __device__ __forceinline__ double wave_transpose_sum32(const double (&v)[32], in
 }
 
 // One source's contribution to the 30 term slots (layout below), in a fixed operation order:
-// every terms pass (terms_block, the persistent grid loop) adds a source through this function,
+// every terms pass (terms_block, single device or shard) adds a source through this function,
 // so equal winners give equal bits.  Q = the fp64 transformed source, q / n its winner's point and
 // normal, d2 = the winner's fp64 d², c = the source centre (point-to-point).
 __device__ __forceinline__ void terms_add(double (&acc)[30], const double (&Q)[3], const double (&q)[3],
@@ -871,9 +821,6 @@ struct TermsArgs {
   const int64_t* dmin;
   int64_t* dprev;
   int32_t* corr;
-  float4* sq;             // grid NN seed records (nnkey.h seed_rec) in the source's Morton order
-  const int32_t* minv;    //   at position minv[i]
-  const float4* tgt32;    //   from the shard's centred fp32 targets
   int est;
   double c[3];
   int64_t* reset_keys;   // fused single-device loop: hand the keys back as kKeyNone
@@ -988,10 +935,6 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
     }
     const int64_t i = ii[u];
     if (a.corr != nullptr) a.corr[i] = (int32_t)gj[u];
-    if (a.sq != nullptr) {
-      const bool local = gj[u] >= a.off && gj[u] < a.off + a.nt_shard;
-      a.sq[a.minv[i]] = seed_rec(gj[u], local, a.tgt32 + (local ? gj[u] - a.off : 0), d2[u]);
-    }
     if (gj[u] < a.off || gj[u] >= a.off + a.nt_shard) continue;  // none, or another shard's target
     terms_add(acc, vs[u], tq[u], tn[u], d2[u], a.est, a.c);
   }
@@ -1133,11 +1076,7 @@ __device__ __forceinline__ void solve_in(const IcpState* s, SolveIn& in) {
   for (int k = 0; k < 12; ++k) in.rt[k] = s->Rt32[k];
 }
 
-// clk (diagnostics, null in production): wall clock at entry, after the LDLT, after the update
-// matrix, after T ← ΔT·T, at the end (the persistent loop's M3D_PERSIST_PROF)
-__device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp, const SolveIn& in,
-                            unsigned long long* clk = nullptr) {
-  if (clk != nullptr) clk[0] = wall_clock64();
+__device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp, const SolveIn& in) {
   double sm[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) sm[k] = sums[k];
@@ -1189,9 +1128,7 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
         }
       for (int a = 0; a < 6; ++a) b[a] = -sm[21 + a];
       ldlt6_solve(A, b, x);
-      if (clk != nullptr) clk[1] = wall_clock64();
       vec6_to_matrix_wave(x, upd);
-      if (clk != nullptr) clk[2] = wall_clock64();
     } else {
       const double n = count;
       double mp[3], mq[3], Hm[9], R[9];
@@ -1214,12 +1151,10 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   if (!finite)
     for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
   matmul4(upd, T, T);
-  if (clk != nullptr) clk[3] = wall_clock64();
 #pragma unroll
   for (int k = 0; k < 16; ++k) s->T[k] = T[k];
   s->iters = iters + 1;
   refresh_rt32_from(s, T, r2, sp.f);
-  if (clk != nullptr) clk[4] = wall_clock64();
 }
 
 __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
@@ -1299,429 +1234,6 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     if (threadIdx.x == 0) s->ticket = 0;
     if (do_solve) solve_state(red[0], s, sp, in);
   }
-}
-
-// ------------------------------------------------------------------------------- persistent grid loop
-// Round 4: n iterations of the single-device grid-NN ICP loop in ONE launch (m3d_icp_steps; the
-// two-launch loop above stays; m3d_icp_params.flags / M3D_ICP_PERSIST choose).  One workgroup of
-// 512 threads per 512-source tile (the terms pass's block: kTermsBlock threads × 2 sources), all
-// resident (api.cpp checks the grid against the occupancy before choosing this path).  Per
-// iteration a workgroup
-//   (1) scans its 512 queries, one lane each, seeded from the previous winner, whose centred fp32
-//       point it keeps in LDS.  The sorted-array ranges of a query's cell-box rows are cached in
-//       LDS (up to kPRows rows, with the box they came from): when the next iteration's box is the
-//       same box — the usual case once the transform has settled — the query loads exactly the
-//       same targets straight away, skipping the dependent row-start loads (same set ⇒ same key
-//       and runner-up: the scan state is order-free, nnkey.h near_push);
-//   (2) decides the fp64 winners and adds the terms of its sources exactly as terms_block does
-//       (same thread ↔ source map, same terms_add order, same wave/LDS reduction), writing corr;
-//   (3) publishes its block partial write-through (sc1) into one of two buffers, drains it, and
-//       arrives on a launch-wide counter (agent-scope add); polls the counter (sc1 loads) until
-//       every tile has arrived — MI355X_MICROARCH.md hand-off table, first row;
-//   (4) reduces ALL tile partials in terms_solve_kernel's fixed group order (sc1 loads) and runs
-//       solve_state on its own LDS copy of the loop state.
-// Every workgroup therefore holds bit-identical sums and state (nobody broadcasts a transform),
-// the same bits as the fused two-launch loop (test_gpu_icp persistent cases).  Partials are
-// double-buffered: a workgroup writes iteration k + 2's partial only after every workgroup has
-// arrived at iteration k + 1, i.e. finished reading iteration k's.  Every spin is bounded: a
-// workgroup that waits too long (a tile not resident) flags `fault` and leaves the loop.
-constexpr int kPTile = 2 * kTermsBlock;  // sources per tile (= per workgroup, one lane per query)
-constexpr int kPRows = 9;                // cached row ranges per query (a seeded box: ≤ 3 × 3 rows)
-constexpr uint32_t kPersistMaxSpin = 1u << 22;
-
-struct PersistArgs {
-  const float4* src32;  // the source in Morton slot order (centred fp32)
-  const double* src64;
-  int64_t ns;
-  GridDev g;            // the target grid
-  const double* tgt64;
-  const double* rec64;  // target records (point, normal)
-  const double* nrm64;
-  const float4* tgt32;
-  int64_t nt;
-  int32_t* corr;        // slot order: read once (seeds), written every iteration
-  double* pp;           // 2 × ntiles × kTermSlots
-  uint32_t* counter;    // arrivals, zero at launch
-  int32_t* fault;
-  int32_t n;            // iterations (m3d_icp_step calls) to run
-  int est;
-  double c[3];
-  unsigned long long* prof;  // M3D_PERSIST_PROF=1: per-phase wall-clock ticks (else null)
-};
-
-// One query's scan over a list of cell-box rows [a, b) in the target grid's sorted array, kR rows
-// × kB points per load batch (nnkey.h grid_scan's loop with the row ranges given).
-template <int kR, int kB>
-__device__ __forceinline__ void scan_ranges(const GridDev& g, const int2* __restrict__ rr, int nrows,
-                                            int r_begin, int32_t p_begin, float qx, float qy, float qz,
-                                            float r2_hi, uint64_t& k1, float& k1d, float& n2) {
-  for (int r0 = r_begin; r0 < nrows; r0 += kR) {
-    int32_t ra[kR], rb[kR], len = 0;
-#pragma unroll
-    for (int k = 0; k < kR; ++k) {
-      const int2 ab = r0 + k < nrows ? rr[r0 + k] : make_int2(0, 0);
-      ra[k] = ab.x;
-      rb[k] = ab.y;
-      len = max(len, rb[k] - ra[k]);
-    }
-    for (int32_t b0 = r0 == r_begin ? p_begin : 0; b0 < len; b0 += kB) {
-      float4 v[kR][kB];
-#pragma unroll
-      for (int k = 0; k < kR; ++k)
-#pragma unroll
-        for (int m = 0; m < kB; ++m) {
-          const int32_t j = ra[k] + b0 + m;
-          if (j < rb[k]) v[k][m] = g.pts[j];
-        }
-#pragma unroll
-      for (int k = 0; k < kR; ++k)
-#pragma unroll
-        for (int m = 0; m < kB; ++m) {
-          const int32_t j = ra[k] + b0 + m;
-          if (j < rb[k]) {
-            const float d2 = d2f(qx, qy, qz, v[k][m].x, v[k][m].y, v[k][m].z);
-            if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)__float_as_int(v[k][m].w)), d2);
-          }
-        }
-    }
-  }
-}
-
-template <int kR, int kB, bool kProf>
-__global__ __launch_bounds__(kTermsBlock) void icp_grid_persist_kernel(PersistArgs a, IcpState* gs, SolveParams sp) {
-  constexpr int kT = kTermsBlock;  // 4 waves, one per SIMD: the whole register file per wave
-  constexpr int kP = 2;            // sources per thread: u·256 + tid of the tile (terms_block's map)
-  __shared__ IcpState S;
-  __shared__ double red[kTermSlots][kTermsBlock / kWave];
-  __shared__ double gsum[kReduceGroups][kTermSlots];
-  __shared__ int32_t cbox[6][kPTile];   // cached cell box (x0, x1, y0, y1, z0, z1) per query
-  __shared__ int32_t cnum[kPTile];      // its row count (−1: no cache)
-  __shared__ int2 crow[kPTile][kPRows]; // its rows' [a, b) in the target grid's sorted array
-  __shared__ int bad;
-  const int tid = threadIdx.x;
-  const int64_t ntiles = gridDim.x;
-  const int64_t base = (int64_t)blockIdx.x * kPTile;
-  for (int k = tid; k < (int)(sizeof(IcpState) / 4); k += kT)
-    reinterpret_cast<uint32_t*>(&S)[k] = reinterpret_cast<const uint32_t*>(gs)[k];
-  if (tid == 0) bad = 0;
-  const GridDev& g = a.g;
-  // per source: centred fp32 point, fp64 point, the seed (previous winner's fp32 point + index)
-  float4 p[kP], seed[kP];
-  double p64[kP][3];
-  bool valid[kP];
-  int64_t ii[kP];
-#pragma unroll
-  for (int u = 0; u < kP; ++u) {
-    const int64_t i = base + u * kTermsBlock + tid;
-    valid[u] = i < a.ns;
-    ii[u] = valid[u] ? i : 0;
-    p[u] = valid[u] ? a.src32[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) p64[u][k] = valid[u] ? a.src64[3 * i + k] : 0.0;
-    const int32_t j = valid[u] ? a.corr[i] : -1;  // the loop's correspondences on entry
-    seed[u] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
-    if (j >= 0) {
-      const float4 w = a.tgt32[j];
-      seed[u] = make_float4(w.x, w.y, w.z, __int_as_float(j));
-    }
-    cnum[u * kTermsBlock + tid] = -1;
-  }
-  const int lane = tid & (kWave - 1), wave = tid / kWave;
-  unsigned long long tph[7] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;  // phase timer (diagnostics)
-  const bool prof = kProf && tid == 0;
-  if (prof) tlast = wall_clock64();
-  auto mark = [&](int k) {
-    if (kProf && prof) {
-      const unsigned long long tn_ = wall_clock64();
-      tph[k] += tn_ - tlast;
-      tlast = tn_;
-    }
-  };
-  for (int it = 0; it < a.n; ++it) {
-    __syncthreads();  // S of this iteration
-    mark(0);
-    if (S.done || bad) break;
-    // (1) scan both queries of this thread
-    const float r2_hi = S.r2_hi, be = S.band_e;
-    const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
-    uint64_t k1[kP];
-    float k1d[kP], n2[kP], qx[kP], qy[kP], qz[kP];
-    int bx[kP][6], m0[kP];
-    bool hit[kP];
-#pragma unroll
-    for (int u = 0; u < kP; ++u) {
-      k1[u] = key0;
-      k1d[u] = n2[u] = kInf;
-      hit[u] = false;
-      m0[u] = 0;
-      xform32(S.Rt32, p[u], qx[u], qy[u], qz[u]);
-      const int32_t sj = __float_as_int(seed[u].w);
-      if (valid[u] && sj >= 0) {  // nnkey.h seed_key, single device: the previous winner re-evaluated
-        const float d2 = d2f(qx[u], qy[u], qz[u], seed[u].x, seed[u].y, seed[u].z);
-        if (d2 <= r2_hi) k1[u] = make_key(d2, (uint32_t)sj);
-      }
-      k1d[u] = key_real_d2(k1[u]);
-      const float R = sqrtf(search_bound(key_d2(k1[u]), be, r2_hi)) * 1.001f;
-      bx[u][0] = grid_coord(qx[u] - R, g.o[0], g.inv_h, g.n[0]);
-      bx[u][1] = grid_coord(qx[u] + R, g.o[0], g.inv_h, g.n[0]);
-      bx[u][2] = grid_coord(qy[u] - R, g.o[1], g.inv_h, g.n[1]);
-      bx[u][3] = grid_coord(qy[u] + R, g.o[1], g.inv_h, g.n[1]);
-      bx[u][4] = grid_coord(qz[u] - R, g.o[2], g.inv_h, g.n[2]);
-      bx[u][5] = grid_coord(qz[u] + R, g.o[2], g.inv_h, g.n[2]);
-      const int ql = u * kTermsBlock + tid;
-      const int mc = cnum[ql];
-      hit[u] = valid[u] && g.ncells > 0 && mc >= 0 && cbox[0][ql] == bx[u][0] && cbox[1][ql] == bx[u][1] &&
-               cbox[2][ql] == bx[u][2] && cbox[3][ql] == bx[u][3] && cbox[4][ql] == bx[u][4] &&
-               cbox[5][ql] == bx[u][5];
-      m0[u] = hit[u] ? mc : 0;
-    }
-    if (kProf && it < 64) {  // one atomic per wave
-      const unsigned long long nh = (unsigned long long)__popcll(__ballot(hit[0])) + __popcll(__ballot(hit[1]));
-      if (lane == 0 && nh) atomicAdd(a.prof + 520 + it, nh);
-    }
-    // hits: the first kR rows × kB points of BOTH queries in one batch of loads (one round trip
-    // for a typical seeded box), then any remainder per query
-    {
-      float4 v[kP][kR][kB];
-      int32_t ra[kP][kR], rb[kP][kR];
-#pragma unroll
-      for (int u = 0; u < kP; ++u)
-#pragma unroll
-        for (int k = 0; k < kR; ++k) {
-          const int2 ab = hit[u] && k < m0[u] ? crow[u * kTermsBlock + tid][k] : make_int2(0, 0);
-          ra[u][k] = ab.x;
-          rb[u][k] = ab.y;
-        }
-#pragma unroll
-      for (int u = 0; u < kP; ++u)
-#pragma unroll
-        for (int k = 0; k < kR; ++k)
-#pragma unroll
-          for (int m = 0; m < kB; ++m)
-            if (ra[u][k] + m < rb[u][k]) v[u][k][m] = g.pts[ra[u][k] + m];
-#pragma unroll
-      for (int u = 0; u < kP; ++u)
-#pragma unroll
-        for (int k = 0; k < kR; ++k)
-#pragma unroll
-          for (int m = 0; m < kB; ++m)
-            if (ra[u][k] + m < rb[u][k]) {
-              const float d2 = d2f(qx[u], qy[u], qz[u], v[u][k][m].x, v[u][k][m].y, v[u][k][m].z);
-              if (d2 <= r2_hi)
-                near_push(k1[u], k1d[u], n2[u], make_key(d2, (uint32_t)__float_as_int(v[u][k][m].w)), d2);
-            }
-#pragma unroll
-      for (int u = 0; u < kP; ++u) {
-        if (!hit[u]) continue;
-        const int2* rr = crow[u * kTermsBlock + tid];
-        int32_t more = 0;  // points beyond kB in the first kR rows
-#pragma unroll
-        for (int k = 0; k < kR; ++k) more = max(more, rb[u][k] - ra[u][k] - kB);
-        if (more > 0) scan_ranges<kR, kB>(g, rr, min(m0[u], kR), 0, kB, qx[u], qy[u], qz[u], r2_hi, k1[u], k1d[u], n2[u]);
-        if (m0[u] > kR) scan_ranges<kR, kB>(g, rr, m0[u], kR, 0, qx[u], qy[u], qz[u], r2_hi, k1[u], k1d[u], n2[u]);
-      }
-    }
-    // misses: the box's row starts from the grid, the ranges cached (≤ kPRows rows)
-#pragma unroll
-    for (int u = 0; u < kP; ++u) {
-      if (hit[u] || !valid[u] || g.ncells == 0) continue;
-      const int ql = u * kTermsBlock + tid;
-      const int ny = bx[u][3] - bx[u][2] + 1;
-      const int rows = ny * (bx[u][5] - bx[u][4] + 1);
-      int2* rr = crow[ql];
-      for (int r0 = 0; r0 < rows; r0 += kPRows) {
-        int2 ab[kPRows];
-#pragma unroll
-        for (int k = 0; k < kPRows; ++k) {
-          const int r = r0 + k;
-          ab[k] = make_int2(0, 0);
-          if (r < rows) {
-            const int64_t row = ((int64_t)(bx[u][4] + r / ny) * g.n[1] + (bx[u][2] + r % ny)) * g.n[0];
-            ab[k] = make_int2(g.start[row + bx[u][0]], g.start[row + bx[u][1] + 1]);
-          }
-        }
-        if (rows <= kPRows) {  // cache the box (one batch of starts covers it)
-#pragma unroll
-          for (int k = 0; k < kPRows; ++k)
-            if (k < rows) rr[k] = ab[k];
-          scan_ranges<kR, kB>(g, rr, rows, 0, 0, qx[u], qy[u], qz[u], r2_hi, k1[u], k1d[u], n2[u]);
-        } else {
-          for (int k = 0; k < kPRows && r0 + k < rows; ++k) {
-            int2 one[1] = {ab[k]};
-            scan_ranges<1, kB>(g, one, 1, 0, 0, qx[u], qy[u], qz[u], r2_hi, k1[u], k1d[u], n2[u]);
-          }
-        }
-      }
-      cnum[ql] = rows <= kPRows ? rows : -1;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) cbox[k][ql] = bx[u][k];
-    }
-#pragma unroll
-    for (int u = 0; u < kP; ++u)
-      if (!valid[u] || k1[u] == key0) k1[u] = (uint64_t)kKeyNone;
-    mark(1);
-    // (2) terms: terms_block's per-thread part for kP = 2, on the scan results in registers
-    {
-      double acc[30];
-#pragma unroll
-      for (int k = 0; k < 30; ++k) acc[k] = 0.0;
-      bool fixed[kP];
-      int64_t gj[kP];
-      double vs[kP][3], d2[kP];
-#pragma unroll
-      for (int u = 0; u < kP; ++u) {
-        gj[u] = -1;
-        d2[u] = 0.0;
-        fixed[u] = true;
-        q64_of(S.T, p64[u], vs[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < kP; ++u) {
-        const float X = valid[u] && k1[u] != (uint64_t)kKeyNone ? search_bound(key_d2(k1[u]), S.band_e, S.r2_hi) : -1.0f;
-        const bool amb = X >= 0.0f && (valid[u] ? n2[u] : kInf) <= X;
-        int64_t bj = -1;
-        double bd = 0.0;
-        resolve_wave(amb, g, a.tgt64, 0, qx[u], qy[u], qz[u], X, vs[u], S.r2, bj, bd);
-        if (amb) {
-          gj[u] = bj;
-          d2[u] = bd;
-        } else if (valid[u] && key_real(k1[u])) {
-          const int64_t c = (int64_t)(uint32_t)k1[u];
-          if (c < a.nt) {
-            gj[u] = c;
-            fixed[u] = false;
-          }
-        }
-      }
-      double tq[kP][3], tn[kP][3];
-      float4 t32[kP];
-#pragma unroll
-      for (int u = 0; u < kP; ++u) {
-        const bool own = valid[u] && gj[u] >= 0 && gj[u] < a.nt;
-        const int64_t l = own ? gj[u] : 0;
-        if (a.rec64 != nullptr) {
-          const double4 r0 = reinterpret_cast<const double4*>(a.rec64)[2 * l];
-          const double4 r1 = reinterpret_cast<const double4*>(a.rec64)[2 * l + 1];
-          tq[u][0] = r0.x;
-          tq[u][1] = r0.y;
-          tq[u][2] = r0.z;
-          tn[u][0] = r0.w;
-          tn[u][1] = r1.x;
-          tn[u][2] = r1.y;
-        } else {
-#pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            tq[u][k] = a.tgt64[3 * l + k];
-            tn[u][k] = a.est == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
-          }
-        }
-        t32[u] = a.tgt32[l];  // the next iteration's seed point
-      }
-#pragma unroll
-      for (int u = 0; u < kP; ++u) {
-        if (!valid[u]) continue;
-        if (!fixed[u]) {
-          const double d = d2_64(vs[u], tq[u]);
-          if (d < S.r2) {
-            d2[u] = d;
-          } else {
-            gj[u] = -1;
-          }
-        }
-        a.corr[ii[u]] = (int32_t)gj[u];
-        seed[u] = gj[u] >= 0 ? make_float4(t32[u].x, t32[u].y, t32[u].z, __int_as_float((int32_t)gj[u]))
-                             : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
-        if (gj[u] < 0 || gj[u] >= a.nt) continue;
-        terms_add(acc, vs[u], tq[u], tn[u], d2[u], a.est, a.c);
-      }
-      double v[32];
-#pragma unroll
-      for (int k = 0; k < 32; ++k) v[k] = k < 30 ? acc[k] : 0.0;
-      const double w = wave_transpose_sum32(v, lane);
-      if ((lane & 1) == 0) red[lane >> 1][wave] = w;
-    }
-    __syncthreads();
-    mark(2);
-    // (3) publish this tile's partial, arrive, wait for every tile
-    double* P = a.pp + (int64_t)(it & 1) * ntiles * kTermSlots;
-    if (tid < kTermSlots) {
-      double v = 0.0;
-      if (tid < 30)
-        for (int w = 0; w < kTermsBlock / kWave; ++w) v += red[tid][w];
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(P + (int64_t)blockIdx.x * kTermSlots + tid),
-                         __double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    mark(3);
-    if (tid == 0) {
-      __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t want = (uint32_t)(ntiles * (it + 1));
-      uint32_t spins = 0;
-      while (__hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > kPersistMaxSpin) {
-          bad = 1;
-          *a.fault = 1;
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    mark(4);
-    if (bad) break;
-    // (4) every tile's partial in terms_solve_kernel's order: group g = tiles g, g + 32, … (each
-    // out-of-range tile adds +0.0 as there), then the 32 group sums in group order
-    {
-      const int slot = tid & (kTermSlots - 1);
-      for (int gg = tid / kTermSlots; gg < kReduceGroups; gg += kT / kTermSlots) {
-        constexpr int kMaxPer = 8;  // ntiles ≤ 256 (api.cpp)
-        double tv[kMaxPer];
-#pragma unroll
-        for (int r = 0; r < kMaxPer; ++r) {
-          const int64_t b = gg + (int64_t)r * kReduceGroups;
-          tv[r] = b < ntiles ? __longlong_as_double(__hip_atomic_load(
-                                   reinterpret_cast<unsigned long long*>(P + b * kTermSlots + slot),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                             : 0.0;
-        }
-        double gv = 0.0;
-#pragma unroll
-        for (int r = 0; r < kMaxPer; ++r) gv += tv[r];
-        gsum[gg][slot] = gv;
-      }
-    }
-    __syncthreads();
-    if (tid < kTermSlots) {
-      double tt = 0.0;
-      for (int k = 0; k < kReduceGroups; ++k) tt += gsum[k][tid];
-      gsum[0][tid] = tt;
-    }
-    __syncthreads();
-    mark(5);
-    if (tid < kWave) {
-      SolveIn in;
-      solve_in(&S, in);
-      unsigned long long clk[5] = {0, 0, 0, 0, 0};
-      solve_state(gsum[0], &S, sp, in, kProf ? clk : nullptr);
-      if (kProf && prof && clk[4] != 0) {
-        atomicAdd(a.prof + 600, clk[1] - clk[0]);
-        atomicAdd(a.prof + 601, clk[2] - clk[1]);
-        atomicAdd(a.prof + 602, clk[3] - clk[2]);
-        atomicAdd(a.prof + 603, clk[4] - clk[3]);
-      }
-    }
-  }
-  if (kProf && prof) {  // [0..6] workgroup 0's phases; [8 + 2b], [9 + 2b]: workgroup b's scan, terms
-    if (blockIdx.x == 0)
-      for (int k = 0; k < 7; ++k) atomicAdd(a.prof + k, tph[k]);
-    a.prof[8 + 2 * blockIdx.x] = tph[1];
-    a.prof[9 + 2 * blockIdx.x] = tph[2];
-  }
-  __syncthreads();
-  if (blockIdx.x == 0)
-    for (int k = tid; k < (int)(sizeof(IcpState) / 4); k += kT)
-      reinterpret_cast<uint32_t*>(gs)[k] = reinterpret_cast<const uint32_t*>(&S)[k];
 }
 
 // finalize standalone NN (m3d_nn1): the fp64 winner (nnkey.h winner_fp64) and its d64
@@ -1905,19 +1417,12 @@ static dim3 nn_grid(int64_t bx, int64_t nt_pad, int64_t mult, int64_t* slice_out
 }
 
 static bool icp_nn_uses_mfma(const m3d_icp* s) {
-  static const bool mfma_env = [] {
-    const char* e = getenv("M3D_NN_MFMA");
-    return !(e && atoi(e) == 0);
-  }();
-  return mfma_env && s->tgrid != nullptr && s->tgrid->mf16 != nullptr;
+  return s->tgrid != nullptr && s->tgrid->mf16 != nullptr;
 }
 
 bool icp_nn_range_ok(const m3d_icp* s) {
-  if (s->params.nn_method == M3D_NN_GRID) {
-    const char* e = getenv("M3D_GRID_BATCHED");
-    return !(e && atoi(e) == 0) && s->sgrid != nullptr && s->sgrid->mpts != nullptr;
-  }
-  return icp_nn_uses_mfma(s) && s->qorder == nullptr;
+  if (s->params.nn_method == M3D_NN_GRID) return s->sgrid != nullptr && s->sgrid->mpts != nullptr;
+  return icp_nn_uses_mfma(s);
 }
 
 // Brute-force NN into s->keys (after launch_icp_keyinit, or self_seed: keys all kKeyNone, see
@@ -1928,112 +1433,42 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
   const int64_t ns = q1 < 0 ? s->src->n : q1;  // queries: visit positions [q0, ns)
   const int64_t nt_pad = s->tgt->n_pad;
   if (ns <= q0 || s->tgt->n == 0) return hipSuccess;
-  static const int Q = [] {
-    const char* e = getenv("M3D_NN_Q");
-    const int v = e ? atoi(e) : kNNQDefault;
-    return (v == 1 || v == 2 || v == 4) ? v : kNNQDefault;
-  }();
   const Grid* tg = s->tgrid;
   int64_t slice = 0;
   if (icp_nn_uses_mfma(s)) {
-    static const int MG = [] {
-      const char* e = getenv("M3D_NN_MG");
-      const int v = e ? atoi(e) : kMGDefault;
-      return (v == 1 || v == 2 || v == 4) ? v : kMGDefault;
-    }();
-    static const uint64_t exp_mask = [] {
-      const char* e = getenv("M3D_NN_EXP");
-      return (e && atoi(e) == 1) ? 0ull : ~0ull;
-    }();
-    // M3D_NN_STATS=1 (diagnostics): count flagged sub-tiles, print after every launch (syncs)
-    static unsigned long long* nn_stats = [] {
-      const char* e = getenv("M3D_NN_STATS");
-      unsigned long long* p = nullptr;
-      if (e && atoi(e) == 1 && hipMalloc(&p, 2 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
-      return p;
-    }();
-    if (nn_stats != nullptr) (void)hipMemsetAsync(nn_stats, 0, 2 * sizeof(unsigned long long), st);
-    // grid.y blocks take every S-th target tile instead of a contiguous slice (M3D_NN_STRIDED=0:
-    // slices).  Targets are stored in cell order, so a query block's few candidate tiles are
-    // adjacent: in a contiguous slice they all land in ONE block, whose exact-path work then
-    // sets the kernel's tail; strided, they spread over S blocks (cfg1: 0.334 → 0.305 ms).
-    static const int strided = [] {
-      const char* e = getenv("M3D_NN_STRIDED");
-      return (e && atoi(e) == 0) ? 0 : 1;
-    }();
-    static const bool fill = [] {
-      const char* e = getenv("M3D_NN_FILL");
-      return !(e && atoi(e) == 0);
-    }();
-    // target tile = TH × 256 (one barrier per tile; M3D_NN_TH = 1 | 2 | 4)
-    static const int TH = [] {
-      const char* e = getenv("M3D_NN_TH");
-      const int v = e ? atoi(e) : kTHDefault;
-      return (v == 1 || v == 2 || v == 4) ? v : kTHDefault;
-    }();
-    const int64_t tt = (int64_t)TH * kMTile;
+    const int64_t tt = (int64_t)kTH * kMTile;
     if (tg->mf_npad % tt != 0) return hipErrorInvalidValue;  // pack16 pads to kMTilePad
-    const int64_t mq = MG == 4 ? mqueries<4>() : (MG == 2 ? mqueries<2>() : mqueries<1>());
-    dim3 gm = nn_grid((ns - q0 + mq - 1) / mq, tg->mf_npad, tt, &slice);
-    if (strided && fill) {
-      // Strided tiles decouple grid.y from slice boundaries: pick S in [S0, 2·S0] so that the
-      // block count fills the resident block slots in whole rounds (the last partial round of
-      // equal-length blocks idles the rest of the chip: 196 × 11 blocks on 512 slots = 4.2
-      // rounds ran as 5).
-      static const int64_t slots = [] {
-        int dev = 0, per = 0;
-        hipDeviceProp_t p;
-        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, nn_mfma_kernel<kMGDefault, kTHDefault>, kMBlock, 0) != hipSuccess)
-          return (int64_t)0;
-        return (int64_t)p.multiProcessorCount * (per > 0 ? per : 1);
-      }();
-      const int64_t bx = gm.x, ntiles = tg->mf_npad / tt;
-      if (slots > 0 && ntiles > 1) {
-        int64_t s0 = std::min<int64_t>(std::max<int64_t>((2048 + bx - 1) / bx, 1), ntiles);
-        int64_t best = s0;
-        double best_eff = 0.0;
-        for (int64_t S = s0; S <= std::min<int64_t>(2 * s0, ntiles); ++S) {
-          const int64_t blocks = bx * S, rounds = (blocks + slots - 1) / slots;
-          const double eff = (double)blocks / (double)(rounds * slots);
-          if (eff > best_eff + 1e-9) {
-            best_eff = eff;
-            best = S;
-          }
+    dim3 gm = nn_grid((ns - q0 + kMQueries - 1) / kMQueries, tg->mf_npad, tt, &slice);
+    // Strided tiles decouple grid.y from slice boundaries: pick S in [S0, 2·S0] so that the
+    // block count fills the resident block slots in whole rounds (the last partial round of
+    // equal-length blocks idles the rest of the chip: 196 × 11 blocks on 512 slots = 4.2
+    // rounds ran as 5).
+    static const int64_t slots = [] {
+      int dev = 0, per = 0;
+      hipDeviceProp_t p;
+      if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, nn_mfma_kernel, kMBlock, 0) != hipSuccess)
+        return (int64_t)0;
+      return (int64_t)p.multiProcessorCount * (per > 0 ? per : 1);
+    }();
+    const int64_t bx = gm.x, ntiles = tg->mf_npad / tt;
+    if (slots > 0 && ntiles > 1) {
+      int64_t s0 = std::min<int64_t>(std::max<int64_t>((2048 + bx - 1) / bx, 1), ntiles);
+      int64_t best = s0;
+      double best_eff = 0.0;
+      for (int64_t S = s0; S <= std::min<int64_t>(2 * s0, ntiles); ++S) {
+        const int64_t blocks = bx * S, rounds = (blocks + slots - 1) / slots;
+        const double eff = (double)blocks / (double)(rounds * slots);
+        if (eff > best_eff + 1e-9) {
+          best_eff = eff;
+          best = S;
         }
-        gm.y = (unsigned)best;
       }
-      static const int64_t gy_env = [] {  // M3D_NN_GY: grid.y override (tuning sweeps)
-        const char* e = getenv("M3D_NN_GY");
-        return e ? (int64_t)atoll(e) : (int64_t)0;
-      }();
-      if (gy_env > 0) gm.y = (unsigned)std::min<int64_t>(gy_env, ntiles);
+      gm.y = (unsigned)best;
     }
     const SeedArgs sa{s->corr, s->tgt->xyz32, s->tgt->n, self_seed ? 1 : 0};
-    // seeded groups resolve their flagged sub-tiles after the sweep (M3D_NN_DEFER=0: in the tile)
-    static const int defer = [] {
-      const char* e = getenv("M3D_NN_DEFER");
-      return (e && atoi(e) == 0) ? 0 : 1;
-    }();
-#define M3D_NN_LAUNCH(MGV, THV)                                                                  \
-  nn_mfma_kernel<MGV, THV><<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, s->qorder, tg->mf16,         \
-                                                   tg->mf32, tg->mf_npad, slice, off, s->state,    \
-                                                   s->keys, s->near2, exp_mask, nn_stats, strided, sa, q0, defer)
-    if (MG == 4) {
-      if (TH == 2) M3D_NN_LAUNCH(4, 2); else M3D_NN_LAUNCH(4, 1);
-    } else if (MG == 2) {
-      if (TH == 4) M3D_NN_LAUNCH(2, 4); else if (TH == 2) M3D_NN_LAUNCH(2, 2); else M3D_NN_LAUNCH(2, 1);
-    } else {
-      if (TH == 4) M3D_NN_LAUNCH(1, 4); else if (TH == 2) M3D_NN_LAUNCH(1, 2); else M3D_NN_LAUNCH(1, 1);
-    }
-#undef M3D_NN_LAUNCH
-    if (nn_stats != nullptr) {
-      unsigned long long h[2] = {0, 0};
-      if (hipMemcpyAsync(h, nn_stats, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
-          hipStreamSynchronize(st) == hipSuccess)
-        fprintf(stderr, "[m3d nn stats] flagged %llu of %llu steps (%.3f%%)\n", h[0], h[1],
-                h[1] ? 100.0 * (double)h[0] / (double)h[1] : 0.0);
-    }
+    nn_mfma_kernel<<<gm, kMBlock, 0, st>>>(s->src->xyz32, ns, tg->mf16, tg->mf32, tg->mf_npad, off,
+                                           s->state, s->keys, s->near2, sa, q0);
     return hipGetLastError();
   }
   if (q0 != 0 || ns != s->src->n) return hipErrorInvalidValue;  // the VALU form scans every source
@@ -2041,14 +1476,9 @@ hipError_t launch_icp_nn(const m3d_icp* s, int64_t off, bool self_seed, hipStrea
     const hipError_t e = launch_icp_keyinit(s, off, st);
     if (e != hipSuccess) return e;
   }
-  const dim3 grid = nn_grid((ns + kNNBlock * Q - 1) / (kNNBlock * Q), nt_pad, kNNLds, &slice);
-  const float4* tp = s->tgt->xyz32;
-  if (Q == 4)
-    nn_kernel<4><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, s->near2);
-  else if (Q == 2)
-    nn_kernel<2><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, s->near2);
-  else
-    nn_kernel<1><<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, tp, nt_pad, slice, off, s->state, s->keys, s->near2);
+  const dim3 grid = nn_grid((ns + kNNBlock * kNNQ - 1) / (kNNBlock * kNNQ), nt_pad, kNNLds, &slice);
+  nn_kernel<<<grid, kNNBlock, 0, st>>>(s->src->xyz32, ns, s->tgt->xyz32, nt_pad, slice, off, s->state,
+                                             s->keys, s->near2);
   return hipGetLastError();
 }
 
@@ -2100,10 +1530,6 @@ static TermsArgs terms_args(const m3d_icp* s, int64_t off, const int32_t* claim,
   a.dmin = dmin;
   a.dprev = claim != nullptr ? s->dprev : nullptr;
   a.corr = s->corr;
-  a.sq = s->sq;
-  a.minv = s->sgrid != nullptr ? s->sgrid->minv : nullptr;
-  a.tgt32 = s->tgt->xyz32;
-  if (a.minv == nullptr) a.sq = nullptr;
   a.est = s->params.estimation;
   for (int k = 0; k < 3; ++k) a.c[k] = s->src->center[k];
   a.reset_keys = reset_keys ? s->keys : nullptr;
@@ -2179,151 +1605,6 @@ hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t
     return e == hipSuccess ? launch_icp_solve(s, s->sums, st) : e;
   }
   launch_terms_solve(terms_args(s, 0, nullptr, nullptr, reset_keys), s, s->sums, 1, st);
-  return hipGetLastError();
-}
-
-// The persistent grid loop (icp_grid_persist_kernel): usable when the loop runs the grid NN on
-// one device with 512-source terms tiles, at most 256 tiles (the reduction's unrolled depth), and
-// the whole grid is resident.  Flags M3D_ICP_PERSIST / M3D_ICP_NO_PERSIST, else the env default
-// M3D_ICP_PERSIST = 1 | 0 (off when unset); M3D_PERSIST_LANES = 1 | 2
-// (lanes per query, 512 or 1024 threads per workgroup).
-// rows × points per lane and load batch (M3D_PERSIST_RB = 22 | 24 | 28 | 44, tuning)
-static int persist_rb() {
-  static const int v = [] {
-    const char* e = getenv("M3D_PERSIST_RB");
-    const int k = e ? atoi(e) : 24;
-    return (k == 22 || k == 24 || k == 28 || k == 44) ? k : 24;
-  }();
-  return v;
-}
-
-template <bool kProf>
-static void persist_launch(int rb, unsigned grid, const PersistArgs& a, IcpState* st_, const SolveParams& sp,
-                           hipStream_t st) {
-  switch (rb) {
-    case 22: icp_grid_persist_kernel<2, 2, kProf><<<grid, kTermsBlock, 0, st>>>(a, st_, sp); break;
-    case 28: icp_grid_persist_kernel<2, 8, kProf><<<grid, kTermsBlock, 0, st>>>(a, st_, sp); break;
-    case 44: icp_grid_persist_kernel<4, 4, kProf><<<grid, kTermsBlock, 0, st>>>(a, st_, sp); break;
-    default: icp_grid_persist_kernel<2, 4, kProf><<<grid, kTermsBlock, 0, st>>>(a, st_, sp); break;
-  }
-}
-
-static const void* persist_fn() {
-  switch (persist_rb()) {
-    case 22: return reinterpret_cast<const void*>(&icp_grid_persist_kernel<2, 2, false>);
-    case 28: return reinterpret_cast<const void*>(&icp_grid_persist_kernel<2, 8, false>);
-    case 44: return reinterpret_cast<const void*>(&icp_grid_persist_kernel<4, 4, false>);
-    default: return reinterpret_cast<const void*>(&icp_grid_persist_kernel<2, 4, false>);
-  }
-}
-
-bool icp_persist_ok(const m3d_icp* s) {
-  static const bool dflt = [] {  // M3D_ICP_PERSIST = 1 | 0: the default when the flags say neither
-    const char* e = getenv("M3D_ICP_PERSIST");
-    return e != nullptr && atoi(e) == 1;
-  }();
-  const bool want = (s->params.flags & M3D_ICP_PERSIST) ? true : (s->params.flags & M3D_ICP_NO_PERSIST) ? false : dflt;
-  if (!want || s->params.nn_method != M3D_NN_GRID || s->ns_total > 0 || s->src->n == 0 ||
-      terms_pts() != 2 || s->tgrid == nullptr)
-    return false;
-  const int64_t ntiles = (s->src->n + kPTile - 1) / kPTile;
-  if (ntiles > 8 * kReduceGroups) return false;
-  static int cap = -1;  // resident workgroups of the kernel on this device (per process, device 0 form)
-  if (cap < 0) {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, persist_fn(), kTermsBlock, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      cap = 0;
-    } else {
-      // one workgroup per CU at most (the hand-off form this kernel uses is measured at one per
-      // CU), and a margin of 8 CUs for anything else resident
-      cap = per >= 1 ? std::max(0, cus - 8) : 0;
-    }
-  }
-  return ntiles <= cap;
-}
-
-hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st) {
-  const int64_t ntiles = (s->src->n + kPTile - 1) / kPTile;
-  if (s->pp == nullptr) {
-    hipError_t e = hipMalloc(&s->pp, sizeof(double) * 2 * kTermSlots * ntiles);
-    if (e == hipSuccess) e = hipMalloc(&s->pcounter, 64);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(s->pcounter, 0, 64, st);
-    if (e != hipSuccess) return e;
-  }
-  hipError_t e = hipMemsetAsync(s->pcounter, 0, sizeof(uint32_t), st);
-  if (e != hipSuccess) return e;
-  PersistArgs a;
-  a.src32 = s->src->xyz32;
-  a.src64 = s->src->xyz64;
-  a.ns = s->src->n;
-  a.g = s->tgrid->dev;
-  a.tgt64 = s->tgt->xyz64;
-  a.rec64 = s->tgt->rec64;
-  a.nrm64 = s->tgt->nrm64;
-  a.tgt32 = s->tgt->xyz32;
-  a.nt = s->tgt->n;
-  a.corr = s->corr;
-  a.pp = s->pp;
-  a.counter = s->pcounter;
-  a.fault = reinterpret_cast<int32_t*>(s->pcounter) + 8;  // its own 32-B sector of the 64-B block
-  a.n = n;
-  a.est = s->params.estimation;
-  for (int k = 0; k < 3; ++k) a.c[k] = s->src->center[k];
-  static unsigned long long* prof = [] {  // M3D_PERSIST_PROF=1: phase ticks, printed per launch
-    const char* e = getenv("M3D_PERSIST_PROF");
-    unsigned long long* p = nullptr;
-    if (e && atoi(e) == 1 && hipMalloc(&p, 640 * sizeof(unsigned long long)) != hipSuccess) p = nullptr;
-    return p;
-  }();
-  a.prof = prof;
-  if (prof != nullptr) (void)hipMemsetAsync(prof, 0, 640 * sizeof(unsigned long long), st);
-  const SolveParams sp = solve_params(s);
-  if (prof != nullptr)
-    persist_launch<true>(persist_rb(), (unsigned)ntiles, a, s->state, sp, st);
-  else
-    persist_launch<false>(persist_rb(), (unsigned)ntiles, a, s->state, sp, st);
-  if (prof != nullptr) {
-    std::vector<unsigned long long> h(640);
-    int khz = 0, dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-    if (hipMemcpyAsync(h.data(), prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, st) == hipSuccess &&
-        hipStreamSynchronize(st) == hipSuccess && khz > 0) {
-      const double us = 1e3 / khz;
-      fprintf(stderr, "[m3d persist] %lld tiles, n=%d, us per iteration: top %.2f scan %.2f terms %.2f "
-              "publish %.2f wait %.2f reduce %.2f (solve in 'top')\n", (long long)ntiles, n,
-              h[0] * us / n, h[1] * us / n, h[2] * us / n, h[3] * us / n, h[4] * us / n, h[5] * us / n);
-      std::vector<double> sc, te, tot;
-      for (int64_t b = 0; b < ntiles; ++b) {
-        sc.push_back(h[8 + 2 * b] * us / n);
-        te.push_back(h[9 + 2 * b] * us / n);
-        tot.push_back(sc.back() + te.back());
-      }
-      auto q = [](std::vector<double> v, double f) {
-        std::sort(v.begin(), v.end());
-        return v[(size_t)std::min<double>(v.size() - 1, f * (v.size() - 1))];
-      };
-      int64_t worst = 0;
-      for (int64_t b = 0; b < ntiles; ++b) worst = tot[b] > tot[worst] ? b : worst;
-      fprintf(stderr, "[m3d persist]   per workgroup scan min %.2f med %.2f p90 %.2f max %.2f | terms min %.2f "
-              "med %.2f p90 %.2f max %.2f | worst tile %lld (scan %.2f terms %.2f)\n",
-              q(sc, 0), q(sc, 0.5), q(sc, 0.9), q(sc, 1), q(te, 0), q(te, 0.5), q(te, 0.9), q(te, 1),
-              (long long)worst, sc[worst], te[worst]);
-      std::string hs;
-      for (int k = 0; k < std::min(n, 64); ++k) {
-        char b[16];
-        snprintf(b, sizeof(b), " %.1f", 100.0 * h[520 + k] / std::max<double>(1.0, (double)s->src->n));
-        hs += b;
-      }
-      fprintf(stderr, "[m3d persist]   box hits per iteration (%%):%s\n", hs.c_str());
-      fprintf(stderr, "[m3d persist]   solve (all workgroups' wave 0, us per solve): ldlt+entry %.2f update %.2f matmul %.2f refresh %.2f\n",
-              h[600] * us / (n * ntiles), h[601] * us / (n * ntiles), h[602] * us / (n * ntiles), h[603] * us / (n * ntiles));
-    }
-  }
   return hipGetLastError();
 }
 

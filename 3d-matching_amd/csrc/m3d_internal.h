@@ -219,12 +219,6 @@ struct m3d_ctx {
   size_t prep_bytes = 0;
   m3d::TmpArena tmp;  // setup temporaries (grids, Morton copies, cloud packing)
   m3d::TmpArena run;  // loop arrays of the synchronous one-shot ICP / NN calls (api.cpp icp_create)
-  // pinned staging memory of the host-array uploads (api.cpp upload_host); stage_ev follows the
-  // last DMA out of it
-  void* stage = nullptr;
-  size_t stage_cap = 0;
-  hipEvent_t stage_ev = nullptr;
-  bool stage_pending = false;
 };
 
 struct m3d_corrset {
@@ -241,17 +235,6 @@ struct m3d_corrset {
   // splits of S·p_c / S·q_c (plane 0: the p part, planes 1-3: the q_x / q_y / q_z parts)
   uint4* ca16 = nullptr;
   double s16 = 0.0;  // the power-of-two scale S (0: MFMA scoring unavailable)
-  // Tile culling of the a4 batches (round 4, ransac.hip ensure_cull; built on the first culled
-  // run, in stream order): the rows in the Morton order of (p_c, q_c), their MFMA operands, and
-  // per 32-row tile the centre's operands and the bounds (S·ρ, S·e) of
-  // | |d_i| − |d_c| | ≤ ‖R − R0‖_F·ρ + e (R0: the Kabsch rotation of the whole set)
-  mutable void* cull_block = nullptr;
-  mutable uint4* cas16 = nullptr;    // 4 planes × nc_pad, sorted rows
-  mutable int32_t* rowmap = nullptr; // nc_pad: sorted row → original row
-  mutable uint4* cca16 = nullptr;    // 4 planes × nsub_pad: tile centres
-  mutable float2* tstat = nullptr;   // nsub_pad: (S·ρ, S·e); e = +inf: never decided
-  mutable double R0h[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // R0 (host copy, passed by value)
-  mutable int64_t nsub = 0, nsub_pad = 0;
 };
 
 struct m3d_cloud {
@@ -301,9 +284,6 @@ struct m3d_icp {
   int64_t* dprev = nullptr;        // ns: target-sharded loops, bits of the global winner's d64
   int64_t* ld64 = nullptr;         // ns: target-sharded loops, bits of this shard's winner's d64
   int32_t* lidx = nullptr;         // ns: target-sharded loops, this shard's fp64 winner (-1 none)
-  // grid NN: each source's seed record in the source's Morton order (nnkey.h SeedRec), written by
-  // the terms pass with the correspondence, read by the grid scan beside the query point
-  float4* sq = nullptr;
   // grid NN on a target with dense cells (grid.hip grid_nn_heavy_kernel): the queries deferred
   // by the per-query scan (ns slots), their count and the kernel's block ticket; cand_cap = 0: no
   // deferral
@@ -315,7 +295,6 @@ struct m3d_icp {
   double* partials = nullptr;      // nblocks × kTermSlots
   double* sums = nullptr;          // kTermSlots
   int64_t nblocks = 0;
-  const int32_t* qorder = nullptr;  // grid NN: source visit order (source cell order)
   const m3d::Grid* sgrid = nullptr;  // the source's grid (Morton query order of the grid NN)
   const m3d::Grid* tgrid = nullptr;  // grid NN: the target's grid (owned by the target cloud)
   int64_t ns_total = 0;  // source-sharded multi-GPU: sources over all ranks (fitness denominator)
@@ -329,10 +308,6 @@ struct m3d_icp {
   double* xsums = nullptr;  // kTermSlots, SUM-reduced
   // m3d_icp_steps replays: an n-step sequence captured into a HIP graph (api.cpp), one slot per
   // keys_clean state on entry; a slot captures a sequence requested a second time
-  // the persistent grid loop (icp.hip icp_grid_persist_kernel): double-buffered tile partials,
-  // the arrival counter (word 0) and the fault flag (word 8) of one 64-B block
-  double* pp = nullptr;
-  uint32_t* pcounter = nullptr;
   hipStream_t cap_stream = nullptr;
   hipGraphExec_t graph[2] = {nullptr, nullptr};
   int32_t graph_n[2] = {-1, -1};
@@ -409,25 +384,6 @@ int64_t score_mf_hpad(int64_t H);
 hipError_t launch_corr16(m3d_corrset* cs, hipStream_t st);  // cs->ca16, cs->s16
 hipError_t launch_score_prep(const m3d_corrset* cs, const double* T64, int64_t H, double thr,
                              int mode, const ScoreMf& mf, hipStream_t st);
-// a4 batch scoring with tile culling (ransac.hip): scratch of one batch of h_pad hypotheses
-struct ScoreCull {
-  uint32_t* key = nullptr;    // h_pad sort keys (‖R − R0‖_F bits)
-  uint32_t* key2 = nullptr;   // h_pad
-  int32_t* val = nullptr;     // h_pad
-  int32_t* perm = nullptr;    // h_pad: position → hypothesis
-  float* a = nullptr;         // h_pad: ‖R − R0‖_F (rounded up) by hypothesis
-  float* apos = nullptr;      // h_pad: by position
-  float* edpos = nullptr;     // h_pad: the screen's per-component error bound E_d by position
-  uint32_t* skip = nullptr;   // (h_pad / 32) × (nsub_pad / 32) bits: (group, tile) decided
-  void* sort_tmp = nullptr;
-  size_t sort_bytes = 0;
-};
-size_t cull_sort_bytes(int64_t h_pad);
-bool score_cull_on(const m3d_corrset* cs, double thr_sq);
-hipError_t ensure_cull(const m3d_corrset* cs, hipStream_t st);
-hipError_t launch_score_culled(const m3d_corrset* cs, const double* T64, int64_t H, double thr, int mode,
-                               int32_t* counts, int64_t* stats, const int32_t* done, const ScoreMf& mf,
-                               const ScoreCull& cc, hipStream_t st);
 hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, int32_t* counts,
                         const double* T64, double thr, int mode, int64_t* stats,
                         const int32_t* done, const ScoreMf& mf, hipStream_t st);
@@ -468,9 +424,6 @@ hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hip
                                int64_t q0 = 0, int64_t q1 = -1);
 hipError_t launch_shard_claim(const m3d_icp* s, const int64_t* dmin, int32_t* claim, hipStream_t st);
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st);
-// n grid-loop steps in one persistent launch (icp.hip; icp_persist_ok decides when it applies)
-bool icp_persist_ok(const m3d_icp* s);
-hipError_t launch_icp_persist(m3d_icp* s, int32_t n, hipStream_t st);
 // grid over xyz32[0, n) with cell ≈ `cell`: asynchronous when `lohi` (per-axis min[3], max[3] of
 // the points) is given, else one sync for the bounds; temporaries from `ta` (null: hipMalloc)
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g,
@@ -479,20 +432,14 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
 hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st);
 void grid_free(Grid* g);
 // prev/dprev/tgt32/nt_shard: seed each query with seed_key (nnkey.h); prev == nullptr: no seeds
-// qgrid: the query cloud's grid (its Morton-ordered points, grid_morton) — the cooperative kernel
-// sq: seed records in qgrid's Morton order (nnkey.h SeedRec) or null (seeds from prev/dprev)
+// qgrid: the query cloud's Morton-slot grid (its Morton-ordered points, morton_source)
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, const Grid* g,
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
-                          const float4* sq, const int32_t* prev, const int64_t* dprev,
-                          const float4* tgt32, int64_t nt_shard, hipStream_t st, int64_t q0 = 0,
-                          int64_t q1 = -1, int32_t* hlist = nullptr, uint32_t* hcnt = nullptr,
-                          int32_t cand_cap = 0, const double* src64 = nullptr,
+                          const int32_t* prev, const int64_t* dprev, const float4* tgt32, int64_t nt_shard,
+                          hipStream_t st, int64_t q0 = 0, int64_t q1 = -1, int32_t* hlist = nullptr,
+                          uint32_t* hcnt = nullptr, int32_t cand_cap = 0, const double* src64 = nullptr,
                           const double* tgt64 = nullptr);
-hipError_t grid_morton(Grid* g, hipStream_t st, TmpArena* ta = nullptr);
-// the Morton-slot copy of an ICP source (out, gout freshly allocated structs; see grid.hip);
-// asynchronous (stream order)
-hipError_t morton_copy(const m3d_cloud* src, const Grid* sg, m3d_cloud* out, Grid* gout, hipStream_t st);
-// the same copy straight from the source's points (no source grid): grid.hip morton_source
+// the ICP source's Morton-slot copy (out, gout freshly allocated structs): grid.hip morton_source
 hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid* gout, TmpArena* ta,
                          hipStream_t st);
 // dst[slot[k]] = v[k], k < n (slot-ordered loop arrays → the caller's source order)

@@ -325,30 +325,4 @@ __device__ __forceinline__ int64_t seed_key(const IcpState* __restrict__ s, int6
   return bound_key(s, __double2float_ru(__longlong_as_double(dp)), p, qx, qy, qz);
 }
 
-// Seed record of a source (grid NN; written by the terms pass in the source's Morton order):
-//   w = 0xFFFFFFFF                  none
-//   w = j < 2³¹, (x, y, z)          the previous winner j lies in this shard: its centred fp32
-//                                   coordinates (an exact candidate, as seed_key's first case)
-//   w = j | 2³¹, x = d64 (rounded up) the winner j lies in another shard: the bound of seed_key
-__device__ __forceinline__ float4 seed_rec(int64_t gj, bool local, const float4* tgt32_local, double d64) {
-  if (gj < 0) return make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0xFFFFFFFFu));
-  if (local) {
-    const float4 t = *tgt32_local;
-    return make_float4(t.x, t.y, t.z, __uint_as_float((uint32_t)gj));
-  }
-  return make_float4(__double2float_ru(d64), 0.0f, 0.0f, __uint_as_float((uint32_t)gj | 0x80000000u));
-}
-
-__device__ __forceinline__ int64_t seed_from_rec(const IcpState* __restrict__ s, float4 rec, float4 p,
-                                                 float qx, float qy, float qz) {
-  const uint32_t w = __float_as_uint(rec.w);
-  if (w == 0xFFFFFFFFu) return kKeyNone;
-  if (!(w & 0x80000000u)) {
-    const float d2 = d2f(qx, qy, qz, rec.x, rec.y, rec.z);
-    return d2 <= s->r2_hi ? (int64_t)make_key(d2, w) : kKeyNone;
-  }
-  if (!s->bound_ok) return kKeyNone;
-  return bound_key(s, rec.x, p, qx, qy, qz);
-}
-
 }  // namespace m3d

@@ -839,12 +839,8 @@ static float box_half_width(const m3d_cloud* c, double radius) {
 }
 
 double hybrid_fine_radius(const Grid* g, double radius, int k) {
-  // M3D_HYBRID_FINE=0: single-stage search (A/B); otherwise the expected-count factor below
-  static const double c = [] {
-    const char* e = getenv("M3D_HYBRID_FINE");
-    return e ? atof(e) : 0.5;
-  }();
-  if (!(c > 0.0) || k > 128 || g == nullptr || g->n_occ <= 0) return 0.0;
+  constexpr double c = 0.5;  // the expected-count factor below
+  if (k > 128 || g == nullptr || g->n_occ <= 0) return 0.0;
   // m = points per occupied radius-cell.  On a scanned surface ≈ 8 m (h / r)² points lie within
   // h (measured: the cfg4 scan, 1144 points within r against m = 139), so h = r·√(c·k / m)
   // expects ≈ 4 k of them at c = 0.5 (measured best of 0.3 / 0.5 / 0.8 once chunks merge in one
@@ -873,16 +869,12 @@ hipError_t hybrid_search(const m3d_cloud* c, const Grid* g, double radius, int k
   const int L = k <= 40 ? 64 : (k <= 80 ? 32 : (k <= 160 ? 16 : 8));
   const size_t lds = (size_t)k * L * (sizeof(double) + sizeof(int32_t));
   const double eabs = 3.4641016151377544 * c->rmax * 5.9604644775390625e-08 * 1.01;
-  static const int mode = [] {  // M3D_HYBRID_WAVE=0: the per-lane kernel (A/B)
-    const char* e = getenv("M3D_HYBRID_WAVE");
-    return e ? atoi(e) : 1;
-  }();
   const unsigned wb = (unsigned)((c->n + 3) / 4);  // 4 waves (queries) per 256-thread block
-  if (mode != 0 && k <= 64) {
+  if (k <= 64) {
     hybrid_search_wave_kernel<1><<<wb, 256, 0, st>>>(c->xyz64, c->xyz32, c->n, g->dev, Rf,
                                                      radius * radius, eabs, k, gfd, Hf, h2safe,
                                                      idx, d2, cnt);
-  } else if (mode != 0 && k <= 128) {
+  } else if (k <= 128) {
     hybrid_search_wave_kernel<2><<<wb, 256, 0, st>>>(c->xyz64, c->xyz32, c->n, g->dev, Rf,
                                                      radius * radius, eabs, k, gfd, Hf, h2safe,
                                                      idx, d2, cnt);

@@ -7,7 +7,7 @@
 //                                                                   fp32 VALU score_kernel
 //   step-RANSAC loop             _visualize_matcher.py:343-470   → select_kernel (batched, on device)
 //
-// fp32 VALU scoring design (score_kernel: the fallback, and M3D_SCORE_MFMA=0):
+// fp32 VALU scoring design (score_kernel: the fallback when the MFMA operands do not apply):
 //   * One lane holds kScoreK = 8 correspondences (centred fp32, 6 VGPRs each) for the whole block;
 //     a block of 4 waves covers 2048 correspondences and sweeps 64 hypotheses.
 //   * The block's 64 hypothesis blocks (R, t', guard band: 64 B each) are staged in LDS and read
@@ -255,7 +255,7 @@ struct Hyp16Fuse {
 // (defined with the MFMA screen below; declared inline here as it is there)
 __device__ __forceinline__ void hyp16_one(const double* T, bool valid, int64_t j, int64_t h_pad,
                                           const Mf16Params& m, uint4* __restrict__ hb16,
-                                          float* __restrict__ heps, float* ed_out);
+                                          float* __restrict__ heps);
 
 __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__ p64,
                                                       const double* __restrict__ q64, int64_t nc,
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__
   const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   zero_scoring_state(z, h, H);
   if (h >= H) {  // padding hypotheses of the MFMA operands
-    if (hf.on && h < hf.h_pad) hyp16_one(nullptr, false, h, hf.h_pad, hf.m, hf.hb16, hf.heps, nullptr);
+    if (hf.on && h < hf.h_pad) hyp16_one(nullptr, false, h, hf.h_pad, hf.m, hf.hb16, hf.heps);
     return;
   }
   double T[16];
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) void kabsch3_kernel(const double* __restrict__
   if (status != nullptr) status[h] = (uint8_t)st;
   // the fp32 VALU screen's block: not written when the MFMA screen scores this batch (hf.on)
   if (hypf != nullptr) hypf[h] = make_hypf(T, g);
-  if (hf.on) hyp16_one(T, true, h, hf.h_pad, hf.m, hf.hb16, hf.heps, nullptr);
+  if (hf.on) hyp16_one(T, true, h, hf.h_pad, hf.m, hf.hb16, hf.heps);
 }
 
 __global__ __launch_bounds__(256) void hypf_from_T_kernel(const double* __restrict__ T, int64_t H,
@@ -339,7 +339,6 @@ struct ExactArgs {
   double thr;
   int mode;
   int64_t* stats;  // [0] pairs re-evaluated in fp64
-  const int32_t* rowmap = nullptr;  // culled scoring: sorted row → row of p64 / q64
 };
 
 __global__ __launch_bounds__(kScoreBlock) void score_kernel(
@@ -456,15 +455,12 @@ union SH8 {
   s_half8 h;
 };
 
-constexpr int kSMGDefault = 2;                // 32-hypothesis groups per wave (M3D_SCORE_MG)
+constexpr int kSGroups = 2;                   // 32-hypothesis groups per wave
 constexpr int kSBlock = 512;                  // 8 waves
 template <int kSMG>
 constexpr int shyps() { return (kSBlock / 64) * kSMG * 32; }  // hypotheses per block
 constexpr int kSHypPad = shyps<4>();          // batch padding: a multiple of every variant's
-#ifndef M3D_SCORE_TILE
-#define M3D_SCORE_TILE 512
-#endif
-constexpr int kSTile = M3D_SCORE_TILE;        // correspondences per LDS tile (256 | 512)
+constexpr int kSTile = 512;                   // correspondences per LDS tile
 static_assert(kSTile % 64 == 0 && (4 * kSTile) % 512 == 0, "a wave stages 64 consecutive rows");
 constexpr double kU16 = 4.8828125e-04;        // 2^-11
 constexpr double kSig16 = 2.98023223876953125e-08;  // 2^-25: half the fp16 subnormal spacing
@@ -482,14 +478,13 @@ __global__ __launch_bounds__(256) void corr16_kernel(const double* __restrict__ 
                                                      int64_t nc_pad, double cs0, double cs1,
                                                      double cs2, double ct0, double ct1,
                                                      double ct2, double S,
-                                                     uint4* __restrict__ ca16,
-                                                     const int32_t* __restrict__ rowmap) {
+                                                     uint4* __restrict__ ca16) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= nc_pad) return;
   const _Float16 one = (_Float16)1.0f, zero = (_Float16)0.0f;
   SH8 P, Q[3];
   if (i < nc) {
-    const int64_t r = rowmap != nullptr ? rowmap[i] : i;  // culled scoring: rows in sorted order
+    const int64_t r = i;
     _Float16 h[3], l[3];
     split16d(S * (p64[3 * r] - cs0), h[0], l[0]);
     split16d(S * (p64[3 * r + 1] - cs1), h[1], l[1]);
@@ -513,15 +508,12 @@ __global__ __launch_bounds__(256) void corr16_kernel(const double* __restrict__ 
 // B operands + guard band of hypotheses [0, h_pad) of a batch (fp64 transforms T64).
 // hypothesis j's B operands + guard band from its fp64 transform T (valid: j < H; the padding
 // hypotheses get far operands)
-// ed_out (culled scoring, else null): the per-component error bound E_d of the screen's S·d for
-// this hypothesis (0 far, +inf not a rotation)
 __device__ __forceinline__ void hyp16_one(const double* T, bool valid, int64_t j, int64_t h_pad,
                                           const Mf16Params& m, uint4* __restrict__ hb16,
-                                          float* __restrict__ heps, float* ed_out) {
+                                          float* __restrict__ heps) {
   const _Float16 zero = (_Float16)0.0f, mone = (_Float16)-1.0f;
   SH8 B0[3], B1[3];
   float eps = -1.0f;  // no guard band: v is never inside (−1, 1)·ε
-  float ed = 0.0f;
   bool far = true, general = false;
   if (valid) {
     double tp[3], rowl1 = 0.0, tinf = 0.0;
@@ -547,7 +539,6 @@ __device__ __forceinline__ void hyp16_one(const double* T, bool valid, int64_t j
         B1[c].h = s_half8{zero, zero, zero, mone, mone, zero, zero, zero};
       }
       eps = FLT_MAX;  // v = S²thr² − |S·q_c|² is finite: |v| < ε for every pair
-      ed = INFINITY;
     } else if (!far) {
       const double S = m.S;
       for (int c = 0; c < 3; ++c) {
@@ -572,10 +563,8 @@ __device__ __forceinline__ void hyp16_one(const double* T, bool valid, int64_t j
       const double e = kU32 * T2 + 2.0 * 1.7320508075688772 * dm * Ed + 3.0 * Ed * Ed +
                        3.0 * kU32 * (T2 + dc * dc);
       eps = __double2float_ru(1.25 * e + 8.0 * DBL_EPSILON * T2);
-      ed = __double2float_ru(Ed);
     }
   }
-  if (ed_out != nullptr) *ed_out = ed;
   if (far) {
     for (int c = 0; c < 3; ++c) {
       B0[c].u = make_uint4(0, 0, 0, 0);
@@ -595,7 +584,7 @@ __global__ __launch_bounds__(256) void hyp16_kernel(const double* __restrict__ T
                                                     float* __restrict__ heps) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= h_pad) return;
-  hyp16_one(j < H ? T64 + 16 * j : nullptr, j < H, j, h_pad, m, hb16, heps, nullptr);
+  hyp16_one(j < H ? T64 + 16 * j : nullptr, j < H, j, h_pad, m, hb16, heps);
 }
 
 // acc − x·x as one scalar v_fma_f32 (single rounding, = fma(−x, x, acc)).  The empty asm makes
@@ -613,33 +602,16 @@ __device__ __forceinline__ float vmin3a(float a, float b, float c) {
   return __builtin_elementwise_minimum(__builtin_elementwise_minimum(fabsf(a), fabsf(b)), fabsf(c));
 }
 
-#ifndef M3D_SCORE_PERM_COUNT
-#define M3D_SCORE_PERM_COUNT 1
-#endif
-#ifndef M3D_SCORE_PERM_OR
-#define M3D_SCORE_PERM_OR 1
-#endif
-#ifndef M3D_SCORE_DMA
-#define M3D_SCORE_DMA 1  // 0: the register-staged tile prefetch (measured 2-3 % slower)
-#endif
 // units of score_mfma_kernel's per-lane outlier counter (the v_perm count adds 8 per outlier)
-constexpr uint32_t kOutlUnit = M3D_SCORE_PERM_COUNT ? 8u : 1u;
+constexpr uint32_t kOutlUnit = 8u;
 
 // grid: x = hypothesis blocks of shyps<kSMG>(), y = correspondence slices of slice_len (multiple
 // of kSTile); block = 8 waves, wave w owns hypotheses hb + (w·kSMG + g)·32 + (lane & 31).
-// kCull (a4 batches with tile culling): the B operands are in sorted POSITION order, position j
-// scores hypothesis perm[j]; a (32-position group, 32-row tile) whose skip bit is set
-// (cull_classify_kernel: every hypothesis of the group decided for every row of the tile) is not
-// screened — its decided inliers were counted by the classifier; the band queue maps sorted rows
-// back through ex.rowmap.
-template <int kSMG, bool kCull>
+template <int kSMG>
 __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
     const uint4* __restrict__ ca16, int64_t nc_pad, const uint4* __restrict__ hb16,
     const float* __restrict__ heps, int64_t h_pad, int64_t H, int64_t slice_len, float T2,
-    int32_t* __restrict__ counts, ExactArgs ex, const int32_t* __restrict__ done, float band_on, int xcd,
-    const int32_t* __restrict__ perm, const uint32_t* __restrict__ skip, int64_t nwords) {
-  // band_on: 1; M3D_SCORE_EXP=1 passes −1 to time the screen without the fp64 band path
-  // (profiling experiment only: counts are then those of the screen alone)
+    int32_t* __restrict__ counts, ExactArgs ex, const int32_t* __restrict__ done, int xcd) {
   if (done != nullptr && *done) return;
   // xcd: the dispatch order is remapped so that each XCD (linear block id mod 8) walks one
   // contiguous run of a group-major order — hypothesis blocks in 4 groups, within a group slice
@@ -665,12 +637,10 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   float eps[kSMG];
   uint32_t outl[kSMG];
   int64_t hyp[kSMG];
-  uint32_t scored[kSMG];  // kCull: 32-row tiles this group screened
 #pragma unroll
   for (int g = 0; g < kSMG; ++g) {
     const int64_t j = bxi * shyps<kSMG>() + (wave * kSMG + g) * 32 + c;  // < h_pad
-    hyp[g] = kCull ? (int64_t)perm[j] : j;
-    scored[g] = 0;
+    hyp[g] = j;
     SH8 t;
     t.u = hb16[(3 * h + 0) * h_pad + j];
     bx[g] = t.h;
@@ -678,7 +648,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
     by[g] = t.h;
     t.u = hb16[(3 * h + 2) * h_pad + j];
     bz[g] = t.h;
-    eps[g] = heps[j] * band_on;
+    eps[g] = heps[j];
     outl[g] = 0;
   }
   const s_floatx16 zacc = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
@@ -714,17 +684,6 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   for (int64_t j0 = jb; j0 < je; j0 += tstep) {
     ++tiles_seen;
     const bool has_next = j0 + tstep < je;
-    uint32_t msk[kSMG];  // kCull: skip bits of this LDS tile's 32-row tiles, per group (SGPRs)
-    if (kCull) {
-      const int64_t sb = j0 / 32;
-      const int wv = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-      for (int g = 0; g < kSMG; ++g) {
-        const int64_t grp = (bxi * shyps<kSMG>() + (wv * kSMG + g) * 32) / 32;
-        msk[g] = __builtin_amdgcn_readfirstlane(skip[grp * nwords + sb / 32] >> (sb % 32));
-      }
-    }
-#if M3D_SCORE_DMA
     // the next tile goes global → LDS by DMA (global_load_lds_dwordx4: wave-uniform base + lane ×
     // 16 B; the a16 rows are lane-linear) while this tile is swept, so no prefetch registers.  The
     // register prefetch (2 × uint4 live across the sweep) was spilled to scratch at the 128-VGPR
@@ -739,20 +698,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
         lds_dma16(ca16 + (e / kSTile) * nc_pad + j0 + tstep + e % kSTile, &a16[buf ^ 1][e / kSTile][(e % kSTile) & ~63]);
       }
     }
-#else
-    uint4 pre[kStage];
-    if (has_next) {
-#pragma unroll
-      for (int u = 0; u < kStage; ++u) {
-        const int e = threadIdx.x + u * kSBlock;
-        pre[u] = ca16[(e / kSTile) * nc_pad + j0 + tstep + e % kSTile];
-      }
-    }
-#endif
-#ifndef M3D_SCORE_UNROLL
-#define M3D_SCORE_UNROLL 2
-#endif
-#pragma unroll M3D_SCORE_UNROLL
+#pragma unroll 2
     for (int sub = 0; sub < kSTile / 32; ++sub) {
       SH8 ax, ay, az;
       ax.u = a16[buf][pa * 1][sub * 32 + c];
@@ -760,7 +706,6 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
       az.u = a16[buf][pa * 3][sub * 32 + c];
 #pragma unroll
       for (int g = 0; g < kSMG; ++g) {
-        if (kCull && ((msk[g] >> sub) & 1u)) continue;  // decided tile (wave-uniform)
         const s_floatx16 dx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax.h, bx[g], zacc, 0, 0, 0);
         const s_floatx16 dy = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay.h, by[g], zacc, 0, 0, 0);
         const s_floatx16 dz = __builtin_amdgcn_mfma_f32_32x32x16_f16(az.h, bz[g], zacc, 0, 0, 0);
@@ -769,29 +714,15 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
         for (int r = 0; r < 16; ++r) v[r] = fnmsq(dz[r], fnmsq(dy[r], fnmsq(dx[r], t2r)));
         // v > 0 ⇔ inlier (outside the band): count sign bits (outliers) per lane
         uint32_t s = 0;
-#if M3D_SCORE_PERM_COUNT
         // v_perm selectors 9 / 11 give a byte of 0xFF when S1 / S0 is negative: two sign masks
-        // per word, counted by v_bcnt (accumulating) — 8 per outlier, so outl holds 8× the count
-        // (2 VALU per 2 values instead of 2 shifts + an add3)
-#if M3D_SCORE_PERM_OR
-        // four sign bytes per v_bcnt: two v_perm fill bytes 0–1 and 2–3, one full-rate OR joins
-        // them (per 4 values 2 perm + 1 or + 1 bcnt instead of 2 perm + 2 bcnt)
+        // per word, and one full-rate OR joins two such words, so one v_bcnt (accumulating) counts
+        // four sign bytes — 8 per outlier, so outl holds 8× the count (per 4 values 2 perm + 1 or
+        // + 1 bcnt instead of 4 shifts + 2 add3)
 #pragma unroll
         for (int r = 0; r < 16; r += 4)
           s += __builtin_popcount(
               __builtin_amdgcn_perm(__float_as_uint(v[r]), __float_as_uint(v[r + 1]), 0x0C0C0B09u) |
               __builtin_amdgcn_perm(__float_as_uint(v[r + 2]), __float_as_uint(v[r + 3]), 0x0B090C0Cu));
-#else
-#pragma unroll
-        for (int r = 0; r < 16; r += 2)
-          s += __builtin_popcount(__builtin_amdgcn_perm(__float_as_uint(v[r]),
-                                                        __float_as_uint(v[r + 1]), 0x0C0C0B09u));
-#endif
-#else
-#pragma unroll
-        for (int r = 0; r < 16; r += 2)
-          s += (__float_as_uint(v[r]) >> 31) + (__float_as_uint(v[r + 1]) >> 31);
-#endif
         outl[g] += s;
         const float m0 = vmin3a(v[0], v[1], v[2]), m1 = vmin3a(v[3], v[4], v[5]);
         const float m2 = vmin3a(v[6], v[7], v[8]), m3 = vmin3a(v[9], v[10], v[11]);
@@ -822,9 +753,8 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
             if (slot < kSQueue) {
               qbuf[slot] = make_uint2((uint32_t)i, (uint32_t)hyp[g] | (sgn << 31));
             } else {
-              const int64_t ri = ex.rowmap != nullptr && i < ex.nc ? (int64_t)ex.rowmap[i] : i;
               const bool in = hyp[g] < H && i < ex.nc &&
-                              exact_inlier(ex.T64 + 16 * hyp[g], ex.p64 + 3 * ri, ex.q64 + 3 * ri,
+                              exact_inlier(ex.T64 + 16 * hyp[g], ex.p64 + 3 * i, ex.q64 + 3 * i,
                                            ex.thr, ex.mode);
               outl[g] += kOutlUnit * ((in ? 0u : 1u) - sgn);
             }
@@ -833,21 +763,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
         }
       }
     }
-    if (kCull) {
-#pragma unroll
-      for (int g = 0; g < kSMG; ++g) scored[g] += kSTile / 32 - __builtin_popcount(msk[g] & ((1u << (kSTile / 32)) - 1u));
-    }
-#if M3D_SCORE_DMA
     lds_dma_wait();
-#else
-    if (has_next) {
-#pragma unroll
-      for (int u = 0; u < kStage; ++u) {
-        const int e = threadIdx.x + u * kSBlock;
-        a16[buf ^ 1][e / kSTile][e % kSTile] = pre[u];
-      }
-    }
-#endif
     __syncthreads();
     buf ^= 1;
   }
@@ -855,8 +771,7 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
   const uint32_t rows = tiles_seen * (kSTile / 2);  // each lane half sees half of every 32-row block
 #pragma unroll
   for (int g = 0; g < kSMG; ++g) {
-    const uint32_t rg = kCull ? 16 * __builtin_amdgcn_readfirstlane(scored[g]) : rows;
-    const uint32_t in = 2 * rg - (outl[g] + (uint32_t)__shfl_xor((int)outl[g], 32)) / kOutlUnit;
+    const uint32_t in = 2 * rows - (outl[g] + (uint32_t)__shfl_xor((int)outl[g], 32)) / kOutlUnit;
     if (h == 0 && hyp[g] < H && in != 0) atomicAdd(&counts[hyp[g]], (int32_t)in);
   }
   // the queued guard-band pairs, one per thread: fp64 in numpy order, count correction
@@ -867,9 +782,8 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
     const int64_t i = (int64_t)q.x;
     const int64_t j = (int64_t)(q.y & 0x7FFFFFFFu);
     const int sgn = (int)(q.y >> 31);
-    const int64_t ri = ex.rowmap != nullptr && i < ex.nc ? (int64_t)ex.rowmap[i] : i;
     const bool in = j < H && i < ex.nc &&
-                    exact_inlier(ex.T64 + 16 * j, ex.p64 + 3 * ri, ex.q64 + 3 * ri, ex.thr, ex.mode);
+                    exact_inlier(ex.T64 + 16 * j, ex.p64 + 3 * i, ex.q64 + 3 * i, ex.thr, ex.mode);
     const int corr = sgn - (in ? 0 : 1);  // +1: a screen outlier is an inlier, −1: the reverse
     if (corr != 0 && j < H) atomicAdd(&counts[j], corr);
   }
@@ -1175,7 +1089,7 @@ hipError_t launch_corr16(m3d_corrset* cs, hipStream_t st) {
   }
   corr16_kernel<<<blocks_for(cs->nc_pad, 256), 256, 0, st>>>(
       cs->p64, cs->q64, cs->nc, cs->nc_pad, cs->cs[0], cs->cs[1], cs->cs[2], cs->ct[0], cs->ct[1],
-      cs->ct[2], S, cs->ca16, nullptr);
+      cs->ct[2], S, cs->ca16);
   e = hipGetLastError();
   if (e == hipSuccess) cs->s16 = S;
   return e;
@@ -1184,11 +1098,7 @@ hipError_t launch_corr16(m3d_corrset* cs, hipStream_t st) {
 // MFMA scoring applies when the operands exist and the threshold stays inside the cloud's
 // scaled range (S·thr ≤ 1024: thresholds beyond the cloud extent use the fp32 screen)
 static bool use_mfma_score(const m3d_corrset* cs, const ScoreMf& mf, double thr_sq) {
-  static const bool env = [] {
-    const char* e = getenv("M3D_SCORE_MFMA");
-    return !(e && atoi(e) == 0);
-  }();
-  return env && mf.hb16 != nullptr && cs->ca16 != nullptr && cs->s16 > 0.0 &&
+  return mf.hb16 != nullptr && cs->ca16 != nullptr && cs->s16 > 0.0 &&
          cs->s16 * sqrt(thr_sq) <= 1024.0;
 }
 
@@ -1339,7 +1249,7 @@ static int64_t score_grid_y(const m3d_corrset* cs, int64_t bx) {
       int dev = 0, per = 0;
       hipDeviceProp_t p;
       if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return (int64_t)0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, score_mfma_kernel<kSMGDefault, false>, kSBlock, 0) != hipSuccess)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, score_mfma_kernel<kSGroups>, kSBlock, 0) != hipSuccess)
         return (int64_t)0;
       return (int64_t)p.multiProcessorCount * (per > 0 ? per : 1);
     }();
@@ -1356,11 +1266,6 @@ static int64_t score_grid_y(const m3d_corrset* cs, int64_t bx) {
       }
     }
   }
-  static const int64_t gy_env = [] {  // M3D_SCORE_GY: grid.y override (tuning sweeps)
-    const char* e = getenv("M3D_SCORE_GY");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  if (gy_env > 0) sy = std::min<int64_t>(gy_env, tiles);
   return sy;
 }
 
@@ -1371,37 +1276,13 @@ hipError_t launch_score(const m3d_corrset* cs, const HypF32* hypf, int64_t H, in
   ExactArgs ex{T64, cs->p64, cs->q64, cs->nc, thr, mode, stats};
   const double thr_sq = thr_sq_mode(thr, mode);
   if (use_mfma_score(cs, mf, thr_sq)) {
-    static const int MG = [] {
-      const char* e = getenv("M3D_SCORE_MG");
-      const int v = e ? atoi(e) : kSMGDefault;
-      return (v == 1 || v == 2 || v == 4) ? v : kSMGDefault;
-    }();
     const int64_t hp = score_mf_hpad(H);
-    const int64_t bx = hp / (MG == 4 ? shyps<4>() : (MG == 2 ? shyps<2>() : shyps<1>()));
+    const int64_t bx = hp / shyps<kSGroups>();
     const int64_t sy = score_grid_y(cs, bx);
-    const int64_t slice = 0;  // strided tiles
     const float T2 = (float)(cs->s16 * cs->s16 * thr_sq);
-    static const float band_on = [] {
-      const char* e = getenv("M3D_SCORE_EXP");
-      return (e && atoi(e) == 1) ? -1.0f : 1.0f;
-    }();
-    const dim3 grid((unsigned)bx, (unsigned)sy);
-    static const int xcd = [] {  // M3D_SCORE_XCD=0: the plain (x, y) dispatch order
-      const char* e = getenv("M3D_SCORE_XCD");
-      return (e && atoi(e) == 0) ? 0 : 1;
-    }();
-    if (MG == 4)
-      score_mfma_kernel<4, false><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
-                                                            slice, T2, counts, ex, done, band_on, xcd,
-                                                            nullptr, nullptr, 0);
-    else if (MG == 2)
-      score_mfma_kernel<2, false><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
-                                                            slice, T2, counts, ex, done, band_on, xcd,
-                                                            nullptr, nullptr, 0);
-    else
-      score_mfma_kernel<1, false><<<grid, kSBlock, 0, st>>>(cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H,
-                                                            slice, T2, counts, ex, done, band_on, xcd,
-                                                            nullptr, nullptr, 0);
+    // slice_len 0: block y visits every sy-th correspondence tile; xcd 1: the XCD-aware dispatch
+    score_mfma_kernel<kSGroups><<<dim3((unsigned)bx, (unsigned)sy), kSBlock, 0, st>>>(
+        cs->ca16, cs->nc_pad, mf.hb16, mf.heps, hp, H, 0, T2, counts, ex, done, 1);
     return hipGetLastError();
   }
   const int64_t per_launch = (int64_t)65535 * kScoreHyps;  // grid.y limit
@@ -1501,453 +1382,6 @@ hipError_t launch_ransac_shard_key(const m3d_ransac_result* r, int64_t hyp0, int
 hipError_t launch_ransac_shard_pack(const m3d_ransac_result* r, int64_t hyp0, int64_t* buf,
                                     hipStream_t st) {
   ransac_shard_pack_kernel<<<1, 64, 0, st>>>(r, hyp0, buf);
-  return hipGetLastError();
-}
-
-
-// ------------------------------------------------------------------------------- tile culling
-// Round 4: exact culling of (32-hypothesis group, 32-row tile) blocks of the
-// a4 batches' MFMA screen.  The correspondence rows are sorted by the Morton key of (p_c, q_c), so
-// a 32-row tile is compact in both clouds; per tile the centre (c_p, c_q) — fp32 values, exact
-// reals — and ρ = max |p_c,i − c_p|, e = max |R0 (p_c,i − c_p) − (q_c,i − c_q)| with R0 the Kabsch
-// rotation of the whole set.  For a hypothesis (R, t′) every row of the tile then satisfies
-//   | |d_i| − |d_c| | ≤ ‖R − R0‖₂·ρ + e ≤ a·ρ + e,  a = ‖R − R0‖_F,  d_c = R c_p + t′ − c_q,
-// in real arithmetic.  The classifier screens the tile CENTRES with the same fp16-split MFMA
-// (|S d̃_c − S d_c| ≤ √3·E_d, hyp16_one's bound) and calls a (hypothesis, tile) decided when that
-// interval, widened by the fp32 rounding of the screen and a margin for numpy's fp64 evaluation of
-// every row, lies wholly on one side of the threshold; a (group, tile) block whose 32
-// hypotheses are all decided is skipped by the screen, its decided-inlier rows counted here.
-// Every count therefore equals the unculled screen's (exact fp64 semantics either way).  The
-// hypotheses of a batch are scored in the order of a (stable radix sort by a), so that a
-// 32-hypothesis group holds transforms alike — with random groups a block is almost never
-// decided for all 32 (tools/ransac_cull_sim.py: 0.3 % of the blocks at noise 0, 37 % sorted).
-constexpr int kCullSub = 32;   // rows per culling tile (one MFMA A block)
-constexpr int kCullSB = 8;     // 32-tile blocks per classifier wave
-
-__global__ __launch_bounds__(256) void cull_cov_kernel(const double* __restrict__ p64,
-                                                       const double* __restrict__ q64, int64_t nc,
-                                                       double cs0, double cs1, double cs2, double ct0,
-                                                       double ct1, double ct2, double* __restrict__ part) {
-  double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nc; i += (int64_t)gridDim.x * 256) {
-    const double p[3] = {p64[3 * i] - cs0, p64[3 * i + 1] - cs1, p64[3 * i + 2] - cs2};
-    const double q[3] = {q64[3 * i] - ct0, q64[3 * i + 1] - ct1, q64[3 * i + 2] - ct2};
-    for (int x = 0; x < 3; ++x)
-      for (int y = 0; y < 3; ++y) a[3 * x + y] += p[x] * q[y];
-  }
-  __shared__ double red[9][4];
-  for (int k = 0; k < 9; ++k) {
-    double v = a[k];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < 9) part[9 * blockIdx.x + threadIdx.x] = red[threadIdx.x][0] + red[threadIdx.x][1] +
-                                                              red[threadIdx.x][2] + red[threadIdx.x][3];
-}
-
-__device__ __forceinline__ uint64_t spread6(uint64_t v) {  // 10 bits → every 6th bit
-  uint64_t r = 0;
-  for (int b = 0; b < 10; ++b) r |= ((v >> b) & 1ull) << (6 * b);
-  return r;
-}
-
-__global__ __launch_bounds__(256) void cull_rowkey_kernel(const double* __restrict__ p64,
-                                                          const double* __restrict__ q64, int64_t nc,
-                                                          int64_t nc_pad, double cs0, double cs1,
-                                                          double cs2, double ct0, double ct1, double ct2,
-                                                          double pinf, double qinf,
-                                                          uint64_t* __restrict__ key, int32_t* __restrict__ val) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nc_pad) return;
-  uint64_t k = (1ull << 60) - 1;  // pads last
-  if (i < nc) {
-    const double x[6] = {p64[3 * i] - cs0, p64[3 * i + 1] - cs1, p64[3 * i + 2] - cs2,
-                         q64[3 * i] - ct0, q64[3 * i + 1] - ct1, q64[3 * i + 2] - ct2};
-    k = 0;
-    for (int c = 0; c < 6; ++c) {
-      const double m = c < 3 ? pinf : qinf;
-      double u = m > 0.0 ? (x[c] + m) / (2.0 * m) : 0.5;
-      u = fmin(fmax(u, 0.0), 1.0);
-      k |= spread6((uint64_t)(u * 1023.0)) << c;
-    }
-  }
-  key[i] = k;
-  val[i] = (int32_t)i;
-}
-
-struct R0Arg {
-  double r[9];
-};
-
-// one thread per tile: centre (fp32-rounded means: exact reals from here on), ρ and e in fp64 with
-// outward margins, the centre's MFMA operands (corr16's layout); tiles with a padding row (or
-// beyond the rows) get e = +inf: never decided
-__global__ __launch_bounds__(256) void cull_stats_kernel(const double* __restrict__ p64,
-                                                         const double* __restrict__ q64,
-                                                         const int32_t* __restrict__ rowmap, int64_t nc,
-                                                         int64_t nsub_pad, double cs0, double cs1, double cs2,
-                                                         double ct0, double ct1, double ct2, double S,
-                                                         double marg, R0Arg R0, uint4* __restrict__ cca16,
-                                                         float2* __restrict__ tstat) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= nsub_pad) return;
-  const double cs[3] = {cs0, cs1, cs2}, ct[3] = {ct0, ct1, ct2};
-  const int64_t i0 = j * kCullSub;
-  const bool full = i0 + kCullSub <= nc;
-  const _Float16 one = (_Float16)1.0f, zero = (_Float16)0.0f;
-  SH8 P, Q[3];
-  float2 st = make_float2(0.0f, INFINITY);
-  if (full) {
-    double mp[3] = {0, 0, 0}, mq[3] = {0, 0, 0};
-    for (int k = 0; k < kCullSub; ++k) {
-      const int64_t r = rowmap[i0 + k];
-      for (int c = 0; c < 3; ++c) {
-        mp[c] += p64[3 * r + c] - cs[c];
-        mq[c] += q64[3 * r + c] - ct[c];
-      }
-    }
-    double cp[3], cq[3];
-    for (int c = 0; c < 3; ++c) {
-      cp[c] = (double)(float)(mp[c] / kCullSub);
-      cq[c] = (double)(float)(mq[c] / kCullSub);
-    }
-    double rho = 0.0, e = 0.0;
-    for (int k = 0; k < kCullSub; ++k) {
-      const int64_t r = rowmap[i0 + k];
-      double dp[3], dq[3];
-      for (int c = 0; c < 3; ++c) {
-        dp[c] = (p64[3 * r + c] - cs[c]) - cp[c];
-        dq[c] = (q64[3 * r + c] - ct[c]) - cq[c];
-      }
-      rho = fmax(rho, sqrt(dp[0] * dp[0] + dp[1] * dp[1] + dp[2] * dp[2]));
-      double w2 = 0.0;
-      for (int c = 0; c < 3; ++c) {
-        const double w = R0.r[3 * c] * dp[0] + R0.r[3 * c + 1] * dp[1] + R0.r[3 * c + 2] * dp[2] - dq[c];
-        w2 += w * w;
-      }
-      e = fmax(e, sqrt(w2));
-    }
-    st = make_float2(__double2float_ru(S * rho * (1.0 + 1e-9) + 1e-30),
-                     __double2float_ru(S * (e * (1.0 + 1e-9) + marg) + 1e-30));
-    _Float16 h[3], l[3];
-    for (int c = 0; c < 3; ++c) split16d(S * cp[c], h[c], l[c]);
-    P.h = s_half8{h[0], l[0], h[0], h[1], l[1], h[1], h[2], l[2]};
-    for (int c = 0; c < 3; ++c) {
-      _Float16 qh, ql;
-      split16d(S * cq[c], qh, ql);
-      Q[c].h = s_half8{h[2], one, one, qh, ql, zero, zero, zero};
-    }
-  } else {
-    P.u = make_uint4(0, 0, 0, 0);
-    for (int c = 0; c < 3; ++c) Q[c].h = s_half8{zero, one, one, (_Float16)kPadQ, zero, zero, zero, zero};
-  }
-  cca16[j] = P.u;
-  for (int c = 0; c < 3; ++c) cca16[(1 + c) * nsub_pad + j] = Q[c].u;
-  tstat[j] = st;
-}
-
-// per hypothesis of the batch: a = ‖R − R0‖_F (rounded up; +inf non-finite), its sort key, and
-// the identity values; padding hypotheses sort last
-__global__ __launch_bounds__(256) void cull_akey_kernel(const double* __restrict__ T64, int64_t H, int64_t h_pad,
-                                                        R0Arg R0, float* __restrict__ a_out,
-                                                        uint32_t* __restrict__ key, int32_t* __restrict__ val) {
-  const int64_t h = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (h >= h_pad) return;
-  uint32_t k = 0xFFFFFFFFu;
-  if (h < H) {
-    double s2 = 0.0;
-    for (int x = 0; x < 3; ++x)
-      for (int y = 0; y < 3; ++y) {
-        const double d = T64[16 * h + 4 * x + y] - R0.r[3 * x + y];
-        s2 += d * d;
-      }
-    const double a = sqrt(s2) * (1.0 + 1e-12);
-    const float af = isfinite(a) ? __double2float_ru(a) : INFINITY;
-    a_out[h] = af;
-    k = __float_as_uint(af);  // a ≥ 0: the bits order as the values (+inf below the pads' key)
-  }
-  key[h] = k;
-  val[h] = (int32_t)h;
-}
-
-// the B operands of position j from hypothesis perm[j], with its E_d and a (0: far — decided
-// outlier everywhere by the screen values; +inf: not a rotation — never decided)
-__global__ __launch_bounds__(256) void hyp16_perm_kernel(const double* __restrict__ T64, int64_t H, int64_t h_pad,
-                                                         Mf16Params m, const int32_t* __restrict__ perm,
-                                                         const float* __restrict__ a_h,
-                                                         uint4* __restrict__ hb16, float* __restrict__ heps,
-                                                         float* __restrict__ apos, float* __restrict__ edpos) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= h_pad) return;
-  const int64_t h = perm[j];
-  const bool valid = h < H;
-  float ed = 0.0f;
-  hyp16_one(valid ? T64 + 16 * h : nullptr, valid, j, h_pad, m, hb16, heps, &ed);
-  edpos[j] = ed;
-  apos[j] = ed == 0.0f ? 0.0f : (isinf(ed) ? INFINITY : a_h[h]);
-}
-
-// grid: x = position groups / 8 (one 32-hypothesis group per wave), y = runs of kCullSB 32-tile
-// blocks.  The block's centre operands and tile bounds (kCullSB·32 tiles: 18 KB) are staged in LDS
-// once and read by its 8 waves.  Lane (c, half) holds position group·32 + c and tiles row(r, half)
-// of each 32-tile block.  X = |S d̃_c|² straight from the three MFMA outputs (positive terms: ≤ 3u
-// relative rounding, folded into the comparison constants).
-__global__ __launch_bounds__(512) void cull_classify_kernel(
-    const uint4* __restrict__ cca16, int64_t nsub_pad, const float2* __restrict__ tstat,
-    const uint4* __restrict__ hb16, int64_t h_pad, int64_t H, const float* __restrict__ apos,
-    const float* __restrict__ edpos, const int32_t* __restrict__ perm, float Sthr, float Smarg,
-    uint32_t* __restrict__ skip, int32_t* __restrict__ counts, const int32_t* __restrict__ done,
-    unsigned long long* __restrict__ cstats) {
-  // cstats (m3d_get_stats [4], [5]): (group, tile) blocks skipped / classified
-  if (done != nullptr && *done) return;
-  constexpr int kT = kCullSB * kCullSub;  // tiles staged per block
-  __shared__ uint4 sa[4][kT];
-  __shared__ float2 sst[kT];
-  const int64_t nwords = nsub_pad / kCullSub;
-  const int64_t t0 = (int64_t)blockIdx.y * kT;
-  const int64_t nt = min((int64_t)kT, nsub_pad - t0);
-  for (int e = threadIdx.x; e < 4 * kT; e += 512) {
-    const int pl = e / kT, k = e % kT;
-    if (k < nt) sa[pl][k] = cca16[pl * nsub_pad + t0 + k];
-  }
-  for (int k = threadIdx.x; k < nt; k += 512) sst[k] = tstat[t0 + k];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane & 31, h = lane >> 5;
-  const int64_t grp = (int64_t)blockIdx.x * 8 + wave;
-  if (grp * 32 >= h_pad) return;  // wave-uniform; no barrier below
-  const int64_t pos = grp * 32 + c;
-  SH8 t;
-  t.u = hb16[(3 * h + 0) * h_pad + pos];
-  const s_half8 bx = t.h;
-  t.u = hb16[(3 * h + 1) * h_pad + pos];
-  const s_half8 by = t.h;
-  t.u = hb16[(3 * h + 2) * h_pad + pos];
-  const s_half8 bz = t.h;
-  const float a = apos[pos];
-  const float ed3 = 1.7320508f * 1.01f * edpos[pos];
-  const float kout = Sthr + ed3 + Smarg, kin = Sthr - ed3 - Smarg;
-  constexpr float c_out = 1.0f + 1e-6f, c_in = 1.0f - 1e-6f;  // ≥ the 3u rounding of X, and of bo², bi²
-  const s_floatx16 zacc = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
-                           0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  const int pa = h == 0 ? 0 : 1;
-  int32_t inl = 0;  // rows of skipped tiles decided inlier for this lane's hypothesis
-  uint32_t nskip = 0, nblk = 0;
-  const int nwb = (int)((nt + kCullSub - 1) / kCullSub);
-  for (int q = 0; q < nwb; ++q) {
-    const int j = q * kCullSub + c;
-    SH8 ax, ay, az;
-    ax.u = sa[pa * 1][j];
-    ay.u = sa[pa * 2][j];
-    az.u = sa[pa * 3][j];
-    const s_floatx16 dx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax.h, bx, zacc, 0, 0, 0);
-    const s_floatx16 dy = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay.h, by, zacc, 0, 0, 0);
-    const s_floatx16 dz = __builtin_amdgcn_mfma_f32_32x32x16_f16(az.h, bz, zacc, 0, 0, 0);
-    // branch-free: the decisions as lane bits (no short-circuit control flow), the all-32
-    // tests on the wave masks in scalar registers
-    uint32_t dec = 0, inb = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float2 ts = sst[q * kCullSub + row];
-      const float X = fmaf(dx[r], dx[r], fmaf(dy[r], dy[r], dz[r] * dz[r]));  // S²|d̃_c|²
-      const float w = fmaf(a, ts.x, ts.y);                                   // S·(a·ρ + e)
-      const float bo = kout + w, bi = fmaxf(kin - w, 0.0f);  // bi ≤ 0: never inside (X ≥ 0)
-      const uint32_t o = X >= bo * bo * c_out ? 1u : 0u;
-      const uint32_t i_ = X * c_out < bi * bi * c_in ? 1u : 0u;
-      dec |= (o | i_) << r;
-      inb |= i_ << r;
-    }
-    uint32_t sk = 0;  // bit = tile of the block decided for all 32 hypotheses of the group
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint64_t bd = __ballot((dec >> r) & 1u);
-      const int row0 = (r & 3) + 8 * (r >> 2);
-      sk |= ((uint32_t)bd == 0xFFFFFFFFu ? 1u : 0u) << row0;
-      sk |= ((uint32_t)(bd >> 32) == 0xFFFFFFFFu ? 1u : 0u) << (row0 + 4);
-    }
-    if (lane == 0) skip[grp * nwords + blockIdx.y * kCullSB + q] = sk;
-    nskip += __builtin_popcount(sk);
-    nblk += kCullSub;
-    // this lane's tiles (rows row0 + 4h) that were skipped AND decided inlier for its hypothesis
-    uint32_t mine = 0;  // bit r: tile row(r, h) skipped
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mine |= ((sk >> ((r & 3) + 8 * (r >> 2) + 4 * h)) & 1u) << r;
-    inl += kCullSub * __builtin_popcount(mine & inb);
-  }
-  inl += __shfl_xor(inl, 32);
-  const int64_t hyp = perm[pos];
-  if (h == 0 && hyp < H && inl != 0) atomicAdd(&counts[hyp], inl);
-  if (lane == 0 && cstats != nullptr) {
-    atomicAdd(&cstats[0], (unsigned long long)nskip);
-    atomicAdd(&cstats[1], (unsigned long long)nblk);
-  }
-}
-
-// M3D_CULL_STATS=1 (diagnostics): the classifier counts skipped / classified blocks into
-// m3d_get_stats [4] / [5] — two same-address atomics per wave, which serialise at the memory side
-// (≈ 0.7 ms per 1e5-hypothesis batch), so off by default (read per call)
-static bool cull_stats_on() {
-  const char* e = getenv("M3D_CULL_STATS");
-  return e && atoi(e) == 1;
-}
-
-bool score_cull_on(const m3d_corrset* cs, double thr_sq) {
-  // opt-in (M3D_SCORE_CULL=1; read per call: the tests compare both forms in one process) —
-  // measured no faster than the plain screen at cfg2: the screen saves 18 % / 11 %
-  // of its time at Nc = 1e5 / 3e5 but the classification costs about as much
-  const char* e = getenv("M3D_SCORE_CULL");
-  if (!(e && atoi(e) == 1)) return false;
-  return cs->nc >= 4 * kSTile && cs->ca16 != nullptr && cs->s16 > 0.0 && cs->s16 * sqrt(thr_sq) <= 1024.0;
-}
-
-size_t cull_sort_bytes(int64_t h_pad) {
-  size_t b = 0;
-  uint32_t* k = nullptr;
-  int32_t* v = nullptr;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, k, k, v, v, (int)h_pad, 0, 32, (hipStream_t)0);
-  return std::max<size_t>(b, 1);
-}
-
-// the corrset's culling data, built once (synchronous: R0 from the host's 3×3 SVD; the first
-// culled run per corrset pays it)
-hipError_t ensure_cull(const m3d_corrset* cs, hipStream_t st) {
-  if (cs->cull_block != nullptr) return hipSuccess;
-  const int64_t nc = cs->nc, ncp = cs->nc_pad;
-  const int64_t nsub = ncp / kCullSub, nsub_pad = (nsub + kCullSub - 1) / kCullSub * kCullSub;
-  const int cov_blocks = 256;
-  hipError_t e = hipSuccess;
-  // temporaries: covariance partials, row keys / values, sort storage
-  size_t sb = 0;
-  {
-    uint64_t* k = nullptr;
-    int32_t* v = nullptr;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, sb, k, k, v, v, (int)ncp, 0, 60, st)) != hipSuccess) return e;
-  }
-  void* tb = nullptr;
-  size_t tbytes = 0;
-  double* part = nullptr;
-  uint64_t *k0 = nullptr, *k1 = nullptr;
-  int32_t* v0 = nullptr;
-  void* stmp = nullptr;
-  {
-    Carve cv;
-    cv.add(&part, 9 * (size_t)cov_blocks);
-    cv.add(&k0, (size_t)ncp);
-    cv.add(&k1, (size_t)ncp);
-    cv.add(&v0, (size_t)ncp);
-    cv.add(reinterpret_cast<char**>(&stmp), sb);
-    if ((e = cv.alloc(&tb, &tbytes)) != hipSuccess) return e;
-  }
-  void* blk = nullptr;
-  size_t bbytes = 0;
-  uint4 *cas16 = nullptr, *cca16 = nullptr;
-  int32_t* rowmap = nullptr;
-  float2* tstat = nullptr;
-  {
-    Carve cv;
-    cv.add(&cas16, 4 * (size_t)ncp);
-    cv.add(&rowmap, (size_t)ncp);
-    cv.add(&cca16, 4 * (size_t)nsub_pad);
-    cv.add(&tstat, (size_t)nsub_pad);
-    if ((e = cv.alloc(&blk, &bbytes)) != hipSuccess) {
-      block_release(tb);
-      return e;
-    }
-  }
-  R0Arg R0{};
-  cull_cov_kernel<<<cov_blocks, 256, 0, st>>>(cs->p64, cs->q64, nc, cs->cs[0], cs->cs[1], cs->cs[2], cs->ct[0],
-                                              cs->ct[1], cs->ct[2], part);
-  std::vector<double> hp(9 * (size_t)cov_blocks);
-  if ((e = hipGetLastError()) == hipSuccess)
-    e = hipMemcpyAsync(hp.data(), part, sizeof(double) * hp.size(), hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e == hipSuccess) {
-    double Hm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int b = 0; b < cov_blocks; ++b)
-      for (int k = 0; k < 9; ++k) Hm[k] += hp[9 * (size_t)b + k];
-    double R[9];
-    rotation_from_cov(Hm, R);  // linalg.h (host side): the Kabsch rotation of the whole set
-    bool ok = true;
-    for (int k = 0; k < 9; ++k) ok = ok && std::isfinite(R[k]);
-    for (int k = 0; k < 9; ++k) R0.r[k] = ok ? R[k] : (k % 4 == 0 ? 1.0 : 0.0);
-    cull_rowkey_kernel<<<blocks_for(ncp, 256), 256, 0, st>>>(cs->p64, cs->q64, nc, ncp, cs->cs[0], cs->cs[1],
-                                                             cs->cs[2], cs->ct[0], cs->ct[1], cs->ct[2], cs->pmax2,
-                                                             cs->qmaxinf, k0, v0);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(stmp, sb, k0, k1, v0, rowmap, (int)ncp, 0, 60, st);
-  if (e == hipSuccess) {
-    corr16_kernel<<<blocks_for(ncp, 256), 256, 0, st>>>(cs->p64, cs->q64, nc, ncp, cs->cs[0], cs->cs[1], cs->cs[2],
-                                                        cs->ct[0], cs->ct[1], cs->ct[2], cs->s16, cas16, rowmap);
-    const double marg = 1e-12 * (1.0 + cs->pmax2 + cs->qmaxinf);
-    cull_stats_kernel<<<blocks_for(nsub_pad, 256), 256, 0, st>>>(cs->p64, cs->q64, rowmap, nc, nsub_pad, cs->cs[0],
-                                                                 cs->cs[1], cs->cs[2], cs->ct[0], cs->ct[1],
-                                                                 cs->ct[2], cs->s16, marg, R0, cca16, tstat);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  block_release(tb);
-  if (e != hipSuccess) {
-    block_release(blk);
-    return e;
-  }
-  cs->cull_block = blk;
-  cs->cas16 = cas16;
-  cs->rowmap = rowmap;
-  cs->cca16 = cca16;
-  cs->tstat = tstat;
-  for (int k = 0; k < 9; ++k) cs->R0h[k] = R0.r[k];
-  cs->nsub = nsub;
-  cs->nsub_pad = nsub_pad;
-  return hipSuccess;
-}
-
-hipError_t launch_score_culled(const m3d_corrset* cs, const double* T64, int64_t H, double thr, int mode,
-                               int32_t* counts, int64_t* stats, const int32_t* done, const ScoreMf& mf,
-                               const ScoreCull& cc, hipStream_t st) {
-  if (H == 0 || cs->nc == 0) return hipSuccess;
-  Mf16Params m;
-  int64_t hp = 0;
-  if (!score_prep_params(cs, H, thr, mode, mf, &m, &hp)) return hipErrorInvalidValue;
-  const double thr_sq = m.thr_sq;
-  R0Arg R0{};
-  for (int k = 0; k < 9; ++k) R0.r[k] = cs->R0h[k];
-  cull_akey_kernel<<<blocks_for(hp, 256), 256, 0, st>>>(T64, H, hp, R0, cc.a, cc.key, cc.val);
-  hipError_t e = hipGetLastError();
-  size_t sb = cc.sort_bytes;
-  if (e == hipSuccess)
-    e = hipcub::DeviceRadixSort::SortPairs(cc.sort_tmp, sb, cc.key, cc.key2, cc.val, cc.perm, (int)hp, 0, 32, st);
-  if (e != hipSuccess) return e;
-  hyp16_perm_kernel<<<blocks_for(hp, 256), 256, 0, st>>>(T64, H, hp, m, cc.perm, cc.a, mf.hb16, mf.heps, cc.apos,
-                                                         cc.edpos);
-  const double S = cs->s16, thr_d = sqrt(thr_sq);
-  const float T2 = (float)(S * S * thr_sq);
-  const float Sthr = (float)(S * thr_d);
-  // numpy's fp64 evaluation of a row vs the real value, the fp32 roundings of S·thr and of the
-  // bound arithmetic: generous absolute + relative terms
-  const float Smarg = (float)(S * (1e-12 * (1.0 + cs->pmax2 + cs->qmaxinf) + 1e-9 * thr_d) + 1e-6 * S * thr_d);
-  const int64_t nwords = cs->nsub_pad / kCullSub;
-  const dim3 cg((unsigned)((hp / 32 + 7) / 8), (unsigned)((nwords + kCullSB - 1) / kCullSB));
-  cull_classify_kernel<<<cg, 512, 0, st>>>(cs->cca16, cs->nsub_pad, cs->tstat, mf.hb16, hp, H, cc.apos, cc.edpos,
-                                           cc.perm, Sthr, Smarg, cc.skip, counts, done,
-                                           (stats != nullptr && cull_stats_on()) ? reinterpret_cast<unsigned long long*>(stats + 4)
-                                                                                 : nullptr);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  ExactArgs ex{T64, cs->p64, cs->q64, cs->nc, thr, mode, stats, cs->rowmap};
-  const int64_t bx = hp / shyps<kSMGDefault>();
-  const int64_t sy = score_grid_y(cs, bx);
-  // the plain (x, y) dispatch order: consecutive blocks take consecutive hypothesis blocks, so the
-  // sorted batch's light (mostly decided) and heavy blocks are dealt over all 8 XCDs alike — the
-  // XCD-contiguous order would give whole XCDs only heavy blocks (M3D_SCORE_CULL_XCD=1: A/B)
-  static const int xcd = [] {
-    const char* en = getenv("M3D_SCORE_CULL_XCD");
-    return (en && atoi(en) == 1) ? 1 : 0;
-  }();
-  score_mfma_kernel<kSMGDefault, true><<<dim3((unsigned)bx, (unsigned)sy), kSBlock, 0, st>>>(
-      cs->cas16, cs->nc_pad, mf.hb16, mf.heps, hp, H, 0, T2, counts, ex, done, 1.0f, xcd, cc.perm, cc.skip,
-      nwords);
   return hipGetLastError();
 }
 

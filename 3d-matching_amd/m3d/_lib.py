@@ -24,7 +24,7 @@ HYP_OK, HYP_DEGENERATE, HYP_NONFINITE = 0, 1, 2
 SCORE_SQUARED, SCORE_NORM = 0, 1
 EST_POINT_TO_POINT, EST_POINT_TO_PLANE = 0, 1
 KERNEL_NN, KERNEL_SCORE, KERNEL_KABSCH, KERNEL_TERMS, KERNEL_LOOP, KERNEL_COMM = 0, 1, 2, 3, 4, 5
-ICP_NO_PERSIST, ICP_NO_SPLIT, ICP_PERSIST = 1, 2, 4
+ICP_NO_SPLIT = 2
 NN_BRUTE, NN_GRID = 0, 1
 COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2

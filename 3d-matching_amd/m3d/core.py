@@ -398,10 +398,6 @@ def _nn_method(nn: str) -> int:
         raise ValueError(f"nn must be one of {sorted(_lib.NN_METHODS)}, got {nn!r}") from None
 
 
-def _persist_flags(persist) -> int:
-    return 0 if persist is None else (_lib.ICP_PERSIST if persist else _lib.ICP_NO_PERSIST)
-
-
 def nn1(src: Cloud, tgt: Cloud, T, max_dist: float, nn: str = "grid"):
     """Radius-bounded 1-NN of T·src in tgt → (idx int32 (-1 none), d2 f64) torch cuda.
 
@@ -439,12 +435,11 @@ def corr_pairs(ctx: Context, corr, n: int) -> np.ndarray:
 
 def icp(src: Cloud, tgt: Cloud, max_dist: float, init=None, estimation=_lib.EST_POINT_TO_PLANE,
         relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30, with_correspondences=True,
-        nn: str = "grid", persist=None):
-    """registration_icp on the device (m3d_icp_run).  persist: True / False force the grid NN's
-    one-launch persistent loop / its two-launch loop (the same bits), None = library default."""
+        nn: str = "grid"):
+    """registration_icp on the device (m3d_icp_run)."""
     torch = _torch()
     p = _lib.IcpParams(float(relative_fitness), float(relative_rmse), int(max_iteration), int(estimation),
-                       _nn_method(nn), _persist_flags(persist))
+                       _nn_method(nn), 0)
     res = _lib.IcpResult()
     corr = torch.empty((max(src.n, 1),), dtype=torch.int32, device="cuda") if with_correspondences else None
     init16 = _T16(np.eye(4) if init is None else init)
@@ -460,13 +455,12 @@ class IcpLoop:
 
     def __init__(self, src: Cloud, tgt: Cloud, max_dist: float, estimation=_lib.EST_POINT_TO_PLANE,
                  relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30, nn: str = "brute",
-                 persist=None, split: bool = True):
-        """persist: True / False force the grid loop's steps as one persistent launch / as two
-        launches each (None: library default); split=False: the target-shard loop exchanges its
-        keys in one piece (no overlap with the second half's NN)."""
+                 split: bool = True):
+        """split=False: the target-shard loop exchanges its keys in one piece (no overlap with
+        the second half's NN)."""
         self.ctx = src.ctx
         self.src, self.tgt = src, tgt
-        flags = _persist_flags(persist) | (0 if split else _lib.ICP_NO_SPLIT)
+        flags = 0 if split else _lib.ICP_NO_SPLIT
         self.p = _lib.IcpParams(float(relative_fitness), float(relative_rmse), int(max_iteration),
                                 int(estimation), _nn_method(nn), flags)
         h = C.c_void_p()
@@ -488,9 +482,8 @@ class IcpLoop:
         self.ctx.check(self.ctx.lib.m3d_icp_step(self.h, stream_handle()), "icp_step")
 
     def steps(self, n: int):
-        """n iterations enqueued by the library in one call (m3d_icp_steps): the single-device
-        grid loop as ONE persistent launch, else the steps (a sequence requested again is replayed
-        from a captured HIP graph)."""
+        """n iterations enqueued by the library in one call (m3d_icp_steps; a sequence requested
+        again is replayed from a captured HIP graph)."""
         self.ctx.check(self.ctx.lib.m3d_icp_steps(self.h, int(n), stream_handle()), "icp_steps")
 
     def prepare_steps(self, n: int):

@@ -363,7 +363,7 @@ def main():
         tgt_c = (Cloud(tgt_all, nrm_all) if not multi else
                  Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0)))
     src_c = Cloud(src)
-    K_NN, K_TERMS, K_COMM, K_LOOP = _lib.KERNEL_NN, _lib.KERNEL_TERMS, _lib.KERNEL_COMM, _lib.KERNEL_LOOP
+    K_NN, K_TERMS, K_COMM = _lib.KERNEL_NN, _lib.KERNEL_TERMS, _lib.KERNEL_COMM
 
     def split_times(prof, el_ev, evals):
         """Per evaluation (one NN + terms + exchange), from the events pass: the NN, terms and
@@ -378,20 +378,16 @@ def main():
                 "exchange_note": ("library RCCL all-reduces timed by events on their streams"
                                   if comm_name == "libm3d-rccl" else "exchange not issued by the library")}
 
-    def bench_icp(nn, persist=None):
-        loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters, nn=nn,
-                       persist=persist)
+    def bench_icp(nn):
+        loop = IcpLoop(src_c, tgt_c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=iters, nn=nn)
         if mode1 == "source":
             loop.set_source_total(ns * world)
         run = icp_runner(loop, iters, mode1, off, ns * world)
         for _ in range(args.warmup):
             run()
         torch.cuda.synchronize()
-        el, el_ev, prof = timed(run, args.steps, (K_NN, K_TERMS, K_LOOP))
+        el, el_ev, prof = timed(run, args.steps, (K_NN, K_TERMS))
         (nn_ms, nn_n), (t_ms, t_n) = prof[K_NN], prof[K_TERMS]
-        if persist:  # one persistent launch per step: per-evaluation time of that launch
-            lp_ms, lp_n = prof[K_LOOP]
-            return el, el_ev, max_over_ranks(lp_ms / max(lp_n, 1) / (iters + 1)), lp_n, None, loop.result()
         return el, el_ev, max_over_ranks(nn_ms / max(nn_n, 1)), nn_n, t_ms / max(t_n, 1), loop.result()
 
     el, el_ev, nn_avg_ms, nn_n, terms_avg_ms, res = bench_icp("brute")
@@ -417,22 +413,7 @@ def main():
         IcpLoop(src_c, tgt_c, r, max_iteration=0, nn="grid")  # builds both clouds' grids once
         torch.cuda.synchronize()
         build_ms = (time.perf_counter() - tg0) * 1e3
-        gel, gel_ev, g_ms, g_n, g_terms_ms, gres = bench_icp("grid", persist=False)
-        # the same loop as ONE persistent launch per step (icp.hip icp_grid_persist_kernel; the
-        # same bits), single device only
-        persist = None
-        if not multi:
-            pel, pel_ev, p_ms, p_n, _, pres = bench_icp("grid", persist=True)
-            p_bytes = 28 * ns + 16 * nt + 84 * ns  # the scan's bytes + the terms' 84 B per source
-            persist = {"value": iters * args.steps / pel, "ms_per_step": pel / args.steps * 1e3,
-                       "same_result_as_two_launch": bool(np.array_equal(pres.transformation, gres.transformation)
-                                                          and pres.fitness == gres.fitness),
-                       "per_evaluation_ms": p_ms,
-                       "roofline": {"bound": "hbm", "kernel": "icp_grid_persist_kernel",
-                                    "achieved": p_bytes / (p_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                                    "unit": "GB/s", "frac": p_bytes / (p_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                    "bytes_per_evaluation": p_bytes,
-                                    "note": "algorithmic bytes of one scan + terms pass per evaluation"}}
+        gel, gel_ev, g_ms, g_n, g_terms_ms, gres = bench_icp("grid")
         g_bytes = 28 * ns + 16 * nt
         g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
         icp_grid = {
@@ -446,7 +427,6 @@ def main():
                          "traffic": pmc_traffic("grid_nn")[0], "avg_launch_ms": g_ms,
                          "launches": g_n, "bytes_per_launch": g_bytes,
                          "terms_avg_launch_ms": g_terms_ms},
-            "persistent": persist,
         }
 
     # ------------------------------------------------------------------ cfg1 strong scaling
@@ -667,49 +647,6 @@ def main():
                          "mfma_issue_frac": SCORE_MFMA_FLOP_PER_PAIR * pairs3 / (sc3_avg * 1e-3) / 1e12
                          / MFMA_F16_PEAK_TF},
         }
-        # the tile-culled screen (ransac.hip cull_classify_kernel; library opt-in M3D_SCORE_CULL=1,
-        # DESIGN.md §3.2d) on both cfg2 workloads, beside the plain screen above: same winner, the
-        # share of (32-hypothesis group, 32-row tile) blocks it skipped (one extra run with the
-        # classifier's counters on), and its rate on the pairs it actually screened
-        culled = None
-        if not multi:
-            culled = {}
-            for key, cset, pp, base in (("nc1e5", cs, params, (rel, out)), ("nc3e5", cs3, p3, (rel3, out3))):
-                os.environ["M3D_SCORE_CULL"] = "1"
-                rb = torch.zeros(RESULT_WORDS, dtype=torch.int64, device=dev)
-                try:
-                    for _ in range(3):
-                        cset.run_async(pp, rb)
-                    torch.cuda.synchronize()
-                    relc, _, profc = timed(lambda: cset.run_async(pp, rb), args.ransac_steps, (K_SC,))
-                    oc = RansacOutcome.from_device(rb, cset.nc)
-                    os.environ["M3D_CULL_STATS"] = "1"
-                    s0 = ctx.stats()
-                    cset.run_async(pp, rb)
-                    torch.cuda.synchronize()
-                    s1 = ctx.stats()
-                finally:
-                    os.environ.pop("M3D_SCORE_CULL", None)
-                    os.environ.pop("M3D_CULL_STATS", None)
-                skip = float((s1[4] - s0[4]) / max(s1[5] - s0[5], 1))
-                sc_ms = profc[K_SC][0] / max(profc[K_SC][1], 1)
-                scr_pairs = cset.nc * H * (1.0 - skip)  # per run (one launch sequence per batch)
-                culled[key] = {
-                    "value": H * args.ransac_steps / relc, "unit": "hyp/s",
-                    "ms_per_run": relc / args.ransac_steps * 1e3,
-                    "plain_ms_per_run": base[0] / args.ransac_steps * 1e3,
-                    "same_winner_as_plain": bool(oc.best_index == base[1].best_index
-                                                 and oc.best_count == base[1].best_count),
-                    "blocks_skipped_frac": skip,
-                    "roofline": {"bound": "mfma", "kernel": "cull_classify_kernel + score_mfma_kernel<2, true>",
-                                 "achieved": SCORE_FLOP_PER_PAIR * scr_pairs / (sc_ms * 1e-3 * profc[K_SC][1] / args.ransac_steps) / 1e12,
-                                 "peak": MFMA_F16_PEAK_TF, "unit": "TFLOP/s",
-                                 "basis": "27 flop per (hypothesis, correspondence) pair actually screened",
-                                 "pairs_screened_per_run": scr_pairs,
-                                 "score_ms_per_launch": sc_ms},
-                    "note": "opt-in (M3D_SCORE_CULL=1): not the library default, measured no faster end to end",
-                }
-                culled[key]["roofline"]["frac"] = culled[key]["roofline"]["achieved"] / MFMA_F16_PEAK_TF
         del cs3
         ransac = {
             "metric": "RANSAC hypotheses/sec (cfg2: Nc=1e5, a1+a2, no early stop)",
@@ -729,7 +666,6 @@ def main():
             "kabsch_avg_launch_ms": kb_ms / max(kb_n, 1),
             "strong": ransac_strong,
             "nc3e5": ransac_nc3e5,
-            "culled": culled,
         }
 
     # ------------------------------------------------------------------ drop-in per-call path

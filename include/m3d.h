@@ -69,9 +69,8 @@ int m3d_device_count(int* count);
 int m3d_create(int device, m3d_ctx** out);
 void m3d_destroy(m3d_ctx* ctx);
 const char* m3d_last_error(const m3d_ctx* ctx);
-/* Device-side hit counters (cumulative): [0] pairs rechecked by chunk, [1] by full hypothesis;
- * [4] / [5] (group, tile) blocks skipped / classified by the a4 batches' tile culling (counted only
- * with M3D_CULL_STATS=1; the culling itself is opt-in, M3D_SCORE_CULL=1 — exact, same counts). */
+/* Device-side hit counters (cumulative): [0] pairs rechecked in fp64 by the scoring screens
+ * (guard band), [1] by full hypothesis; the others are reserved (0). */
 int m3d_get_stats(m3d_ctx* ctx, int64_t* out8 /* [host] 8 values */);
 
 /* Kernel timing with HIP events recorded on the launch stream immediately before and after each
@@ -80,7 +79,7 @@ int m3d_get_stats(m3d_ctx* ctx, int64_t* out8 /* [host] 8 values */);
 #define M3D_KERNEL_SCORE 1  /* RANSAC fp32 scoring screen       */
 #define M3D_KERNEL_KABSCH 2 /* RANSAC batched 3-point Kabsch    */
 #define M3D_KERNEL_TERMS 3  /* ICP fp64 estimation terms        */
-#define M3D_KERNEL_LOOP 4   /* ICP persistent grid loop: one launch for n steps (ABI 10) */
+#define M3D_KERNEL_LOOP 4   /* reserved (ABI 10-11: the persistent grid loop, removed in ABI 12) */
 #define M3D_KERNEL_COMM 5   /* RCCL all-reduces issued by the library, on their streams (ABI 10) */
 int m3d_profile_enable(m3d_ctx* ctx, int enable);
 /* Synchronises, returns Σ launch durations (ms) and launch count since the last read, resets. */
@@ -218,9 +217,8 @@ typedef struct {
   int32_t nn_method;       /* M3D_NN_* */
   int32_t flags;           /* M3D_ICP_* (ABI 10; 0 = defaults) */
 } m3d_icp_params;
-/* m3d_icp_params.flags: the grid loop's steps as ONE persistent launch (M3D_ICP_PERSIST) or as
- * two launches per step (M3D_ICP_NO_PERSIST); neither: the library default.  The persistent loop
- * applies to a single device, grid NN, ≤ 248 tiles of 512 sources; both give the same bits. */
+/* m3d_icp_params.flags 1 and 4 (ABI 10-11: the persistent grid loop on / off) are accepted and
+ * ignored since ABI 12, which removed that loop (measured slower than the two-launch steps). */
 #define M3D_ICP_NO_PERSIST 1
 #define M3D_ICP_PERSIST 4
 /* m3d_icp_params.flags: the target-shard loop exchanges all keys in one MIN instead of two halves

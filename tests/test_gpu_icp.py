@@ -192,53 +192,6 @@ def test_morton_copies_stay_bounded_per_cloud():
         check_nn(src, tgt, T, r, idx.cpu().numpy(), d2.cpu().numpy())
 
 
-@pytest.mark.parametrize("ns,est,crit", [(1, "plane", "fixed"), (511, "plane", "fixed"), (513, "point", "fixed"),
-                                         (20000, "plane", "open3d"), (100_000, "plane", "fixed"),
-                                         (100_000, "point", "open3d"), (126_000, "plane", "fixed"),
-                                         (140_000, "plane", "fixed")])
-def test_persistent_grid_loop_matches_two_launch_loop(ns, est, crit):
-    """The single-device grid loop as ONE persistent launch (icp.hip icp_grid_persist_kernel: every
-    workgroup reduces all tile partials and solves on its own copy of the state) computes the same
-    bits as the two-launch loop (grid scan + fused terms/solve per step): transform, fitness, rmse,
-    iterations, convergence and every correspondence — ragged tile counts, both estimations,
-    fixed iteration counts and Open3D's convergence test (an exit inside the launch), a second
-    launch continuing from the first one's state, and the one-shot m3d_icp_run path."""
-    src, tgt, nrm, _ = synth.icp_pair(max(ns, 2), 100_000, seed=23)
-    src = src[:ns]
-    e = _lib.EST_POINT_TO_PLANE if est == "plane" else _lib.EST_POINT_TO_POINT
-    s, t = Cloud(src), Cloud(tgt, nrm if e == _lib.EST_POINT_TO_PLANE else None)
-    kw = dict(estimation=e, max_iteration=40, nn="grid")
-    if crit == "fixed":
-        kw.update(relative_fitness=-1, relative_rmse=-1)
-    a = IcpLoop(s, t, 0.12, persist=True, **kw)
-    b = IcpLoop(s, t, 0.12, persist=False, **kw)
-
-    def state(lp):
-        r = lp.result()
-        return (r.transformation, r.fitness, r.inlier_rmse, r.iterations, r.converged,
-                lp.correspondences().cpu().numpy())
-
-    for lp in (a, b):
-        lp.reset(np.eye(4))
-        lp.steps(17)
-    x, y = state(a), state(b)
-    np.testing.assert_array_equal(x[0], y[0])
-    assert x[1:5] == y[1:5]
-    np.testing.assert_array_equal(x[5], y[5])
-    for lp in (a, b):  # continue from the state the first launch left
-        lp.steps(30)
-    x, y = state(a), state(b)
-    np.testing.assert_array_equal(x[0], y[0])
-    assert x[1:5] == y[1:5]
-    np.testing.assert_array_equal(x[5], y[5])
-    one = icp(s, t, 0.12, np.eye(4), persist=True, **kw)
-    two = icp(s, t, 0.12, np.eye(4), persist=False, **kw)
-    np.testing.assert_array_equal(one.transformation, two.transformation)
-    assert (one.fitness, one.inlier_rmse, one.iterations, one.converged) == \
-        (two.fitness, two.inlier_rmse, two.iterations, two.converged)
-    np.testing.assert_array_equal(one.correspondence_set, two.correspondence_set)
-
-
 def test_no_overlap_gives_identity_and_zero_fitness():
     src, _ = synth.surface_points(2000, seed=1)
     tgt, nrm = synth.surface_points(2000, seed=2)
@@ -277,9 +230,9 @@ def test_run_chunks_match_stepped_loop(nn, max_iteration):
     s, t = Cloud(src), Cloud(tgt, nrm)
     for crit in ((1e-6, 1e-6), (-1.0, -1.0)):
         full = icp(s, t, 0.12, np.eye(4), relative_fitness=crit[0], relative_rmse=crit[1],
-                   max_iteration=max_iteration, nn=nn, persist=False)
+                   max_iteration=max_iteration, nn=nn)
         loop = IcpLoop(s, t, 0.12, relative_fitness=crit[0], relative_rmse=crit[1],
-                       max_iteration=max_iteration, nn=nn, persist=False)
+                       max_iteration=max_iteration, nn=nn)
         loop.reset(np.eye(4))
         for _ in range(max_iteration + 1):
             loop.step()
@@ -345,9 +298,7 @@ def test_graph_replay_matches_enqueued_steps(nn):
 
     src, tgt, nrm, _ = synth.icp_pair(30000, seed=13)
     s, t = Cloud(src), Cloud(tgt, nrm)
-    # persist=False: the grid loop's n steps would otherwise run as one persistent launch
-    # (test_persistent_grid_loop_matches_two_launch_loop), not as a captured graph
-    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=80, nn=nn, persist=False)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=80, nn=nn)
     a = IcpLoop(s, t, 0.12, **kw)
     b = IcpLoop(s, t, 0.12, **kw)
 
@@ -646,40 +597,6 @@ print(json.dumps(out))
     assert res["1"]["brute"] == res["1"]["grid"]
 
 
-@pytest.mark.parametrize("mode", ["stage", "register"])
-def test_host_upload_modes_give_the_same_cloud(mode):
-    """The alternative host uploads of m3d_cloud_create_host (M3D_UPLOAD=stage: pinned staging
-    filled by the host pool, 1 MB chunks and rounds past the 64 MB cap; register: page-locked in
-    place) build the cloud the default pageable copy builds — the same NN bits (one subprocess each:
-    the mode is read once per process)."""
-    import os
-    import subprocess
-    import sys
-    from pathlib import Path
-
-    code = r'''
-import sys
-sys.path[:0] = [sys.argv[1]]
-import numpy as np, torch
-from m3d.core import Cloud, nn1
-rng = np.random.default_rng(9)
-for n in (1, 70_000, 3_000_000):
-    pts = rng.normal(size=(n, 3)) * 3.0
-    nrm = rng.normal(size=(n, 3))
-    a = Cloud(pts, nrm)
-    b = Cloud(torch.from_numpy(pts).cuda(), torch.from_numpy(nrm).cuda())
-    q = Cloud(pts[: min(n, 5000)] + 0.01)
-    i1, d1 = nn1(q, a, np.eye(4), 0.05, nn="grid")
-    i2, d2 = nn1(q, b, np.eye(4), 0.05, nn="grid")
-    assert np.array_equal(i1.cpu().numpy(), i2.cpu().numpy()) and np.array_equal(d1.cpu().numpy(), d2.cpu().numpy()), n
-print("ok")
-'''
-    env = dict(os.environ, M3D_UPLOAD=mode)
-    pkg = str(Path(__file__).resolve().parents[1] / "3d-matching_amd")
-    r = subprocess.run([sys.executable, "-c", code, pkg], env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
-
-
 def test_deferred_dense_queries_give_the_same_bits():
     """grid_nn_heavy_kernel (one block per query with more than the candidate cap, and every
     ambiguous query decided in fp64) gives the per-query scan + terms pass's bits:
@@ -707,13 +624,24 @@ src = np.vstack([src, tgt[11] + rng.normal(scale=0.05, size=(3000, 3))])
 s, t = Cloud(src), Cloud(tgt, nrm)
 out = {}
 for nn in ("brute", "grid"):
-    lp = IcpLoop(s, t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=40, nn=nn, persist=False)
+    lp = IcpLoop(s, t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=40, nn=nn)
     lp.reset(synth.random_rigid(3, rot_range=0.03, trans_range=0.05))
     for _ in range(41):  # back to back, no host sync: each launch must start from an empty list
         lp.step()
     r = lp.result()
     c = lp.correspondences().cpu().numpy()
     out[nn] = [r.transformation.tolist(), r.fitness, r.inlier_rmse, r.iterations, int(c.sum()), int((c >= 0).sum())]
+    # the same 41 steps as captured HIP graphs: a sequence requested twice is captured, then
+    # replayed (api.cpp capture_steps) — the deferral list is used inside the graph too
+    g = IcpLoop(s, t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=40, nn=nn)
+    for _ in range(3):
+        g.reset(synth.random_rigid(3, rot_range=0.03, trans_range=0.05))
+        for _ in range(4):
+            g.steps(10)
+        g.step()
+    r = g.result()
+    c = g.correspondences().cpu().numpy()
+    out[nn + "_graph"] = [r.transformation.tolist(), r.fitness, r.inlier_rmse, r.iterations, int(c.sum()), int((c >= 0).sum())]
 i, d = nn1(Cloud(src), t, np.eye(4), 0.12, nn="grid")
 out["nn1"] = [int(i.sum().item()), float(d.sum().item())]
 print(json.dumps(out))
@@ -730,4 +658,4 @@ print(json.dumps(out))
         assert r.returncode == 0, r.stderr[-2000:]
         res[mode] = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["0"] == res["8"] == res[None]
-    assert res[None]["brute"] == res[None]["grid"]
+    assert res[None]["brute"] == res[None]["grid"] == res[None]["brute_graph"] == res[None]["grid_graph"]

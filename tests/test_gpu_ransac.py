@@ -463,52 +463,32 @@ def test_gui_loop_early_stop_at_baseline_scale(golden, cfg2, key):
 
 
 def test_fused_hyp16_equals_separate_launch():
-    """kabsch3 writes the MFMA screen's per-hypothesis operands itself for a4 batches
-    (M3D_RANSAC_FUSE, latched per process): a subprocess with FUSE=0 (separate hyp16 launch) and one
-    with FUSE=1 give identical counts, at a ragged H whose padding hypotheses are exercised."""
-    import json
-    import os
-    import subprocess
-    import sys
-    from pathlib import Path
+    """For a4 batches kabsch3 writes the MFMA screen's per-hypothesis operands itself (ScoreFuse);
+    m3d_ransac_score builds them in a separate hyp16 launch.  Both give identical counts for the
+    same native hypotheses, at a ragged H whose padding hypotheses are exercised, both comparators,
+    several batch sizes."""
+    import ctypes
 
-    code = r'''
-import json, sys
-import numpy as np
-sys.path[:0] = [sys.argv[1]]
-import torch
-import ctypes
-from m3d import _lib, synth
-from m3d.core import CorrSet, RansacParams, ptr, stream_handle
-src, tgt, corr, _ = synth.ransac_pair(30011, seed=12, noise_ratio=1.5)
-cs = CorrSet(src, tgt, corr)
-H = 2049 + 30
-counts = torch.zeros(H, dtype=torch.int32, device="cuda")
-buf = torch.zeros(64, dtype=torch.int64, device="cuda")
-out = {}
-for mode, thr in ((_lib.SCORE_NORM, 0.45), (_lib.SCORE_SQUARED, 0.45 * 0.45)):
-    p = RansacParams(max_iter=H, seed=5, thr=thr, mode=mode, early_stop=False, batch=1000)
-    cs.ctx.check(cs.ctx.lib.m3d_ransac_run_async(cs.ctx.h, cs.h, ctypes.byref(p.to_c()), None, ptr(counts), ptr(buf),
-                                                 stream_handle()), "run")
-    out[str(mode)] = counts.cpu().numpy().tolist()
-print(json.dumps(out))
-'''
-    pkg = str(Path(__file__).resolve().parents[1] / "3d-matching_amd")
-    res = {}
-    for fuse in ("0", "1"):
-        env = dict(os.environ, M3D_RANSAC_FUSE=fuse)
-        r = subprocess.run([sys.executable, "-c", code, pkg], env=env, capture_output=True, text=True,
-                           timeout=120)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res[fuse] = json.loads(r.stdout.strip().splitlines()[-1])
-    assert res["0"] == res["1"]
-    from m3d import synth
+    import torch
+
+    from m3d.core import ptr, stream_handle
 
     src, tgt, corr, _ = synth.ransac_pair(30011, seed=12, noise_ratio=1.5)
-    T, _ = CorrSet(src, tgt, corr).kabsch3(2079, seed=5)
-    pick = np.arange(0, 2079, 97)
+    cs = CorrSet(src, tgt, corr)
+    H = 2049 + 30
+    T, _ = cs.kabsch3(H, seed=5)
+    counts = torch.zeros(H, dtype=torch.int32, device="cuda")
+    buf = torch.zeros(64, dtype=torch.int64, device="cuda")
+    for mode, thr in ((_lib.SCORE_NORM, 0.45), (_lib.SCORE_SQUARED, 0.45 * 0.45)):
+        sep = cs.score(T, thr, mode).cpu().numpy()
+        for batch in (1000, 0):
+            p = RansacParams(max_iter=H, seed=5, thr=thr, mode=mode, early_stop=False, batch=batch)
+            cs.ctx.check(cs.ctx.lib.m3d_ransac_run_async(cs.ctx.h, cs.h, ctypes.byref(p.to_c()), None, ptr(counts),
+                                                         ptr(buf), stream_handle()), "run")
+            np.testing.assert_array_equal(counts.cpu().numpy(), sep)
+    pick = np.arange(0, H, 97)
     pp, qq = src[corr[:, 0]], tgt[corr[:, 1]]
-    np.testing.assert_array_equal(np.array(res["1"][str(_lib.SCORE_NORM)])[pick],
+    np.testing.assert_array_equal(cs.score(T, 0.45, _lib.SCORE_NORM).cpu().numpy()[pick],
                                   O.inlier_counts(pp, qq, T.cpu().numpy()[pick], 0.45, 1))
 
 
@@ -642,77 +622,3 @@ def test_drop_in_sees_in_place_mutation_between_calls():
     idx = ref_rng.choice(len(corr), 3, replace=False)
     T_ref, _ = O.kabsch3(sp[corr[idx, 0]], tp[corr[idx, 1]])
     np.testing.assert_allclose(r.transformation, T_ref, atol=1e-9)
-
-
-def _run_counts(cs, H, thr, mode, cull, seed=42, early_stop=False):
-    """One a4 run of H native hypotheses with the tile culling on or off (M3D_SCORE_CULL, read per
-    call): per-hypothesis counts and the outcome."""
-    import ctypes
-    import os
-
-    import torch
-
-    from m3d.core import RESULT_WORDS, RansacOutcome, ptr, stream_handle
-
-    old = os.environ.get("M3D_SCORE_CULL")
-    os.environ["M3D_SCORE_CULL"] = "1" if cull else "0"
-    try:
-        counts = torch.zeros(H, dtype=torch.int32, device="cuda")
-        buf = torch.zeros(RESULT_WORDS, dtype=torch.int64, device="cuda")
-        p = RansacParams(max_iter=H, seed=seed, thr=thr, mode=mode, early_stop=early_stop)
-        cs.ctx.check(cs.ctx.lib.m3d_ransac_run_async(cs.ctx.h, cs.h, ctypes.byref(p.to_c()), None,
-                                                     ptr(counts), ptr(buf), stream_handle()), "run_async")
-        return counts.cpu().numpy(), RansacOutcome.from_device(buf, cs.nc)
-    finally:
-        if old is None:
-            del os.environ["M3D_SCORE_CULL"]
-        else:
-            os.environ["M3D_SCORE_CULL"] = old
-
-
-def _same_run(a, b):
-    (ca, oa), (cb, ob) = a, b
-    np.testing.assert_array_equal(ca, cb)
-    assert (oa.best_index, oa.best_count, oa.iterations) == (ob.best_index, ob.best_count, ob.iterations)
-    np.testing.assert_array_equal(oa.transformation, ob.transformation)
-
-
-@pytest.mark.parametrize("key", ("n1e5", "n3e5"))
-def test_tile_culling_counts_equal_unculled_at_cfg2(cfg2, key):
-    """The a4 batches' tile culling (ransac.hip cull_classify_kernel + the culled screen) gives every
-    one of the 1e5 counts of the unculled screen, and so the same winner, on both cfg2 sets and both
-    comparators (the bench's: norm at Nc = 1e5; the GUI's: squared at Nc = 3e5)."""
-    g, src, tgt, corr, noise, cs, csn = cfg2
-    s = cs if key == "n1e5" else csn
-    for thr, mode in ((THR, _lib.SCORE_NORM), (THR * THR, _lib.SCORE_SQUARED)):
-        _same_run(_run_counts(s, 100_000, thr, mode, True), _run_counts(s, 100_000, thr, mode, False))
-
-
-@pytest.mark.parametrize("name", ("clean", "noise", "mid"))
-@pytest.mark.parametrize("rows", (None, 2049, 3001))
-def test_tile_culling_counts_equal_unculled_5k(sets, pts5k, name, rows):
-    """Culled and unculled screens agree bit for bit on the 5k reference sets, also cut to ragged
-    row counts (partial last tiles), for several thresholds, both comparators, with early stop."""
-    cs_full, corr = sets[name]
-    cs = cs_full if rows is None else CorrSet(pts5k["src"], pts5k["tgt"], corr[:rows])
-    for thr in (0.05, THR, 2.0):
-        for mode, t in ((_lib.SCORE_NORM, thr), (_lib.SCORE_SQUARED, thr * thr)):
-            _same_run(_run_counts(cs, 20_000, t, mode, True, seed=7), _run_counts(cs, 20_000, t, mode, False, seed=7))
-    _same_run(_run_counts(cs, 20_000, THR, _lib.SCORE_NORM, True, early_stop=True),
-              _run_counts(cs, 20_000, THR, _lib.SCORE_NORM, False, early_stop=True))
-
-
-def test_tile_culling_on_degenerate_and_duplicated_rows():
-    """Rows that repeat one point (every sample rank-deficient), a set with a far outlier cluster,
-    and a tiny-threshold run: the culled counts equal the unculled ones."""
-    rng = np.random.default_rng(3)
-    src = rng.normal(size=(6000, 3))
-    tgt = src @ synth.random_rigid(1, rot_range=0.3, trans_range=0.5)[:3, :3].T + 0.2
-    tgt[:500] += 50.0
-    corr = np.stack([np.arange(6000), np.arange(6000)], 1).astype(np.int32)
-    dup = np.zeros((4096, 2), np.int32)
-    for c in (corr, dup):
-        cs = CorrSet(src, tgt, c)
-        for thr in (1e-3, 0.3):
-            _same_run(_run_counts(cs, 8192, thr, _lib.SCORE_NORM, True, seed=1),
-                      _run_counts(cs, 8192, thr, _lib.SCORE_NORM, False, seed=1))
