@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -62,41 +63,114 @@ KTimer::~KTimer() {
 
 static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+
 namespace m3d {
+// ------------------------------------------------------------------------------- block cache
+// Released device blocks (clouds, grids, Morton copies, target records, MFMA tiles) wait in a
+// process-wide cache for an allocation of a size in [need, 2·need].  Each carries the RELEASE
+// MARK of the object that freed it: an event recorded, on its context's order stream, after
+// every stream the context had enqueued work on (ctx_touch) up to the release — so a reuse only
+// makes the ALLOCATING stream wait on the device (hipStreamWaitEvent) for the work that could
+// still read the block, never the host, and never work on streams the context never used.
+// Blocks freed outside a release scope (a rebuild inside a call) have no mark and are reused
+// after a hipDeviceSynchronize, as before round 5.  Bounded (M3D_BLOCK_CACHE MiB, default
+// 2048; 64 blocks; oldest freed first); trimmed when the last context of a device is destroyed,
+// by m3d_trim_block_cache, and before any device allocation of the library is retried after
+// an out-of-memory failure (dev_malloc_raw).
 namespace {
 struct CachedBlock {
   void* p;
   size_t bytes;
   int dev;
-  bool safe;  // a hipDeviceSynchronize on its device has run since the release
+  std::shared_ptr<ReleaseMark> mark;  // null: unknown users, device sync before reuse
 };
 std::mutex g_bc_mu;
 std::vector<CachedBlock> g_bc;  // released, oldest first
 std::unordered_map<void*, std::pair<size_t, int>> g_bc_live;  // from block_alloc: size, device
+std::vector<hipEvent_t> g_ev_retired;  // marks' events, destroyed once complete
+std::unordered_map<int, int> g_ctx_live;  // live contexts per device
 size_t g_bc_bytes = 0;
-constexpr size_t kBcMaxBytes = (size_t)2 << 30;
 constexpr size_t kBcMaxCount = 64;
-bool bc_on() {
-  static const bool on = [] {
+thread_local std::shared_ptr<ReleaseMark> t_mark;  // the active ReleaseScope's mark
+
+size_t bc_cap() {
+  static const size_t cap = [] {
     const char* e = getenv("M3D_BLOCK_CACHE");
-    return !(e && atoi(e) == 0);
+    const long long mib = e ? atoll(e) : 2048;
+    return mib > 0 ? (size_t)mib << 20 : (size_t)0;
   }();
-  return on;
+  return cap;
 }
-void bc_trim_locked(size_t max_bytes, size_t max_count) {
-  while (!g_bc.empty() && (g_bc_bytes > max_bytes || g_bc.size() > max_count)) {
-    (void)hipFree(g_bc.front().p);
-    g_bc_bytes -= g_bc.front().bytes;
-    g_bc.erase(g_bc.begin());
+bool bc_on() { return bc_cap() > 0; }
+
+void retire_events_locked(bool wait) {
+  for (size_t k = 0; k < g_ev_retired.size();) {
+    hipEvent_t ev = g_ev_retired[k];
+    if (wait) (void)hipEventSynchronize(ev);
+    if (hipEventQuery(ev) == hipSuccess) {
+      (void)hipEventDestroy(ev);
+      g_ev_retired[k] = g_ev_retired.back();
+      g_ev_retired.pop_back();
+    } else {
+      ++k;
+    }
   }
+  (void)hipGetLastError();
+}
+
+// free cached blocks (of device dev, or every device when dev < 0) until the cache holds at most
+// max_bytes / max_count; a block is freed only after its release point has passed on the device
+size_t bc_trim_locked(int dev, size_t max_bytes, size_t max_count) {
+  size_t freed = 0;
+  for (size_t k = 0; k < g_bc.size() && (g_bc_bytes > max_bytes || g_bc.size() > max_count);) {
+    CachedBlock& b = g_bc[k];
+    if (dev >= 0 && b.dev != dev) {
+      ++k;
+      continue;
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != b.dev) (void)hipSetDevice(b.dev);
+    if (b.mark && b.mark->ev) (void)hipEventSynchronize(b.mark->ev);
+    (void)hipFree(b.p);  // (hipFree itself waits for the device)
+    if (cur != b.dev) (void)hipSetDevice(cur);
+    g_bc_bytes -= b.bytes;
+    freed += b.bytes;
+    g_bc.erase(g_bc.begin() + (ptrdiff_t)k);
+  }
+  retire_events_locked(false);
+  return freed;
 }
 }  // namespace
 
-hipError_t block_alloc(void** out, size_t bytes) {
+ReleaseMark::~ReleaseMark() {
+  if (ev == nullptr) return;
+  std::lock_guard<std::mutex> lk(g_bc_mu);
+  g_ev_retired.push_back(ev);
+}
+
+size_t block_cache_trim(int dev) {
+  std::lock_guard<std::mutex> lk(g_bc_mu);
+  return bc_trim_locked(dev, 0, 0);
+}
+
+hipError_t dev_malloc_raw(void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+    (void)hipGetLastError();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (block_cache_trim(dev) > 0) e = hipMalloc(p, bytes);
+  }
+  if (e != hipSuccess) *p = nullptr;
+  return e;
+}
+
+hipError_t block_alloc(void** out, size_t bytes, hipStream_t st) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (bc_on()) {
-    std::lock_guard<std::mutex> lk(g_bc_mu);
+    std::unique_lock<std::mutex> lk(g_bc_mu);
     int best = -1;
     for (int k = 0; k < (int)g_bc.size(); ++k) {
       const CachedBlock& b = g_bc[(size_t)k];
@@ -104,29 +178,26 @@ hipError_t block_alloc(void** out, size_t bytes) {
         best = k;
     }
     if (best >= 0) {
-      if (!g_bc[(size_t)best].safe) {
-        const hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) return e;
-        for (CachedBlock& b : g_bc)
-          if (b.dev == dev) b.safe = true;
-      }
       const CachedBlock b = g_bc[(size_t)best];
       g_bc.erase(g_bc.begin() + best);
       g_bc_bytes -= b.bytes;
       g_bc_live[b.p] = {b.bytes, dev};
+      lk.unlock();
+      hipError_t e = hipSuccess;
+      if (!b.mark)
+        e = hipDeviceSynchronize();  // released outside a scope: unknown users
+      else if (b.mark->ev != nullptr)
+        e = hipStreamWaitEvent(st, b.mark->ev, 0);  // stream order: the allocating stream waits
+      if (e != hipSuccess) {
+        block_release(b.p);
+        return e;
+      }
       *out = b.p;
       return hipSuccess;
     }
   }
   void* p = nullptr;
-  hipError_t e = hipMalloc(&p, bytes);
-  if (e != hipSuccess && bc_on()) {  // out of memory: give the cached blocks back and retry
-    std::lock_guard<std::mutex> lk(g_bc_mu);
-    (void)hipDeviceSynchronize();
-    bc_trim_locked(0, 0);
-    (void)hipGetLastError();
-    e = hipMalloc(&p, bytes);
-  }
+  const hipError_t e = dev_malloc_raw(&p, bytes);
   if (e != hipSuccess) return e;
   if (bc_on()) {
     std::lock_guard<std::mutex> lk(g_bc_mu);
@@ -142,14 +213,69 @@ void block_release(void* p) {
     std::lock_guard<std::mutex> lk(g_bc_mu);
     auto it = g_bc_live.find(p);
     if (it != g_bc_live.end()) {
-      g_bc.push_back(CachedBlock{p, it->second.first, it->second.second, false});
+      g_bc.push_back(CachedBlock{p, it->second.first, it->second.second, t_mark});
       g_bc_bytes += it->second.first;
       g_bc_live.erase(it);
-      bc_trim_locked(kBcMaxBytes, kBcMaxCount);
+      bc_trim_locked(-1, bc_cap(), kBcMaxCount);
       return;
     }
   }
   (void)hipFree(p);
+}
+
+void ctx_touch(m3d_ctx* ctx, hipStream_t st) {
+  if (ctx == nullptr) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();  // a capture: its graph launch is touched when it is replayed
+    return;
+  }
+  hipEvent_t ev = nullptr;
+  for (auto& u : ctx->uses)
+    if (u.first == st) ev = u.second;
+  if (ev == nullptr) {
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      ctx->uses_lost = true;  // no event: releases fall back to a device sync before reuse
+      return;
+    }
+    ctx->uses.emplace_back(st, ev);
+  }
+  if (hipEventRecord(ev, st) != hipSuccess) ctx->uses_lost = true;
+}
+
+ReleaseScope::ReleaseScope(m3d_ctx* ctx) {
+  prev = t_mark;
+  std::shared_ptr<ReleaseMark> m;
+  if (ctx != nullptr && !ctx->uses_lost) {
+    m = std::make_shared<ReleaseMark>();
+    if (!ctx->uses.empty()) {
+      (void)hipSetDevice(ctx->device);
+      bool ok = ctx->order != nullptr || hipStreamCreateWithFlags(&ctx->order, hipStreamNonBlocking) == hipSuccess;
+      hipEvent_t ev = nullptr;
+      ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+      for (auto& u : ctx->uses) ok = ok && hipStreamWaitEvent(ctx->order, u.second, 0) == hipSuccess;
+      ok = ok && hipEventRecord(ev, ctx->order) == hipSuccess;
+      if (ok) {
+        m->ev = ev;
+      } else {
+        if (ev != nullptr) (void)hipEventDestroy(ev);
+        m.reset();
+        (void)hipGetLastError();
+      }
+    }
+  }
+  t_mark = m;
+}
+
+ReleaseScope::~ReleaseScope() { t_mark = prev; }
+
+void ctx_count(int dev, int delta) {
+  std::lock_guard<std::mutex> lk(g_bc_mu);
+  const int n = (g_ctx_live[dev] += delta);
+  if (n <= 0) {
+    g_ctx_live.erase(dev);
+    bc_trim_locked(dev, 0, 0);  // the last context of the device: give the cache back
+  }
 }
 }  // namespace m3d
 
@@ -163,7 +289,7 @@ template <class T>
 int dev_alloc(m3d_ctx* ctx, T** p, int64_t count) {
   *p = nullptr;
   if (count <= 0) return M3D_OK;
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (size_t)count);
+  hipError_t e = dev_malloc(reinterpret_cast<void**>(p), sizeof(T) * (size_t)count);
   if (e != hipSuccess) {
     *p = nullptr;
     return m3d_fail(ctx, M3D_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -205,7 +331,7 @@ struct Arena {
       ctx->scratch_bytes = 0;
     }
     size_t want = std::max(off, ctx->scratch_bytes * 3 / 2);
-    hipError_t e = hipMalloc(&ctx->scratch, want);
+    hipError_t e = dev_malloc(&ctx->scratch, want);
     if (e != hipSuccess) {
       ctx->scratch = nullptr;
       return m3d_fail(ctx, M3D_ERR_OOM, "scratch hipMalloc failed");
@@ -348,13 +474,15 @@ int m3d_create(int device, m3d_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return M3D_ERR_HIP;
   m3d_ctx* ctx = new m3d_ctx();
   ctx->device = device;
-  if (hipMalloc(&ctx->stats, 8 * sizeof(int64_t)) != hipSuccess ||
-      hipMalloc(&ctx->rstate, sizeof(RansacState)) != hipSuccess ||
+  if (dev_malloc(&ctx->stats, 8 * sizeof(int64_t)) != hipSuccess ||
+      dev_malloc(&ctx->rstate, sizeof(RansacState)) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess ||
       hipMemset(ctx->stats, 0, 8 * sizeof(int64_t)) != hipSuccess) {
     m3d_destroy(ctx);
     return M3D_ERR_OOM;
   }
+  ctx_count(device, +1);
+  ctx->counted = true;
   *out = ctx;
   return M3D_OK;
 }
@@ -363,6 +491,8 @@ void m3d_destroy(m3d_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipDeviceSynchronize();
+  for (auto& u : ctx->uses) hipEventDestroy(u.second);
+  if (ctx->order) hipStreamDestroy(ctx->order);
   if (ctx->scratch) hipFree(ctx->scratch);
   if (ctx->stats) hipFree(ctx->stats);
   if (ctx->rstate) hipFree(ctx->rstate);
@@ -377,7 +507,17 @@ void m3d_destroy(m3d_ctx* ctx) {
       hipEventDestroy(pr.first);
       hipEventDestroy(pr.second);
     }
+  const int dev = ctx->device;
+  const bool counted = ctx->counted;
   delete ctx;
+  if (counted) ctx_count(dev, -1);  // the device's last context gives the block cache back
+}
+
+int m3d_trim_block_cache(m3d_ctx* ctx, int64_t* freed_bytes) {
+  if (!ctx) return M3D_ERR_INVALID;
+  const size_t f = block_cache_trim(ctx->device);
+  if (freed_bytes) *freed_bytes = (int64_t)f;
+  return M3D_OK;
 }
 
 const char* m3d_last_error(const m3d_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -617,7 +757,7 @@ int pin_ensure(m3d_ctx* ctx) {
     return m3d_fail(ctx, M3D_ERR_HIP, "hipHostGetDevicePointer failed");
   }
   uint32_t* tk = nullptr;
-  if (hipMalloc(&tk, sizeof(uint32_t)) != hipSuccess || hipMemset(tk, 0, sizeof(uint32_t)) != hipSuccess) {
+  if (dev_malloc(&tk, sizeof(uint32_t)) != hipSuccess || hipMemset(tk, 0, sizeof(uint32_t)) != hipSuccess) {
     if (tk) hipFree(tk);
     hipHostFree(h);
     return m3d_fail(ctx, M3D_ERR_OOM, "ticket hipMalloc failed");
@@ -924,6 +1064,7 @@ int cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t
             "non-finite centre");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
+  Touch tch{ctx, st};
   m3d_cloud* c = new m3d_cloud();
   c->ctx = ctx;
   c->n = n;
@@ -934,7 +1075,7 @@ int cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t
     if (n > 0) cv.add(&c->xyz64, 3 * (size_t)n);
     if (n > 0 && normals) cv.add(&c->nrm64, 3 * (size_t)n);
     cv.add(&c->xyz32, (size_t)c->n_pad);
-    if (cv.alloc(&c->block, &c->block_bytes) != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_OOM, "hipMalloc failed (cloud)");
+    if (cv.alloc(&c->block, &c->block_bytes, st) != hipSuccess) rc = m3d_fail(ctx, M3D_ERR_OOM, "device allocation failed (cloud)");
   }
   if (rc) {
     m3d_cloud_destroy(c);
@@ -980,11 +1121,21 @@ int cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t
 
 void m3d_cloud_destroy(m3d_cloud* c) {
   if (!c) return;
+  // the blocks go back to the cache marked after every stream the context used (stream-ordered
+  // reuse, no device sync)
+  ReleaseScope rs(c->ctx);
   for (Grid* g : c->grids) {
     grid_free(g);
     delete g;
   }
-  for (auto& m : c->morton) m3d_cloud_destroy(m.second);
+  // Morton copies a live ICP loop still runs on are detached, not freed: the last loop to go
+  // frees them (m3d_icp_destroy), so destroying the source before its loops stays safe
+  for (auto& m : c->morton) {
+    if (m.second->refs > 0)
+      m.second->orphan = true;
+    else
+      m3d_cloud_destroy(m.second);
+  }
   for (void** p : {reinterpret_cast<void**>(&c->slot), reinterpret_cast<void**>(&c->xyz64),
                    reinterpret_cast<void**>(&c->nrm64), reinterpret_cast<void**>(&c->xyz32)})
     if (in_block(*p, c->block, c->block_bytes)) *p = nullptr;
@@ -1220,7 +1371,7 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
     char* b = nullptr;
     if (run_arena) {
       if (ctx->run.reserve(tot) == hipSuccess) b = ctx->run.base;
-    } else if (hipMalloc(&s->block, tot) == hipSuccess) {
+    } else if (dev_malloc(&s->block, tot) == hipSuccess) {
       b = static_cast<char*>(s->block);
     } else {
       s->block = nullptr;
@@ -1259,7 +1410,10 @@ void m3d_icp_destroy(m3d_icp* s) {
   for (hipGraphExec_t g : s->graph)
     if (g != nullptr) hipGraphExecDestroy(g);
   if (s->cap_stream != nullptr) hipStreamDestroy(s->cap_stream);
-  if (s->src != nullptr) s->src->refs -= 1;
+  if (s->src != nullptr) {
+    m3d_cloud* ms = const_cast<m3d_cloud*>(s->src);
+    if (--ms->refs == 0 && ms->orphan) m3d_cloud_destroy(ms);  // its parent cloud is gone
+  }
   hipFree(s->block);  // state, keys, near2, dprev, ld64, lidx, corr, partials, sums
   hipFree(s->xdk);
   hipFree(s->xcl);
@@ -1269,6 +1423,7 @@ void m3d_icp_destroy(m3d_icp* s) {
 
 int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
   if (!s) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   m3d_ctx* ctx = s->ctx;
   double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
   const double* T = init ? init : I;
@@ -1300,6 +1455,7 @@ bool fused_tail(const m3d_icp* s, bool keys_back) {
 
 int m3d_icp_step(m3d_icp* s, void* stream) {
   if (!s) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   m3d_ctx* ctx = s->ctx;
   hipStream_t st = S(stream);
   // brute force: the fused tail hands the keys back as kKeyNone, the next NN seeds itself
@@ -1380,6 +1536,7 @@ int m3d_icp_prepare_steps(m3d_icp* s, int32_t n) {
 
 int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream) {
   if (!s) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   CHECK_ARG(s->ctx, n >= 0, "n must be >= 0");
   if (n >= 2 && icp_graphs_on() && !s->graph_off && !s->ctx->profiling) {
     const int slot = s->keys_clean ? 1 : 0;
@@ -1405,6 +1562,7 @@ int m3d_icp_steps(m3d_icp* s, int32_t n, void* stream) {
 
 int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* dkeys, void* stream) {
   if (!s) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   m3d_ctx* ctx = s->ctx;
   CHECK_ARG(ctx, off >= 0, "negative shard offset");
   CHECK_ARG(ctx, dkeys != nullptr || off == 0, "a target shard (offset > 0) needs the dkeys exchange buffer");
@@ -1418,6 +1576,7 @@ int m3d_icp_shard_nn(m3d_icp* s, int64_t off, int64_t* dkeys, void* stream) {
 
 int m3d_icp_shard_nn_range(m3d_icp* s, int64_t off, int64_t q0, int64_t q1, int64_t* dkeys, void* stream) {
   if (!s) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   m3d_ctx* ctx = s->ctx;
   CHECK_ARG(ctx, off >= 0, "negative shard offset");
   CHECK_ARG(ctx, dkeys != nullptr, "null dkeys");
@@ -1436,6 +1595,7 @@ int m3d_icp_shard_claim(m3d_icp* s, const int64_t* dmin, int32_t* claim, void* s
 int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* dmin, const int32_t* claim,
                         double* sums, void* stream) {
   if (!s) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   m3d_ctx* ctx = s->ctx;
   CHECK_ARG(ctx, sums != nullptr, "null sums");
   CHECK_ARG(ctx, (dmin == nullptr) == (claim == nullptr), "dmin and claim go together");
@@ -1517,6 +1677,7 @@ const int32_t* m3d_icp_corr(const m3d_icp* s) { return s ? s->corr : nullptr; }
 
 int m3d_icp_copy_corr(const m3d_icp* s, int32_t* dst, void* stream) {
   if (!s || !dst) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   if (s->src->n == 0) return M3D_OK;
   HIPX(s->ctx, launch_scatter_i32(s->corr, s->src->slot, s->src->n, dst, S(stream)));
   return M3D_OK;
@@ -1524,6 +1685,7 @@ int m3d_icp_copy_corr(const m3d_icp* s, int32_t* dst, void* stream) {
 
 int m3d_icp_copy_slots(const m3d_icp* s, int32_t* dst, void* stream) {
   if (!s || !dst) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   if (s->src->n == 0) return M3D_OK;
   HIPX(s->ctx, hipMemcpyAsync(dst, s->src->slot, sizeof(int32_t) * s->src->n, hipMemcpyDeviceToDevice,
                               S(stream)));
@@ -1534,6 +1696,7 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
                 double max_dist, const m3d_icp_params* params, m3d_icp_result* out,
                 int32_t* corr_idx, void* stream) {
   if (!ctx) return M3D_ERR_INVALID;
+  Touch tch{ctx, S(stream)};
   CHECK_ARG(ctx, out != nullptr, "null output");
   m3d_icp* s = nullptr;
   int rc = icp_create(ctx, src, tgt, max_dist, params, &s, true);
@@ -1574,6 +1737,7 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
 int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const double* T_host,
             double max_dist, int32_t nn_method, int32_t* idx, double* d2, void* stream) {
   if (!ctx) return M3D_ERR_INVALID;
+  Touch tch{ctx, S(stream)};
   CHECK_ARG(ctx, src && tgt && (idx || src->n == 0), "invalid arguments");
   CHECK_ARG(ctx, max_dist > 0.0, "max_dist must be > 0");
   m3d_icp_params p{1e-6, 1e-6, 0, M3D_EST_POINT_TO_POINT, nn_method, 0};
@@ -1633,7 +1797,7 @@ int prep_buffer(m3d_ctx* ctx, size_t need, char** out) {
     if (ctx->prep) hipFree(ctx->prep);
     ctx->prep = nullptr;
     ctx->prep_bytes = 0;
-    if (hipMalloc(&ctx->prep, need) != hipSuccess) {
+    if (dev_malloc(&ctx->prep, need) != hipSuccess) {
       ctx->prep = nullptr;
       return m3d_fail(ctx, M3D_ERR_OOM, "hipMalloc: preprocessing scratch");
     }
@@ -1700,6 +1864,7 @@ int m3d_hybrid_search(m3d_ctx* ctx, const m3d_cloud* cloud, double radius, int32
   CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
+  Touch tch{ctx, st};
   const Grid *g = nullptr, *gf = nullptr;
   double hf = 0.0;
   int rc = search_grids(ctx, cloud, radius, max_nn, st, &g, &gf, &hf);
@@ -1716,6 +1881,7 @@ int m3d_estimate_normals(m3d_ctx* ctx, const m3d_cloud* cloud, double radius, in
   CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
+  Touch tch{ctx, st};
   NbrLists L;
   int rc = neighbourhoods(ctx, cloud, radius, max_nn, st, 0, &L);
   if (rc) return rc;
@@ -1732,6 +1898,7 @@ int m3d_compute_fpfh(m3d_ctx* ctx, const m3d_cloud* cloud, const double* normals
   CHECK_ARG(ctx, radius > 0.0 && max_nn >= 1 && max_nn <= 256, "radius > 0 and 1 <= max_nn <= 256");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
+  Touch tch{ctx, st};
   NbrLists L;
   int rc = neighbourhoods(ctx, cloud, radius, max_nn, st, 33, &L);
   if (rc) return rc;
@@ -1767,6 +1934,7 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
   CHECK_ARG(ctx, p->max_iteration >= 0, "max_iteration must be >= 0");
   hipSetDevice(ctx->device);
   hipStream_t st = S(stream);
+  Touch tch{ctx, st};
   memset(out, 0, sizeof(*out));
   for (int k = 0; k < 16; ++k) out->T[k] = (k % 5 == 0) ? 1.0 : 0.0;
   out->best_index = -1;

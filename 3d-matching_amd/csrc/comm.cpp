@@ -84,7 +84,7 @@ ncclRedOp_t op_of(int op) { return op == M3D_OP_MIN ? ncclMin : (op == M3D_OP_MA
 template <class T>
 int alloc_once(m3d_ctx* ctx, T** p, int64_t count) {
   if (*p != nullptr) return M3D_OK;
-  if (hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (size_t)std::max<int64_t>(count, 1)) != hipSuccess) {
+  if (dev_malloc(reinterpret_cast<void**>(p), sizeof(T) * (size_t)std::max<int64_t>(count, 1)) != hipSuccess) {
     *p = nullptr;
     return m3d_fail(ctx, M3D_ERR_OOM, "exchange buffer hipMalloc failed");
   }
@@ -145,9 +145,9 @@ int m3d_comm_init(m3d_ctx* ctx, const uint8_t* id, int rank, int world, m3d_comm
     return comm_fail(ctx, r, "ncclCommInitRank");
   }
   // every buffer the collectives use is allocated here, once (no allocation between collectives)
-  if (hipMalloc(&c->key, sizeof(int64_t)) != hipSuccess || hipMalloc(&c->rbuf, 20 * sizeof(int64_t)) != hipSuccess ||
-      hipMalloc(&c->flag, sizeof(int32_t)) != hipSuccess ||
-      hipMalloc(&c->dres, sizeof(m3d_ransac_result)) != hipSuccess ||
+  if (dev_malloc(&c->key, sizeof(int64_t)) != hipSuccess || dev_malloc(&c->rbuf, 20 * sizeof(int64_t)) != hipSuccess ||
+      dev_malloc(&c->flag, sizeof(int32_t)) != hipSuccess ||
+      dev_malloc(&c->dres, sizeof(m3d_ransac_result)) != hipSuccess ||
       hipHostMalloc(&c->hbuf, 20 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_a, hipEventDisableTiming) != hipSuccess ||
@@ -188,6 +188,7 @@ int m3d_icp_shard_steps(m3d_icp* s, m3d_comm* c, int64_t off, int32_t n, void* s
   if (c->poisoned) return poisoned_error(c);
   if (n < 0) return m3d_fail(ctx, M3D_ERR_INVALID, "n must be >= 0");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  Touch tch{ctx, st};
   const int64_t ns = s->src->n;
   int rc;
   if (!s->xready_tgt) {  // scratch before the first collective, then every rank agrees
@@ -237,6 +238,7 @@ int m3d_icp_source_shard_steps(m3d_icp* s, m3d_comm* c, int32_t n, void* stream)
   if (c->poisoned) return poisoned_error(c);
   if (n < 0) return m3d_fail(ctx, M3D_ERR_INVALID, "n must be >= 0");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  Touch tch{ctx, st};
   int rc;
   if (!s->xready_src) {
     rc = alloc_once(ctx, &s->xsums, kTermSlots);

@@ -126,8 +126,8 @@ hipError_t feature_nn(const double* fq, int64_t nq, const double* fr, int64_t nr
   S = std::max<int64_t>(1, (nr + slice - 1) / slice);
   double* bd = nullptr;
   int32_t* bi = nullptr;
-  hipError_t e = hipMalloc(&bd, sizeof(double) * S * nq);
-  if (e == hipSuccess) e = hipMalloc(&bi, sizeof(int32_t) * S * nq);
+  hipError_t e = dev_malloc(&bd, sizeof(double) * S * nq);
+  if (e == hipSuccess) e = dev_malloc(&bi, sizeof(int32_t) * S * nq);
   if (e == hipSuccess) {
     feature_nn_kernel<<<dim3((unsigned)bx, (unsigned)S), kFnnBlock, 0, st>>>(fq, nq, fr, nr, slice, bd, bi);
     feature_nn_merge_kernel<<<(unsigned)((nq + 255) / 256), 256, 0, st>>>(bd, bi, nq, (int)S, out);
@@ -168,7 +168,7 @@ hipError_t feature_correspondences(const double* fs, int64_t ns, const double* f
     hipFree(keep);
     hipFree(tmp);
   };
-  hipError_t e = hipMalloc(&ij, 4 * ns);
+  hipError_t e = dev_malloc(&ij, 4 * ns);
   if (e == hipSuccess) e = feature_nn(fs, ns, ft, nt, ij, st);
   if (e == hipSuccess && !mutual) {  // corres_ij only: (i, nn(i)) for every source feature
     mutual_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(ij, nullptr, ns, corr_out, nullptr);
@@ -178,11 +178,11 @@ hipError_t feature_correspondences(const double* fs, int64_t ns, const double* f
     *n_out = ns;
     return e;
   }
-  if (e == hipSuccess) e = hipMalloc(&ji, 4 * nt);
+  if (e == hipSuccess) e = dev_malloc(&ji, 4 * nt);
   if (e == hipSuccess) e = feature_nn(ft, nt, fs, ns, ji, st);
-  if (e == hipSuccess) e = hipMalloc(&pairs, 8 * ns);
-  if (e == hipSuccess) e = hipMalloc(&keep, ns);
-  if (e == hipSuccess) e = hipMalloc(&nsel, 4);
+  if (e == hipSuccess) e = dev_malloc(&pairs, 8 * ns);
+  if (e == hipSuccess) e = dev_malloc(&keep, ns);
+  if (e == hipSuccess) e = dev_malloc(&nsel, 4);
   if (e == hipSuccess) {
     mutual_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(ij, ji, ns, pairs, keep);
     e = hipGetLastError();
@@ -190,7 +190,7 @@ hipError_t feature_correspondences(const double* fs, int64_t ns, const double* f
   size_t tb = 0;
   if (e == hipSuccess)
     e = hipcub::DeviceSelect::Flagged(nullptr, tb, (const int2*)pairs, keep, (int2*)corr_out, nsel, (int)ns, st);
-  if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tb, 1));
+  if (e == hipSuccess) e = dev_malloc(&tmp, std::max<size_t>(tb, 1));
   if (e == hipSuccess)
     e = hipcub::DeviceSelect::Flagged(tmp, tb, (const int2*)pairs, keep, (int2*)corr_out, nsel, (int)ns, st);
   int32_t h = 0;

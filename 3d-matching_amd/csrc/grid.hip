@@ -553,7 +553,7 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   } else {  // per-axis bounds: one pass + one sync
     const int nb = (int)std::min<int64_t>(1024, (n + kGridBlock - 1) / kGridBlock);
     float* part = nullptr;
-    e = hipMalloc(&part, sizeof(float) * 6 * nb);
+    e = dev_malloc(&part, sizeof(float) * 6 * nb);
     if (e != hipSuccess) return e;
     minmax3_kernel<<<nb, kGridBlock, 0, st>>>(xyz32, n, part);
     std::vector<float> hp(6 * (size_t)nb);
@@ -599,8 +599,8 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
     kout = reinterpret_cast<uint32_t*>(ta->base + a4);
     vin = reinterpret_cast<int32_t*>(ta->base + 2 * a4);
     tmp = ta->base + 3 * a4;
-  } else if ((e = hipMalloc(&kin, a4)) != hipSuccess || (e = hipMalloc(&kout, a4)) != hipSuccess ||
-             (e = hipMalloc(&vin, a4)) != hipSuccess || (e = hipMalloc(&tmp, tmp_bytes)) != hipSuccess) {
+  } else if ((e = dev_malloc(&kin, a4)) != hipSuccess || (e = dev_malloc(&kout, a4)) != hipSuccess ||
+             (e = dev_malloc(&vin, a4)) != hipSuccess || (e = dev_malloc(&tmp, tmp_bytes)) != hipSuccess) {
     return grid_fail(e, kin, kout, vin, nullptr, tmp);
   }
   auto done = [&](hipError_t r) { return ta != nullptr ? r : grid_fail(r, kin, kout, vin, nullptr, tmp); };
@@ -609,7 +609,7 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
     cv.add(&g->order, (size_t)n);
     cv.add(&g->start, (size_t)total + 1);
     cv.add(&g->pts, (size_t)n);
-    if ((e = cv.alloc(&g->block, &g->block_bytes)) != hipSuccess) return done(e);
+    if ((e = cv.alloc(&g->block, &g->block_bytes, st)) != hipSuccess) return done(e);
   }
   const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
   cell_id_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, n, d, kin, vin);
@@ -638,7 +638,7 @@ hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st) {
   if (ta != nullptr) {
     if ((e = ta->reserve(256)) != hipSuccess) return e;
     cnt = reinterpret_cast<unsigned long long*>(ta->base);
-  } else if ((e = hipMalloc(&cnt, 2 * sizeof(unsigned long long))) != hipSuccess) {
+  } else if ((e = dev_malloc(&cnt, 2 * sizeof(unsigned long long))) != hipSuccess) {
     return e;
   }
   unsigned long long occ[2] = {0, 0};
@@ -777,8 +777,8 @@ hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid
     cc.add(&out->slot, n1);
     cg.add(&gout->mpts, n1);
     cg.add(&gout->minv, n1);
-    if ((e = cc.alloc(&out->block, &out->block_bytes)) != hipSuccess ||
-        (e = cg.alloc(&gout->block, &gout->block_bytes)) != hipSuccess)
+    if ((e = cc.alloc(&out->block, &out->block_bytes, st)) != hipSuccess ||
+        (e = cg.alloc(&gout->block, &gout->block_bytes, st)) != hipSuccess)
       return e;
   }
   if (n == 0) return hipSuccess;

@@ -421,8 +421,8 @@ __global__ __launch_bounds__(256) void pack16_sorted_kernel(const float4* __rest
 hipError_t build_mfma_tiles(const m3d_cloud* c, Grid* g, hipStream_t st) {
   const int64_t n = c->n;
   const int64_t n_pad = std::max<int64_t>((n + kMTilePad - 1) / kMTilePad * kMTilePad, kMTilePad);
-  hipError_t e = block_alloc(reinterpret_cast<void**>(&g->mf16), sizeof(uint4) * 2 * n_pad);
-  if (e == hipSuccess) e = block_alloc(reinterpret_cast<void**>(&g->mf32), sizeof(float4) * n_pad);
+  hipError_t e = block_alloc(reinterpret_cast<void**>(&g->mf16), sizeof(uint4) * 2 * n_pad, st);
+  if (e == hipSuccess) e = block_alloc(reinterpret_cast<void**>(&g->mf32), sizeof(float4) * n_pad, st);
   if (e != hipSuccess) return e;
   g->mf_npad = n_pad;
   pack16_sorted_kernel<<<(unsigned)((n_pad + 255) / 256), 256, 0, st>>>(
@@ -1500,7 +1500,7 @@ __global__ __launch_bounds__(256) void pack_rec_kernel(const double* __restrict_
 hipError_t ensure_target_rec(const m3d_cloud* c, hipStream_t st) {
   if (c->rec64 != nullptr || c->n == 0) return hipSuccess;
   double* rec = nullptr;
-  hipError_t e = block_alloc(reinterpret_cast<void**>(&rec), sizeof(double) * 8 * c->n);
+  hipError_t e = block_alloc(reinterpret_cast<void**>(&rec), sizeof(double) * 8 * c->n, st);
   if (e != hipSuccess) return e;
   pack_rec_kernel<<<(unsigned)((c->n + 255) / 256), 256, 0, st>>>(c->xyz64, c->nrm64, c->n, rec);
   e = hipGetLastError();  // asynchronous (stream order); m3d_icp_create synchronises once

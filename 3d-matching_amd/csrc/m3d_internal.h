@@ -8,6 +8,7 @@
 #include <string>
 #include <utility>
 #include <functional>
+#include <memory>
 #include <vector>
 
 #include "../../include/m3d.h"
@@ -120,6 +121,7 @@ struct Grid {
 // users on one stream reuse it without a host sync; an outgrown buffer is retired (freed with the
 // context), never freed under work still in flight.  Replaces a hipMalloc/hipFree pair per
 // temporary (hipFree waits for the device).
+hipError_t dev_malloc_raw(void** p, size_t bytes);  // (below: the block cache)
 struct TmpArena {
   char* base = nullptr;
   size_t cap = 0;
@@ -128,7 +130,7 @@ struct TmpArena {
     if (bytes <= cap) return hipSuccess;
     const size_t want = std::max(bytes, 2 * cap);
     void* p = nullptr;
-    const hipError_t e = hipMalloc(&p, want);
+    const hipError_t e = dev_malloc_raw(&p, want);
     if (e != hipSuccess) return e;
     if (base != nullptr) retired.push_back(base);
     base = static_cast<char*>(p);
@@ -149,29 +151,57 @@ void host_pipeline(int64_t n, const std::function<void(int64_t)>& fn, const std:
 // 256-B aligned carve-out of a TmpArena reservation
 inline size_t tmp_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// Several device arrays in ONE allocation (256-B aligned pieces): the setup paths make one
-// hipMalloc per object instead of one per array, and the owner one hipFree.
 // Device block cache (api.cpp): the blocks of clouds, grids, Morton copies, target records and
 // MFMA tiles go back to a process-wide cache when their object dies, and a later allocation of
-// a size in [need, 2·need] takes one — after one hipDeviceSynchronize, so that no work enqueued
-// before the release can still use it.  hipFree of a 2–5 MB block costs ≈ 160 µs on the box
+// a size in [need, 2·need] takes one.  hipFree of a 2–5 MB block costs ≈ 160 µs on the box
 // (unmapping; tools/ubench_alloc.hip), which a caller registering many pairs paid on every call
-// that evicted older clouds from the drop-in cache (tools/multipair_timing.py).  Bounded (64
-// blocks, 2 GiB; the oldest are freed first); M3D_BLOCK_CACHE=0 frees at once.
-hipError_t block_alloc(void** p, size_t bytes);
+// that evicted older clouds from the drop-in cache (tools/multipair_timing.py).  Reuse is
+// stream-ordered: a block released inside a ReleaseScope carries that scope's mark (an event
+// after all work its context had enqueued, on every stream it used: ctx_touch), and the
+// allocating stream waits for it on the device.
+struct ReleaseMark {
+  hipEvent_t ev = nullptr;  // null: nothing had been enqueued
+  ~ReleaseMark();
+};
+// record that ctx enqueued work on st (entry points that read or write cached blocks)
+void ctx_touch(m3d_ctx* ctx, hipStream_t st);
+// an entry point that enqueues work reading or writing cached device blocks (clouds, grids, loop
+// sources) records, when it returns, that its context used this stream
+struct Touch {
+  m3d_ctx* ctx;
+  hipStream_t st;
+  ~Touch() { ctx_touch(ctx, st); }
+};
+// blocks released while a scope is alive carry its mark (m3d_cloud_destroy, m3d_icp_destroy)
+struct ReleaseScope {
+  std::shared_ptr<ReleaseMark> prev;
+  explicit ReleaseScope(m3d_ctx* ctx);
+  ~ReleaseScope();
+};
+hipError_t block_alloc(void** p, size_t bytes, hipStream_t st = nullptr);
 void block_release(void* p);
+size_t block_cache_trim(int dev);  // free the cached blocks of device dev; returns bytes freed
+void ctx_count(int dev, int delta);  // live contexts per device (the last one trims the cache)
+// hipMalloc that trims the block cache and retries once on out-of-memory
+hipError_t dev_malloc_raw(void** p, size_t bytes);
+template <class T>
+hipError_t dev_malloc(T** p, size_t bytes) {
+  return dev_malloc_raw(reinterpret_cast<void**>(p), bytes);
+}
 
+// Several device arrays in ONE allocation (256-B aligned pieces): the setup paths make one
+// hipMalloc per object instead of one per array, and the owner one hipFree.
 struct Carve {
   std::vector<std::pair<void**, size_t>> parts;
   template <class T>
   void add(T** p, size_t count) {
     parts.emplace_back(reinterpret_cast<void**>(p), tmp_align(sizeof(T) * std::max<size_t>(count, 1)));
   }
-  hipError_t alloc(void** block, size_t* bytes) {
+  hipError_t alloc(void** block, size_t* bytes, hipStream_t st = nullptr) {
     size_t tot = 0;
     for (auto& q : parts) tot += q.second;
     void* b = nullptr;
-    const hipError_t e = block_alloc(&b, std::max<size_t>(tot, 1));
+    const hipError_t e = block_alloc(&b, std::max<size_t>(tot, 1), st);
     *block = e == hipSuccess ? b : nullptr;
     *bytes = e == hipSuccess ? tot : 0;
     if (e != hipSuccess) return e;
@@ -219,6 +249,12 @@ struct m3d_ctx {
   size_t prep_bytes = 0;
   m3d::TmpArena tmp;  // setup temporaries (grids, Morton copies, cloud packing)
   m3d::TmpArena run;  // loop arrays of the synchronous one-shot ICP / NN calls (api.cpp icp_create)
+  // streams this context enqueued work on, each with an event re-recorded at every such call
+  // (api.cpp ctx_touch): the release marks of the block cache wait for all of them on `order`
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+  bool uses_lost = false;  // an event could not be made: releases fall back to a device sync
+  hipStream_t order = nullptr;
+  bool counted = false;  // counted among its device's live contexts (api.cpp ctx_count)
 };
 
 struct m3d_corrset {
@@ -263,6 +299,7 @@ struct m3d_cloud {
   // a Morton copy: live ICP loops running on it (m3d_icp_create / _destroy); the parent keeps at
   // most kMortonKeep copies and evicts the oldest unreferenced one beyond that (api.cpp)
   mutable int refs = 0;
+  bool orphan = false;  // a Morton copy whose parent was destroyed while loops still ran on it
   // one allocation holding the point arrays (Carve; m3d_cloud_destroy frees it, not them)
   void* block = nullptr;
   size_t block_bytes = 0;

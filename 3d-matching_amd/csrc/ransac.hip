@@ -1082,7 +1082,7 @@ hipError_t launch_corr16(m3d_corrset* cs, hipStream_t st) {
   double S = 1.0;
   if (mx > 0.0) S = exp2(floor(log2(1024.0 / mx)));
   S = fmin(fmax(S, 0x1p-40), 0x1p40);
-  hipError_t e = hipMalloc(&cs->ca16, sizeof(uint4) * 4 * cs->nc_pad);
+  hipError_t e = dev_malloc(&cs->ca16, sizeof(uint4) * 4 * cs->nc_pad);
   if (e != hipSuccess) {
     cs->ca16 = nullptr;
     return e;

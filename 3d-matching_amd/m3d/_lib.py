@@ -30,7 +30,7 @@ COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2
 OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -78,6 +78,7 @@ SIGNATURES = {
     "m3d_destroy": (None, [vp]),
     "m3d_last_error": (C.c_char_p, [vp]),
     "m3d_get_stats": (C.c_int, [vp, C.POINTER(i64)]),
+    "m3d_trim_block_cache": (C.c_int, [vp, C.POINTER(i64)]),
     "m3d_profile_enable": (C.c_int, [vp, C.c_int]),
     "m3d_profile_read": (C.c_int, [vp, C.c_int, C.POINTER(dbl), C.POINTER(i64)]),
     "m3d_corrset_create": (C.c_int, [vp, vp, i64, vp, i64, vp, i64, vp, C.POINTER(vp)]),

@@ -60,6 +60,12 @@ class Context:
     def check(self, rc, what):
         check(rc, self.h, what)
 
+    def trim_block_cache(self) -> int:
+        """Give libm3d's idle cached device blocks back (m3d_trim_block_cache); bytes freed."""
+        n = C.c_int64(0)
+        self.check(self.lib.m3d_trim_block_cache(self.h, C.byref(n)), "m3d_trim_block_cache")
+        return n.value
+
     def profile(self, enable: bool = True):
         """Record HIP events around every launch of the timed kernels (m3d_profile_enable)."""
         self.check(self.lib.m3d_profile_enable(self.h, int(enable)), "m3d_profile_enable")
@@ -87,6 +93,19 @@ def context(device: int | None = None) -> Context:
     if dev not in cache:
         cache[dev] = Context(dev)
     return cache[dev]
+
+
+def device_empty(shape, dtype):
+    """torch.empty on the current cuda device.  On out-of-memory the idle blocks of libm3d's
+    block cache (destroyed clouds) and torch's own cache are given back, and the allocation is
+    retried once."""
+    torch = _torch()
+    try:
+        return torch.empty(shape, dtype=dtype, device="cuda")
+    except torch.cuda.OutOfMemoryError:
+        context().trim_block_cache()
+        torch.cuda.empty_cache()
+        return torch.empty(shape, dtype=dtype, device="cuda")
 
 
 def stream_handle():
@@ -153,8 +172,8 @@ class CorrSet:
     def kabsch3(self, H: int, triples=None, seed: int = 0, hyp0: int = 0):
         """Batched a1: returns (T (H,4,4) torch f64 cuda, status (H,) uint8)."""
         torch = _torch()
-        T = torch.empty((H, 4, 4), dtype=torch.float64, device="cuda")
-        status = torch.empty((H,), dtype=torch.uint8, device="cuda")
+        T = device_empty((H, 4, 4), torch.float64)
+        status = device_empty((H,), torch.uint8)
         tri = None if triples is None else to_device(triples, "int32", (3,))
         self.ctx.check(self.ctx.lib.m3d_kabsch3_batch(self.ctx.h, self.h, ptr(tri), seed, hyp0, H,
                                                       ptr(T), ptr(status), stream_handle()),
@@ -166,7 +185,7 @@ class CorrSet:
         torch = _torch()
         Td = to_device(T, "float64", (4, 4))
         H = Td.shape[0]
-        counts = torch.empty((H,), dtype=torch.int32, device="cuda")
+        counts = device_empty((H,), torch.int32)
         self.ctx.check(self.ctx.lib.m3d_ransac_score(self.ctx.h, self.h, ptr(Td), H, float(thr),
                                                      int(mode), ptr(counts), stream_handle()),
                        "ransac_score")
@@ -404,8 +423,8 @@ def nn1(src: Cloud, tgt: Cloud, T, max_dist: float, nn: str = "grid"):
     nn="brute" scans every target, nn="grid" only the uniform-grid cells within the radius;
     both return the identical result (grid.hip header)."""
     torch = _torch()
-    idx = torch.empty((src.n,), dtype=torch.int32, device="cuda")
-    d2 = torch.empty((src.n,), dtype=torch.float64, device="cuda")
+    idx = device_empty((src.n,), torch.int32)
+    d2 = device_empty((src.n,), torch.float64)
     src.ctx.check(src.ctx.lib.m3d_nn1(src.ctx.h, src.h, tgt.h, _T16(T), float(max_dist),
                                       _nn_method(nn), ptr(idx), ptr(d2), stream_handle()), "nn1")
     return idx, d2
@@ -441,7 +460,7 @@ def icp(src: Cloud, tgt: Cloud, max_dist: float, init=None, estimation=_lib.EST_
     p = _lib.IcpParams(float(relative_fitness), float(relative_rmse), int(max_iteration), int(estimation),
                        _nn_method(nn), 0)
     res = _lib.IcpResult()
-    corr = torch.empty((max(src.n, 1),), dtype=torch.int32, device="cuda") if with_correspondences else None
+    corr = device_empty((max(src.n, 1),), torch.int32) if with_correspondences else None
     init16 = _T16(np.eye(4) if init is None else init)
     src.ctx.check(src.ctx.lib.m3d_icp_run(src.ctx.h, src.h, tgt.h, init16, float(max_dist), C.byref(p),
                                           C.byref(res), ptr(corr), stream_handle()), "icp_run")
@@ -542,13 +561,13 @@ class IcpLoop:
         """Slot → source point index (int32 torch cuda): the loop holds its source in the Morton
         order of the source grid; exchange buffers (dkeys / claims) are indexed by slot."""
         torch = _torch()
-        out = torch.empty((max(self.src.n, 1),), dtype=torch.int32, device="cuda")
+        out = device_empty((max(self.src.n, 1),), torch.int32)
         self.ctx.check(self.ctx.lib.m3d_icp_copy_slots(self.h, ptr(out), stream_handle()), "icp_copy_slots")
         return out[: self.src.n]
 
     def correspondences(self):
         """Current correspondence target per source point (int32, -1 = none), torch cuda."""
         torch = _torch()
-        out = torch.empty((max(self.src.n, 1),), dtype=torch.int32, device="cuda")
+        out = device_empty((max(self.src.n, 1),), torch.int32)
         self.ctx.check(self.ctx.lib.m3d_icp_copy_corr(self.h, ptr(out), stream_handle()), "icp_copy_corr")
         return out[: self.src.n]

@@ -23,7 +23,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from .core import Cloud, _torch, context, corr_pairs, ptr, stream_handle, to_device
+from .core import Cloud, _torch, context, corr_pairs, device_empty, ptr, stream_handle, to_device
 
 
 def voxel_down_sample(points, voxel_size: float, normals=None):
@@ -33,8 +33,8 @@ def voxel_down_sample(points, voxel_size: float, normals=None):
     p = to_device(points)
     nrm = None if normals is None else to_device(normals)
     n = p.shape[0]
-    out = torch.empty((max(n, 1), 3), dtype=torch.float64, device="cuda")
-    out_n = torch.empty((max(n, 1), 3), dtype=torch.float64, device="cuda") if nrm is not None else None
+    out = device_empty((max(n, 1), 3), torch.float64)
+    out_n = device_empty((max(n, 1), 3), torch.float64) if nrm is not None else None
     m = C.c_int64()
     ctx.check(ctx.lib.m3d_voxel_down_sample(ctx.h, ptr(p), ptr(nrm), n, float(voxel_size), ptr(out),
                                             ptr(out_n), C.byref(m), stream_handle()), "voxel_down_sample")
@@ -52,9 +52,9 @@ def hybrid_search(points, radius: float, max_nn: int):
     c = _cloud(points)
     ctx = c.ctx
     n = max(c.n, 1)
-    idx = torch.empty((n, max_nn), dtype=torch.int32, device="cuda")
-    d2 = torch.empty((n, max_nn), dtype=torch.float64, device="cuda")
-    cnt = torch.empty((n,), dtype=torch.int32, device="cuda")
+    idx = device_empty((n, max_nn), torch.int32)
+    d2 = device_empty((n, max_nn), torch.float64)
+    cnt = device_empty((n,), torch.int32)
     ctx.check(ctx.lib.m3d_hybrid_search(ctx.h, c.h, float(radius), int(max_nn), ptr(idx), ptr(d2),
                                         ptr(cnt), stream_handle()), "hybrid_search")
     return idx[: c.n].cpu().numpy(), d2[: c.n].cpu().numpy(), cnt[: c.n].cpu().numpy()
@@ -66,7 +66,7 @@ def estimate_normals(points, radius: float, max_nn: int = 30, normals=None):
     torch = _torch()
     c = _cloud(points, normals)
     ctx = c.ctx
-    out = torch.empty((max(c.n, 1), 3), dtype=torch.float64, device="cuda")
+    out = device_empty((max(c.n, 1), 3), torch.float64)
     ctx.check(ctx.lib.m3d_estimate_normals(ctx.h, c.h, float(radius), int(max_nn), ptr(out),
                                            stream_handle()), "estimate_normals")
     return out[: c.n].cpu().numpy()
@@ -80,7 +80,7 @@ def compute_fpfh(points, normals, radius: float, max_nn: int = 100):
     nrm = to_device(normals)
     if nrm.shape != (c.n, 3):
         raise ValueError("normals must be N×3")
-    out = torch.empty((max(c.n, 1), 33), dtype=torch.float64, device="cuda")
+    out = device_empty((max(c.n, 1), 33), torch.float64)
     ctx.check(ctx.lib.m3d_compute_fpfh(ctx.h, c.h, ptr(nrm), float(radius), int(max_nn), ptr(out),
                                        stream_handle()), "compute_fpfh")
     return out[: c.n].cpu().numpy()
@@ -105,7 +105,7 @@ def feature_correspondences(f_src, f_tgt, mutual_filter: bool = False,
     if fs.ndim != 2 or ft.ndim != 2 or fs.shape[1] != ft.shape[1]:
         raise ValueError("features must be N×33 arrays")
     ns, nt = fs.shape[0], ft.shape[0]
-    out = torch.empty((max(ns, 1), 2), dtype=torch.int32, device="cuda")
+    out = device_empty((max(ns, 1), 2), torch.int32)
     m = C.c_int64()
     ctx.check(ctx.lib.m3d_feature_correspondences(ctx.h, ptr(fs), ns, ptr(ft), nt, fs.shape[1],
                                                   int(bool(mutual_filter)), float(mutual_consistent_ratio),
@@ -140,7 +140,7 @@ def ransac_on_correspondences(src, tgt, corres, max_correspondence_distance: flo
                                  float(distance) if distance is not None else 0.0,
                                  int(seed) & ((1 << 64) - 1), int(max_iteration), int(ransac_n))
     r = _lib.FeatureRansacResult()
-    cs = torch.empty((max(sc.n, 1),), dtype=torch.int32, device="cuda")
+    cs = device_empty((max(sc.n, 1),), torch.int32)
     ctx.check(ctx.lib.m3d_ransac_on_correspondences(ctx.h, sc.h, tc.h, ptr(corr), corr.shape[0], C.byref(p),
                                                     C.byref(r), ptr(cs), stream_handle()),
               "ransac_on_correspondences")

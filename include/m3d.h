@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 11
+#define M3D_ABI_VERSION 12
 
 /* return codes */
 #define M3D_OK 0
@@ -189,14 +189,25 @@ int m3d_cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int
 int m3d_cloud_create_framed(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
                             const double* center, void* stream, m3d_cloud** out);
 /* The same from HOST arrays (ABI 11): xyz [host] n×3 f64, normals [host] n×3 f64 or NULL, center
- * [host] 3 f64 or NULL (the cloud's mean).  The library's host threads copy the arrays in 256 KB
- * chunks into the context's pinned staging memory and each chunk's DMA is issued as soon as it is
- * staged (copies and DMAs overlap) — instead of a caller's single-threaded pageable upload plus a
- * device-to-device copy.  The same cloud, bit for bit.  Synchronous. */
+ * [host] 3 f64 or NULL (the cloud's mean).  The arrays go straight into the cloud's buffers
+ * (one pageable copy each) instead of a caller's upload plus a device-to-device copy.  The same
+ * cloud, bit for bit.  Synchronous. */
 int m3d_cloud_create_host(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t n,
                           const double* center, void* stream, m3d_cloud** out);
+/* Destroy a cloud.  Its device blocks go to the library's block cache, marked after all work
+ * its context had enqueued on any stream; a later allocation reuses them in stream order (the
+ * allocating stream waits on the device; no host or device-wide synchronisation, ABI 12).
+ * An m3d_icp created on this cloud may outlive it: the loop keeps the data it runs on and frees
+ * it in m3d_icp_destroy (ABI 12); stepping a loop whose TARGET cloud is gone is undefined.
+ * Destroy every object before its context. */
 void m3d_cloud_destroy(m3d_cloud* c);
 int64_t m3d_cloud_size(const m3d_cloud* c);
+/* Give the block cache's idle blocks of ctx's device back to the driver (each after its release
+ * point has passed on the device); freed_bytes may be NULL.  The Python layer calls this when a
+ * device allocation fails; the library does so itself before retrying its own allocations, and
+ * when the last context of a device is destroyed.  M3D_BLOCK_CACHE=<MiB> caps the cache (default
+ * 2048, 0 = no cache).  ABI 12. */
+int m3d_trim_block_cache(m3d_ctx* ctx, int64_t* freed_bytes);
 
 /* Nearest-neighbour search method.  Both return the identical (d², index) result: BRUTE scans
  * every target (cfg1's LDS-tiled brute force), GRID visits only the uniform-grid cells that can
