@@ -87,6 +87,7 @@ struct CachedBlock {
 std::mutex g_bc_mu;
 std::vector<CachedBlock> g_bc;  // released, oldest first
 std::unordered_map<void*, std::pair<size_t, int>> g_bc_live;  // from block_alloc: size, device
+std::mutex g_ev_mu;  // guards g_ev_retired; taken after g_bc_mu (a mark may die under g_bc_mu)
 std::vector<hipEvent_t> g_ev_retired;  // marks' events, destroyed once complete
 std::unordered_map<int, int> g_ctx_live;  // live contexts per device
 size_t g_bc_bytes = 0;
@@ -103,7 +104,8 @@ size_t bc_cap() {
 }
 bool bc_on() { return bc_cap() > 0; }
 
-void retire_events_locked(bool wait) {
+void retire_events(bool wait) {
+  std::lock_guard<std::mutex> lk(g_ev_mu);
   for (size_t k = 0; k < g_ev_retired.size();) {
     hipEvent_t ev = g_ev_retired[k];
     if (wait) (void)hipEventSynchronize(ev);
@@ -138,14 +140,14 @@ size_t bc_trim_locked(int dev, size_t max_bytes, size_t max_count) {
     freed += b.bytes;
     g_bc.erase(g_bc.begin() + (ptrdiff_t)k);
   }
-  retire_events_locked(false);
+  retire_events(false);
   return freed;
 }
 }  // namespace
 
 ReleaseMark::~ReleaseMark() {
   if (ev == nullptr) return;
-  std::lock_guard<std::mutex> lk(g_bc_mu);
+  std::lock_guard<std::mutex> lk(g_ev_mu);
   g_ev_retired.push_back(ev);
 }
 

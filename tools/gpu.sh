@@ -30,7 +30,7 @@ pmc_run() {  # dir name "args" rocprof-args...
 for step in "$@"; do
   case "$step" in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
         --timeout-method thread -rf ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
       rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
       [ $rc -eq 0 ] || stop tests $rc ;;
