@@ -84,13 +84,30 @@ struct CachedBlock {
   int dev;
   std::shared_ptr<ReleaseMark> mark;  // null: unknown users, device sync before reuse
 };
-std::mutex g_bc_mu;
-std::vector<CachedBlock> g_bc;  // released, oldest first
-std::unordered_map<void*, std::pair<size_t, int>> g_bc_live;  // from block_alloc: size, device
-std::mutex g_ev_mu;  // guards g_ev_retired; taken after g_bc_mu (a mark may die under g_bc_mu)
-std::vector<hipEvent_t> g_ev_retired;  // marks' events, destroyed once complete
-std::unordered_map<int, int> g_ctx_live;  // live contexts per device
-size_t g_bc_bytes = 0;
+// The cache's state lives in one heap object that is never destroyed: objects (and their
+// marks) may still be released while static destructors run at process exit.
+struct CacheState {
+  std::mutex mu;
+  std::vector<CachedBlock> blocks;  // released, oldest first
+  std::unordered_map<void*, std::pair<size_t, int>> live;  // from block_alloc: size, device
+  std::mutex ev_mu;  // guards ev_retired; taken after mu (a mark may die under mu)
+  std::vector<hipEvent_t> ev_retired;  // marks' events, destroyed once complete
+  std::unordered_map<int, int> ctx_per_dev;  // live contexts per device
+  std::unordered_map<const m3d_ctx*, uint64_t> ctx_ids;  // live contexts and their ids
+  uint64_t next_id = 1;
+  size_t bytes = 0;
+};
+CacheState& cache_state() {
+  static CacheState* p = new CacheState();
+  return *p;
+}
+std::mutex& g_bc_mu = cache_state().mu;
+std::vector<CachedBlock>& g_bc = cache_state().blocks;
+std::unordered_map<void*, std::pair<size_t, int>>& g_bc_live = cache_state().live;
+std::mutex& g_ev_mu = cache_state().ev_mu;
+std::vector<hipEvent_t>& g_ev_retired = cache_state().ev_retired;
+std::unordered_map<int, int>& g_ctx_live = cache_state().ctx_per_dev;
+size_t& g_bc_bytes = cache_state().bytes;
 constexpr size_t kBcMaxCount = 64;
 thread_local std::shared_ptr<ReleaseMark> t_mark;  // the active ReleaseScope's mark
 
@@ -245,9 +262,14 @@ void ctx_touch(m3d_ctx* ctx, hipStream_t st) {
   if (hipEventRecord(ev, st) != hipSuccess) ctx->uses_lost = true;
 }
 
-ReleaseScope::ReleaseScope(m3d_ctx* ctx) {
+ReleaseScope::ReleaseScope(m3d_ctx* ctx, uint64_t ctx_id) {
   prev = t_mark;
   std::shared_ptr<ReleaseMark> m;
+  if (ctx != nullptr) {  // a destroyed context (e.g. Python teardown order): no mark, device sync
+    std::lock_guard<std::mutex> lk(g_bc_mu);
+    auto it = cache_state().ctx_ids.find(ctx);
+    if (it == cache_state().ctx_ids.end() || it->second != ctx_id) ctx = nullptr;
+  }
   if (ctx != nullptr && !ctx->uses_lost) {
     m = std::make_shared<ReleaseMark>();
     if (!ctx->uses.empty()) {
@@ -270,6 +292,16 @@ ReleaseScope::ReleaseScope(m3d_ctx* ctx) {
 }
 
 ReleaseScope::~ReleaseScope() { t_mark = prev; }
+
+void ctx_register(m3d_ctx* ctx, bool live) {
+  std::lock_guard<std::mutex> lk(g_bc_mu);
+  if (live) {
+    ctx->id = cache_state().next_id++;
+    cache_state().ctx_ids[ctx] = ctx->id;
+  } else {
+    cache_state().ctx_ids.erase(ctx);
+  }
+}
 
 void ctx_count(int dev, int delta) {
   std::lock_guard<std::mutex> lk(g_bc_mu);
@@ -483,6 +515,7 @@ int m3d_create(int device, m3d_ctx** out) {
     m3d_destroy(ctx);
     return M3D_ERR_OOM;
   }
+  ctx_register(ctx, true);
   ctx_count(device, +1);
   ctx->counted = true;
   *out = ctx;
@@ -511,6 +544,7 @@ void m3d_destroy(m3d_ctx* ctx) {
     }
   const int dev = ctx->device;
   const bool counted = ctx->counted;
+  if (counted) ctx_register(ctx, false);
   delete ctx;
   if (counted) ctx_count(dev, -1);  // the device's last context gives the block cache back
 }
@@ -1069,6 +1103,7 @@ int cloud_create(m3d_ctx* ctx, const double* xyz, const double* normals, int64_t
   Touch tch{ctx, st};
   m3d_cloud* c = new m3d_cloud();
   c->ctx = ctx;
+  c->ctx_id = ctx->id;
   c->n = n;
   c->n_pad = round_up(std::max<int64_t>(n, 1), kCloudPad);
   int rc = M3D_OK;
@@ -1125,7 +1160,7 @@ void m3d_cloud_destroy(m3d_cloud* c) {
   if (!c) return;
   // the blocks go back to the cache marked after every stream the context used (stream-ordered
   // reuse, no device sync)
-  ReleaseScope rs(c->ctx);
+  ReleaseScope rs(c->ctx, c->ctx_id);
   for (Grid* g : c->grids) {
     grid_free(g);
     delete g;
@@ -1194,6 +1229,7 @@ int ensure_morton_source(m3d_ctx* ctx, const m3d_cloud* c, double cell, const m3
   // straight from the points (grid.hip morton_source: the slots without the source's cell grid)
   m3d_cloud* mc = new m3d_cloud();
   mc->ctx = ctx;
+  mc->ctx_id = ctx->id;
   Grid* g = new Grid();
   mc->grids.push_back(g);
   hipError_t e = morton_source(c, cell, mc, g, &ctx->tmp, nullptr);

@@ -175,13 +175,14 @@ struct Touch {
 // blocks released while a scope is alive carry its mark (m3d_cloud_destroy, m3d_icp_destroy)
 struct ReleaseScope {
   std::shared_ptr<ReleaseMark> prev;
-  explicit ReleaseScope(m3d_ctx* ctx);
+  ReleaseScope(m3d_ctx* ctx, uint64_t ctx_id);  // ctx_id: m3d_ctx::id when the object was made
   ~ReleaseScope();
 };
 hipError_t block_alloc(void** p, size_t bytes, hipStream_t st = nullptr);
 void block_release(void* p);
 size_t block_cache_trim(int dev);  // free the cached blocks of device dev; returns bytes freed
 void ctx_count(int dev, int delta);  // live contexts per device (the last one trims the cache)
+void ctx_register(m3d_ctx* ctx, bool live);  // the live-context registry (ReleaseScope checks it)
 // hipMalloc that trims the block cache and retries once on out-of-memory
 hipError_t dev_malloc_raw(void** p, size_t bytes);
 template <class T>
@@ -255,6 +256,7 @@ struct m3d_ctx {
   bool uses_lost = false;  // an event could not be made: releases fall back to a device sync
   hipStream_t order = nullptr;
   bool counted = false;  // counted among its device's live contexts (api.cpp ctx_count)
+  uint64_t id = 0;       // unique per process (api.cpp ctx_register)
 };
 
 struct m3d_corrset {
@@ -275,6 +277,7 @@ struct m3d_corrset {
 
 struct m3d_cloud {
   m3d_ctx* ctx = nullptr;
+  uint64_t ctx_id = 0;  // ctx->id at creation (a cloud may outlive its context at teardown)
   int64_t n = 0, n_pad = 0;
   double* xyz64 = nullptr;  // n×3
   double* nrm64 = nullptr;  // n×3 or null
