@@ -110,17 +110,22 @@ __global__ __launch_bounds__(256) void center_pack_kernel(const double* __restri
   if (threadIdx.x == 0) maxpart[blockIdx.x] = s[0];
 }
 
-// Cloud packing (m3d_cloud_create): the mean from sum3_kernel's partials reduced on the device in
-// the host's order (partial b = 0, 1, … per axis, then ÷ n: the same double), then the centred
-// fp32 copy with, per block, max |x_c|∞ and the per-axis min / max of the fp32 coordinates (the
-// grid bounds, grid.hip minmax3_kernel's values) — one host sync for the whole cloud.
-__global__ void mean3_final_kernel(const double* __restrict__ part, int blocks, int64_t n,
-                                   double* __restrict__ c) {
-  if (threadIdx.x != 0) return;
+// Cloud packing (m3d_cloud_create): the mean from sum3_kernel's partials reduced on the device by
+// one wave in a fixed order (lane l adds partials l, l + 64, …, then a fixed xor butterfly; every
+// lane ends with the same bits), ÷ n; then the centred fp32 copy with, per block, max |x_c|∞ and
+// the per-axis min / max of the fp32 coordinates (the grid bounds, grid.hip minmax3_kernel's
+// values) — one host sync for the whole cloud.  (Round 4 summed the partials in one thread:
+// 384 dependent loads, 13-19 µs per cloud.)
+__global__ __launch_bounds__(64) void mean3_final_kernel(const double* __restrict__ part, int blocks, int64_t n,
+                                                         double* __restrict__ c) {
+  const int l = threadIdx.x;
   double o[3] = {0.0, 0.0, 0.0};
-  for (int b = 0; b < blocks; ++b)
+  for (int b = l; b < blocks; b += 64)
     for (int k = 0; k < 3; ++k) o[k] += part[3 * b + k];
-  for (int k = 0; k < 3; ++k) c[k] = o[k] / (double)n;
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1)
+    for (int k = 0; k < 3; ++k) o[k] += __shfl_xor(o[k], m, 64);
+  if (l < 3) c[l] = o[l] / (double)n;
 }
 
 __global__ __launch_bounds__(256) void cloud_pack_kernel(const double* __restrict__ a, int64_t n,

@@ -533,6 +533,10 @@ def main():
                 cfg3["grid"] = sec
             del lp
         del s3c, t3c
+        # the same pair from nothing (H2D + centring, grids, Morton copy, records; the 1M cold
+        # path of refine_registration, which Open3D pays per call with its KD-tree build)
+        if rank == 0 and world == 1:
+            cfg3["cold"] = bench_cold(args, s3, t3, nr3, r, it3, reps=2, nns=("grid",), tag="cfg3")
 
     # ------------------------------------------------------------------ cfg2: RANSAC
     ransac = None
@@ -730,8 +734,8 @@ def main():
         dist.destroy_process_group()
 
 
-def bench_cold(args, src, tgt, nrm, r, iters, reps=3):
-    """cfg1 from nothing on the device: per-stage wall ms (median of `reps` after one warm call)."""
+def bench_cold(args, src, tgt, nrm, r, iters, reps=3, nns=("brute", "grid"), tag="cfg1"):
+    """A pair from nothing on the device: per-stage wall ms (median of `reps` after one warm call)."""
     import numpy as np
     import torch
 
@@ -765,9 +769,9 @@ def bench_cold(args, src, tgt, nrm, r, iters, reps=3):
         t1 = time.perf_counter()
         return (t1 - t0) * 1e3, res
 
-    out = {"workload": f"cfg1 pair {len(src)}<->{len(tgt)}, {iters} iterations, every device object built "
+    out = {"workload": f"{tag} pair {len(src)}<->{len(tgt)}, {iters} iterations, every device object built "
                        "inside the timed region"}
-    for nn in ("brute", "grid"):
+    for nn in nns:
         once(nn)
         runs = [once(nn) for _ in range(reps)]
         out[nn] = {k: float(np.median([x[k] for x in runs])) for k in runs[0]}
