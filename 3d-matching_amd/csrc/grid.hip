@@ -79,13 +79,15 @@ __global__ __launch_bounds__(kGridBlock) void cell_id_kernel(const float4* __res
   val[i] = (int32_t)i;
 }
 
-// points per cell (integer atomics: the counts, and so the starts, do not depend on the order);
-// start = the exclusive scan of the counts (hipcub), start[ncells] = n.  Round 4 ran a binary
-// search over all n keys per cell: up to 207 µs at 1M points, against one O(n) + O(ncells) pass.
-__global__ __launch_bounds__(kGridBlock) void cell_count_kernel(const uint32_t* __restrict__ key, int64_t n,
-                                                                int32_t* __restrict__ cnt) {
+// Cell starts from the sorted keys without a search: the last point of each cell's run writes
+// its end position into end[cell + 1] (end zeroed first), and start = the inclusive MAX scan of
+// end (hipcub): start[c] = the end of the last occupied cell before c = the number of points whose
+// cell is < c, start[ncells] = n.  Round 4 ran a binary search over all n keys for every cell: up
+// to 207 µs at 1M points.
+__global__ __launch_bounds__(kGridBlock) void cell_end_kernel(const uint32_t* __restrict__ key, int64_t n,
+                                                              int32_t* __restrict__ end) {
   const int64_t k = (int64_t)blockIdx.x * kGridBlock + threadIdx.x;
-  if (k < n) atomicAdd(&cnt[key[k]], 1);
+  if (k < n && (k == n - 1 || key[k] != key[k + 1])) end[(int64_t)key[k] + 1] = (int32_t)(k + 1);
 }
 
 // occupied cells: sorted positions that start a new cell
@@ -167,13 +169,16 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     }
   }
   grid_merge_lanes<kL>(k1, k1d, n2);
+  // deferral mode: an ambiguous query (the terms pass's test, nnkey.h winner_fp64) is decided in
+  // fp64 by grid_nn_heavy_kernel too — a dense cluster makes whole waves ambiguous, and the terms
+  // pass resolves a wave's queries one after another.  (Deciding them here in the scan for every
+  // loop was measured in round 5: the scan grew by what the terms pass saved)
+  const float X = kDefer && i >= 0 && k1 != key0 ? search_bound(key_d2(k1), be, r2_hi) : -1.0f;
+  const bool amb = X >= 0.0f && n2 <= X;
   if (i >= 0 && sub == 0) {
     keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
     near2[i] = __float_as_uint(n2);
-    // deferral mode: an ambiguous query (the terms pass's test, nnkey.h winner_fp64) is decided in
-    // fp64 by grid_nn_heavy_kernel too — a dense cluster makes whole waves ambiguous, and the
-    // terms pass resolves a wave's queries one after another
-    if (kDefer && k1 != key0 && n2 <= search_bound(key_d2(k1), be, r2_hi)) {
+    if (kDefer && amb) {
       const uint32_t slot = atomicAdd(hcnt, 1u);
 #ifdef M3D_DEBUG_GUARDS
       if ((int64_t)slot >= ns) printf("[guard] amb slot %u >= ns %lld (t %lld)\n", slot, (long long)ns, (long long)t); else
@@ -632,7 +637,7 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   size_t scan_bytes = 0;
   e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, g->order, (int)n, 0, bits, st);
   if (e == hipSuccess)
-    e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, cnt, g->start, (int)(total + 1), st);
+    e = hipcub::DeviceScan::InclusiveScan(nullptr, scan_bytes, cnt, g->start, hipcub::Max(), (int)(total + 1), st);
   if (e != hipSuccess) return e;
   tmp_bytes = std::max<size_t>({tmp_bytes, scan_bytes, 1});  // the sort's and the scan's temporaries
   const size_t a4 = tmp_align(sizeof(uint32_t) * (size_t)n);
@@ -660,10 +665,12 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   const unsigned blocks = (unsigned)((n + kGridBlock - 1) / kGridBlock);
   if ((e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t)(total + 1), st)) != hipSuccess) return done(e);
   cell_id_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, n, d, kin, vin);
-  cell_count_kernel<<<blocks, kGridBlock, 0, st>>>(kin, n, cnt);
   if ((e = hipGetLastError()) != hipSuccess) return done(e);
   e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, g->order, (int)n, 0, bits, st);
-  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, g->start, (int)(total + 1), st);
+  if (e == hipSuccess) {
+    cell_end_kernel<<<blocks, kGridBlock, 0, st>>>(kout, n, cnt);
+    e = hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, cnt, g->start, hipcub::Max(), (int)(total + 1), st);
+  }
   if (e != hipSuccess) return done(e);
   grid_gather_kernel<<<blocks, kGridBlock, 0, st>>>(xyz32, g->order, n, g->pts);
   e = hipGetLastError();

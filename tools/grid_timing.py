@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Grid-NN ICP timing at cfg1 (100k x 100k) and cfg3's per-rank geometry (1M sources x one 125k
+"""Grid-NN ICP timing (AB_LIB=path: another build of libm3d.so) at cfg1 (100k x 100k) and cfg3's per-rank geometry (1M sources x one 125k
 target shard) and 1M x 1M: per-launch averages of the NN and terms kernels (library HIP events).
 Usage: python tools/grid_timing.py [iters]"""
 import sys
@@ -9,7 +9,12 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "3d-matching_amd"))
 import numpy as np
 import torch
 
+import os
+
 from m3d import _lib, synth
+
+if os.environ.get("AB_LIB"):  # time another build of the library (tools/ab/*.so)
+    _lib.LIB_PATH = Path(os.environ["AB_LIB"]).resolve()
 from m3d.core import Cloud, IcpLoop, context
 
 it = int(sys.argv[1]) if len(sys.argv) > 1 else 20
