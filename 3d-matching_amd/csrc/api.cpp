@@ -18,7 +18,8 @@
 #include "m3d_internal.h"
 
 namespace m3d {
-hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st);
+hipError_t launch_icp_reset(const m3d_icp* s, const double* T, bool apply_init, hipStream_t st);
+hipError_t launch_copy_points(const m3d_icp* s, double* dst, hipStream_t st);
 hipError_t launch_icp_terms_solve(const m3d_icp* s, bool reset_keys, hipStream_t st);
 hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStream_t st);
 int64_t terms_blocks(int64_t ns);
@@ -1268,7 +1269,7 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = 
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->sgrid, s->tgrid, off, s->state, s->keys,
                           s->near2, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st, q0, q1,
-                          s->hlist, s->hcnt, s->cand_cap, s->src->xyz64, s->tgt->xyz64);
+                          s->hlist, s->hcnt, s->cand_cap, s->pcd64, s->tgt->xyz64);
   }
   if (!seeded) {
     hipError_t e = launch_icp_keyinit(s, off, st, q0, q1);
@@ -1398,11 +1399,11 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
   {
     const size_t n1 = (size_t)std::max<int64_t>(src->n, 1);
     const size_t nh = s->cand_cap > 0 ? n1 : 0;
-    const size_t sz[10] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
+    const size_t sz[11] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
                            sizeof(double) * (size_t)(s->nblocks * kTermSlots + kTermSlots), 4 * nh,
-                           2 * sizeof(uint32_t)};
-    size_t off[10], tot = 0;
-    for (int k = 0; k < 10; ++k) {
+                           2 * sizeof(uint32_t), 24 * n1};
+    size_t off[11], tot = 0;
+    for (int k = 0; k < 11; ++k) {
       off[k] = tot;
       tot += tmp_align(sz[k]);
     }
@@ -1426,6 +1427,7 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
       s->corr = reinterpret_cast<int32_t*>(b + off[6]);
       s->partials = reinterpret_cast<double*>(b + off[7]);
       s->sums = s->partials + s->nblocks * kTermSlots;
+      s->pcd64 = reinterpret_cast<double*>(b + off[10]);
       if (nh > 0) {  // count + ticket start at zero; grid_nn_heavy_kernel re-zeroes them
         s->hlist = reinterpret_cast<int32_t*>(b + off[8]);
         s->hcnt = reinterpret_cast<uint32_t*>(b + off[9]);
@@ -1459,7 +1461,20 @@ void m3d_icp_destroy(m3d_icp* s) {
   delete s;
 }
 
-int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
+namespace {
+// Eigen's Matrix4d::isIdentity() (dummy precision 1e-12), as RegistrationICP tests its init:
+// |a_ii − 1| ≤ 1e-12·min(|a_ii|, 1), |a_ij| ≤ 1e-12
+bool eigen_is_identity(const double* T) {
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      const double a = T[4 * i + j];
+      if (i == j ? !(std::fabs(a - 1.0) <= 1e-12 * std::min(std::fabs(a), 1.0)) : !(std::fabs(a) <= 1e-12))
+        return false;
+    }
+  return true;
+}
+
+int icp_reset(m3d_icp* s, const double* init, bool open3d_init, void* stream) {
   if (!s) return M3D_ERR_INVALID;
   Touch tch{s->ctx, S(stream)};
   m3d_ctx* ctx = s->ctx;
@@ -1470,8 +1485,19 @@ int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) {
   HIPX(ctx, hipMemsetAsync(s->corr, 0xFF, sizeof(int32_t) * std::max<int64_t>(s->src->n, 1), st));
   // all-ones bits = a NaN distance: no bound seed until a target-shard exchange wrote dprev
   HIPX(ctx, hipMemsetAsync(s->dprev, 0xFF, sizeof(int64_t) * std::max<int64_t>(s->src->n, 1), st));
-  HIPX(ctx, launch_icp_reset(s, T, st));
+  // RegistrationICP (Registration.cpp): pcd = source; if (!init.isIdentity()) pcd.Transform(init)
+  HIPX(ctx, launch_icp_reset(s, T, !(open3d_init && eigen_is_identity(T)), st));
   s->keys_clean = false;
+  return M3D_OK;
+}
+}  // namespace
+
+int m3d_icp_reset(m3d_icp* s, const double* init, void* stream) { return icp_reset(s, init, true, stream); }
+
+int m3d_icp_copy_points(const m3d_icp* s, double* dst, void* stream) {
+  if (!s || (!dst && s->src->n > 0)) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
+  HIPX(s->ctx, launch_copy_points(s, dst, S(stream)));
   return M3D_OK;
 }
 
@@ -1674,7 +1700,10 @@ int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream) {
   IcpState h;
   HIPX(ctx, hipMemcpyAsync(&h, s->state, sizeof(h), hipMemcpyDeviceToHost, S(stream)));
   HIPX(ctx, hipStreamSynchronize(S(stream)));
-  for (int k = 0; k < 16; ++k) out->T[k] = h.T[k];
+  for (int k = 0; k < 16; ++k) {
+    out->T[k] = h.T[k];
+    out->update[k] = h.dT[k];
+  }
   out->fitness = h.fitness;
   out->inlier_rmse = h.rmse;
   out->num_correspondences = h.count;
@@ -1783,7 +1812,7 @@ int m3d_nn1(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const doub
   int rc = icp_create(ctx, src, tgt, max_dist, &p, &s, true);
   if (rc) return rc;
   hipStream_t st = S(stream);
-  rc = m3d_icp_reset(s, T_host, stream);
+  rc = icp_reset(s, T_host, false, stream);  // the 1-NN of T·src for any T
   hipError_t e = hipSuccess;
   if (!rc) e = enqueue_nn(s, 0, st);
   if (e == hipSuccess) e = launch_nn_finalize(s, idx, d2, st);

@@ -277,7 +277,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
       }
     } else {
       double Q[3];
-      q64_of(s->T, src64 + 3 * i, Q);
+      q64_of(s->dT, src64 + 3 * i, Q);  // src64: the loop's points (dT·pcd64, icp.hip)
       double dl = kInf;
       int64_t jl = INT64_MAX;
       const float RX = sqrtf(X) * 1.001f;

@@ -58,7 +58,7 @@ struct FrameParams {
 
 // Refresh the fp32 search transform and radius bound for transform T (device side; T and
 // r2 = s->r2 passed in registers by the solve, which has them already).
-__device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const FrameParams& f) {
+__device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const FrameParams& f, int iters) {
   const double* cs = f.cs;
   const double* ct = f.ct;
   const double pinf = f.pinf, qinf = f.qinf;
@@ -73,16 +73,21 @@ __device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const
   }
   // E: per-coordinate bound on |fp32 query − fp64 query| + |fp32 target − fp64 target| in the
   // centred frame: the fp32 roundings of p_c, R, t' and the three fmas (≤ 5u·Σ|r||p| + 4u|t'|),
-  // the target's u|t_c|, and the fp64 evaluation of the contract's query Q (nnkey.h q64_of) in
-  // absolute coordinates (≤ 4 roundings of 2⁻⁵³ of the magnitudes involved)
+  // the target's u|t_c|, and the fp64 query Q of the contract against T·p: Q is the source
+  // transformed update by update (Open3D's pcd.Transform(update), IcpState::dT), so each of the
+  // iters + 1 applications adds ≤ 4 roundings of 2⁻⁵³ of the magnitudes involved; the updates
+  // are rotations to fp64 accuracy, which carry the earlier errors over without growth in the
+  // 2-norm (√3 per coordinate).  The last term covers an init within 1e-12 of the identity,
+  // which Open3D does not apply to the points (Eigen isIdentity) while T = init.
   double tabs = 0.0, csinf = 0.0, ctinf = 0.0;
   for (int i = 0; i < 3; ++i) {
     tabs = fmax(tabs, fabs(T[4 * i + 3]));
     csinf = fmax(csinf, fabs(cs[i]));
     ctinf = fmax(ctinf, fabs(ct[i]));
   }
+  const double mag = rowl1 * (csinf + pinf) + tabs + ctinf + qinf;
   const double E = 8.0 * kU * (rowl1 * pinf + tinf + qinf) +
-                   8.0 * kU64 * (rowl1 * (csinf + pinf) + tabs + ctinf + qinf);
+                   8.0 * kU64 * 1.7320508075688772 * (double)(iters + 2) * mag + 1e-11 * (mag + 1.0);
   // nnkey.h: |√d2f − |Q − t|| ≤ e_q + 3u√d2f with e_q = √3·E; band_of's absolute term 2·e_q
   const double eq = 1.7320508075688772 * E * 1.01;
   const float eqf = __double2float_ru(eq), bef = __double2float_ru(2.0 * eq * 1.01);
@@ -128,17 +133,24 @@ __device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const
 __device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
   double T[16];
   for (int k = 0; k < 16; ++k) T[k] = s->T[k];
-  refresh_rt32_from(s, T, s->r2, f);
+  refresh_rt32_from(s, T, s->r2, f, s->iters);
 }
 
+__device__ __forceinline__ void set_identity(double* M) {
+  for (int k = 0; k < 16; ++k) M[k] = (k % 5 == 0) ? 1.0 : 0.0;
+}
+
+// apply_init: the points start as init·p (the loop's pcd64 holds p, dT = init); 0: as p (dT = I),
+// Open3D's RegistrationICP for an init that isIdentity() — T still starts at init
 __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, double T3, double T4,
                                 double T5, double T6, double T7, double T8, double T9, double T10,
-                                double T11, double r2, FrameParams f) {
+                                double T11, double r2, FrameParams f, int apply_init) {
   if (threadIdx.x != 0) return;
   const double T[12] = {T0, T1, T2, T3, T4, T5, T6, T7, T8, T9, T10, T11};
   for (int k = 0; k < 12; ++k) s->T[k] = T[k];
   s->T[12] = s->T[13] = s->T[14] = 0.0;
   s->T[15] = 1.0;
+  for (int k = 0; k < 16; ++k) s->dT[k] = apply_init ? s->T[k] : ((k % 5 == 0) ? 1.0 : 0.0);
   s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
@@ -152,7 +164,7 @@ __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, do
 // state for evaluating transform T (device, row-major 4×4): feature-RANSAC validation (a6)
 __global__ void icp_set_T_kernel(IcpState* s, const double* __restrict__ T, double r2, FrameParams f) {
   if (threadIdx.x != 0) return;
-  for (int k = 0; k < 16; ++k) s->T[k] = T[k];
+  for (int k = 0; k < 16; ++k) s->T[k] = s->dT[k] = T[k];  // the loop's pcd64 holds p
   s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
@@ -173,7 +185,7 @@ __global__ __launch_bounds__(64) void val_states_kernel(IcpState* __restrict__ s
   if (k >= n) return;
   IcpState* s = states + k;
   const double* Th = T + 16 * (int64_t)list[k];
-  for (int j = 0; j < 16; ++j) s->T[j] = Th[j];
+  for (int j = 0; j < 16; ++j) s->T[j] = s->dT[j] = Th[j];  // validation reads the source itself
   s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
@@ -807,7 +819,8 @@ __device__ __forceinline__ void terms_add(double (&acc)[30], const double (&Q)[3
 //    the global winner (INT32_MAX none), whose fp64 d² every rank knows from dmin; the rank
 //    owning the target adds its terms.  dmin is kept in dprev for the next bound seeds.
 struct TermsArgs {
-  const double* src64;
+  double* pcd64;          // the loop's fp64 points: the query is dT·pcd64[i], written back (Open3D's
+                          // pcd.Transform(update): the next update applies to these)
   const float4* src32;
   int64_t ns;
   const double* tgt64;
@@ -869,7 +882,9 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
       }
       if (a.dprev != nullptr) a.dprev[ii[u]] = dm;
     }
-    q64_of(s->T, a.src64 + 3 * ii[u], vs[u]);
+    q64_of(s->dT, a.pcd64 + 3 * ii[u], vs[u]);
+    if (valid[u])
+      for (int k = 0; k < 3; ++k) a.pcd64[3 * ii[u] + k] = vs[u][k];
   }
   if (a.claim == nullptr) {
 #pragma unroll
@@ -971,7 +986,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_kernel(TermsArgs a, const I
 // (winner_fp64 over the shard's targets) → lidx / ld64 and the exchange key dkey = bits(d64)
 // (INT64_MAX none; d64 ≥ +0, so the integer MIN over ranks is the fp64 minimum).
 __global__ __launch_bounds__(256) void shard_winner_kernel(
-    const double* __restrict__ src64, const float4* __restrict__ src32, int64_t ns,
+    const double* __restrict__ pcd64, const float4* __restrict__ src32, int64_t ns,
     const double* __restrict__ tgt64, int64_t nt_shard, int64_t off, GridDev g,
     const IcpState* __restrict__ s, const int64_t* __restrict__ keys,
     const uint32_t* __restrict__ near2, int32_t* __restrict__ lidx, int64_t* __restrict__ ld64,
@@ -981,7 +996,7 @@ __global__ __launch_bounds__(256) void shard_winner_kernel(
   const bool valid = i0 < ns;
   const int64_t i = valid ? i0 : 0;
   double Q[3];
-  q64_of(s->T, src64 + 3 * i, Q);
+  q64_of(s->dT, pcd64 + 3 * i, Q);
   int64_t gj;
   double d;
   winner_fp64(valid, valid ? (uint64_t)keys[i] : (uint64_t)kKeyNone,
@@ -1150,11 +1165,14 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   for (int k = 0; k < 16; ++k) finite = finite && isfinite(upd[k]);
   if (!finite)
     for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  // T ← ΔT·T and the points ← ΔT·points (applied by the next evaluation's query, IcpState::dT)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s->dT[k] = upd[k];
   matmul4(upd, T, T);
 #pragma unroll
   for (int k = 0; k < 16; ++k) s->T[k] = T[k];
   s->iters = iters + 1;
-  refresh_rt32_from(s, T, r2, sp.f);
+  refresh_rt32_from(s, T, r2, sp.f, iters + 1);
 }
 
 __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
@@ -1237,7 +1255,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
 }
 
 // finalize standalone NN (m3d_nn1): the fp64 winner (nnkey.h winner_fp64) and its d64
-__global__ __launch_bounds__(256) void nn_finalize_kernel(const double* __restrict__ src64,
+__global__ __launch_bounds__(256) void nn_finalize_kernel(const double* __restrict__ pcd64,
                                                           const float4* __restrict__ src32,
                                                           int64_t ns,
                                                           const double* __restrict__ tgt64,
@@ -1252,7 +1270,7 @@ __global__ __launch_bounds__(256) void nn_finalize_kernel(const double* __restri
   const bool valid = i0 < ns;
   const int64_t i = valid ? i0 : 0;
   double Q[3];
-  q64_of(s->T, src64 + 3 * i, Q);
+  q64_of(s->dT, pcd64 + 3 * i, Q);
   int64_t gj;
   double d;
   winner_fp64(valid, valid ? (uint64_t)keys[i] : (uint64_t)kKeyNone,
@@ -1373,15 +1391,40 @@ static FrameParams frame_of(const m3d_icp* s) {
   return f;
 }
 
-hipError_t launch_icp_reset(const m3d_icp* s, const double* T, hipStream_t st) {
+// the loop's fp64 points start as the source itself (the init, if applied, is dT)
+static hipError_t reset_points(const m3d_icp* s, hipStream_t st) {
+  if (s->src->n == 0) return hipSuccess;
+  return hipMemcpyAsync(s->pcd64, s->src->xyz64, sizeof(double) * 3 * s->src->n, hipMemcpyDeviceToDevice, st);
+}
+
+hipError_t launch_icp_reset(const m3d_icp* s, const double* T, bool apply_init, hipStream_t st) {
+  hipError_t e = reset_points(s, st);
+  if (e != hipSuccess) return e;
   icp_init_kernel<<<1, 64, 0, st>>>(s->state, T[0], T[1], T[2], T[3], T[4], T[5], T[6], T[7],
                                     T[8], T[9], T[10], T[11], s->max_dist * s->max_dist,
-                                    frame_of(s));
+                                    frame_of(s), apply_init ? 1 : 0);
   return hipGetLastError();
 }
 
 hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t st) {
+  hipError_t e = reset_points(s, st);
+  if (e != hipSuccess) return e;
   icp_set_T_kernel<<<1, 64, 0, st>>>(s->state, T_dev, s->max_dist * s->max_dist, frame_of(s));
+  return hipGetLastError();
+}
+
+__global__ void scatter3_f64_kernel(const double* __restrict__ v, const int32_t* __restrict__ slot, int64_t n,
+                                    double* __restrict__ dst) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const int64_t o = slot != nullptr ? (int64_t)slot[k] : k;
+  for (int c = 0; c < 3; ++c) dst[3 * o + c] = v[3 * k + c];
+}
+
+hipError_t launch_copy_points(const m3d_icp* s, double* dst, hipStream_t st) {
+  const int64_t n = s->src->n;
+  if (n == 0) return hipSuccess;
+  scatter3_f64_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s->pcd64, s->src->slot, n, dst);
   return hipGetLastError();
 }
 
@@ -1515,7 +1558,7 @@ hipError_t ensure_target_rec(const m3d_cloud* c, hipStream_t st) {
 static TermsArgs terms_args(const m3d_icp* s, int64_t off, const int32_t* claim,
                             const int64_t* dmin, bool reset_keys) {
   TermsArgs a;
-  a.src64 = s->src->xyz64;
+  a.pcd64 = s->pcd64;
   a.src32 = s->src->xyz32;
   a.ns = s->src->n;
   a.tgt64 = s->tgt->xyz64;
@@ -1612,7 +1655,7 @@ hipError_t launch_nn_finalize(const m3d_icp* s, int32_t* idx, double* d2, hipStr
   const int64_t ns = s->src->n;
   if (ns == 0) return hipSuccess;
   nn_finalize_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(
-      s->src->xyz64, s->src->xyz32, ns, s->tgt->xyz64, s->tgt->n, s->tgrid->dev, s->state, s->keys,
+      s->pcd64, s->src->xyz32, ns, s->tgt->xyz64, s->tgt->n, s->tgrid->dev, s->state, s->keys,
       s->near2, s->src->slot, idx, d2);
   return hipGetLastError();
 }
@@ -1639,7 +1682,7 @@ hipError_t launch_shard_winner(const m3d_icp* s, int64_t off, int64_t* dkey, hip
   const int64_t ns = q1 < 0 ? s->src->n : q1;
   if (ns <= q0) return hipSuccess;
   shard_winner_kernel<<<(unsigned)((ns - q0 + 255) / 256), 256, 0, st>>>(
-      s->src->xyz64, s->src->xyz32, ns, s->tgt->xyz64, s->tgt->n, off, s->tgrid->dev, s->state,
+      s->pcd64, s->src->xyz32, ns, s->tgt->xyz64, s->tgt->n, off, s->tgrid->dev, s->state,
       s->keys, s->near2, s->lidx, s->ld64, dkey, q0);
   return hipGetLastError();
 }

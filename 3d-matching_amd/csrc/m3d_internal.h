@@ -79,6 +79,9 @@ struct IcpState {
   float band_e;         // 2·e_q·1.01: absolute term of nnkey.h band_of (fp32 → fp64 ambiguity)
   float eq;             // e_q: bound on |fp32 distance − fp64 distance| for the current T
   float eq_prev;        // e_q of the previous evaluation (seed_key bounds)
+  // the last update ΔT: an evaluation's fp64 queries are dT·pcd64[i] (Open3D transforms its copy
+  // of the source by every update, pcd.Transform(update)); I after a reset without init
+  double dT[16];
 };
 
 // Uniform grid over a cloud's centred fp32 points (grid.hip): kernel view + owner.
@@ -332,6 +335,8 @@ struct m3d_icp {
   int32_t cand_cap = 0;
   bool keys_clean = false;         // host view: every key is kKeyNone (fused tail reset them)
   int32_t* corr = nullptr;         // ns current correspondence (-1 none)
+  double* pcd64 = nullptr;         // ns×3: the source as Open3D's RegistrationICP holds it — the
+                                   // points after every update but the last (dT, IcpState)
   double* partials = nullptr;      // nblocks × kTermSlots
   double* sums = nullptr;          // kTermSlots
   int64_t nblocks = 0;

@@ -711,9 +711,27 @@ __global__ __launch_bounds__(kSBlock) void score_mfma_kernel(
       az.u = a16[buf][pa * 3][sub * 32 + c];
 #pragma unroll
       for (int g = 0; g < kSMG; ++g) {
+#ifndef M3D_SCORE_PRICE
+#define M3D_SCORE_PRICE 0  // pricing builds (timing only, wrong counts): 1 MFMA only, 2 VALU only
+#endif
+#if M3D_SCORE_PRICE == 2
+        s_floatx16 dx, dy, dz;  // the LDS operands' bits as stand-in residuals (no MFMA)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t w[4] = {ax.u.x, ax.u.y, ay.u.z, az.u.w};
+          dx[r] = __uint_as_float(w[r & 3] & 0x3FFFFFFFu);
+          dy[r] = __uint_as_float(w[(r + 1) & 3] & 0x3FFFFFFFu);
+          dz[r] = __uint_as_float(w[(r + 2) & 3] & 0x3FFFFFFFu);
+        }
+#else
         const s_floatx16 dx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax.h, bx[g], zacc, 0, 0, 0);
         const s_floatx16 dy = __builtin_amdgcn_mfma_f32_32x32x16_f16(ay.h, by[g], zacc, 0, 0, 0);
         const s_floatx16 dz = __builtin_amdgcn_mfma_f32_32x32x16_f16(az.h, bz[g], zacc, 0, 0, 0);
+#endif
+#if M3D_SCORE_PRICE == 1
+        outl[g] += __float_as_uint(dx[g]) ^ __float_as_uint(dy[5]) ^ __float_as_uint(dz[11]);
+        continue;
+#endif
         float v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = fnmsq(dz[r], fnmsq(dy[r], fnmsq(dx[r], t2r)));

@@ -243,6 +243,7 @@ typedef struct {
   int64_t num_correspondences;
   int32_t iterations; /* updates applied */
   int32_t converged;
+  double update[16];  /* the last update ΔT (identity after a reset), ABI 12 */
 } m3d_icp_result;
 
 /* registration_icp (icp.py:42-48 → Open3D RegistrationICP).  init [host] 16 f64.
@@ -257,7 +258,15 @@ int m3d_icp_run(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, const 
 int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
                    const m3d_icp_params* params, m3d_icp** out);
 void m3d_icp_destroy(m3d_icp* s);
+/* init [host] 16 f64 or NULL (identity).  As RegistrationICP (Registration.cpp): T starts at
+ * init, and the loop's copy of the source is transformed by init only when init is not
+ * Eigen-isIdentity() (|a − δ| ≤ 1e-12); every update ΔT then transforms that copy again
+ * (pcd.Transform(update)), and each evaluation's fp64 queries are those points (ABI 12: before,
+ * the queries were T·p of the original source). */
 int m3d_icp_reset(m3d_icp* s, const double* init_host, void* stream);
+/* The loop's fp64 points of the last evaluation (the source after init and every update but the
+ * one the evaluation produced), dst [device] ns×3 f64 in the caller's source order.  ABI 12. */
+int m3d_icp_copy_points(const m3d_icp* s, double* dst, void* stream);
 /* One full iteration on one device: NN evaluation + estimation terms + solve/update. */
 int m3d_icp_step(m3d_icp* s, void* stream);
 /* n iterations (n × m3d_icp_step, enqueued from native code: no per-iteration host binding
