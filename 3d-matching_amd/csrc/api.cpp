@@ -1702,7 +1702,7 @@ int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream) {
   HIPX(ctx, hipStreamSynchronize(S(stream)));
   for (int k = 0; k < 16; ++k) {
     out->T[k] = h.T[k];
-    out->update[k] = h.dT[k];
+    out->update[k] = h.last_upd[k];
   }
   out->fitness = h.fitness;
   out->inlier_rmse = h.rmse;

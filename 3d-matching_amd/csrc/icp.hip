@@ -151,6 +151,7 @@ __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, do
   s->T[12] = s->T[13] = s->T[14] = 0.0;
   s->T[15] = 1.0;
   for (int k = 0; k < 16; ++k) s->dT[k] = apply_init ? s->T[k] : ((k % 5 == 0) ? 1.0 : 0.0);
+  set_identity(s->last_upd);
   s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
@@ -165,6 +166,7 @@ __global__ void icp_init_kernel(IcpState* s, double T0, double T1, double T2, do
 __global__ void icp_set_T_kernel(IcpState* s, const double* __restrict__ T, double r2, FrameParams f) {
   if (threadIdx.x != 0) return;
   for (int k = 0; k < 16; ++k) s->T[k] = s->dT[k] = T[k];  // the loop's pcd64 holds p
+  set_identity(s->last_upd);
   s->fitness = s->rmse = s->prev_fitness = s->prev_rmse = 0.0;
   s->count = 0;
   s->evals = s->iters = s->done = s->converged = 0;
@@ -1167,7 +1169,7 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
     for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
   // T ← ΔT·T and the points ← ΔT·points (applied by the next evaluation's query, IcpState::dT)
 #pragma unroll
-  for (int k = 0; k < 16; ++k) s->dT[k] = upd[k];
+  for (int k = 0; k < 16; ++k) s->dT[k] = s->last_upd[k] = upd[k];
   matmul4(upd, T, T);
 #pragma unroll
   for (int k = 0; k < 16; ++k) s->T[k] = T[k];

@@ -79,9 +79,11 @@ struct IcpState {
   float band_e;         // 2·e_q·1.01: absolute term of nnkey.h band_of (fp32 → fp64 ambiguity)
   float eq;             // e_q: bound on |fp32 distance − fp64 distance| for the current T
   float eq_prev;        // e_q of the previous evaluation (seed_key bounds)
-  // the last update ΔT: an evaluation's fp64 queries are dT·pcd64[i] (Open3D transforms its copy
-  // of the source by every update, pcd.Transform(update)); I after a reset without init
+  // the transform the next evaluation applies to the loop's points: its fp64 queries are
+  // dT·pcd64[i], written back (Open3D transforms its copy of the source by every update,
+  // pcd.Transform(update)); after a reset, init (or I when init isIdentity()), then each ΔT
   double dT[16];
+  double last_upd[16];  // the last ΔT a solve produced (I since the reset): m3d_icp_result.update
 };
 
 // Uniform grid over a cloud's centred fp32 points (grid.hip): kernel view + owner.

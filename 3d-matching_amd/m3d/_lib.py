@@ -67,7 +67,8 @@ class FeatureRansacResult(C.Structure):
 
 class IcpResult(C.Structure):
     _fields_ = [("T", dbl * 16), ("fitness", dbl), ("inlier_rmse", dbl),
-                ("num_correspondences", i64), ("iterations", i32), ("converged", i32)]
+                ("num_correspondences", i64), ("iterations", i32), ("converged", i32),
+                ("update", dbl * 16)]
 
 
 # name -> (restype, argtypes)
@@ -118,6 +119,7 @@ SIGNATURES = {
     "m3d_icp_copy_corr": (C.c_int, [vp, vp, vp]),
     "m3d_corr_pairs": (C.c_int, [vp, vp, i64, vp, C.POINTER(i64), vp]),
     "m3d_icp_copy_slots": (C.c_int, [vp, vp, vp]),
+    "m3d_icp_copy_points": (C.c_int, [vp, vp, vp]),
     "m3d_voxel_down_sample": (C.c_int, [vp, vp, vp, i64, dbl, vp, vp, C.POINTER(i64), vp]),
     "m3d_hybrid_search": (C.c_int, [vp, vp, dbl, i32, vp, vp, vp, vp]),
     "m3d_estimate_normals": (C.c_int, [vp, vp, dbl, i32, vp, vp]),

@@ -439,6 +439,7 @@ class IcpOutcome:
     iterations: int
     converged: bool
     correspondence_set: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.int32))
+    update: np.ndarray = field(default_factory=lambda: np.eye(4))  # the last ΔT (I since reset)
 
 
 def corr_pairs(ctx: Context, corr, n: int) -> np.ndarray:
@@ -466,7 +467,8 @@ def icp(src: Cloud, tgt: Cloud, max_dist: float, init=None, estimation=_lib.EST_
                                           C.byref(res), ptr(corr), stream_handle()), "icp_run")
     cs = corr_pairs(src.ctx, corr, src.n) if with_correspondences else np.zeros((0, 2), np.int32)
     return IcpOutcome(np.array(res.T[:]).reshape(4, 4), res.fitness, res.inlier_rmse,
-                      res.num_correspondences, res.iterations, bool(res.converged), cs)
+                      res.num_correspondences, res.iterations, bool(res.converged), cs,
+                      np.array(res.update[:]).reshape(4, 4))
 
 
 class IcpLoop:
@@ -555,7 +557,17 @@ class IcpLoop:
         r = _lib.IcpResult()
         self.ctx.check(self.ctx.lib.m3d_icp_result_get(self.h, C.byref(r), stream_handle()), "icp_result")
         return IcpOutcome(np.array(r.T[:]).reshape(4, 4), r.fitness, r.inlier_rmse,
-                          r.num_correspondences, r.iterations, bool(r.converged))
+                          r.num_correspondences, r.iterations, bool(r.converged),
+                          update=np.array(r.update[:]).reshape(4, 4))
+
+    def points(self):
+        """The loop's fp64 points of the last evaluation (ns×3 f64 torch cuda, source order):
+        RegistrationICP's transformed copy of the source (init applied unless it isIdentity(),
+        then every update), from which that evaluation's correspondences and terms were taken."""
+        torch = _torch()
+        out = device_empty((max(self.src.n, 1), 3), torch.float64)
+        self.ctx.check(self.ctx.lib.m3d_icp_copy_points(self.h, ptr(out), stream_handle()), "icp_copy_points")
+        return out[: self.src.n]
 
     def source_slots(self):
         """Slot → source point index (int32 torch cuda): the loop holds its source in the Morton

@@ -979,14 +979,16 @@ def cpu_baseline(src, tgt, nrm, r, args, with_ransac):
     # ICP: Open3D-semantics iterations (KD-tree built once, like RegistrationICP)
     tree = cKDTree(tgt)
     T = np.eye(4)
+    pcd = I.initial_points(T, src)
     n_it = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < args.cpu_budget and n_it < 200:
-        pcd = I.transform_points(T, src)
         d, j = tree.query(pcd, k=1, workers=cores)
         ok = d * d < r * r
         corr = np.stack([np.nonzero(ok)[0], j[ok]], axis=1)
-        T = I.point_to_plane_update(pcd, tgt, nrm, corr) @ T
+        upd = I.point_to_plane_update(pcd, tgt, nrm, corr)
+        T = upd @ T
+        pcd = I.transform_points(upd, pcd)  # RegistrationICP: pcd.Transform(update)
         n_it += 1
     icp_el = time.perf_counter() - t0
     out = {"value": n_it / icp_el, "unit": "ICP iter/s (100k src x 100k tgt)", "cores": cores,

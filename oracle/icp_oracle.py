@@ -18,8 +18,11 @@ published algorithm (Open3D 0.19 ``pipelines/registration/Registration.cpp``,
   JTJ·x = −JTr (SolveLinearSystemPSD → LDLT), x → Rz(x2)·Ry(x1)·Rx(x0) | t = x[3:6]
   (TransformVector6dToMatrix4d); identity for an empty correspondence set.
 * ``point_to_point_update`` — Umeyama without scaling (Eigen::umeyama).
-* ``registration_icp``      — the RegistrationICP loop: Eval(init); for i < max_iteration:
-  update; T ← update·T; re-Eval; break when |Δfitness| < rel_fitness and |Δrmse| < rel_rmse.
+* ``registration_icp``      — the RegistrationICP loop (Registration.cpp): pcd = source, and
+  pcd.Transform(init) only when ``!init.isIdentity()`` (``is_identity``: Eigen's dummy precision
+  1e-12); Eval(pcd); for i < max_iteration: update from pcd; T ← update·T; pcd.Transform(update)
+  (INCREMENTAL — the points are the previous points moved by the update, not T·source); re-Eval;
+  break when |Δfitness| < rel_fitness and |Δrmse| < rel_rmse.
 
 PARITY UNPINNED against Open3D itself (no Open3D in this container, and the reference's tests
 pin no ICP output).  It is pinned instead by known-R|t recovery on synthetic pairs
@@ -50,6 +53,38 @@ def transform_points(T: np.ndarray, pts: np.ndarray) -> np.ndarray:
     for k in range(3):
         out[:, k] = ((T[k, 0] * x + T[k, 1] * y) + T[k, 2] * z) + T[k, 3]
     return out
+
+
+def is_identity(T: np.ndarray, prec: float = 1e-12) -> bool:
+    """Eigen's Matrix4d::isIdentity(): |a_ii − 1| ≤ prec·min(|a_ii|, 1), |a_ij| ≤ prec (i ≠ j)."""
+    T = np.asarray(T, np.float64)
+    for i in range(4):
+        for j in range(4):
+            a = T[i, j]
+            if i == j:
+                if not abs(a - 1.0) <= prec * min(abs(a), 1.0):
+                    return False
+            elif not abs(a) <= prec:
+                return False
+    return True
+
+
+def matmul4(A: np.ndarray, B: np.ndarray) -> np.ndarray:
+    """4×4 product with each entry summed ((a0·b0 + a1·b1) + a2·b2) + a3·b3 (no BLAS)."""
+    A = np.asarray(A, np.float64)
+    B = np.asarray(B, np.float64)
+    out = np.empty((4, 4))
+    for i in range(4):
+        for j in range(4):
+            out[i, j] = ((A[i, 0] * B[0, j] + A[i, 1] * B[1, j]) + A[i, 2] * B[2, j]) + A[i, 3] * B[3, j]
+    return out
+
+
+def initial_points(init: np.ndarray, src: np.ndarray) -> np.ndarray:
+    """RegistrationICP's pcd before the first evaluation: the source, transformed by init only
+    when init is not isIdentity()."""
+    src = np.asarray(src, np.float64).reshape(-1, 3)
+    return src.copy() if is_identity(init) else transform_points(init, src)
 
 
 def sq_dist(a: np.ndarray, b: np.ndarray) -> np.ndarray:
@@ -206,28 +241,30 @@ def point_to_point_update(src_t, tgt, corr) -> np.ndarray:
 def registration_icp(src, tgt, max_dist, init=None, tgt_normals=None, estimation="point_to_plane",
                      relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30):
     """RegistrationICP (Open3D 0.19).  Returns dict(transformation, fitness, inlier_rmse,
-    correspondence_set, iterations (updates applied), history of (fitness, rmse))."""
+    correspondence_set, iterations (updates applied), history of (fitness, rmse), points (the
+    last evaluation's pcd), update (the last update applied; I when none))."""
     if max_dist <= 0:
         raise ValueError("Invalid max_correspondence_distance.")
     if estimation == "point_to_plane" and tgt_normals is None:
         raise ValueError("TransformationEstimationPointToPlane requires target normals.")
     T = np.eye(4) if init is None else np.asarray(init, dtype=np.float64).copy()
     tree = cKDTree(tgt)
-    pcd = transform_points(T, src)
+    pcd = initial_points(T, src)
     fit, rmse, corr, _ = registration_result(pcd, tgt, max_dist, tree)
     hist = [(fit, rmse)]
     it = 0
+    upd = np.eye(4)
     for it in range(1, max_iteration + 1):
         if estimation == "point_to_plane":
             upd = point_to_plane_update(pcd, tgt, tgt_normals, corr)
         else:
             upd = point_to_point_update(pcd, tgt, corr)
-        T = upd @ T
-        pcd = transform_points(T, src)
+        T = matmul4(upd, T)
+        pcd = transform_points(upd, pcd)
         bfit, brmse = fit, rmse
         fit, rmse, corr, _ = registration_result(pcd, tgt, max_dist, tree)
         hist.append((fit, rmse))
         if abs(bfit - fit) < relative_fitness and abs(brmse - rmse) < relative_rmse:
             break
     return dict(transformation=T, fitness=fit, inlier_rmse=rmse, correspondence_set=corr,
-                iterations=it, history=hist)
+                iterations=it, history=hist, points=pcd, update=upd)

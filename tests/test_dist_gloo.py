@@ -42,13 +42,14 @@ class OracleShard:
 
     def reset(self, init):
         self.T = np.array(init, np.float64)
+        self.pcd = I.initial_points(self.T, self.src)  # RegistrationICP's copy of the source
         self.iters = 0
         self.evals = 0
         self.done = False
         self.fitness = self.rmse = 0.0
 
     def _local(self, off):
-        j, d2 = I.nn_exact(self.tree, self.tgt, I.transform_points(self.T, self.src), self.r)
+        j, d2 = I.nn_exact(self.tree, self.tgt, self.pcd, self.r)
         return np.where(j >= 0, j + off, -1), d2
 
     def shard_nn(self, off, dkeys):
@@ -86,7 +87,7 @@ class OracleShard:
         mine = (idx >= off) & (idx < off + len(self.tgt))
         i = np.nonzero(mine)[0]
         j = idx[mine] - off
-        pcd = I.transform_points(self.T, self.src)
+        pcd = self.pcd
         out = np.zeros(32)
         if len(i):
             JTJ, JTr, r2 = I.point_to_plane_terms(pcd, self.tgt, self.nrm, np.stack([i, j], 1))
@@ -112,7 +113,9 @@ class OracleShard:
             A = np.zeros((6, 6))
             A[np.triu_indices(6)] = s[:21]
             A = A + np.triu(A, 1).T
-            self.T = I.vec6_to_matrix(I.ldlt_solve(A, -s[21:27])) @ self.T
+            upd = I.vec6_to_matrix(I.ldlt_solve(A, -s[21:27]))
+            self.T = I.matmul4(upd, self.T)
+            self.pcd = I.transform_points(upd, self.pcd)  # pcd.Transform(update)
         self.iters += 1
 
     def result(self):

@@ -4,10 +4,12 @@
 NN contract (nnkey.h, icp_oracle.nn_exact): for every source point the exact lexicographic
 (d64, index) minimum over the targets with d64 < r², d64 the fp64 d² of the fp64 transformed
 point — checked BIT FOR BIT (indices and d²) against the oracle, for brute force and the grid.
-ICP transforms: the device reduces the fp64 terms in a different order than numpy, so a loop's
-transform differs from the oracle's by rounding (~1e-15); per-iteration correspondence sets are
-checked exactly against the oracle evaluated at the device's own transform
-(test_icp_cfg1_matches_oracle); whole runs within 1e-9 / fitness exactly where stated.
+ICP loops follow RegistrationICP's incremental points (pcd.Transform(init) unless init
+isIdentity(), then pcd.Transform(update) per iteration).  The device reduces the fp64 terms in a
+different order than numpy, so a loop's updates differ from the oracle's by rounding (~1e-15);
+per evaluation the device's points are checked bit for bit against its previous points moved by
+its own update, and its correspondence set against the oracle's exact NN of those points
+(_check_evaluations); whole runs within 1e-9 / fitness exactly where stated.
 """
 import numpy as np
 import pytest
@@ -503,50 +505,78 @@ def test_target_shard_duplicates_across_shards_lowest_index():
     assert np.all(ref_j < 4000)
 
 
+def _check_evaluations(lp, src, tgt, init, n_evals, r=0.12):
+    """Step lp n_evals times from reset(init).  At every evaluation the loop's points are
+    RegistrationICP's incremental pcd, BIT FOR BIT: the source (init applied unless it
+    isIdentity()) for the first, the previous points moved by the update the device produced
+    (pcd.Transform(update)) after that; its correspondence set is the oracle's exact fp64 NN of
+    those points, bit for bit."""
+    tree = cKDTree(tgt)
+    lp.reset(init)
+    want = I.initial_points(init, src)
+    for it in range(n_evals):
+        lp.step()
+        pts = lp.points().cpu().numpy()
+        np.testing.assert_array_equal(pts, want, err_msg=f"points, evaluation {it}")
+        ref_j, _ = I.nn_exact(tree, tgt, pts, r)
+        np.testing.assert_array_equal(lp.correspondences().cpu().numpy(), ref_j, err_msg=f"evaluation {it}")
+        want = I.transform_points(lp.result().update, pts)
+    return lp.result()
+
+
 @pytest.mark.parametrize("nn", ["brute", "grid"])
 def test_icp_cfg1_matches_oracle(nn):
     """cfg1 itself (bench.py's pair: 100k ↔ 100k, seed 0, r = 0.12, 50 fixed point-to-plane
-    iterations = 51 evaluations).  At every evaluation the device's correspondence set is the
-    oracle's exact fp64 NN at the device's own transform, bit for bit; the device's final
-    transform and fitness agree with the oracle's own 50-iteration run (the only difference is
-    the order of the fp64 term sums: measured ≲ 1e-15, bound stated 1e-9)."""
+    iterations = 51 evaluations), every evaluation checked by _check_evaluations; the device's
+    final transform and fitness agree with the oracle's own 50-iteration run (the only difference
+    is the order of the fp64 term sums: measured ≲ 1e-15, bound stated 1e-9)."""
     src, tgt, nrm, T_true = synth.icp_pair(100_000, 100_000, seed=0)
     lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
                  max_iteration=50, nn=nn)
-    lp.reset(np.eye(4))
-    tree = cKDTree(tgt)
-    for it in range(51):
-        T = lp.result().transformation
-        lp.step()
-        corr = lp.correspondences().cpu().numpy()
-        ref_j, _ = I.nn_exact(tree, tgt, I.transform_points(T, src), 0.12)
-        np.testing.assert_array_equal(corr, ref_j, err_msg=f"evaluation {it}")
-    r = lp.result()
+    r = _check_evaluations(lp, src, tgt, np.eye(4), 51)
     ref = I.registration_icp(src, tgt, 0.12, init=np.eye(4), tgt_normals=nrm, relative_fitness=-1,
                              relative_rmse=-1, max_iteration=50)
     assert r.iterations == ref["iterations"] == 50
     np.testing.assert_allclose(r.transformation, ref["transformation"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(lp.points().cpu().numpy(), ref["points"], rtol=0, atol=1e-9)
     assert r.fitness == ref["fitness"]
     assert abs(r.inlier_rmse - ref["inlier_rmse"]) < 1e-12
     np.testing.assert_allclose(r.transformation, T_true, atol=5e-4)
 
 
+@pytest.mark.parametrize("which", ["rigid", "fuzzy_identity"])
+def test_icp_init_applied_as_registration_icp(which):
+    """A non-identity init moves the loop's points before the first evaluation; an init within
+    Eigen's 1e-12 of I does not (the points stay the source's own bits), while T starts at init
+    either way (Registration.cpp)."""
+    src, tgt, nrm, _ = synth.icp_pair(30_000, 30_000, seed=6)
+    if which == "rigid":
+        init = synth.random_rigid(9, rot_range=0.01, trans_range=0.01)
+    else:
+        init = np.eye(4)
+        init[0, 3] = 5e-13
+        init[1, 2] = -3e-13
+    lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
+                 max_iteration=6, nn="grid")
+    r = _check_evaluations(lp, src, tgt, init, 7)
+    ref = I.registration_icp(src, tgt, 0.12, init=init, tgt_normals=nrm, relative_fitness=-1,
+                             relative_rmse=-1, max_iteration=6)
+    np.testing.assert_allclose(r.transformation, ref["transformation"], rtol=0, atol=1e-9)
+    assert r.fitness == ref["fitness"]
+    out = icp(Cloud(src), Cloud(tgt, nrm), 0.12, init, relative_fitness=-1, relative_rmse=-1,
+              max_iteration=6)
+    np.testing.assert_array_equal(out.transformation, r.transformation)
+    np.testing.assert_array_equal(out.update, r.update)
+
+
 def test_icp_cfg1_point_to_point_matches_oracle():
     """cfg1's pair with TransformationEstimationPointToPoint (a10: Umeyama over the 15 centred
-    sums, rotation_from_cov shared with a1), 30 fixed iterations, grid NN: correspondences
-    equal to the oracle's exact NN at every evaluation, final transform / fitness / rmse against
-    the oracle's own run."""
+    sums, rotation_from_cov shared with a1), 30 fixed iterations, grid NN: every evaluation
+    checked by _check_evaluations, final transform / fitness / rmse against the oracle's own run."""
     src, tgt, nrm, _ = synth.icp_pair(100_000, 100_000, seed=0)
     lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
                  max_iteration=30, nn="grid", estimation=_lib.EST_POINT_TO_POINT)
-    lp.reset(np.eye(4))
-    tree = cKDTree(tgt)
-    for it in range(31):
-        T = lp.result().transformation
-        lp.step()
-        ref_j, _ = I.nn_exact(tree, tgt, I.transform_points(T, src), 0.12)
-        np.testing.assert_array_equal(lp.correspondences().cpu().numpy(), ref_j, err_msg=f"evaluation {it}")
-    r = lp.result()
+    r = _check_evaluations(lp, src, tgt, np.eye(4), 31)
     ref = I.registration_icp(src, tgt, 0.12, init=np.eye(4), estimation="point_to_point",
                              relative_fitness=-1, relative_rmse=-1, max_iteration=30)
     assert r.iterations == ref["iterations"] == 30
