@@ -238,11 +238,20 @@ def point_to_point_update(src_t, tgt, corr) -> np.ndarray:
     return umeyama(src_t[corr[:, 0]], tgt[corr[:, 1]])
 
 
+def _report(on_eval, k, pcd, corr):
+    if on_eval is not None:
+        j = np.full(len(pcd), -1, np.int64)
+        j[corr[:, 0]] = corr[:, 1]
+        on_eval(k, pcd, j)
+
+
 def registration_icp(src, tgt, max_dist, init=None, tgt_normals=None, estimation="point_to_plane",
-                     relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30):
+                     relative_fitness=1e-6, relative_rmse=1e-6, max_iteration=30, on_eval=None):
     """RegistrationICP (Open3D 0.19).  Returns dict(transformation, fitness, inlier_rmse,
     correspondence_set, iterations (updates applied), history of (fitness, rmse), points (the
-    last evaluation's pcd), update (the last update applied; I when none))."""
+    last evaluation's pcd), update (the last update applied; I when none)).
+    on_eval(k, pcd, j): called at every evaluation k with its points and per-source winner
+    (-1 none) — the tests' per-evaluation comparison."""
     if max_dist <= 0:
         raise ValueError("Invalid max_correspondence_distance.")
     if estimation == "point_to_plane" and tgt_normals is None:
@@ -251,6 +260,7 @@ def registration_icp(src, tgt, max_dist, init=None, tgt_normals=None, estimation
     tree = cKDTree(tgt)
     pcd = initial_points(T, src)
     fit, rmse, corr, _ = registration_result(pcd, tgt, max_dist, tree)
+    _report(on_eval, 0, pcd, corr)
     hist = [(fit, rmse)]
     it = 0
     upd = np.eye(4)
@@ -263,6 +273,7 @@ def registration_icp(src, tgt, max_dist, init=None, tgt_normals=None, estimation
         pcd = transform_points(upd, pcd)
         bfit, brmse = fit, rmse
         fit, rmse, corr, _ = registration_result(pcd, tgt, max_dist, tree)
+        _report(on_eval, it, pcd, corr)
         hist.append((fit, rmse))
         if abs(bfit - fit) < relative_fitness and abs(brmse - rmse) < relative_rmse:
             break

@@ -505,7 +505,7 @@ def test_target_shard_duplicates_across_shards_lowest_index():
     assert np.all(ref_j < 4000)
 
 
-def _check_evaluations(lp, src, tgt, init, n_evals, r=0.12):
+def _check_evaluations(lp, src, tgt, init, n_evals, r=0.12, keep=None):
     """Step lp n_evals times from reset(init).  At every evaluation the loop's points are
     RegistrationICP's incremental pcd, BIT FOR BIT: the source (init applied unless it
     isIdentity()) for the first, the previous points moved by the update the device produced
@@ -519,9 +519,33 @@ def _check_evaluations(lp, src, tgt, init, n_evals, r=0.12):
         pts = lp.points().cpu().numpy()
         np.testing.assert_array_equal(pts, want, err_msg=f"points, evaluation {it}")
         ref_j, _ = I.nn_exact(tree, tgt, pts, r)
-        np.testing.assert_array_equal(lp.correspondences().cpu().numpy(), ref_j, err_msg=f"evaluation {it}")
+        corr = lp.correspondences().cpu().numpy()
+        np.testing.assert_array_equal(corr, ref_j, err_msg=f"evaluation {it}")
+        if keep is not None:
+            keep.append((pts, corr))
         want = I.transform_points(lp.result().update, pts)
     return lp.result()
+
+
+def _against_oracle_run(dev, src, tgt, nrm, r, n_iter, **kw):
+    """The oracle's own incremental run beside the device's evaluations (dev: [(points, corr)]):
+    per evaluation the number of correspondences that differ and the largest point difference
+    (the two runs' updates differ only by the order of the fp64 term sums).  Stated bound: 0
+    differing correspondences and ≤ 1e-12 per coordinate at every evaluation."""
+    diffs = []
+
+    def cmp(k, pcd, j):
+        pts, corr = dev[k]
+        diffs.append((k, int(np.count_nonzero(corr != j)), float(np.max(np.abs(pts - pcd)))))
+
+    ref = I.registration_icp(src, tgt, r, init=np.eye(4), tgt_normals=nrm, relative_fitness=-1,
+                             relative_rmse=-1, max_iteration=n_iter, on_eval=cmp, **kw)
+    assert len(diffs) == len(dev)
+    print("evaluation, correspondences differing from the incremental oracle, max |Δpoint|:")
+    print(" ".join(f"{k}:{n}/{d:.1e}" for k, n, d in diffs))
+    assert all(n == 0 for _, n, _ in diffs), diffs
+    assert max(d for _, _, d in diffs) <= 1e-12, diffs
+    return ref
 
 
 @pytest.mark.parametrize("nn", ["brute", "grid"])
@@ -533,9 +557,9 @@ def test_icp_cfg1_matches_oracle(nn):
     src, tgt, nrm, T_true = synth.icp_pair(100_000, 100_000, seed=0)
     lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
                  max_iteration=50, nn=nn)
-    r = _check_evaluations(lp, src, tgt, np.eye(4), 51)
-    ref = I.registration_icp(src, tgt, 0.12, init=np.eye(4), tgt_normals=nrm, relative_fitness=-1,
-                             relative_rmse=-1, max_iteration=50)
+    dev = []
+    r = _check_evaluations(lp, src, tgt, np.eye(4), 51, keep=dev)
+    ref = _against_oracle_run(dev, src, tgt, nrm, 0.12, 50)
     assert r.iterations == ref["iterations"] == 50
     np.testing.assert_allclose(r.transformation, ref["transformation"], rtol=0, atol=1e-9)
     np.testing.assert_allclose(lp.points().cpu().numpy(), ref["points"], rtol=0, atol=1e-9)
@@ -576,9 +600,9 @@ def test_icp_cfg1_point_to_point_matches_oracle():
     src, tgt, nrm, _ = synth.icp_pair(100_000, 100_000, seed=0)
     lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
                  max_iteration=30, nn="grid", estimation=_lib.EST_POINT_TO_POINT)
-    r = _check_evaluations(lp, src, tgt, np.eye(4), 31)
-    ref = I.registration_icp(src, tgt, 0.12, init=np.eye(4), estimation="point_to_point",
-                             relative_fitness=-1, relative_rmse=-1, max_iteration=30)
+    dev = []
+    r = _check_evaluations(lp, src, tgt, np.eye(4), 31, keep=dev)
+    ref = _against_oracle_run(dev, src, tgt, None, 0.12, 30, estimation="point_to_point")
     assert r.iterations == ref["iterations"] == 30
     np.testing.assert_allclose(r.transformation, ref["transformation"], rtol=0, atol=1e-9)
     assert r.fitness == ref["fitness"]
