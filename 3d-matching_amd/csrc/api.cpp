@@ -404,14 +404,25 @@ int device_mean3(m3d_ctx* ctx, const double* a, int64_t n, double out[3], hipStr
 // A cloud's centre (mean, unless given), centred fp32 copy, rmax and grid bounds with ONE host
 // sync (ransac.hip cloud_pack_kernel); the same values as device_mean3 + center_pack + the grid
 // build's bounds pass, which took three syncs.  Temporaries from the context's arena.
+// mapped pinned memory of the context (pin_ensure): kernels write their few results into it and
+// the host reads them after one stream sync — no device-to-host copy (a pageable copy is a staging
+// blit plus its own wait: ≈ 20 µs per readback on the cold path)
+int pin_ensure(m3d_ctx* ctx);
+constexpr size_t kPinRead = 2048;  // the cold path's readbacks: cloud summary, grid occupancy
+template <class T>
+T* pin_read(const m3d_ctx* ctx, bool dev) {
+  return reinterpret_cast<T*>(static_cast<char*>(dev ? ctx->pin_dev : ctx->pin) + kPinRead);
+}
+
 int cloud_pack(m3d_ctx* ctx, m3d_cloud* c, int64_t n, bool mean, hipStream_t st) {
   c->rmax = 0.0;
   c->has_bounds = false;
   if (c->n_pad == 0) return M3D_OK;
+  int rc = pin_ensure(ctx);
+  if (rc) return rc;
   const int sblocks = 128;
   const int blocks = (int)std::min<int64_t>(1024, (c->n_pad + 255) / 256);
-  // [block sums | centre | block (rmax, lo, hi)]: the centre and the bounds partials adjacent, so
-  // that ONE device-to-host copy brings both back
+  // scratch [block sums | centre | block (rmax, lo, hi)]; the summary goes to pinned memory
   const size_t o_sum = 0, o_c = tmp_align(sizeof(double) * 3 * sblocks), o_p7 = o_c + tmp_align(3 * sizeof(double));
   const size_t bytes = o_p7 + tmp_align(sizeof(float) * 7 * blocks);
   hipError_t e = ctx->tmp.reserve(bytes);
@@ -421,31 +432,23 @@ int cloud_pack(m3d_ctx* ctx, m3d_cloud* c, int64_t n, bool mean, hipStream_t st)
   double* sum_part = reinterpret_cast<double*>(b + o_sum);
   float* p7 = reinterpret_cast<float*>(b + o_p7);
   const bool dmean = mean && n > 0;
+  double* pin_c = pin_read<double>(ctx, true);
+  float* pin7 = reinterpret_cast<float*>(pin_c + 3);
   if (dmean) e = launch_sum3(c->xyz64, n, sum_part, sblocks, st);
   if (e == hipSuccess)
     e = launch_cloud_pack(c->xyz64, n, c->n_pad, dmean ? sum_part : nullptr, sblocks, cdev, c->center, c->xyz32,
-                          kFar, p7, blocks, st);
-  const size_t span = o_p7 - o_c + sizeof(float) * 7 * (size_t)blocks;
-  std::vector<double> hb((span + sizeof(double) - 1) / sizeof(double));
-  if (e == hipSuccess) e = hipMemcpyAsync(hb.data(), b + o_c, span, hipMemcpyDeviceToHost, st);
+                          kFar, p7, blocks, pin_c, pin7, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return m3d_fail(ctx, M3D_ERR_HIP, hipGetErrorString(e));
-  const float* h = reinterpret_cast<const float*>(reinterpret_cast<const char*>(hb.data()) + (o_p7 - o_c));
+  const volatile double* hc = pin_read<double>(ctx, false);
+  const volatile float* h = reinterpret_cast<const volatile float*>(hc + 3);
   if (dmean)
-    for (int k = 0; k < 3; ++k) c->center[k] = hb[(size_t)k];
-  float m = 0.0f;
+    for (int k = 0; k < 3; ++k) c->center[k] = hc[k];
   for (int k = 0; k < 3; ++k) {
-    c->lo[k] = FLT_MAX;
-    c->hi[k] = -FLT_MAX;
+    c->lo[k] = h[1 + k];
+    c->hi[k] = h[4 + k];
   }
-  for (int bl = 0; bl < blocks; ++bl) {
-    m = std::max(m, h[7 * bl]);
-    for (int k = 0; k < 3; ++k) {
-      c->lo[k] = std::min(c->lo[k], h[7 * bl + 1 + k]);
-      c->hi[k] = std::max(c->hi[k], h[7 * bl + 4 + k]);
-    }
-  }
-  c->rmax = (double)m * (1.0 + 1e-6);
+  c->rmax = (double)h[0] * (1.0 + 1e-6);
   c->has_bounds = n > 0;
   return M3D_OK;
 }
@@ -1294,6 +1297,10 @@ int icp_shard_nn_range(m3d_icp* s, int64_t off, int64_t q0, int64_t q1, int64_t*
 namespace {
 int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
                const m3d_icp_params* params, m3d_icp** out, bool run_arena);
+constexpr int kLoopArrays = 11;
+struct LoopLayout {
+  bool heavy;
+};
 }
 
 int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double max_dist,
@@ -1302,6 +1309,38 @@ int m3d_icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, dou
 }
 
 namespace {
+// Dense target cells (a cell at ≈ r holding ≥ kHeavyCell points — e.g. the vertex fan at a
+// UV-sphere pole, ~30× the mean density): queries with more than kHeavyCand candidates are
+// deferred to grid_nn_heavy_kernel (one block per query) so that the few waves of such queries
+// do not set the launch time (cfg4: up to 250 µs per evaluation).  M3D_GRID_HEAVY=0: never,
+// =N: always, with cap N (tests).  Off on evenly dense clouds (cfg1's largest cell ≈ 20).
+int32_t heavy_cap(const m3d_icp_params* params, int64_t coarse_max_occ) {
+  constexpr int64_t kHeavyCell = 256;
+  constexpr int32_t kHeavyCand = 256;
+  static const int heavy_env = [] {
+    const char* e = getenv("M3D_GRID_HEAVY");
+    return e ? std::max(0, atoi(e)) : -1;
+  }();
+  if (params->nn_method != M3D_NN_GRID) return 0;
+  return heavy_env > 0 ? heavy_env : (heavy_env < 0 && coarse_max_occ >= kHeavyCell ? kHeavyCand : 0);
+}
+
+// the loop's arrays: state, keys, near2, dprev, ld64, lidx, corr, partials + sums, hlist, hcnt
+// (+ ticket), pcd64 — offsets into one block
+LoopLayout loop_layout(int64_t ns, int32_t cand_cap, size_t* off, size_t* tot) {
+  const size_t n1 = (size_t)std::max<int64_t>(ns, 1);
+  const size_t nh = cand_cap > 0 ? n1 : 0;
+  const size_t sz[kLoopArrays] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
+                                  sizeof(double) * (size_t)(terms_blocks(ns) * kTermSlots + kTermSlots), 4 * nh,
+                                  2 * sizeof(uint32_t), 24 * n1};
+  *tot = 0;
+  for (int k = 0; k < kLoopArrays; ++k) {
+    off[k] = *tot;
+    *tot += tmp_align(sz[k]);
+  }
+  return LoopLayout{nh > 0};
+}
+
 // run_arena: the loop's arrays come from the context's run arena (kept between calls) instead of
 // their own allocation — for the synchronous one-shot entry points (m3d_icp_run, m3d_nn1), whose
 // loop object dies inside the call: no hipMalloc / hipFree (≈0.2 ms, the free waits for the
@@ -1324,6 +1363,10 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
   const Grid *tg = nullptr, *sg = nullptr;
   const m3d_cloud* src_m = nullptr;
   int64_t coarse_max_occ = 0;  // most target points in one cell at cell ≈ r (grid NN)
+  int32_t cand_cap = 0;
+  size_t off[kLoopArrays] = {}, tot = 0;
+  LoopLayout layout{};
+  void* blk = nullptr;
   {
     // Grid NN: cell ≈ the search radius, a query visits 3 cells per axis.  Brute force: the
     // same grids only ORDER the points (targets and queries in cell order make the MFMA
@@ -1347,7 +1390,10 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
     // measured (tools/grid_cell_sweep.sh) 1M × 1M (m ≈ 33) 206 → 128 µs per scan at div 3;
     // cfg1 (m ≈ 3.9) and the 1M × 125k shard (m ≈ 4.7) are fastest at div 1.
     if (!grc && params->nn_method == M3D_NN_GRID) {
-      hipError_t e = grid_occupancy(const_cast<Grid*>(tg), &ctx->tmp, nullptr);  // one sync, once per grid
+      hipError_t e = pin_ensure(ctx) == M3D_OK ? hipSuccess : hipErrorOutOfMemory;
+      if (e == hipSuccess)  // one sync, once per grid
+        e = grid_occupancy(const_cast<Grid*>(tg), &ctx->tmp, nullptr, pin_read<unsigned long long>(ctx, true),
+                           pin_read<unsigned long long>(ctx, false));
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("grid occupancy: ") + hipGetErrorString(e));
     }
     if (!grc && params->nn_method == M3D_NN_GRID && tg->n_occ > 0) {
@@ -1360,16 +1406,28 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
       hipError_t e = build_mfma_tiles(tgt, const_cast<Grid*>(tg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("mfma tiles: ") + hipGetErrorString(e));
     }
+    // the loop's arrays in ONE block (from the block cache: a reused block's release mark is
+    // waited for on the null stream, and so covered by the sync below)
+    if (!grc) {
+      cand_cap = heavy_cap(params, coarse_max_occ);
+      layout = loop_layout(src->n, cand_cap, off, &tot);
+      if (!run_arena && block_alloc(&blk, tot, nullptr) != hipSuccess)
+        grc = m3d_fail(ctx, M3D_ERR_OOM, "device allocation failed (ICP loop arrays)");
+    }
     // the setup above ran asynchronously on the null stream: finish it before the loop object is
     // used on the caller's streams
     if (!grc) {
       hipError_t e = hipStreamSynchronize(nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("loop setup: ") + hipGetErrorString(e));
     }
-    if (grc) return grc;
+    if (grc) {
+      block_release(blk);
+      return grc;
+    }
   }
   m3d_icp* s = new m3d_icp();
   s->ctx = ctx;
+  s->ctx_id = ctx->id;
   s->src = src_m;
   src_m->refs += 1;  // the Morton copy stays cached while this loop runs on it
   s->user_src = src;
@@ -1381,59 +1439,32 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
   // brute-force query order: the Morton slots themselves (compact 64-query waves, contiguous
   // slot ranges for the split exchange of the target-shard loop)
   s->sgrid = sg;
-  // Dense target cells (a cell at ≈ r holding ≥ kHeavyCell points — e.g. the vertex fan at a
-  // UV-sphere pole, ~30× the mean density): queries with more than kHeavyCand candidates are
-  // deferred to grid_nn_heavy_kernel (one block per query) so that the few waves of such queries
-  // do not set the launch time (cfg4: up to 250 µs per evaluation).  M3D_GRID_HEAVY=0: never,
-  // =N: always, with cap N (tests).  Off on evenly dense clouds (cfg1's largest cell ≈ 20).
-  constexpr int64_t kHeavyCell = 256;
-  constexpr int32_t kHeavyCand = 256;
-  static const int heavy_env = [] {
-    const char* e = getenv("M3D_GRID_HEAVY");
-    return e ? std::max(0, atoi(e)) : -1;
-  }();
-  if (params->nn_method == M3D_NN_GRID)
-    s->cand_cap = heavy_env > 0 ? heavy_env : (heavy_env < 0 && coarse_max_occ >= kHeavyCell ? kHeavyCand : 0);
-  // the loop's arrays in ONE allocation (one hipMalloc instead of nine)
+  s->cand_cap = cand_cap;
   int rc = M3D_OK;
-  {
-    const size_t n1 = (size_t)std::max<int64_t>(src->n, 1);
-    const size_t nh = s->cand_cap > 0 ? n1 : 0;
-    const size_t sz[11] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
-                           sizeof(double) * (size_t)(s->nblocks * kTermSlots + kTermSlots), 4 * nh,
-                           2 * sizeof(uint32_t), 24 * n1};
-    size_t off[11], tot = 0;
-    for (int k = 0; k < 11; ++k) {
-      off[k] = tot;
-      tot += tmp_align(sz[k]);
-    }
-    char* b = nullptr;
-    if (run_arena) {
-      if (ctx->run.reserve(tot) == hipSuccess) b = ctx->run.base;
-    } else if (dev_malloc(&s->block, tot) == hipSuccess) {
-      b = static_cast<char*>(s->block);
-    } else {
-      s->block = nullptr;
-    }
-    if (b == nullptr) {
-      rc = m3d_fail(ctx, M3D_ERR_OOM, "device allocation failed (ICP loop arrays)");
-    } else {
-      s->state = reinterpret_cast<IcpState*>(b + off[0]);
-      s->keys = reinterpret_cast<int64_t*>(b + off[1]);
-      s->near2 = reinterpret_cast<uint32_t*>(b + off[2]);
-      s->dprev = reinterpret_cast<int64_t*>(b + off[3]);
-      s->ld64 = reinterpret_cast<int64_t*>(b + off[4]);
-      s->lidx = reinterpret_cast<int32_t*>(b + off[5]);
-      s->corr = reinterpret_cast<int32_t*>(b + off[6]);
-      s->partials = reinterpret_cast<double*>(b + off[7]);
-      s->sums = s->partials + s->nblocks * kTermSlots;
-      s->pcd64 = reinterpret_cast<double*>(b + off[10]);
-      if (nh > 0) {  // count + ticket start at zero; grid_nn_heavy_kernel re-zeroes them
-        s->hlist = reinterpret_cast<int32_t*>(b + off[8]);
-        s->hcnt = reinterpret_cast<uint32_t*>(b + off[9]);
-        if (hipMemset(s->hcnt, 0, 2 * sizeof(uint32_t)) != hipSuccess)
-          rc = m3d_fail(ctx, M3D_ERR_HIP, "loop arrays: deferral counter");
-      }
+  char* b = static_cast<char*>(blk);
+  if (run_arena) {
+    if (ctx->run.reserve(tot) == hipSuccess) b = ctx->run.base;
+  } else {
+    s->block = blk;
+  }
+  if (b == nullptr) {
+    rc = m3d_fail(ctx, M3D_ERR_OOM, "device allocation failed (ICP loop arrays)");
+  } else {
+    s->state = reinterpret_cast<IcpState*>(b + off[0]);
+    s->keys = reinterpret_cast<int64_t*>(b + off[1]);
+    s->near2 = reinterpret_cast<uint32_t*>(b + off[2]);
+    s->dprev = reinterpret_cast<int64_t*>(b + off[3]);
+    s->ld64 = reinterpret_cast<int64_t*>(b + off[4]);
+    s->lidx = reinterpret_cast<int32_t*>(b + off[5]);
+    s->corr = reinterpret_cast<int32_t*>(b + off[6]);
+    s->partials = reinterpret_cast<double*>(b + off[7]);
+    s->sums = s->partials + s->nblocks * kTermSlots;
+    s->pcd64 = reinterpret_cast<double*>(b + off[10]);
+    if (layout.heavy) {  // count + ticket start at zero; grid_nn_heavy_kernel re-zeroes them
+      s->hlist = reinterpret_cast<int32_t*>(b + off[8]);
+      s->hcnt = reinterpret_cast<uint32_t*>(b + off[9]);
+      if (hipMemset(s->hcnt, 0, 2 * sizeof(uint32_t)) != hipSuccess)
+        rc = m3d_fail(ctx, M3D_ERR_HIP, "loop arrays: deferral counter");
     }
   }
   if (rc) {
@@ -1454,7 +1485,10 @@ void m3d_icp_destroy(m3d_icp* s) {
     m3d_cloud* ms = const_cast<m3d_cloud*>(s->src);
     if (--ms->refs == 0 && ms->orphan) m3d_cloud_destroy(ms);  // its parent cloud is gone
   }
-  hipFree(s->block);  // state, keys, near2, dprev, ld64, lidx, corr, partials, sums
+  {
+    ReleaseScope rs(s->ctx, s->ctx_id);  // back to the block cache, marked after the loop's work
+    block_release(s->block);             // state, keys, near2, dprev, ld64, lidx, corr, partials, sums
+  }
   hipFree(s->xdk);
   hipFree(s->xcl);
   hipFree(s->xsums);

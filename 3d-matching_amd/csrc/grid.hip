@@ -336,8 +336,9 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
     __syncthreads();
   }
   // the list is consumed: the last block to finish zeroes the count (and this ticket) for the
-  // next launch — in the kernel, ordered with the launches around it (a host-enqueued 4-byte
-  // memset was measured not to be: back-to-back steps saw the previous step's count)
+  // next launch, so a loop needs no per-step memset node (the count is zeroed once at loop
+  // creation).  Round 4's per-scan hipMemsetAsync on the same stream was ordered too; the
+  // corrupted counts seen then are discussed in DESIGN §3.8 ("the round-4 hlist overflow").
   if (threadIdx.x == 0 &&
       __hip_atomic_fetch_add(hcnt + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
     __hip_atomic_store(hcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -680,7 +681,8 @@ hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t s
   return done(e);
 }
 
-hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st) {
+hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st, unsigned long long* pin_dev,
+                          const unsigned long long* pin_host) {
   if (g->occ_known) return hipSuccess;
   if (g->n_pts == 0 || g->dev.ncells == 0) {
     g->n_occ = 0;
@@ -703,12 +705,16 @@ hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st) {
   unsigned long long occ[2] = {0, 0};
   const int nb = (int)std::min<int64_t>(kOccBlocks, (g->n_pts + kGridBlock - 1) / kGridBlock);
   count_occupied_pts_kernel<<<(unsigned)nb, kGridBlock, 0, st>>>(g->pts, g->n_pts, g->dev, part);
-  occ_final_kernel<<<1, kOccBlocks, 0, st>>>(part, nb, cnt);
+  occ_final_kernel<<<1, kOccBlocks, 0, st>>>(part, nb, pin_dev != nullptr ? pin_dev : cnt);
   e = hipGetLastError();
-  if (e == hipSuccess) e = hipMemcpyAsync(occ, cnt, sizeof(occ), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && pin_dev == nullptr) e = hipMemcpyAsync(occ, cnt, sizeof(occ), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (ta == nullptr) hipFree(cnt);
   if (e != hipSuccess) return e;
+  if (pin_dev != nullptr) {
+    occ[0] = reinterpret_cast<const volatile unsigned long long*>(pin_host)[0];
+    occ[1] = reinterpret_cast<const volatile unsigned long long*>(pin_host)[1];
+  }
   g->n_occ = (int64_t)occ[0];
   g->max_occ = (int64_t)occ[1];
   g->occ_known = true;

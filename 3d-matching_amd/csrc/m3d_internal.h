@@ -315,6 +315,7 @@ struct m3d_cloud {
 
 struct m3d_icp {
   m3d_ctx* ctx = nullptr;
+  uint64_t ctx_id = 0;  // the context's registry id (release marks only while it lives)
   // the loop's source: the caller's cloud in Morton slot order (user_src->morton); every per-source
   // array below is indexed by slot, src->slot maps a slot to the caller's point index
   const m3d_cloud* src = nullptr;
@@ -397,7 +398,8 @@ hipError_t launch_center_pack(const double* a, int64_t n, int64_t n_pad, const d
 // lo[3], hi[3])
 hipError_t launch_cloud_pack(const double* a, int64_t n, int64_t n_pad, const double* sum_part,
                              int sum_blocks, double* cdev, const double c[3], float4* out, float pad_value,
-                             float* part7, int blocks, hipStream_t st);
+                             float* part7, int blocks, double* pin_c /*[3], mapped pinned*/,
+                             float* pin7 /*[7], mapped pinned*/, hipStream_t st);
 struct ScoreMf;
 // a4 batches: kabsch3_kernel also writes the MFMA screen's per-hypothesis operands (hyp16) for
 // the score launch that follows (thr/mode of that launch; no effect when it will not use them)
@@ -476,7 +478,10 @@ hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st
 hipError_t grid_build(const float4* xyz32, int64_t n, double cell, hipStream_t st, Grid* g,
                       TmpArena* ta = nullptr, const float* lohi = nullptr);
 // g->n_occ, counted on first use (one sync)
-hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st);
+// pin_dev / pin_host: 16 B of mapped pinned memory the counts are written to (no device-to-host
+// copy), or null (a copy into host memory)
+hipError_t grid_occupancy(Grid* g, TmpArena* ta, hipStream_t st, unsigned long long* pin_dev = nullptr,
+                          const unsigned long long* pin_host = nullptr);
 void grid_free(Grid* g);
 // prev/dprev/tgt32/nt_shard: seed each query with seed_key (nnkey.h); prev == nullptr: no seeds
 // qgrid: the query cloud's Morton-slot grid (its Morton-ordered points, morton_source)

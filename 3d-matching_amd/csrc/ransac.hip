@@ -178,6 +178,33 @@ __global__ __launch_bounds__(256) void cloud_pack_kernel(const double* __restric
   if (threadIdx.x < 7) part7[7 * blockIdx.x + threadIdx.x] = s[threadIdx.x][0];
 }
 
+// The cloud's host-side summary straight into mapped pinned memory (no device-to-host copy, the
+// host reads it after one stream sync): the centre (3 f64, when computed on the device) and the
+// max / min / max of the block partials — order-free, so the same bits as the host fold it replaces.
+__global__ __launch_bounds__(256) void cloud_summary_kernel(const float* __restrict__ part7, int blocks,
+                                                            const double* __restrict__ cdev,
+                                                            double* __restrict__ out_c, float* __restrict__ out7) {
+  __shared__ float s[7][256];
+  float v[7] = {0.0f, FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int b = threadIdx.x; b < blocks; b += 256) {
+    v[0] = fmaxf(v[0], part7[7 * b]);
+    for (int k = 1; k < 4; ++k) v[k] = fminf(v[k], part7[7 * b + k]);
+    for (int k = 4; k < 7; ++k) v[k] = fmaxf(v[k], part7[7 * b + k]);
+  }
+  for (int k = 0; k < 7; ++k) s[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      s[0][threadIdx.x] = fmaxf(s[0][threadIdx.x], s[0][threadIdx.x + w]);
+      for (int k = 1; k < 4; ++k) s[k][threadIdx.x] = fminf(s[k][threadIdx.x], s[k][threadIdx.x + w]);
+      for (int k = 4; k < 7; ++k) s[k][threadIdx.x] = fmaxf(s[k][threadIdx.x], s[k][threadIdx.x + w]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 7) out7[threadIdx.x] = s[threadIdx.x][0];
+  if (cdev != nullptr && threadIdx.x < 3) out_c[threadIdx.x] = cdev[threadIdx.x];
+}
+
 // ------------------------------------------------------------------------------- sampler
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -1039,12 +1066,13 @@ hipError_t launch_sum3(const double* a, int64_t n, double* partial, int blocks, 
 
 hipError_t launch_cloud_pack(const double* a, int64_t n, int64_t n_pad, const double* sum_part,
                              int sum_blocks, double* cdev, const double c[3], float4* out, float pad_value,
-                             float* part7, int blocks, hipStream_t st) {
+                             float* part7, int blocks, double* pin_c, float* pin7, hipStream_t st) {
   if (sum_part != nullptr) {  // mean on the device from sum3 partials (else c is given)
     mean3_final_kernel<<<1, 64, 0, st>>>(sum_part, sum_blocks, n, cdev);
   }
   cloud_pack_kernel<<<blocks, 256, 0, st>>>(a, n, n_pad, sum_part != nullptr ? cdev : nullptr, c[0], c[1], c[2],
                                             out, pad_value, part7);
+  cloud_summary_kernel<<<1, 256, 0, st>>>(part7, blocks, sum_part != nullptr ? cdev : nullptr, pin_c, pin7);
   return hipGetLastError();
 }
 
