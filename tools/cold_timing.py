@@ -1,4 +1,4 @@
-"""Cold cfg1 setup timing (bench.py bench_cold's stages, more repetitions): fresh device clouds,
+"""Cold cfg1 (--n 1000000: cfg3) setup timing (bench.py bench_cold's stages, more repetitions): fresh device clouds,
 then the ICP loop object (grids, Morton source copy, fp16 tiles, target records), per NN method.
 Prints one line per method: median ms of clouds / loop_create over --reps runs after one warm run.
 """
@@ -14,6 +14,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--n", type=int, default=100000, help="points per cloud (cfg3: 1000000)")
+    ap.add_argument("--nns", default="grid,brute")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -21,7 +23,7 @@ def main():
     from m3d import synth
     from m3d.core import Cloud, IcpLoop
 
-    src, tgt, nrm, _ = synth.icp_pair(100000, 100000, seed=0)
+    src, tgt, nrm, _ = synth.icp_pair(a.n, a.n, seed=0)
     r = 0.4 * 0.3
 
     def once(nn):
@@ -39,7 +41,7 @@ def main():
         t3 = time.perf_counter()
         return (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, res.transformation
 
-    for nn in ("grid", "brute"):
+    for nn in a.nns.split(","):
         once(nn)
         runs = [once(nn) for _ in range(a.reps)]
         T = runs[0][3]
