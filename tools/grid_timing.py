@@ -52,5 +52,5 @@ for name, ns, nt_all, shard in (("cfg1 100k x 100k", 100_000, 100_000, 1), ("1M 
     nn = nn_ms / n
     b = 28 * ns + 16 * nt
     print(f"{name}: grid_nn {nn * 1e3:.1f} us ({b / (nn * 1e-3) / 1e9:.0f} GB/s algorithmic, "
-          f"{b / (nn * 1e-3) / 8e12 * 100:.1f}% of 8 TB/s), terms {t_ms / tn * 1e3:.1f} us, iteration {wall_us:.1f} us (no kernel events), fitness {lp.result().fitness:.4f}",
+          f"{b / (nn * 1e-3) / 8e12 * 100:.1f}% of 8 TB/s), terms {t_ms / max(tn, 1) * 1e3:.1f} us, iteration {wall_us:.1f} us (no kernel events), fitness {lp.result().fitness:.4f}",
           flush=True)
