@@ -475,7 +475,7 @@ def main():
     # default convergence criteria).
     cfg1_cold = None
     if rank == 0 and world == 1:
-        cfg1_cold = bench_cold(args, src, tgt_all[:nt], nrm_all[:nt], r, iters)
+        cfg1_cold = bench_cold(args, src, tgt_all[:nt], nrm_all[:nt], r, iters, reps=7)
 
     # ------------------------------------------------------------------ cfg3: 1M <-> 1M, strong
     cfg3 = None
@@ -735,7 +735,8 @@ def main():
 
 
 def bench_cold(args, src, tgt, nrm, r, iters, reps=3, nns=("brute", "grid"), tag="cfg1"):
-    """A pair from nothing on the device: per-stage wall ms (median of `reps` after one warm call)."""
+    """A pair from nothing on the device: per-stage wall ms (median of `reps` after one warm call;
+    the refine leg median of `reps` as well)."""
     import numpy as np
     import torch
 
