@@ -180,6 +180,41 @@ def test_empty_source_icp_and_nn1(nn):
     src, _ = synth.surface_points(500, seed=3)
     idx, _ = nn1(Cloud(src), t, np.eye(4), 0.3, nn=nn)
     assert idx.numel() == 500
+    # the step-wise loop on the empty source: no points, the identity update, T = init
+    init = synth.random_rigid(3, rot_range=0.01, trans_range=0.01)
+    lp = IcpLoop(empty, t, 0.12, max_iteration=3, nn=nn)
+    lp.reset(init)
+    lp.steps(4)
+    r = lp.result()
+    assert lp.points().shape == (0, 3)
+    np.testing.assert_array_equal(r.update, np.eye(4))
+    np.testing.assert_array_equal(r.transformation, init)
+    assert r.fitness == 0.0
+
+
+def test_icp_result_update_and_points_api():
+    """IcpOutcome.update is the identity after a reset and then the last update a solve produced:
+    T_k = update_k · T_(k−1) (to rounding), the one-shot icp() reports the same update as the loop,
+    and the loop's points before any evaluation are the source itself, in the caller's order."""
+    src, tgt, nrm, _ = synth.icp_pair(20_000, 20_000, seed=12)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    lp = IcpLoop(s, t, 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=5, nn="grid")
+    lp.reset(np.eye(4))
+    np.testing.assert_array_equal(lp.result().update, np.eye(4))
+    np.testing.assert_array_equal(lp.points().cpu().numpy(), src)  # before the first evaluation
+    prev = lp.result().transformation
+    for _ in range(5):
+        lp.step()
+        r = lp.result()
+        np.testing.assert_allclose(r.transformation, r.update @ prev, rtol=0, atol=1e-14)
+        prev = r.transformation
+    lp.step()  # the 6th evaluation ends the run (max_iteration): no update, T and update kept
+    r = lp.result()
+    assert r.iterations == 5
+    np.testing.assert_array_equal(r.transformation, prev)
+    out = icp(s, t, 0.12, np.eye(4), relative_fitness=-1, relative_rmse=-1, max_iteration=5)
+    np.testing.assert_array_equal(out.update, lp.result().update)
+    np.testing.assert_array_equal(out.transformation, lp.result().transformation)
 
 
 def test_morton_copies_stay_bounded_per_cloud():

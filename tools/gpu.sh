@@ -1,6 +1,7 @@
 #!/bin/bash
 # The one GPU-box script (run through gpurun):  bash tools/gpu.sh STEP [STEP ...]
-#   tests    pytest -m gpu, one process, per-test timeout ($PYTEST_ARGS)  -> gpurun_out/pytest_gpu.log
+#   tests    pytest -m gpu, one process, per-test timeout ($PYTEST_ARGS; $PYTEST_K: a -k expression)
+#            -> gpurun_out/pytest_gpu.log
 #   smoke    __graft_entry__.smoke()                                       -> gpurun_out/smoke.log
 #   bench    bench.py $BENCH_ARGS                                          -> gpurun_out/bench.log
 #   launch   bench.py --gpus 2 on this one-GPU box: must refuse (exit != 0, no JSON line)
@@ -31,7 +32,7 @@ for step in "$@"; do
   case "$step" in
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
-        --timeout-method thread -rf ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+        --timeout-method thread -rf ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
       rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
       [ $rc -eq 0 ] || stop tests $rc ;;
     smoke)
