@@ -143,12 +143,15 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
   float k1d = kInf, n2 = kInf;
   int64_t i = -1;
   if (t < ns) {
+    // qpts are the loop's Morton copy (morton_copy_kernel: w = position = slot), so i = t, and the
+    // previous correspondence is loaded beside the point instead of after it
+    i = t;
+    const int32_t pj = prev != nullptr ? prev[t] : -1;
     const float4 p = qpts[t];
-    i = (int64_t)__float_as_int(p.w);
     float qx, qy, qz;
     xform32(s->Rt32, p, qx, qy, qz);
     // seed: the previous correspondence re-evaluated (nnkey.h seed_key), or a bound
-    const int64_t seed = seed_key(s, i, p, qx, qy, qz, tgt32, nt_shard, off, prev, dprev);
+    const int64_t seed = seed_key_j(s, pj, i, p, qx, qy, qz, tgt32, nt_shard, off, dprev);
     if (seed != kKeyNone) k1 = (uint64_t)seed;
     k1d = key_real_d2(k1);
     if (g.ncells > 0) {

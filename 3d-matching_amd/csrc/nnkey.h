@@ -306,13 +306,11 @@ __device__ __forceinline__ int64_t bound_key(const IcpState* __restrict__ s, flo
 //    band_of(B), which is the bound the scan screens with (search_bound), so the rank owning
 //    the new winner still finds it, and the MIN over ranks is unchanged.  Without the bound those
 //    ranks searched with r2_hi: on N ranks, N − 1 of every N queries.
-__device__ __forceinline__ int64_t seed_key(const IcpState* __restrict__ s, int64_t i, float4 p,
-                                            float qx, float qy, float qz,
-                                            const float4* __restrict__ tgt32, int64_t nt_shard,
-                                            int64_t off, const int32_t* __restrict__ prev,
-                                            const int64_t* __restrict__ dprev) {
-  if (prev == nullptr) return kKeyNone;
-  const int64_t j = (int64_t)prev[i];
+// (j = prev[i], loaded by the caller: the grid scan issues it beside the query's point load)
+__device__ __forceinline__ int64_t seed_key_j(const IcpState* __restrict__ s, int64_t j, int64_t i, float4 p,
+                                              float qx, float qy, float qz,
+                                              const float4* __restrict__ tgt32, int64_t nt_shard,
+                                              int64_t off, const int64_t* __restrict__ dprev) {
   if (j < 0) return kKeyNone;
   if (j >= off && j < off + nt_shard) {
     const float4 t = tgt32[j - off];
@@ -323,6 +321,15 @@ __device__ __forceinline__ int64_t seed_key(const IcpState* __restrict__ s, int6
   const int64_t dp = dprev[i];
   if (dp == kKeyNone) return kKeyNone;
   return bound_key(s, __double2float_ru(__longlong_as_double(dp)), p, qx, qy, qz);
+}
+
+__device__ __forceinline__ int64_t seed_key(const IcpState* __restrict__ s, int64_t i, float4 p,
+                                            float qx, float qy, float qz,
+                                            const float4* __restrict__ tgt32, int64_t nt_shard,
+                                            int64_t off, const int32_t* __restrict__ prev,
+                                            const int64_t* __restrict__ dprev) {
+  if (prev == nullptr) return kKeyNone;
+  return seed_key_j(s, (int64_t)prev[i], i, p, qx, qy, qz, tgt32, nt_shard, off, dprev);
 }
 
 }  // namespace m3d
