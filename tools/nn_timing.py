@@ -10,7 +10,12 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "3d-matching_amd"))
 import numpy as np
 import torch
 
+import os
+
 from m3d import _lib, synth
+
+if os.environ.get("AB_LIB"):  # time another build of the library (tools/ab_build.sh)
+    _lib.LIB_PATH = Path(os.environ["AB_LIB"]).resolve()
 from m3d.core import Cloud, IcpLoop, context
 
 it = int(sys.argv[1]) if len(sys.argv) > 1 else 20
