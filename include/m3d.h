@@ -265,7 +265,8 @@ void m3d_icp_destroy(m3d_icp* s);
  * the queries were T·p of the original source). */
 int m3d_icp_reset(m3d_icp* s, const double* init_host, void* stream);
 /* The loop's fp64 points of the last evaluation (the source after init and every update but the
- * one the evaluation produced), dst [device] ns×3 f64 in the caller's source order.  ABI 12. */
+ * one the evaluation produced; after a reset and before the first evaluation, the source itself),
+ * dst [device] ns×3 f64 in the caller's source order.  ABI 12. */
 int m3d_icp_copy_points(const m3d_icp* s, double* dst, void* stream);
 /* One full iteration on one device: NN evaluation + estimation terms + solve/update. */
 int m3d_icp_step(m3d_icp* s, void* stream);
