@@ -19,8 +19,12 @@ def main():
     a = ap.parse_args()
     import numpy as np
     import torch
+    from pathlib import Path
 
-    from m3d import synth
+    from m3d import _lib, synth
+
+    if os.environ.get("AB_LIB"):  # time another build of the library (tools/ab_build.sh)
+        _lib.LIB_PATH = Path(os.environ["AB_LIB"]).resolve()
     from m3d.core import Cloud, IcpLoop
 
     src, tgt, nrm, _ = synth.icp_pair(a.n, a.n, seed=0)
