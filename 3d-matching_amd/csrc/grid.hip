@@ -124,6 +124,10 @@ __global__ __launch_bounds__(kGridBlock) void grid_gather_kernel(const float4* _
 // one dependent load per point.  Blocks are remapped XCD-contiguously (blocks b and b + 8 share
 // an XCD's L2: each XCD gets one contiguous slice of the Morton order, so its L2 holds one
 // region's targets and cell starts instead of every region's).
+#if M3D_SCAN_CLOCK  // diagnostic builds only (tools/scan_clock.py): per-wave start / end of the
+                    // grid scan, s_memrealtime (100 MHz)
+__device__ unsigned long long g_scan_clock[2 * 65536];
+#endif
 template <int kL, int kR, int kB, bool kDefer = false>
 __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const float4* __restrict__ qpts, int64_t ns, GridDev g, int64_t off,
@@ -132,6 +136,9 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const float4* __restrict__ tgt32, int64_t nt_shard, int64_t nblocks, int64_t q0,
     int32_t* __restrict__ hlist, uint32_t* __restrict__ hcnt, int cand_cap) {
   if (s->done) return;
+#if M3D_SCAN_CLOCK
+  const unsigned long long clk0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int64_t per = (nblocks + 7) / 8;
   const int64_t blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
   if (blk >= nblocks) return;
@@ -189,6 +196,16 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
       hlist[slot] = (int32_t)t;
     }
   }
+#if M3D_SCAN_CLOCK
+  {
+    const unsigned long long clk1 = __builtin_amdgcn_s_memrealtime();
+    const int64_t gw = (int64_t)blockIdx.x * (kGridBlock / kWave) + threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0 && gw < 65536) {
+      g_scan_clock[2 * gw] = clk0;
+      g_scan_clock[2 * gw + 1] = clk1;
+    }
+  }
+#endif
 }
 
 // Deferred queries of grid_nn_batched_kernel<..., true>: those with more than cand_cap candidates
@@ -883,6 +900,13 @@ hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid
   return hipSuccess;
 }
 
+#if M3D_SCAN_CLOCK
+}  // namespace m3d
+extern "C" int m3d_debug_scan_clock(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(m3d::g_scan_clock), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+namespace m3d {
+#endif
 hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, const Grid* g,
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
                           const int32_t* prev, const int64_t* dprev, const float4* tgt32, int64_t nt_shard,
