@@ -426,7 +426,10 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
                          "traffic": pmc_traffic("grid_nn")[0], "avg_launch_ms": g_ms,
                          "launches": g_n, "bytes_per_launch": g_bytes,
-                         "terms_avg_launch_ms": g_terms_ms},
+                         "terms_avg_launch_ms": g_terms_ms,
+                         "note": "priced against HBM, but not HBM-bound: one resident round of "
+                                 "gather waves (~6 us each), the vector-memory data-return path "
+                                 "~70% busy (TD_TD_BUSY; DESIGN.md 3.8, profiles/r05_grid_scan)"},
         }
 
     # ------------------------------------------------------------------ cfg1 strong scaling
