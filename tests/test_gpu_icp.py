@@ -628,6 +628,28 @@ def test_icp_init_applied_as_registration_icp(which):
     np.testing.assert_array_equal(out.update, r.update)
 
 
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+@pytest.mark.parametrize("ns", [1, 2, 63, 65, 255, 257, 511, 513, 4097])
+def test_icp_ragged_sources_incremental_points(ns, nn):
+    """Ragged source counts around the wave (64), terms-block (256 / 512) and tile sizes: every
+    evaluation's points and correspondences as _check_evaluations requires (bit for bit), against
+    a 20k target, from a rigid init; the final transform against the oracle's run where the 6 × 6
+    system has full rank (ns ≥ 63: with 1–2 sources JTJ has rank ≤ 2, its other pivots are
+    rounding noise, and any two LDLT implementations return different, equally meaningless
+    solutions — Eigen's included)."""
+    src_all, tgt, nrm, _ = synth.icp_pair(20_000, 20_000, seed=23)
+    src = src_all[:ns].copy()
+    init = synth.random_rigid(ns, rot_range=0.005, trans_range=0.005)
+    lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1,
+                 max_iteration=4, nn=nn)
+    r = _check_evaluations(lp, src, tgt, init, 5)
+    ref = I.registration_icp(src, tgt, 0.12, init=init, tgt_normals=nrm, relative_fitness=-1,
+                             relative_rmse=-1, max_iteration=4)
+    if ns >= 63:
+        np.testing.assert_allclose(r.transformation, ref["transformation"], rtol=0, atol=1e-9)
+        assert r.fitness == ref["fitness"]
+
+
 def test_icp_cfg1_point_to_point_matches_oracle():
     """cfg1's pair with TransformationEstimationPointToPoint (a10: Umeyama over the 15 centred
     sums, rotation_from_cov shared with a1), 30 fixed iterations, grid NN: every evaluation
