@@ -1093,6 +1093,18 @@ __device__ __forceinline__ void solve_in(const IcpState* s, SolveIn& in) {
   for (int k = 0; k < 12; ++k) in.rt[k] = s->Rt32[k];
 }
 
+#if M3D_TAIL_CLOCK  // diagnostic builds only (tools/tail_clock.py): per-wave start / end of the
+                    // terms pass, then the last block's ticket, reduce and solve steps (100 MHz)
+__device__ unsigned long long g_tail_clock[2 * 4096 + 8];
+#define M3D_TCLK(k)                                                                   \
+  do {                                                                                \
+    if (threadIdx.x == 0) g_tail_clock[2 * 4096 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define M3D_TCLK(k) \
+  do {              \
+  } while (0)
+#endif
 __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp, const SolveIn& in) {
   double sm[30];
 #pragma unroll
@@ -1144,8 +1156,11 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
           ++k;
         }
       for (int a = 0; a < 6; ++a) b[a] = -sm[21 + a];
+      M3D_TCLK(3);
       ldlt6_solve(A, b, x);
+      M3D_TCLK(4);
       vec6_to_matrix_wave(x, upd);
+      M3D_TCLK(5);
     } else {
       const double n = count;
       double mp[3], mq[3], Hm[9], R[9];
@@ -1174,7 +1189,9 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
 #pragma unroll
   for (int k = 0; k < 16; ++k) s->T[k] = T[k];
   s->iters = iters + 1;
+  M3D_TCLK(6);
   refresh_rt32_from(s, T, r2, sp.f, iters + 1);
+  M3D_TCLK(7);
 }
 
 __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
@@ -1198,7 +1215,20 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
   // do_solve = 0: the sharded tail (m3d_icp_shard_terms) — terms + the fixed-order reduce into
   // `sums` in one launch; the caller all-reduces them and runs m3d_icp_solve
   if (s->done) return;
+#if M3D_TAIL_CLOCK
+  const unsigned long long clk0 = __builtin_amdgcn_s_memrealtime();
+#endif
   terms_block<true, kP>(a, s, partials);
+#if M3D_TAIL_CLOCK
+  {
+    const unsigned long long clk1 = __builtin_amdgcn_s_memrealtime();
+    const int64_t gw = (int64_t)blockIdx.x * (kTermsBlock / kWave) + threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0 && gw < 4096) {
+      g_tail_clock[2 * gw] = clk0;
+      g_tail_clock[2 * gw + 1] = clk1;
+    }
+  }
+#endif
   __shared__ double red[kReduceGroups][kTermSlots];
   __shared__ int last;
   // the partial went out write-through (sc1): drain it, then one lane takes the ticket
@@ -1211,6 +1241,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
   }
   __syncthreads();
   if (!last) return;
+  M3D_TCLK(0);
   SolveIn in;
   if (do_solve && threadIdx.x < kWave) solve_in(s, in);
   // every load of the other blocks' partials is an sc1 load (L2-coherent, bypasses L1)
@@ -1250,10 +1281,12 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     sums[threadIdx.x] = t;
   }
   __syncthreads();
+  M3D_TCLK(1);
   if (threadIdx.x < kWave) {
     if (threadIdx.x == 0) s->ticket = 0;
     if (do_solve) solve_state(red[0], s, sp, in);
   }
+  M3D_TCLK(2);
 }
 
 // finalize standalone NN (m3d_nn1): the fp64 winner (nnkey.h winner_fp64) and its d64
@@ -1709,3 +1742,9 @@ int64_t terms_blocks(int64_t ns) {
 }
 
 }  // namespace m3d
+
+#if M3D_TAIL_CLOCK
+extern "C" int m3d_debug_tail_clock(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(m3d::g_tail_clock), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif

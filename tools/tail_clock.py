@@ -1,0 +1,38 @@
+"""Timeline of the last fused ICP tail (terms_solve_kernel) of a cfg1 grid loop (diagnostic build:
+tools/ab_build.sh tclk -DM3D_TAIL_CLOCK=1, then AB_LIB=tools/ab/tclk.so python tools/tail_clock.py [grid|brute]):
+per-wave terms time, the last block's ticket, reduction and solve.  s_memrealtime ticks at 100 MHz."""
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "3d-matching_amd"))
+import numpy as np
+import torch
+
+from m3d import _lib, synth
+
+_lib.LIB_PATH = Path(os.environ["AB_LIB"]).resolve()
+from m3d.core import Cloud, IcpLoop, context
+
+torch.cuda.set_device(0)
+ctx = context()
+nn = sys.argv[1] if len(sys.argv) > 1 else "grid"
+src, tgt, nrm, _ = synth.icp_pair(100_000, 100_000, seed=0)
+lp = IcpLoop(Cloud(src), Cloud(tgt, nrm), 0.12, relative_fitness=-1, relative_rmse=-1, max_iteration=50, nn=nn)
+lp.reset(np.eye(4))
+lp.steps(20)
+torch.cuda.synchronize()
+buf = (C.c_ulonglong * (2 * 4096 + 8))()
+ctx.lib.m3d_debug_tail_clock(buf, C.c_int(2 * 4096 + 8))
+a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
+w = a[: 2 * 4096].reshape(-1, 2)
+w = w[w[:, 1] > 0]
+t0 = w[:, 0].min()
+st, en = (w[:, 0] - t0) * 1e-2, (w[:, 1] - t0) * 1e-2
+du = en - st
+tk, rd, sv, l0, l1, v6, mm, rf = [(a[2 * 4096 + k] - t0) * 1e-2 for k in range(8)]
+print(f"{nn}: waves {len(w)}; start max {st.max():.2f} us; terms per wave mean {du.mean():.2f} p90 "
+      f"{np.percentile(du, 90):.2f} max {du.max():.2f}; last wave done {en.max():.2f}; ticket won {tk:.2f}; "
+      f"reduced {rd:.2f}; solved {sv:.2f} us | solve: ldlt in {l0:.2f} out {l1:.2f}, vec6 {v6:.2f}, "
+      f"T stored {mm:.2f}, refresh {rf:.2f}")
