@@ -1402,6 +1402,10 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
       const int div = std::min(4, std::max(1, (int)std::floor(std::sqrt(m / 3.5))));
       if (div > 1) grc = ensure_grid(ctx, tgt, cell / div, nullptr, &tg);
     }
+    if (!grc) {  // the terms pass's fp64 walk for ambiguous queries (nnkey.h resolve_wave)
+      hipError_t e = build_grid_pts64(tgt, const_cast<Grid*>(tg), nullptr);
+      if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("grid fp64 points: ") + hipGetErrorString(e));
+    }
     if (!grc && params->nn_method == M3D_NN_BRUTE && tg->mf16 == nullptr) {
       hipError_t e = build_mfma_tiles(tgt, const_cast<Grid*>(tg), nullptr);
       if (e != hipSuccess) grc = m3d_fail(ctx, M3D_ERR_HIP, std::string("mfma tiles: ") + hipGetErrorString(e));

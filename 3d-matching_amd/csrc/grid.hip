@@ -759,6 +759,9 @@ void grid_free(Grid* g) {
   g->minv = nullptr;
   block_release(g->mf16);
   block_release(g->mf32);
+  block_release(g->pts64);
+  g->pts64 = nullptr;
+  g->dev.pts64 = nullptr;
   g->start = nullptr;
   g->pts = nullptr;
   g->order = nullptr;

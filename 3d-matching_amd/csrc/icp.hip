@@ -849,6 +849,17 @@ struct TermsArgs {
 // source's key / runner-up / fp64 point (or claim / dmin), (2) after the fp64 decision, every
 // winner's fp64 target (and normal); the rare ambiguous queries are resolved by the whole wave in
 // between (nnkey.h resolve_wave, one ballot when there are none).
+#if M3D_TAIL_CLOCK  // diagnostic builds only (tools/tail_clock.py): per-wave start / end of the
+                    // terms pass, the last block's ticket, reduce and solve steps (100 MHz), and
+                    // per wave the number of ambiguous queries it resolved
+__device__ unsigned long long g_tail_clock[3 * 4096 + 8];
+#endif
+#ifndef M3D_WALK64
+#define M3D_WALK64 1  // build_grid_pts64 (0: resolve_wave gathers fp64 points after an fp32 screen)
+#endif
+#ifndef M3D_AMB_SKIP
+#define M3D_AMB_SKIP 0  // timing only (wrong winners on ambiguous queries): their cost
+#endif
 template <bool kWT, int kP>
 __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* __restrict__ s,
                                             double* __restrict__ partials) {
@@ -899,7 +910,15 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
       // candidate (k1's target) re-evaluated in fp64 after the batched target loads below
       const float X = valid[u] && k1[u] != (uint64_t)kKeyNone ? search_bound(key_d2(k1[u]), s->band_e, s->r2_hi)
                                                               : -1.0f;
-      const bool amb = X >= 0.0f && n2[u] <= X;
+      const bool amb = !M3D_AMB_SKIP && X >= 0.0f && n2[u] <= X;
+#if M3D_TAIL_CLOCK
+      {
+        const int64_t gw = (int64_t)blockIdx.x * (kTermsBlock / kWave) + threadIdx.x / kWave;
+        const int na = __popcll(__ballot(amb));
+        if ((threadIdx.x & (kWave - 1)) == 0 && gw < 4096)
+          g_tail_clock[2 * 4096 + 8 + gw] = (u == 0 ? 0ull : g_tail_clock[2 * 4096 + 8 + gw]) + na;
+      }
+#endif
       float qx = 0.0f, qy = 0.0f, qz = 0.0f;
       if (amb) xform32(s->Rt32, a.src32[ii[u]], qx, qy, qz);
       int64_t bj = -1;
@@ -1093,9 +1112,7 @@ __device__ __forceinline__ void solve_in(const IcpState* s, SolveIn& in) {
   for (int k = 0; k < 12; ++k) in.rt[k] = s->Rt32[k];
 }
 
-#if M3D_TAIL_CLOCK  // diagnostic builds only (tools/tail_clock.py): per-wave start / end of the
-                    // terms pass, then the last block's ticket, reduce and solve steps (100 MHz)
-__device__ unsigned long long g_tail_clock[2 * 4096 + 8];
+#if M3D_TAIL_CLOCK
 #define M3D_TCLK(k)                                                                   \
   do {                                                                                \
     if (threadIdx.x == 0) g_tail_clock[2 * 4096 + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -1138,6 +1155,9 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
     s->done = 1;
     return;
   }
+#if M3D_SOLVE_SKIP  // timing only: the solve's cost
+  return;
+#endif
   double upd[16];
   for (int k = 0; k < 16; ++k) upd[k] = (k % 5 == 0) ? 1.0 : 0.0;
   // the search transform of the evaluation just reduced: seed_key's bound for the next one
@@ -1157,7 +1177,10 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
         }
       for (int a = 0; a < 6; ++a) b[a] = -sm[21 + a];
       M3D_TCLK(3);
-      ldlt6_solve(A, b, x);
+#ifndef M3D_SOLVE_SPD
+#define M3D_SOLVE_SPD 1
+#endif
+      if (!M3D_SOLVE_SPD || !ldlt6_solve_spd(A, b, x)) ldlt6_solve(A, b, x);
       M3D_TCLK(4);
       vec6_to_matrix_wave(x, upd);
       M3D_TCLK(5);
@@ -1587,6 +1610,35 @@ hipError_t ensure_target_rec(const m3d_cloud* c, hipStream_t st) {
     return e;
   }
   c->rec64 = rec;
+  return hipSuccess;
+}
+
+// The target grid's points in fp64, in the grid's cell order (w = index bits): resolve_wave then
+// reads an ambiguous query's box candidates with their fp64 coordinates in one load instead of the
+// fp32 point and then a gather of the fp64 one
+__global__ __launch_bounds__(256) void pack_pts64_kernel(const float4* __restrict__ pts,
+                                                         const double* __restrict__ xyz, int64_t n,
+                                                         double4* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const int32_t j = __float_as_int(pts[k].w);
+  out[k] = make_double4(xyz[3 * (int64_t)j], xyz[3 * (int64_t)j + 1], xyz[3 * (int64_t)j + 2],
+                        __longlong_as_double((long long)j));
+}
+
+hipError_t build_grid_pts64(const m3d_cloud* c, Grid* g, hipStream_t st) {
+  if (g->pts64 != nullptr || g->n_pts == 0 || M3D_WALK64 == 0) return hipSuccess;
+  double4* p = nullptr;
+  hipError_t e = block_alloc(reinterpret_cast<void**>(&p), sizeof(double4) * g->n_pts, st);
+  if (e != hipSuccess) return e;
+  pack_pts64_kernel<<<(unsigned)((g->n_pts + 255) / 256), 256, 0, st>>>(g->pts, c->xyz64, g->n_pts, p);
+  e = hipGetLastError();  // asynchronous (stream order); m3d_icp_create synchronises once
+  if (e != hipSuccess) {
+    block_release(p);
+    return e;
+  }
+  g->pts64 = p;
+  g->dev.pts64 = p;
   return hipSuccess;
 }
 

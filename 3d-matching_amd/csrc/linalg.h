@@ -9,7 +9,8 @@
 //      deterministic rule (collinear KAT of test_ransac_crash.py:114-139 → I), rank 0 → I
 //      (duplicate-points KAT → I, as LAPACK returns).
 //  * ldlt6_solve: Eigen::LDLT (diagonal pivoting; zero pivots give zero components) as used by
-//      Open3D SolveLinearSystemPSD(JTJ, -JTr).
+//      Open3D SolveLinearSystemPSD(JTJ, -JTr); ldlt6_solve_spd: the same system unpivoted,
+//      for full-rank JTJ (the device solve's fast path, falling back to ldlt6_solve).
 //  * vec6_to_matrix: Open3D TransformVector6dToMatrix4d, R = Rz(x2)·Ry(x1)·Rx(x0).
 #pragma once
 
@@ -249,6 +250,55 @@ M3D_HD void ldlt6_solve(const double A_in[36], const double b_in[6], double x[6]
 #pragma unroll
     for (int j = 0; j < 6; ++j)
       if (perm[i] == j) x[j] = y[i];
+}
+
+// The same system without pivoting, for the device solve's common case: JᵀJ is symmetric
+// positive semi-definite, so while every pivot stays well away from zero the unpivoted
+// factorisation is as stable as the pivoted one and gives the same x up to rounding.  Returns
+// false — x untouched — when a pivot falls below 1e-9 of the largest diagonal entry (a rank-
+// deficient or near-deficient system): the caller then runs ldlt6_solve, whose pivot order
+// decides which components a singular system zeroes, as Eigen's does.
+M3D_HD bool ldlt6_solve_spd(const double A[36], const double b[6], double x[6]) {
+  double M[6][6], D[6], Di[6], y[6];
+  double dmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    dmax = fmax(dmax, A[i * 6 + i]);
+#pragma unroll
+    for (int j = 0; j <= i; ++j) M[i][j] = A[i * 6 + j];
+  }
+  const double lo = 1e-9 * dmax;
+  bool ok = dmax > 0.0 && isfinite(dmax);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    D[k] = M[k][k];
+    ok = ok && D[k] > lo;
+    Di[k] = 1.0 / D[k];
+    // M[i][k] becomes L[i][k]; the trailing lower triangle takes the rank-1 update
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      const double c = M[i][k];
+      M[i][k] = c * Di[k];
+#pragma unroll
+      for (int j = k + 1; j <= i; ++j) M[i][j] -= c * M[j][k];  // L[i][k]·D[k]·L[j][k]
+    }
+  }
+  if (!ok) return false;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double s = b[i];
+#pragma unroll
+    for (int j = 0; j < i; ++j) s -= M[i][j] * y[j];
+    y[i] = s;
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i] * Di[i];
+#pragma unroll
+    for (int j = i + 1; j < 6; ++j) s -= M[j][i] * x[j];
+    x[i] = s;
+  }
+  return true;
 }
 
 // Open3D TransformVector6dToMatrix4d: R = Rz(x2) Ry(x1) Rx(x0), t = x[3..5].

@@ -94,6 +94,8 @@ struct GridDev {
   int64_t ncells = 0;
   const int32_t* start = nullptr;  // ncells + 1 sorted-array offsets
   const float4* pts = nullptr;     // points sorted by cell, w = index bits
+  const double4* pts64 = nullptr;  // the same points in fp64, w = index bits (ICP loops' target
+                                   // grid, nnkey.h resolve_wave), or null
 };
 
 struct Grid {
@@ -116,6 +118,7 @@ struct Grid {
   uint4* mf16 = nullptr;
   float4* mf32 = nullptr;
   int64_t mf_npad = 0;
+  double4* pts64 = nullptr;  // dev.pts64 (build_grid_pts64, icp.hip)
   // one allocation holding several of the arrays above (Carve; grid_free frees it, not them)
   void* block = nullptr;
   size_t block_bytes = 0;
@@ -414,6 +417,7 @@ hipError_t launch_kabsch3(const m3d_corrset* cs, const int32_t* triples, uint64_
                           const ScoreFuse* fuse = nullptr);
 // one hypothesis, host operands by value (m3d_kabsch3_one / m3d_ransac_score_one)
 hipError_t ensure_target_rec(const m3d_cloud* c, hipStream_t st);  // icp.hip: c->rec64
+hipError_t build_grid_pts64(const m3d_cloud* c, Grid* g, hipStream_t st);  // icp.hip: g->pts64
 hipError_t launch_kabsch3_one(const m3d_corrset* cs, const int32_t* tri, double* T_out,
                               int32_t* status, hipStream_t st);
 int64_t count_one_blocks(int64_t nc);

@@ -193,7 +193,9 @@ __device__ __forceinline__ void grid_merge_lanes(uint64_t& k1, float& k1d, float
 // cell box of q ± 1.001·√X (grid.hip header lemma: it holds every target with d2f ≤ X), lanes
 // split over the box's (y, z) rows and the points of a row; every target with d2f(q, t) ≤ X is
 // re-evaluated with the contract's fp64 d² from its fp64 coordinates, and a butterfly takes the
-// lexicographic (d64, global index) minimum among d64 < r2 (bj = −1: none).
+// lexicographic (d64, global index) minimum among d64 < r2 (bj = −1: none).  With the grid's fp64
+// points (g.pts64, the ICP loops' target grid) every target of the box is evaluated from one
+// 32-B load — a superset holding the same minimum — instead of an fp32 screen and a gather.
 __device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
                                              const double* __restrict__ tgt64, int64_t off,
                                              float qx, float qy, float qz, float X,
@@ -224,6 +226,21 @@ __device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
         const int cz = z0 + r / ny, cy = y0 + r % ny;
         const int64_t row = ((int64_t)cz * g.n[1] + cy) * g.n[0];
         const int32_t j1 = g.start[row + x1 + 1];
+        if (g.pts64 != nullptr) {
+          // every target of the box in fp64 (a superset of those with d2f ≤ X: the same minimum),
+          // coordinates and index in one load
+          for (int32_t j = g.start[row + x0] + lane % lpr; j < j1; j += lpr) {
+            const double4 v = g.pts64[j];
+            const double dx = Q0 - v.x, dy = Q1 - v.y, dz = Q2 - v.z;
+            const double d = (dx * dx + dy * dy) + dz * dz;
+            const int64_t gj = off + (int64_t)__double_as_longlong(v.w);
+            if (d < r2 && (d < dl || (d == dl && gj < jl))) {
+              dl = d;
+              jl = gj;
+            }
+          }
+          continue;
+        }
         for (int32_t j = g.start[row + x0] + lane % lpr; j < j1; j += lpr) {
           const float4 v = g.pts[j];
           if (!(d2f(lx, ly, lz, v.x, v.y, v.z) <= lX)) continue;

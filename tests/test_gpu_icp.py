@@ -650,6 +650,30 @@ def test_icp_ragged_sources_incremental_points(ns, nn):
         assert r.fitness == ref["fitness"]
 
 
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_icp_ambiguous_pairs_and_triples_exact(nn):
+    """A target with exact duplicate pairs, exact triples and near-duplicate pairs (1e-9 apart,
+    one fp32 point, two fp64 points): their queries are ambiguous (the runner-up inside the fp32
+    error band).  The grid loop decides a query with exactly two targets in its band from the
+    scan's runner-up (grid.hip alt) and walks the grid for three or more; the brute loop always
+    walks.  Every evaluation's correspondences must equal the oracle's exact fp64 NN (ties: the
+    lowest index) bit for bit."""
+    src, tgt, nrm, _ = synth.icp_pair(20_000, 12_000, seed=31)
+    near = tgt[6000:9000].copy()
+    near[:, 0] += 1e-9
+    tgt2 = np.concatenate([tgt, tgt[:3000], tgt[3000:6000], tgt[3000:6000], near])
+    nrm2 = np.concatenate([nrm, nrm[:3000], nrm[3000:6000], nrm[3000:6000], nrm[6000:9000]])
+    lp = IcpLoop(Cloud(src), Cloud(tgt2, nrm2), 0.12, relative_fitness=-1, relative_rmse=-1,
+                 max_iteration=4, nn=nn)
+    keep = []
+    _check_evaluations(lp, src, tgt2, np.eye(4), 5, keep=keep)
+    # the duplicate sets are met: some correspondences name a copy's lowest index, some a
+    # near-duplicate decided in fp64
+    corr = keep[-1][1]
+    assert np.isin(corr, np.arange(3000)).any() and np.isin(corr, np.arange(3000, 6000)).any()
+    assert np.isin(corr, np.arange(6000, 9000)).any() or np.isin(corr, np.arange(21000, 24000)).any()
+
+
 def test_icp_cfg1_point_to_point_matches_oracle():
     """cfg1's pair with TransformationEstimationPointToPoint (a10: Umeyama over the 15 centred
     sums, rotation_from_cov shared with a1), 30 fixed iterations, grid NN: every evaluation
