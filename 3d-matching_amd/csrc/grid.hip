@@ -128,6 +128,9 @@ __global__ __launch_bounds__(kGridBlock) void grid_gather_kernel(const float4* _
                     // grid scan, s_memrealtime (100 MHz)
 __device__ unsigned long long g_scan_clock[2 * 65536];
 #endif
+#ifndef M3D_SCAN_PHASE1
+#define M3D_SCAN_PHASE1 1
+#endif
 template <int kL, int kR, int kB, bool kDefer = false>
 __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const float4* __restrict__ qpts, int64_t ns, GridDev g, int64_t off,
@@ -162,7 +165,16 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     if (seed != kKeyNone) k1 = (uint64_t)seed;
     k1d = key_real_d2(k1);
     if (g.ncells > 0) {
-      const float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
+      float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
+      if (M3D_SCAN_PHASE1 && 2.0f * R * g.inv_h > 3.0f) {
+        // a box wider than ~4 cells per axis (no seed, or a seed the update moved far — the first
+        // evaluations; a dense target, where the cells are r/2 … r/4): the half-cell box around
+        // the query first, every lane over every point (so each lane's state holds the same
+        // points: the second pass's repeats change neither k1 nor near2), then the box of the
+        // bound that leaves
+        grid_scan<1, kR, kB>(g, qx, qy, qz, 0.5f / g.inv_h, r2_hi, off, 0, k1, k1d, n2);
+        R = fminf(R, sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f);
+      }
       int rows = 0, cand = 0;
       grid_scan<kL, kR, kB>(g, qx, qy, qz, R, r2_hi, off, sub, k1, k1d, n2, &rows, &cand,
                             kDefer ? cand_cap : 0x7FFFFFFF);
