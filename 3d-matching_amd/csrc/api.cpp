@@ -2184,7 +2184,7 @@ int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16) 
 
 int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6) {
   if (!A36 || !b6 || !x6) return M3D_ERR_INVALID;
-  ldlt6_solve(A36, b6, x6);
+  if (!ldlt6_solve_spd(A36, b6, x6)) ldlt6_solve(A36, b6, x6);  // the device solve's rule (icp.hip)
   return M3D_OK;
 }
 

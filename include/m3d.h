@@ -455,7 +455,8 @@ int m3d_ransac_on_correspondences(m3d_ctx* ctx, const m3d_cloud* src, const m3d_
  * Host-compiled copy of the device 3×3 linear algebra (same source), for CPU-side unit tests
  * of the math.  Never used by the product path. */
 int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16);
-int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6);
+int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6);  // the device solve's
+                                                                       // rule: unpivoted, pivoted fallback
 /* XXH64 of [p, p + len) (the chunk hash of m3d_content_keys; known-answer tests). */
 uint64_t m3d_debug_xxh64(const void* p, size_t len, uint64_t seed);
 /* XXH3-128 (default secret, seed 0) of [p, p + len), len >= 241 (the long-input path the content

@@ -147,3 +147,34 @@ def test_host_ldlt_matches_dense_solve():
         x = np.zeros(6)
         lib.m3d_debug_ldlt6_host(A.ctypes.data_as(P), b.ctypes.data_as(P), x.ctypes.data_as(P))
         np.testing.assert_allclose(x, np.linalg.solve(A, b), rtol=1e-9, atol=1e-12)
+
+
+def test_host_solve_rule_matches_oracle():
+    """The device solve's rule (icp.hip solve_state, through the host-compiled hook): a full-rank
+    JᵀJ takes the unpivoted LDLT and agrees with the oracle's pivoted, Eigen-order solve to the
+    system's conditioning; an axis the correspondences never excite (a zero column of J, so a zero
+    pivot) falls back to the pivoted factorisation and gets the zero component Eigen gives it."""
+    import icp_oracle as I
+
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+
+    def solve(A, b):
+        x = np.zeros(6)
+        rc = lib.m3d_debug_ldlt6_host(np.ascontiguousarray(A).ctypes.data_as(P), b.ctypes.data_as(P),
+                                      x.ctypes.data_as(P))
+        assert rc == 0
+        return x
+
+    for _ in range(20):
+        J = rng.standard_normal((50, 6)) * np.array([3.0, 3.0, 3.0, 1.0, 1.0, 1.0])
+        A, b = J.T @ J, rng.standard_normal(6)
+        np.testing.assert_allclose(solve(A, b), I.ldlt_solve(A, b), rtol=1e-10, atol=1e-13)
+    for zero in range(6):
+        J = rng.standard_normal((50, 6))
+        J[:, zero] = 0.0
+        A, b = J.T @ J, rng.standard_normal(6)
+        b[zero] = 0.0
+        x, ref = solve(A, b), I.ldlt_solve(A, b)
+        assert x[zero] == 0.0 and ref[zero] == 0.0
+        np.testing.assert_allclose(x, ref, rtol=1e-10, atol=1e-13)
