@@ -41,7 +41,7 @@ constexpr int kNNTile = 16;   // screen sub-tile (one branch per sub-tile)
 constexpr int kNNLds = 512;   // targets per LDS tile (8 KB, double-buffered)
 constexpr int kNNBlock = 256;
 constexpr int kTermsBlock = 256;
-constexpr int kTermsPtsDefault = 2;  // sources per terms thread (M3D_TERMS_PTS = 1|2|4, tuning):
+constexpr int kTermsPtsDefault = 2;  // sources per terms thread (1 / 4 / 8 were measured slower):
                                      // 2× fewer block partials for the last block to reduce
 static int terms_pts() { return kTermsPtsDefault; }
 constexpr double kU = 5.9604644775390625e-08;
@@ -780,12 +780,13 @@ __device__ __forceinline__ double wave_transpose_sum32(const double (&v)[32], in
 // every terms pass (terms_block, single device or shard) adds a source through this function,
 // so equal winners give equal bits.  Q = the fp64 transformed source, q / n its winner's point and
 // normal, d2 = the winner's fp64 d², c = the source centre (point-to-point).
+template <int kEst>
 __device__ __forceinline__ void terms_add(double (&acc)[30], const double (&Q)[3], const double (&q)[3],
-                                          const double (&n)[3], double d2, int est, const double (&c)[3]) {
+                                          const double (&n)[3], double d2, const double (&c)[3]) {
   const double d[3] = {Q[0] - q[0], Q[1] - q[1], Q[2] - q[2]};
   acc[28] += 1.0;
   acc[29] += d2;
-  if (est == M3D_EST_POINT_TO_PLANE) {
+  if (kEst == M3D_EST_POINT_TO_PLANE) {
     const double r = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
     double J[6];
     cross3(Q, n, J);
@@ -860,7 +861,9 @@ __device__ unsigned long long g_tail_clock[3 * 4096 + 8];
 #ifndef M3D_AMB_SKIP
 #define M3D_AMB_SKIP 0  // timing only (wrong winners on ambiguous queries): their cost
 #endif
-template <bool kWT, int kP>
+// kEst: the estimator as a template parameter (one path compiled per kernel: a runtime branch
+// between the two accumulation forms kept two accumulators in scratch memory)
+template <bool kWT, int kP, int kEst>
 __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* __restrict__ s,
                                             double* __restrict__ partials) {
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
@@ -954,7 +957,7 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         tq[u][k] = a.tgt64[3 * l + k];
-        tn[u][k] = a.est == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
+        tn[u][k] = kEst == M3D_EST_POINT_TO_PLANE ? a.nrm64[3 * l + k] : 0.0;
       }
     }
   }
@@ -972,7 +975,7 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
     const int64_t i = ii[u];
     if (a.corr != nullptr) a.corr[i] = (int32_t)gj[u];
     if (gj[u] < a.off || gj[u] >= a.off + a.nt_shard) continue;  // none, or another shard's target
-    terms_add(acc, vs[u], tq[u], tn[u], d2[u], a.est, a.c);
+    terms_add<kEst>(acc, vs[u], tq[u], tn[u], d2[u], a.c);
   }
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   {
@@ -996,11 +999,11 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
   }
 }
 
-template <int kP>
+template <int kP, int kEst>
 __global__ __launch_bounds__(kTermsBlock) void terms_kernel(TermsArgs a, const IcpState* __restrict__ s,
                                                             double* __restrict__ partials) {
   if (s->done) return;
-  terms_block<false, kP>(a, s, partials);
+  terms_block<false, kP, kEst>(a, s, partials);
 }
 
 // Target-sharded evaluation, step 1 (m3d_icp_shard_nn): this shard's fp64 winner of every query
@@ -1122,6 +1125,7 @@ __device__ __forceinline__ void solve_in(const IcpState* s, SolveIn& in) {
   do {              \
   } while (0)
 #endif
+template <int kEst>
 __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& sp, const SolveIn& in) {
   double sm[30];
 #pragma unroll
@@ -1166,7 +1170,7 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   s->eq_prev = eq;
   s->bound_ok = sp.f.shared;  // bounds compare keys across ranks: only in a shared frame
   if (count > 0.0) {
-    if (sp.est == M3D_EST_POINT_TO_PLANE) {
+    if (kEst == M3D_EST_POINT_TO_PLANE) {
       double A[36], b[6], x[6];
       int k = 0;
       for (int a = 0; a < 6; ++a)
@@ -1217,12 +1221,13 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   M3D_TCLK(7);
 }
 
+template <int kEst>
 __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restrict__ s,
                              SolveParams sp) {
   if (threadIdx.x >= kWave || s->done) return;
   SolveIn in;
   solve_in(s, in);
-  solve_state(sums, s, sp, in);
+  solve_state<kEst>(sums, s, sp, in);
 }
 
 // Fused single-device iteration tail: terms → block partial → the last block to finish (ticket)
@@ -1231,7 +1236,7 @@ __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restri
 // write-through (sc1), drains it (vmcnt(0)) and one lane adds to the agent-scope ticket; the
 // block whose add returned nblocks − 1 reads every partial with sc1 loads.  No L2 write-back or
 // invalidate fences are needed.
-template <int kP>
+template <int kP, int kEst>
 __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     TermsArgs a, IcpState* s, double* partials, int64_t nblocks, double* __restrict__ sums,
     SolveParams sp, int do_solve) {
@@ -1241,7 +1246,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
 #if M3D_TAIL_CLOCK
   const unsigned long long clk0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  terms_block<true, kP>(a, s, partials);
+  terms_block<true, kP, kEst>(a, s, partials);
 #if M3D_TAIL_CLOCK
   {
     const unsigned long long clk1 = __builtin_amdgcn_s_memrealtime();
@@ -1307,7 +1312,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
   M3D_TCLK(1);
   if (threadIdx.x < kWave) {
     if (threadIdx.x == 0) s->ticket = 0;
-    if (do_solve) solve_state(red[0], s, sp, in);
+    if (do_solve) solve_state<kEst>(red[0], s, sp, in);
   }
   M3D_TCLK(2);
 }
@@ -1672,11 +1677,11 @@ hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* c
   if (ns == 0) return hipMemsetAsync(s->partials, 0, sizeof(double) * kTermSlots, st);
   const TermsArgs ta = terms_args(s, off, claim, dmin, false);
   const unsigned nb = (unsigned)s->nblocks;
-  switch (terms_pts()) {
-    case 1: terms_kernel<1><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials); break;
-    case 2: terms_kernel<2><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials); break;
-    default: terms_kernel<4><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials); break;
-  }
+  static_assert(kTermsPtsDefault == 2, "terms kernels are instantiated for 2 sources per thread");
+  if (ta.est == M3D_EST_POINT_TO_PLANE)
+    terms_kernel<2, M3D_EST_POINT_TO_PLANE><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials);
+  else
+    terms_kernel<2, M3D_EST_POINT_TO_POINT><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials);
   return hipGetLastError();
 }
 
@@ -1703,11 +1708,12 @@ static void launch_terms_solve(const TermsArgs& ta, const m3d_icp* s, double* su
                                hipStream_t st) {
   const unsigned nb = (unsigned)s->nblocks;
   const SolveParams sp = solve_params(s);
-  switch (terms_pts()) {
-    case 1: terms_solve_kernel<1><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks, sums, sp, do_solve); break;
-    case 2: terms_solve_kernel<2><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks, sums, sp, do_solve); break;
-    default: terms_solve_kernel<4><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks, sums, sp, do_solve); break;
-  }
+  if (ta.est == M3D_EST_POINT_TO_PLANE)
+    terms_solve_kernel<2, M3D_EST_POINT_TO_PLANE><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks,
+                                                                             sums, sp, do_solve);
+  else
+    terms_solve_kernel<2, M3D_EST_POINT_TO_POINT><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks,
+                                                                             sums, sp, do_solve);
 }
 
 hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, const int32_t* claim,
@@ -1723,7 +1729,10 @@ hipError_t launch_icp_terms_reduce(const m3d_icp* s, int64_t off, const int32_t*
 }
 
 hipError_t launch_icp_solve(const m3d_icp* s, const double* sums, hipStream_t st) {
-  solve_kernel<<<1, 64, 0, st>>>(sums, s->state, solve_params(s));
+  if (s->params.estimation == M3D_EST_POINT_TO_PLANE)
+    solve_kernel<M3D_EST_POINT_TO_PLANE><<<1, 64, 0, st>>>(sums, s->state, solve_params(s));
+  else
+    solve_kernel<M3D_EST_POINT_TO_POINT><<<1, 64, 0, st>>>(sums, s->state, solve_params(s));
   return hipGetLastError();
 }
 
