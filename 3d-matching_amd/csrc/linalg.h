@@ -108,17 +108,19 @@ M3D_HD int rotation_from_cov(const double Hm[9], double R[9]) {
     for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
     return (s0 == s0) ? 0 : -1;
   }
-  // H V = U Σ: u_k = a_k / σ_k (source frame), v_k (target frame).
+  // H V = U Σ: u_k = a_k / σ_k (source frame), v_k (target frame).  The columns o0 / o1 are
+  // picked by selects, not by a runtime index: a dynamically indexed a[][] / v[][] lives in
+  // scratch memory on the device.
   double u0[3], u1[3], v0[3], v1[3];
   for (int r = 0; r < 3; ++r) {
-    u0[r] = a[o0][r] / s0;
-    v0[r] = v[o0][r];
+    u0[r] = (o0 == 0 ? a[0][r] : (o0 == 1 ? a[1][r] : a[2][r])) / s0;
+    v0[r] = o0 == 0 ? v[0][r] : (o0 == 1 ? v[1][r] : v[2][r]);
   }
   int rank;
   if (s1 > 1e-14 * s0) {
     for (int r = 0; r < 3; ++r) {
-      u1[r] = a[o1][r] / s1;
-      v1[r] = v[o1][r];
+      u1[r] = (o1 == 0 ? a[0][r] : (o1 == 1 ? a[1][r] : a[2][r])) / s1;
+      v1[r] = o1 == 0 ? v[0][r] : (o1 == 1 ? v[1][r] : v[2][r]);
     }
     double d = dot3(u0, u1);  // re-orthogonalise (Jacobi leaves it ~eps, harmless)
     for (int r = 0; r < 3; ++r) u1[r] -= d * u0[r];
