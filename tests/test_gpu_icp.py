@@ -55,7 +55,11 @@ def _grid_cases():
     # a vertex fan: 3000 targets within 0.004 of one surface point (≥ 256 in one cell at r: the
     # loop defers the queries near it to grid_nn_heavy_kernel)
     fan = np.vstack([sph, sph[7] + rng.normal(scale=0.002, size=(3000, 3))])
+    # a dense volume (≈ 100 points per r-cell: the loop's cells are r/4, so an unseeded query's
+    # box is 9 cells wide and the scan takes its half-cell first pass, grid.hip M3D_SCAN_PHASE1)
+    cube = rng.uniform(-0.5, 0.5, (60000, 3))
     return {
+        "dense_volume": (cube[::3] + 1e-3, cube, 0.12),
         "dense_cluster": (np.vstack([sph[::3] * 1.001, sph[7] + rng.normal(scale=0.03, size=(2000, 3))]), fan, 0.12),
         "sphere": (sph[::3] * 1.002, sph, 0.12),
         "sphere_big_r": (sph[::7], sph, 50.0),  # radius larger than the cloud
