@@ -863,10 +863,28 @@ __device__ unsigned long long g_tail_clock[3 * 4096 + 8];
 #endif
 // kEst: the estimator as a template parameter (one path compiled per kernel: a runtime branch
 // between the two accumulation forms kept two accumulators in scratch memory)
+#if M3D_TERMS_CLOCK  // diagnostic builds only (tools/terms_phases.py): per wave, stamps at the terms
+                     // pass's phase ends, each after s_waitcnt 0 (the phases serialise), kept in
+                     // registers and stored at the end
+__device__ unsigned long long g_terms_clock[4096 * 8];
+#define M3D_TPH(k)                               \
+  do {                                           \
+    __builtin_amdgcn_s_waitcnt(0);               \
+    tph_[k] = __builtin_amdgcn_s_memrealtime();  \
+  } while (0)
+#else
+#define M3D_TPH(k) \
+  do {             \
+  } while (0)
+#endif
 template <bool kWT, int kP, int kEst>
 __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* __restrict__ s,
                                             double* __restrict__ partials) {
   __shared__ double red[kTermSlots][kTermsBlock / kWave];
+#if M3D_TERMS_CLOCK
+  unsigned long long tph_[8];
+#endif
+  M3D_TPH(0);
   double acc[30];
 #pragma unroll
   for (int k = 0; k < 30; ++k) acc[k] = 0.0;
@@ -902,6 +920,7 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
     if (valid[u])
       for (int k = 0; k < 3; ++k) a.pcd64[3 * ii[u] + k] = vs[u][k];
   }
+  M3D_TPH(1);
   if (a.claim == nullptr) {
 #pragma unroll
     for (int u = 0; u < kP; ++u) {
@@ -939,6 +958,7 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
       }
     }
   }
+  M3D_TPH(2);
   double tq[kP][3], tn[kP][3];
 #pragma unroll
   for (int u = 0; u < kP; ++u) {
@@ -961,6 +981,7 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
       }
     }
   }
+  M3D_TPH(3);
 #pragma unroll
   for (int u = 0; u < kP; ++u) {
     if (!valid[u]) continue;
@@ -977,6 +998,7 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
     if (gj[u] < a.off || gj[u] >= a.off + a.nt_shard) continue;  // none, or another shard's target
     terms_add<kEst>(acc, vs[u], tq[u], tn[u], d2[u], a.c);
   }
+  M3D_TPH(4);
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   {
     double v[32];
@@ -985,7 +1007,9 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
     const double w = wave_transpose_sum32(v, lane);
     if ((lane & 1) == 0) red[lane >> 1][wave] = w;
   }
+  M3D_TPH(5);
   __syncthreads();
+  M3D_TPH(6);
   if (threadIdx.x < kTermSlots) {
     double v = 0.0;
     if (threadIdx.x < 30)
@@ -997,6 +1021,14 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
     else
       *dst = v;
   }
+  M3D_TPH(7);
+#if M3D_TERMS_CLOCK
+  {
+    const int64_t gw = (int64_t)blockIdx.x * (kTermsBlock / kWave) + threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0 && gw < 4096)
+      for (int k = 0; k < 8; ++k) g_terms_clock[8 * gw + k] = tph_[k];
+  }
+#endif
 }
 
 template <int kP, int kEst>
@@ -1804,6 +1836,11 @@ int64_t terms_blocks(int64_t ns) {
 
 }  // namespace m3d
 
+#if M3D_TERMS_CLOCK
+extern "C" int m3d_debug_terms_clock(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(m3d::g_terms_clock), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif
 #if M3D_TAIL_CLOCK
 extern "C" int m3d_debug_tail_clock(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(m3d::g_tail_clock), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
