@@ -1216,6 +1216,8 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
 #ifndef M3D_SOLVE_SPD
 #define M3D_SOLVE_SPD 1
 #endif
+      // a full-rank JᵀJ unpivoted (no scalar-unit row swaps: 1.6 µs of the tail); a
+      // (near-)singular one through Eigen's pivot order, which decides its zero components
       if (!M3D_SOLVE_SPD || !ldlt6_solve_spd(A, b, x)) ldlt6_solve(A, b, x);
       M3D_TCLK(4);
       vec6_to_matrix_wave(x, upd);
