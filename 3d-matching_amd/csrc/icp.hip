@@ -922,6 +922,10 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
   }
   M3D_TPH(1);
   if (a.claim == nullptr) {
+    bool amb[kP];
+    float X[kP], qx[kP], qy[kP], qz[kP];
+    int64_t bj[kP];
+    double bd[kP];
 #pragma unroll
     for (int u = 0; u < kP; ++u) {
       if (valid[u] && a.reset_keys != nullptr) {
@@ -930,25 +934,28 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
       }
       // nnkey.h winner_fp64, split: ambiguous queries resolved here by the wave, the others'
       // candidate (k1's target) re-evaluated in fp64 after the batched target loads below
-      const float X = valid[u] && k1[u] != (uint64_t)kKeyNone ? search_bound(key_d2(k1[u]), s->band_e, s->r2_hi)
-                                                              : -1.0f;
-      const bool amb = !M3D_AMB_SKIP && X >= 0.0f && n2[u] <= X;
+      X[u] = valid[u] && k1[u] != (uint64_t)kKeyNone ? search_bound(key_d2(k1[u]), s->band_e, s->r2_hi) : -1.0f;
+      amb[u] = !M3D_AMB_SKIP && X[u] >= 0.0f && n2[u] <= X[u];
 #if M3D_TAIL_CLOCK
       {
         const int64_t gw = (int64_t)blockIdx.x * (kTermsBlock / kWave) + threadIdx.x / kWave;
-        const int na = __popcll(__ballot(amb));
+        const int na = __popcll(__ballot(amb[u]));
         if ((threadIdx.x & (kWave - 1)) == 0 && gw < 4096)
           g_tail_clock[2 * 4096 + 8 + gw] = (u == 0 ? 0ull : g_tail_clock[2 * 4096 + 8 + gw]) + na;
       }
 #endif
-      float qx = 0.0f, qy = 0.0f, qz = 0.0f;
-      if (amb) xform32(s->Rt32, a.src32[ii[u]], qx, qy, qz);
-      int64_t bj = -1;
-      double bd = 0.0;
-      resolve_wave(amb, a.g, a.tgt64, a.off, qx, qy, qz, X, vs[u], s->r2, bj, bd);
-      if (amb) {
-        gj[u] = bj;
-        d2[u] = bd;
+      qx[u] = qy[u] = qz[u] = 0.0f;
+      if (amb[u]) xform32(s->Rt32, a.src32[ii[u]], qx[u], qy[u], qz[u]);
+      bj[u] = -1;
+      bd[u] = 0.0;
+    }
+    // every source round's ambiguous queries in one walk, two at a time (nnkey.h)
+    resolve_wave_kp<kP>(amb, a.g, a.tgt64, a.off, qx, qy, qz, X, vs, s->r2, bj, bd);
+#pragma unroll
+    for (int u = 0; u < kP; ++u) {
+      if (amb[u]) {
+        gj[u] = bj[u];
+        d2[u] = bd[u];
       } else if (valid[u] && key_real(k1[u])) {
         const int64_t c = (int64_t)(uint32_t)k1[u];
         if (c >= a.off && c < a.off + a.nt_shard) {

@@ -196,18 +196,79 @@ __device__ __forceinline__ void grid_merge_lanes(uint64_t& k1, float& k1d, float
 // lexicographic (d64, global index) minimum among d64 < r2 (bj = −1: none).  With the grid's fp64
 // points (g.pts64, the ICP loops' target grid) every target of the box is evaluated from one
 // 32-B load — a superset holding the same minimum — instead of an fp32 screen and a gather.
-__device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
-                                             const double* __restrict__ tgt64, int64_t off,
-                                             float qx, float qy, float qz, float X,
-                                             const double Q[3], double r2, int64_t& bj,
-                                             double& bd) {
+#ifndef M3D_WALK_PAIRS
+#define M3D_WALK_PAIRS 1
+#endif
+template <int kP, typename T>
+__device__ __forceinline__ T item_of(const T (&v)[kP], int u) {  // v[u] for a wave-uniform u
+  T r = v[0];
+#pragma unroll
+  for (int k = 1; k < kP; ++k)
+    if (u == k) r = v[k];
+  return r;
+}
+template <int kP>
+__device__ __forceinline__ double item_q(const double (&Q)[kP][3], int u, int c) {
+  double r = Q[0][c];
+#pragma unroll
+  for (int k = 1; k < kP; ++k)
+    if (u == k) r = Q[k][c];
+  return r;
+}
+// resolve_wave over kP queries per lane (the terms pass's sources per thread): the ambiguous
+// (u, lane) items of all kP rounds are walked two at a time, one per half-wave (M3D_WALK_PAIRS),
+// so a wave holding two walks them side by side instead of one after the other — its block waits
+// for it.  Any box lane split gives the same minimum.
+template <int kP>
+__device__ __forceinline__ void resolve_wave_kp(const bool (&amb)[kP], const GridDev& g,
+                                                const double* __restrict__ tgt64, int64_t off,
+                                                const float (&qx)[kP], const float (&qy)[kP],
+                                                const float (&qz)[kP], const float (&X)[kP],
+                                                const double (&Q)[kP][3], double r2,
+                                                int64_t (&bj)[kP], double (&bd)[kP]) {
   const int lane = threadIdx.x & (kWave - 1);
-  uint64_t m = __ballot(amb);
-  while (m != 0) {
-    const int L = __builtin_ctzll(m);
-    m &= m - 1;
-    const float lx = __shfl(qx, L), ly = __shfl(qy, L), lz = __shfl(qz, L), lX = __shfl(X, L);
-    const double Q0 = __shfl(Q[0], L), Q1 = __shfl(Q[1], L), Q2 = __shfl(Q[2], L);
+  uint64_t m[kP];
+#pragma unroll
+  for (int u = 0; u < kP; ++u) m[u] = __ballot(amb[u]);
+  auto next = [&](int& u, int& L) {  // the next (u, lane) item, u = −1: none
+    u = -1;
+    L = 0;
+#pragma unroll
+    for (int k = 0; k < kP; ++k)
+      if (u < 0 && m[k] != 0) {
+        u = k;
+        L = __builtin_ctzll(m[k]);
+        m[k] &= m[k] - 1;
+      }
+  };
+  for (;;) {
+    int uA, LA, uB = -1, LB = 0;
+    next(uA, LA);
+    if (uA < 0) break;
+    if (M3D_WALK_PAIRS) next(uB, LB);
+    const bool two = uB >= 0;
+    const int W = two ? kWave / 2 : kWave;  // lanes per query (wave-uniform)
+    const int sl = lane & (W - 1);           // this lane's place among them
+    const bool hb = two && lane >= kWave / 2;
+    float lx = __shfl(item_of(qx, uA), LA), ly = __shfl(item_of(qy, uA), LA);
+    float lz = __shfl(item_of(qz, uA), LA), lX = __shfl(item_of(X, uA), LA);
+    double Q0 = __shfl(item_q(Q, uA, 0), LA), Q1 = __shfl(item_q(Q, uA, 1), LA);
+    double Q2 = __shfl(item_q(Q, uA, 2), LA);
+    if (two) {
+      const float bx = __shfl(item_of(qx, uB), LB), by = __shfl(item_of(qy, uB), LB);
+      const float bz = __shfl(item_of(qz, uB), LB), bX = __shfl(item_of(X, uB), LB);
+      const double b0 = __shfl(item_q(Q, uB, 0), LB), b1 = __shfl(item_q(Q, uB, 1), LB);
+      const double b2 = __shfl(item_q(Q, uB, 2), LB);
+      if (hb) {
+        lx = bx;
+        ly = by;
+        lz = bz;
+        lX = bX;
+        Q0 = b0;
+        Q1 = b1;
+        Q2 = b2;
+      }
+    }
     double dl = kInf;
     int64_t jl = INT64_MAX;
     if (g.ncells > 0 && lX >= 0.0f) {
@@ -220,16 +281,16 @@ __device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
       const int z1 = grid_coord(lz + R, g.o[2], g.inv_h, g.n[2]);
       const int ny = y1 - y0 + 1;
       const int rows = ny * (z1 - z0 + 1);
-      const int lpr = rows >= kWave ? 1 : kWave / rows;  // lanes per row
-      const int rstep = kWave / lpr;
-      for (int r = lane / lpr; r < rows; r += rstep) {
+      const int lpr = rows >= W ? 1 : W / rows;  // lanes per row
+      const int rstep = W / lpr;
+      for (int r = sl / lpr; r < rows; r += rstep) {
         const int cz = z0 + r / ny, cy = y0 + r % ny;
         const int64_t row = ((int64_t)cz * g.n[1] + cy) * g.n[0];
         const int32_t j1 = g.start[row + x1 + 1];
         if (g.pts64 != nullptr) {
-          // every target of the box in fp64 (a superset of those with d2f ≤ X: the same minimum),
-          // coordinates and index in one load
-          for (int32_t j = g.start[row + x0] + lane % lpr; j < j1; j += lpr) {
+          // every target of the box in fp64 (a superset of those with d2f ≤ X: the same
+          // minimum), coordinates and index in one load
+          for (int32_t j = g.start[row + x0] + sl % lpr; j < j1; j += lpr) {
             const double4 v = g.pts64[j];
             const double dx = Q0 - v.x, dy = Q1 - v.y, dz = Q2 - v.z;
             const double d = (dx * dx + dy * dy) + dz * dz;
@@ -241,7 +302,7 @@ __device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
           }
           continue;
         }
-        for (int32_t j = g.start[row + x0] + lane % lpr; j < j1; j += lpr) {
+        for (int32_t j = g.start[row + x0] + sl % lpr; j < j1; j += lpr) {
           const float4 v = g.pts[j];
           if (!(d2f(lx, ly, lz, v.x, v.y, v.z) <= lX)) continue;
           const int64_t lj = (int64_t)__float_as_int(v.w);
@@ -258,6 +319,7 @@ __device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
     }
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
+      if (o >= W) continue;  // two queries: the butterfly stays inside each half
       const double od = __shfl_xor(dl, o);
       const int64_t oj = __shfl_xor(jl, o);
       if (od < dl || (od == dl && oj < jl)) {
@@ -265,11 +327,38 @@ __device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
         jl = oj;
       }
     }
-    if (lane == L) {
-      bj = jl == INT64_MAX ? -1 : jl;
-      bd = dl;
+    // the lower half (lane 0) holds item A's result, the upper half (lane 32) item B's
+    const double dA = __shfl(dl, 0);
+    const int64_t jA = __shfl(jl, 0);
+    const double dB = __shfl(dl, kWave / 2);
+    const int64_t jB = __shfl(jl, kWave / 2);
+#pragma unroll
+    for (int k = 0; k < kP; ++k) {
+      if (uA == k && lane == LA) {
+        bj[k] = jA == INT64_MAX ? -1 : jA;
+        bd[k] = dA;
+      }
+      if (two && uB == k && lane == LB) {
+        bj[k] = jB == INT64_MAX ? -1 : jB;
+        bd[k] = dB;
+      }
     }
   }
+}
+
+__device__ __forceinline__ void resolve_wave(bool amb, const GridDev& g,
+                                             const double* __restrict__ tgt64, int64_t off,
+                                             float qx, float qy, float qz, float X,
+                                             const double Q[3], double r2, int64_t& bj,
+                                             double& bd) {
+  const bool a1[1] = {amb};
+  const float x1[1] = {qx}, y1[1] = {qy}, z1[1] = {qz}, X1[1] = {X};
+  const double Q1[1][3] = {{Q[0], Q[1], Q[2]}};
+  int64_t b1[1] = {bj};
+  double d1[1] = {bd};
+  resolve_wave_kp<1>(a1, g, tgt64, off, x1, y1, z1, X1, Q1, r2, b1, d1);
+  bj = b1[0];
+  bd = d1[0];
 }
 
 // The fp64 winner of query i from its scan results (k1, near2) — see the header.  Q = its fp64
