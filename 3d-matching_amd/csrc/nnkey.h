@@ -177,13 +177,22 @@ __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, 
   if (ncand != nullptr) *ncand = cand;
 }
 
+#ifndef M3D_MERGE_DPP
+#define M3D_MERGE_DPP 1
+#endif
+// v from lane ^ o: a DPP quad permute for o = 1, 2 (no LDS round trip), else a shuffle
+__device__ __forceinline__ int xor_lane(int v, int o, int width) {
+  if (M3D_MERGE_DPP && o == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  if (M3D_MERGE_DPP && o == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  return __shfl_xor(v, o, width);
+}
 template <int kL>
 __device__ __forceinline__ void grid_merge_lanes(uint64_t& k1, float& k1d, float& n2) {
 #pragma unroll
   for (int o = kL / 2; o > 0; o >>= 1) {
-    const uint64_t b1 = ((uint64_t)(uint32_t)__shfl_xor((int)(k1 >> 32), o, kL) << 32) |
-                        (uint32_t)__shfl_xor((int)(uint32_t)k1, o, kL);
-    const float bn2 = __shfl_xor(n2, o, kL);
+    const uint64_t b1 = ((uint64_t)(uint32_t)xor_lane((int)(k1 >> 32), o, kL) << 32) |
+                        (uint32_t)xor_lane((int)(uint32_t)k1, o, kL);
+    const float bn2 = __int_as_float(xor_lane(__float_as_int(n2), o, kL));
     near_merge(k1, k1d, n2, b1, bn2);
   }
 }
