@@ -755,11 +755,27 @@ __device__ __forceinline__ double swap_add(double a, double b) {
   return na + nb;  // lanes of bit 0: a-slot over both halves; bit 1: b-slot
 }
 
+#ifndef M3D_SUM_DPP
+#define M3D_SUM_DPP 1
+#endif
+// v from lane ^ kOff (all lanes active): DPP for 1 and 2 (quad permutes) and 8 (a rotation by 8
+// inside a 16-lane row is lane ^ 8), without the LDS unit's round trip; a shuffle otherwise
+template <int kOff>
+__device__ __forceinline__ double xor_lane64(double v) {
+  constexpr int ctrl = kOff == 1 ? 0xB1 : kOff == 2 ? 0x4E : kOff == 8 ? 0x128 : -1;
+  if (M3D_SUM_DPP && ctrl >= 0) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, ctrl < 0 ? 0 : ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), ctrl < 0 ? 0 : ctrl, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
+  return __shfl_xor(v, kOff, kWave);
+}
 template <int kOff>
 __device__ __forceinline__ double xchg_add(double a, double b, int lane) {
   const bool hi = (lane & kOff) != 0;
   const double keep = hi ? b : a, send = hi ? a : b;
-  return keep + __shfl_xor(send, kOff, kWave);
+  return keep + xor_lane64<kOff>(send);
 }
 
 __device__ __forceinline__ double wave_transpose_sum32(const double (&v)[32], int lane) {
@@ -773,7 +789,7 @@ __device__ __forceinline__ double wave_transpose_sum32(const double (&v)[32], in
 #pragma unroll
   for (int j = 0; j < 2; ++j) w2[j] = xchg_add<4>(w4[j], w4[j + 2], lane);
   const double w1 = xchg_add<2>(w2[0], w2[1], lane);
-  return w1 + __shfl_xor(w1, 1, kWave);  // slot lane >> 1
+  return w1 + xor_lane64<1>(w1);  // slot lane >> 1
 }
 
 // One source's contribution to the 30 term slots (layout below), in a fixed operation order:
