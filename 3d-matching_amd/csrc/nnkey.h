@@ -184,7 +184,17 @@ __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, 
 __device__ __forceinline__ int xor_lane(int v, int o, int width) {
   if (M3D_MERGE_DPP && o == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
   if (M3D_MERGE_DPP && o == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  if (M3D_MERGE_DPP && o == 8) return __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
   return __shfl_xor(v, o, width);
+}
+__device__ __forceinline__ double xor_lane_f64(double v, int o) {
+  const long long b = __double_as_longlong(v);
+  const int lo = xor_lane((int)(uint32_t)b, o, kWave), hi = xor_lane((int)(uint32_t)(b >> 32), o, kWave);
+  return __longlong_as_double(((long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ int64_t xor_lane_i64(int64_t v, int o) {
+  const int lo = xor_lane((int)(uint32_t)v, o, kWave), hi = xor_lane((int)(uint32_t)((uint64_t)v >> 32), o, kWave);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 template <int kL>
 __device__ __forceinline__ void grid_merge_lanes(uint64_t& k1, float& k1d, float& n2) {
@@ -329,8 +339,8 @@ __device__ __forceinline__ void resolve_wave_kp(const bool (&amb)[kP], const Gri
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
       if (o >= W) continue;  // two queries: the butterfly stays inside each half
-      const double od = __shfl_xor(dl, o);
-      const int64_t oj = __shfl_xor(jl, o);
+      const double od = xor_lane_f64(dl, o);
+      const int64_t oj = xor_lane_i64(jl, o);
       if (od < dl || (od == dl && oj < jl)) {
         dl = od;
         jl = oj;
