@@ -758,11 +758,17 @@ __device__ __forceinline__ double swap_add(double a, double b) {
 #ifndef M3D_SUM_DPP
 #define M3D_SUM_DPP 1
 #endif
-// v from lane ^ kOff (all lanes active): DPP for 1 and 2 (quad permutes) and 8 (a rotation by 8
-// inside a 16-lane row is lane ^ 8), without the LDS unit's round trip; a shuffle otherwise
+// v from lane ^ kOff (all lanes active): DPP for 1 and 2 (quad permutes), 4 (two moves, xor4_dpp)
+// and 8 (a rotation by 8 inside a 16-lane row is lane ^ 8), without the LDS unit's round trip; a
+// shuffle otherwise
 template <int kOff>
 __device__ __forceinline__ double xor_lane64(double v) {
   constexpr int ctrl = kOff == 1 ? 0xB1 : kOff == 2 ? 0x4E : kOff == 8 ? 0x128 : -1;
+  if (M3D_SUM_DPP && M3D_DPP_X4 && kOff == 4) {
+    const long long b = __double_as_longlong(v);
+    const int lo = xor4_dpp((int)(uint32_t)b), hi = xor4_dpp((int)(uint32_t)(b >> 32));
+    return __longlong_as_double(((long long)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
   if (M3D_SUM_DPP && ctrl >= 0) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, ctrl < 0 ? 0 : ctrl, 0xF, 0xF, false);

@@ -180,10 +180,20 @@ __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, 
 #ifndef M3D_MERGE_DPP
 #define M3D_MERGE_DPP 1
 #endif
-// v from lane ^ o: a DPP quad permute for o = 1, 2 (no LDS round trip), else a shuffle
+#ifndef M3D_DPP_X4
+#define M3D_DPP_X4 1
+#endif
+// v from lane ^ 4 by two DPP moves: lane ^ 3 (quad permute [3,2,1,0]), then lane ^ 7 (the mirror
+// inside each 8 lanes, row_half_mirror): (i ^ 7) ^ 3 = i ^ 4
+__device__ __forceinline__ int xor4_dpp(int v) {
+  return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x1B, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
+}
+// v from lane ^ o: DPP for o = 1, 2 (quad permutes), 4 (two moves) and 8 (row_ror:8), with no
+// LDS round trip; a shuffle otherwise
 __device__ __forceinline__ int xor_lane(int v, int o, int width) {
   if (M3D_MERGE_DPP && o == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
   if (M3D_MERGE_DPP && o == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  if (M3D_MERGE_DPP && M3D_DPP_X4 && o == 4) return xor4_dpp(v);
   if (M3D_MERGE_DPP && o == 8) return __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
   return __shfl_xor(v, o, width);
 }
