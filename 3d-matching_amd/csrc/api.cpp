@@ -250,6 +250,7 @@ void ctx_touch(m3d_ctx* ctx, hipStream_t st) {
     (void)hipGetLastError();  // a capture: its graph launch is touched when it is replayed
     return;
   }
+  std::lock_guard<std::mutex> lk(ctx->uses_mu);
   hipEvent_t ev = nullptr;
   for (auto& u : ctx->uses)
     if (u.first == st) ev = u.second;
@@ -271,21 +272,39 @@ ReleaseScope::ReleaseScope(m3d_ctx* ctx, uint64_t ctx_id) {
     auto it = cache_state().ctx_ids.find(ctx);
     if (it == cache_state().ctx_ids.end() || it->second != ctx_id) ctx = nullptr;
   }
-  if (ctx != nullptr && !ctx->uses_lost) {
-    m = std::make_shared<ReleaseMark>();
-    if (!ctx->uses.empty()) {
-      (void)hipSetDevice(ctx->device);
-      bool ok = ctx->order != nullptr || hipStreamCreateWithFlags(&ctx->order, hipStreamNonBlocking) == hipSuccess;
-      hipEvent_t ev = nullptr;
-      ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
-      for (auto& u : ctx->uses) ok = ok && hipStreamWaitEvent(ctx->order, u.second, 0) == hipSuccess;
-      ok = ok && hipEventRecord(ev, ctx->order) == hipSuccess;
-      if (ok) {
-        m->ev = ev;
+  if (ctx != nullptr) {
+    std::lock_guard<std::mutex> lk(ctx->uses_mu);  // destroys may run on finaliser threads
+    // streams whose last touched work has completed need no wait: drop them (a destroyed
+    // stream's entry goes this way too), so the list stays as long as the streams still busy
+    for (size_t k = 0; k < ctx->uses.size();) {
+      if (hipEventQuery(ctx->uses[k].second) == hipSuccess) {
+        (void)hipEventDestroy(ctx->uses[k].second);
+        ctx->uses[k] = ctx->uses.back();
+        ctx->uses.pop_back();
       } else {
-        if (ev != nullptr) (void)hipEventDestroy(ev);
-        m.reset();
-        (void)hipGetLastError();
+        ++k;
+      }
+    }
+    (void)hipGetLastError();
+    if (!ctx->uses_lost) {
+      m = std::make_shared<ReleaseMark>();
+      if (!ctx->uses.empty()) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);  // the caller's (e.g. torch's) current device is left as it was
+        if (cur != ctx->device) (void)hipSetDevice(ctx->device);
+        bool ok = ctx->order != nullptr || hipStreamCreateWithFlags(&ctx->order, hipStreamNonBlocking) == hipSuccess;
+        hipEvent_t ev = nullptr;
+        ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+        for (auto& u : ctx->uses) ok = ok && hipStreamWaitEvent(ctx->order, u.second, 0) == hipSuccess;
+        ok = ok && hipEventRecord(ev, ctx->order) == hipSuccess;
+        if (ok) {
+          m->ev = ev;
+        } else {
+          if (ev != nullptr) (void)hipEventDestroy(ev);
+          m.reset();
+          (void)hipGetLastError();
+        }
+        if (cur != ctx->device) (void)hipSetDevice(cur);
       }
     }
   }
@@ -1272,7 +1291,7 @@ hipError_t enqueue_nn(m3d_icp* s, int64_t off, hipStream_t st, bool self_seed = 
     KTimer kt(ctx, M3D_KERNEL_NN, st);
     return launch_grid_nn(s->src->xyz32, s->src->n, s->sgrid, s->tgrid, off, s->state, s->keys,
                           s->near2, s->corr, s->dprev, s->tgt->xyz32, s->tgt->n, st, q0, q1,
-                          s->hlist, s->hcnt, s->cand_cap, s->pcd64, s->tgt->xyz64);
+                          s->hlist, s->hcnt, s->cand_cap, s->pcd64, s->tgt->xyz64, s->hcap);
   }
   if (!seeded) {
     hipError_t e = launch_icp_keyinit(s, off, st, q0, q1);
@@ -1332,7 +1351,7 @@ LoopLayout loop_layout(int64_t ns, int32_t cand_cap, size_t* off, size_t* tot) {
   const size_t nh = cand_cap > 0 ? n1 : 0;
   const size_t sz[kLoopArrays] = {sizeof(IcpState), 8 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1,
                                   sizeof(double) * (size_t)(terms_blocks(ns) * kTermSlots + kTermSlots), 4 * nh,
-                                  2 * sizeof(uint32_t), 24 * n1};
+                                  kDeferWords * sizeof(uint32_t), 24 * n1};
   *tot = 0;
   for (int k = 0; k < kLoopArrays; ++k) {
     off[k] = *tot;
@@ -1417,6 +1436,16 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
       layout = loop_layout(src->n, cand_cap, off, &tot);
       if (!run_arena && block_alloc(&blk, tot, nullptr) != hipSuccess)
         grc = m3d_fail(ctx, M3D_ERR_OOM, "device allocation failed (ICP loop arrays)");
+      if (!grc && run_arena && ctx->run.reserve(tot) != hipSuccess)
+        grc = m3d_fail(ctx, M3D_ERR_OOM, "device allocation failed (ICP loop arrays)");
+    }
+    // the deferral list's count / ticket / fault word start at zero BEFORE the sync below: a block
+    // from the cache may hold any bytes of its previous owner (e.g. 0xFF fills), and a memset left
+    // queued on the null stream is not ordered before a caller's non-blocking stream
+    if (!grc && layout.heavy) {
+      char* b0 = run_arena ? ctx->run.base : static_cast<char*>(blk);
+      if (hipMemsetAsync(b0 + off[9], 0, kDeferWords * sizeof(uint32_t), nullptr) != hipSuccess)
+        grc = m3d_fail(ctx, M3D_ERR_HIP, "loop arrays: deferral counter");
     }
     // the setup above ran asynchronously on the null stream: finish it before the loop object is
     // used on the caller's streams
@@ -1447,7 +1476,7 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
   int rc = M3D_OK;
   char* b = static_cast<char*>(blk);
   if (run_arena) {
-    if (ctx->run.reserve(tot) == hipSuccess) b = ctx->run.base;
+    b = ctx->run.base;  // reserved (and its deferral words zeroed) before the setup sync
   } else {
     s->block = blk;
   }
@@ -1464,11 +1493,10 @@ int icp_create(m3d_ctx* ctx, const m3d_cloud* src, const m3d_cloud* tgt, double 
     s->partials = reinterpret_cast<double*>(b + off[7]);
     s->sums = s->partials + s->nblocks * kTermSlots;
     s->pcd64 = reinterpret_cast<double*>(b + off[10]);
-    if (layout.heavy) {  // count + ticket start at zero; grid_nn_heavy_kernel re-zeroes them
+    if (layout.heavy) {  // zeroed above; grid_nn_heavy_kernel re-zeroes count + ticket, icp_reset all
       s->hlist = reinterpret_cast<int32_t*>(b + off[8]);
       s->hcnt = reinterpret_cast<uint32_t*>(b + off[9]);
-      if (hipMemset(s->hcnt, 0, 2 * sizeof(uint32_t)) != hipSuccess)
-        rc = m3d_fail(ctx, M3D_ERR_HIP, "loop arrays: deferral counter");
+      s->hcap = (int32_t)std::max<int64_t>(src->n, 1);
     }
   }
   if (rc) {
@@ -1523,6 +1551,9 @@ int icp_reset(m3d_icp* s, const double* init, bool open3d_init, void* stream) {
   HIPX(ctx, hipMemsetAsync(s->corr, 0xFF, sizeof(int32_t) * std::max<int64_t>(s->src->n, 1), st));
   // all-ones bits = a NaN distance: no bound seed until a target-shard exchange wrote dprev
   HIPX(ctx, hipMemsetAsync(s->dprev, 0xFF, sizeof(int64_t) * std::max<int64_t>(s->src->n, 1), st));
+  // the deferral list's count, ticket and fault word start at zero on the caller's stream (the
+  // heavy kernel re-zeroes count and ticket after each scan; a reset also clears a fault)
+  if (s->hcnt != nullptr) HIPX(ctx, hipMemsetAsync(s->hcnt, 0, kDeferWords * sizeof(uint32_t), st));
   // RegistrationICP (Registration.cpp): pcd = source; if (!init.isIdentity()) pcd.Transform(init)
   HIPX(ctx, launch_icp_reset(s, T, !(open3d_init && eigen_is_identity(T)), st));
   s->keys_clean = false;
@@ -1689,6 +1720,7 @@ int m3d_icp_shard_nn_range(m3d_icp* s, int64_t off, int64_t q0, int64_t q1, int6
 
 int m3d_icp_shard_claim(m3d_icp* s, const int64_t* dmin, int32_t* claim, void* stream) {
   if (!s) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};  // reads the loop's block: its release mark must cover this launch
   CHECK_ARG(s->ctx, dmin != nullptr && claim != nullptr, "null exchange buffer");
   HIPX(s->ctx, launch_shard_claim(s, dmin, claim, S(stream)));
   return M3D_OK;
@@ -1719,6 +1751,7 @@ int m3d_icp_shard_terms(m3d_icp* s, int64_t off, const int64_t* dmin, const int3
 
 int m3d_icp_solve(m3d_icp* s, const double* sums, void* stream) {
   if (!s) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};  // writes IcpState (the loop's block)
   HIPX(s->ctx, launch_icp_solve(s, sums ? sums : s->sums, S(stream)));
   return M3D_OK;
 }
@@ -1734,10 +1767,20 @@ int m3d_icp_set_source_total(m3d_icp* s, int64_t ns_total) {
 
 int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream) {
   if (!s || !out) return M3D_ERR_INVALID;
+  Touch tch{s->ctx, S(stream)};
   m3d_ctx* ctx = s->ctx;
   IcpState h;
+  uint32_t defer[kDeferWords] = {0, 0, 0, 0};
   HIPX(ctx, hipMemcpyAsync(&h, s->state, sizeof(h), hipMemcpyDeviceToHost, S(stream)));
+  if (s->hcnt != nullptr)
+    HIPX(ctx, hipMemcpyAsync(defer, s->hcnt, sizeof(defer), hipMemcpyDeviceToHost, S(stream)));
   HIPX(ctx, hipStreamSynchronize(S(stream)));
+  // the grid scan's deferral list overflowed (a count the scan found larger than the list — the
+  // loop's own writes were dropped, never out of bounds): the keys of this run are not trustworthy
+  if (defer[kDeferFault] != 0)
+    return m3d_fail(ctx, M3D_ERR_HIP,
+                    "grid NN deferral list overflow (count " + std::to_string(defer[0]) +
+                        "): results since the last m3d_icp_reset are invalid");
   for (int k = 0; k < 16; ++k) {
     out->T[k] = h.T[k];
     out->update[k] = h.last_upd[k];
@@ -2185,6 +2228,32 @@ int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16) 
 int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6) {
   if (!A36 || !b6 || !x6) return M3D_ERR_INVALID;
   if (!ldlt6_solve_spd(A36, b6, x6)) ldlt6_solve(A36, b6, x6);  // the device solve's rule (icp.hip)
+  return M3D_OK;
+}
+
+int m3d_debug_block_cache_fill(int byte) {
+  // synchronous: every idle block's release point has passed before, and the fill is complete
+  // after, so the next owner sees exactly these bytes
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (hipDeviceSynchronize() != hipSuccess) return M3D_ERR_HIP;
+  std::lock_guard<std::mutex> lk(g_bc_mu);
+  int n = 0;
+  for (const CachedBlock& b : g_bc) {
+    if (b.dev != cur) continue;
+    if (hipMemset(b.p, byte & 0xFF, b.bytes) != hipSuccess) return M3D_ERR_HIP;
+    ++n;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return M3D_ERR_HIP;
+  return n;
+}
+
+int m3d_debug_icp_defer_count(m3d_icp* s, uint32_t count, void* stream) {
+  if (!s) return M3D_ERR_INVALID;
+  CHECK_ARG(s->ctx, s->hcnt != nullptr, "this loop has no deferral list (grid NN with a candidate cap only)");
+  Touch tch{s->ctx, S(stream)};
+  HIPX(s->ctx, hipMemcpyAsync(s->hcnt, &count, sizeof(count), hipMemcpyHostToDevice, S(stream)));
+  HIPX(s->ctx, hipStreamSynchronize(S(stream)));
   return M3D_OK;
 }
 

@@ -131,13 +131,25 @@ __device__ unsigned long long g_scan_clock[2 * 65536];
 #ifndef M3D_SCAN_PHASE1
 #define M3D_SCAN_PHASE1 1
 #endif
+// append query t to the deferral list; a slot at or past the list's capacity (a count the loop
+// did not produce: it starts at zero at creation and at every reset) is dropped and flagged in
+// hcnt[kDeferFault] (m3d_icp_result_get then fails) — never written out of bounds
+__device__ __forceinline__ void defer_push(int32_t* __restrict__ hlist, uint32_t* __restrict__ hcnt,
+                                           uint32_t hcap, int32_t t) {
+  const uint32_t slot = atomicAdd(hcnt, 1u);
+  if (slot < hcap)
+    hlist[slot] = t;
+  else
+    __hip_atomic_store(hcnt + kDeferFault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int kL, int kR, int kB, bool kDefer = false>
 __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const float4* __restrict__ qpts, int64_t ns, GridDev g, int64_t off,
     const IcpState* __restrict__ s, int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
     const int32_t* __restrict__ prev, const int64_t* __restrict__ dprev,
     const float4* __restrict__ tgt32, int64_t nt_shard, int64_t nblocks, int64_t q0,
-    int32_t* __restrict__ hlist, uint32_t* __restrict__ hcnt, int cand_cap) {
+    int32_t* __restrict__ hlist, uint32_t* __restrict__ hcnt, int cand_cap, uint32_t hcap) {
   if (s->done) return;
 #if M3D_SCAN_CLOCK
   const unsigned long long clk0 = __builtin_amdgcn_s_memrealtime();
@@ -179,13 +191,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
       grid_scan<kL, kR, kB>(g, qx, qy, qz, R, r2_hi, off, sub, k1, k1d, n2, &rows, &cand,
                             kDefer ? cand_cap : 0x7FFFFFFF);
       if (kDefer && cand > cand_cap) {  // a dense box: grid_nn_heavy_kernel scans it with a whole block
-        if (sub == 0) {
-          const uint32_t slot = atomicAdd(hcnt, 1u);
-#ifdef M3D_DEBUG_GUARDS
-          if ((int64_t)slot >= ns) printf("[guard] defer slot %u >= ns %lld (t %lld)\n", slot, (long long)ns, (long long)t); else
-#endif
-          hlist[slot] = (int32_t)t;
-        }
+        if (sub == 0) defer_push(hlist, hcnt, hcap, (int32_t)t);
         i = -1;
       }
     }
@@ -200,13 +206,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
   if (i >= 0 && sub == 0) {
     keys[i] = k1 == key0 ? kKeyNone : (int64_t)k1;
     near2[i] = __float_as_uint(n2);
-    if (kDefer && amb) {
-      const uint32_t slot = atomicAdd(hcnt, 1u);
-#ifdef M3D_DEBUG_GUARDS
-      if ((int64_t)slot >= ns) printf("[guard] amb slot %u >= ns %lld (t %lld)\n", slot, (long long)ns, (long long)t); else
-#endif
-      hlist[slot] = (int32_t)t;
-    }
+    if (kDefer && amb) defer_push(hlist, hcnt, hcap, (int32_t)t);
   }
 #if M3D_SCAN_CLOCK
   {
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
     int64_t* __restrict__ keys, uint32_t* __restrict__ near2, const int32_t* __restrict__ prev, const int64_t* __restrict__ dprev,
     const float4* __restrict__ tgt32, int64_t nt_shard, const int32_t* __restrict__ hlist,
     uint32_t* __restrict__ hcnt, const double* __restrict__ src64,
-    const double* __restrict__ tgt64, int64_t nq) {
+    const double* __restrict__ tgt64, int64_t nq, uint32_t hcap) {
   constexpr int kWaves = kGridBlock / kWave;
   __shared__ uint64_t wk[kWaves];
   __shared__ float wn[kWaves];
@@ -240,23 +240,19 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
   __shared__ int64_t wj[kWaves];
   if (s->done) return;
   uint32_t nh = __hip_atomic_load(hcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef M3D_DEBUG_GUARDS
-  if ((int64_t)nh > nq) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) printf("[guard] heavy count %u > %lld\n", nh, (long long)nq);
+  if (nh > hcap) {  // an overflowed list (flagged by the scan's defer_push): nothing is read from it
     nh = 0;
+    if (threadIdx.x == 0) __hip_atomic_store(hcnt + kDeferFault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-#endif
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const float r2_hi = s->r2_hi, be = s->band_e;
   const uint64_t key0 = ((uint64_t)__float_as_uint(r2_hi) << 32) | 0xFFFFFFFFull;
   for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
     const int64_t t = hlist[h];
-#ifdef M3D_DEBUG_GUARDS
-    if (t < 0 || t >= nq) {
-      if (threadIdx.x == 0) printf("[guard] heavy h %u of %u: t %lld outside [0, %lld)\n", h, nh, (long long)t, (long long)nq);
+    if (t < 0 || t >= nq) {  // (cannot happen for a list this loop wrote; flagged, never dereferenced)
+      if (threadIdx.x == 0) __hip_atomic_store(hcnt + kDeferFault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       continue;
     }
-#endif
     const float4 p = qpts[t];
     const int64_t i = (int64_t)__float_as_int(p.w);
 #ifdef M3D_DEBUG_GUARDS
@@ -368,9 +364,8 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
     __syncthreads();
   }
   // the list is consumed: the last block to finish zeroes the count (and this ticket) for the
-  // next launch, so a loop needs no per-step memset node (the count is zeroed once at loop
-  // creation).  Round 4's per-scan hipMemsetAsync on the same stream was ordered too; the
-  // corrupted counts seen then are discussed in DESIGN §3.8 ("the round-4 hlist overflow").
+  // next launch, so a loop needs no per-step memset node (count, ticket and fault word are zeroed
+  // at loop creation before the setup sync, and by every m3d_icp_reset on the caller's stream).
   if (threadIdx.x == 0 &&
       __hip_atomic_fetch_add(hcnt + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
     __hip_atomic_store(hcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -926,7 +921,7 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
                           const int32_t* prev, const int64_t* dprev, const float4* tgt32, int64_t nt_shard,
                           hipStream_t st, int64_t q0, int64_t q1, int32_t* hlist, uint32_t* hcnt,
-                          int32_t cand_cap, const double* src64, const double* tgt64) {
+                          int32_t cand_cap, const double* src64, const double* tgt64, int32_t hcap) {
   if (q1 >= 0) ns = q1;
   if (ns <= q0) return hipSuccess;
   if (qgrid == nullptr || qgrid->mpts == nullptr) return hipErrorInvalidValue;  // Morton query order
@@ -937,13 +932,13 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
   const int64_t nb = ((ns - q0) * L + kGridBlock - 1) / kGridBlock;
   const unsigned launch = (unsigned)((nb + 7) / 8 * 8);
   // deferral of dense-cell and ambiguous queries to grid_nn_heavy_kernel (api.cpp icp_create)
-  const bool defer = hlist != nullptr && hcnt != nullptr && cand_cap > 0 && g->dev.ncells > 0 &&
+  const bool defer = hlist != nullptr && hcnt != nullptr && cand_cap > 0 && hcap > 0 && g->dev.ncells > 0 &&
                      src64 != nullptr && tgt64 != nullptr;
   const int cap = defer ? cand_cap : 0x7FFFFFFF;
 #define M3D_GB(LV, DV)                                                                              \
   grid_nn_batched_kernel<LV, 2, 2, DV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, \
                                                                      near2, prev, dprev, tgt32, nt_shard, nb, \
-                                                                     q0, hlist, hcnt, cap)
+                                                                     q0, hlist, hcnt, cap, (uint32_t)hcap)
   if (defer) {
     if (L == 4) M3D_GB(4, true); else M3D_GB(2, true);
   } else {
@@ -953,7 +948,8 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
   if (defer) {  // a fixed grid striding over the deferred queries (their count stays on the device)
     const unsigned hb = (unsigned)std::min<int64_t>(512, ns - q0);
     grid_nn_heavy_kernel<<<hb, kGridBlock, 0, st>>>(qgrid->mpts, g->dev, off, s, keys, near2, prev, dprev,
-                                                    tgt32, nt_shard, hlist, hcnt, src64, tgt64, ns);
+                                                    tgt32, nt_shard, hlist, hcnt, src64, tgt64, ns,
+                                                    (uint32_t)hcap);
   }
   return hipGetLastError();
 }

@@ -1539,18 +1539,34 @@ hipError_t launch_icp_set_T(const m3d_icp* s, const double* T_dev, hipStream_t s
   return hipGetLastError();
 }
 
-__global__ void scatter3_f64_kernel(const double* __restrict__ v, const int32_t* __restrict__ slot, int64_t n,
-                                    double* __restrict__ dst) {
+// m3d_icp_copy_points: the loop's points in the caller's order.  Before the first evaluation the
+// init is still in dT (pcd64 = the source): apply it as the evaluation will (q64_of, Eigen's
+// order) — RegistrationICP's pcd at that point is init·source — unless dT is exactly I
+// (init isIdentity(): Open3D leaves pcd untouched, and I·p could turn a −0 into +0).
+__global__ void copy_points_kernel(const IcpState* __restrict__ s, const double* __restrict__ v,
+                                   const int32_t* __restrict__ slot, int64_t n, double* __restrict__ dst) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= n) return;
-  const int64_t o = slot != nullptr ? (int64_t)slot[k] : k;
-  for (int c = 0; c < 3; ++c) dst[3 * o + c] = v[3 * k + c];
+  const int64_t o = (int64_t)slot[k];
+  bool apply = s->evals == 0;
+  if (apply) {
+    bool eye = true;
+    for (int e = 0; e < 16; ++e) eye = eye && s->dT[e] == ((e % 5) == 0 ? 1.0 : 0.0);
+    apply = !eye;
+  }
+  if (apply) {
+    double q[3];
+    q64_of(s->dT, v + 3 * k, q);
+    for (int c = 0; c < 3; ++c) dst[3 * o + c] = q[c];
+  } else {
+    for (int c = 0; c < 3; ++c) dst[3 * o + c] = v[3 * k + c];
+  }
 }
 
 hipError_t launch_copy_points(const m3d_icp* s, double* dst, hipStream_t st) {
   const int64_t n = s->src->n;
   if (n == 0) return hipSuccess;
-  scatter3_f64_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s->pcd64, s->src->slot, n, dst);
+  copy_points_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s->state, s->pcd64, s->src->slot, n, dst);
   return hipGetLastError();
 }
 

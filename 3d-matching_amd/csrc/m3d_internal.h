@@ -9,6 +9,7 @@
 #include <utility>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/m3d.h"
@@ -227,6 +228,10 @@ inline bool in_block(const void* p, const void* block, size_t bytes) {
   return block != nullptr && p >= block && static_cast<const char*>(p) < static_cast<const char*>(block) + bytes;
 }
 
+// the grid NN's deferral list header (m3d_icp::hcnt): [0] count, [1] grid_nn_heavy_kernel's block
+// ticket, [2] fault (a count beyond the list: the write was dropped), [3] pad
+constexpr int kDeferWords = 4;
+constexpr int kDeferFault = 2;
 constexpr int kTermSlots = 32;  // 21 JTJ + 6 JTr + r² + count + Σd² (+2 pad)
 constexpr int64_t kKeyNone = 0x7FFFFFFFFFFFFFFFll;
 
@@ -260,7 +265,8 @@ struct m3d_ctx {
   m3d::TmpArena run;  // loop arrays of the synchronous one-shot ICP / NN calls (api.cpp icp_create)
   // streams this context enqueued work on, each with an event re-recorded at every such call
   // (api.cpp ctx_touch): the release marks of the block cache wait for all of them on `order`
-  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // (pruned of completed entries per mark)
+  std::mutex uses_mu;  // ctx_touch vs ReleaseScope (destroys may run on finaliser threads)
   bool uses_lost = false;  // an event could not be made: releases fall back to a device sync
   hipStream_t order = nullptr;
   bool counted = false;  // counted among its device's live contexts (api.cpp ctx_count)
@@ -337,7 +343,8 @@ struct m3d_icp {
   // by the per-query scan (ns slots), their count and the kernel's block ticket; cand_cap = 0: no
   // deferral
   int32_t* hlist = nullptr;
-  uint32_t* hcnt = nullptr;
+  uint32_t* hcnt = nullptr;  // kDeferWords: count, ticket, fault
+  int32_t hcap = 0;          // hlist entries (the scan drops, and flags, a slot at or past it)
   int32_t cand_cap = 0;
   bool keys_clean = false;         // host view: every key is kKeyNone (fused tail reset them)
   int32_t* corr = nullptr;         // ns current correspondence (-1 none)
@@ -494,7 +501,7 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           const int32_t* prev, const int64_t* dprev, const float4* tgt32, int64_t nt_shard,
                           hipStream_t st, int64_t q0 = 0, int64_t q1 = -1, int32_t* hlist = nullptr,
                           uint32_t* hcnt = nullptr, int32_t cand_cap = 0, const double* src64 = nullptr,
-                          const double* tgt64 = nullptr);
+                          const double* tgt64 = nullptr, int32_t hcap = 0);
 // the ICP source's Morton-slot copy (out, gout freshly allocated structs): grid.hip morton_source
 hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid* gout, TmpArena* ta,
                          hipStream_t st);

@@ -30,7 +30,7 @@ COMM_ID_BYTES = 128
 DT_I32, DT_I64, DT_F64 = 0, 1, 2
 OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 NN_METHODS = {"brute": NN_BRUTE, "grid": NN_GRID}
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 vp = C.c_void_p
 i64 = C.c_int64
@@ -138,6 +138,8 @@ SIGNATURES = {
     "m3d_ransac_run_sharded": (C.c_int, [vp, vp, vp, C.POINTER(RansacParams), C.POINTER(RansacResult), vp]),
     "m3d_comm_poisoned": (C.c_int, [vp]),
     "m3d_debug_comm_inject": (C.c_int, [vp, C.c_int]),
+    "m3d_debug_block_cache_fill": (C.c_int, [C.c_int]),
+    "m3d_debug_icp_defer_count": (C.c_int, [vp, C.c_uint32, vp]),
     "m3d_parse_ascii_rows": (C.c_int, [C.c_char_p, C.c_size_t, i64, i32, C.POINTER(dbl),
                                        C.POINTER(C.c_size_t)]),
     "m3d_format_ascii_rows": (C.c_int, [C.POINTER(dbl), i64, i32, vp, C.c_size_t, C.POINTER(C.c_size_t)]),

@@ -564,7 +564,8 @@ class IcpLoop:
         """The loop's fp64 points of the last evaluation (ns×3 f64 torch cuda, source order):
         RegistrationICP's transformed copy of the source (init applied unless it isIdentity(),
         then every update), from which that evaluation's correspondences and terms were taken;
-        after a reset and before the first evaluation, the source itself."""
+        after a reset and before the first evaluation, init·source (the source itself when init
+        isIdentity()), as RegistrationICP's pcd at that point."""
         torch = _torch()
         out = device_empty((max(self.src.n, 1), 3), torch.float64)
         self.ctx.check(self.ctx.lib.m3d_icp_copy_points(self.h, ptr(out), stream_handle()), "icp_copy_points")

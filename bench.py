@@ -141,6 +141,50 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _g(d, *path):
+    """d[path[0]][path[1]]..., None where any level is missing."""
+    for k in path:
+        if not isinstance(d, dict) or d.get(k) is None:
+            return None
+        d = d[k]
+    return d
+
+
+def _r(x, nd=4):
+    return None if x is None else (round(x, nd) if isinstance(x, float) else x)
+
+
+# the fields of `summary` (VERDICT r5 #5): the sub-legs the driver's truncated stdout tail must
+# still show — the LAST key of the JSON line, kept under ~600 characters
+SUMMARY_FIELDS = ("icp_brute", "icp_brute_frac", "icp_grid", "icp_grid_frac", "cfg1_cold_grid_ms",
+                  "cfg1_strong", "cfg1_strong_grid", "ransac", "ransac_frac", "ransac_strong",
+                  "ransac_nc3e5", "cfg3_brute", "cfg3_grid", "n_gpus", "comm_ranks")
+
+
+def build_summary(line: dict) -> dict:
+    """The compact digest of a bench line (every SUMMARY_FIELDS key; None where a leg did not run):
+    ICP it/s brute + grid with their roofline fractions, the cold cfg1 grid stages (clouds / loop
+    / iterations / total ms), the strong-scaling legs, RANSAC hyp/s (cfg2, its strong split, the
+    Nc = 3e5 secondary), cfg3 brute + grid it/s, n_gpus and the communicator's rank count."""
+    cold = _g(line, "cfg1_cold", "grid")
+    out = {
+        "icp_brute": _r(line.get("value"), 1), "icp_brute_frac": _r(_g(line, "roofline", "frac")),
+        "icp_grid": _r(_g(line, "icp_grid", "value"), 1),
+        "icp_grid_frac": _r(_g(line, "icp_grid", "roofline", "frac")),
+        "cfg1_cold_grid_ms": (None if cold is None else
+                              [_r(cold.get(k), 3) for k in ("clouds_ms", "loop_create_ms", "iterations_ms", "total_ms")]),
+        "cfg1_strong": _r(_g(line, "cfg1_strong", "value"), 1),
+        "cfg1_strong_grid": _r(_g(line, "cfg1_strong", "grid_value"), 1),
+        "ransac": _r(_g(line, "ransac", "value"), 0), "ransac_frac": _r(_g(line, "ransac", "roofline", "frac")),
+        "ransac_strong": _r(_g(line, "ransac", "strong", "value"), 0),
+        "ransac_nc3e5": _r(_g(line, "ransac", "nc3e5", "value"), 0),
+        "cfg3_brute": _r(_g(line, "cfg3", "value"), 2), "cfg3_grid": _r(_g(line, "cfg3", "grid", "value"), 1),
+        "n_gpus": line.get("n_gpus"), "comm_ranks": _g(line, "config", "comm_ranks"),
+    }
+    assert tuple(out) == SUMMARY_FIELDS
+    return out
+
+
 def launch_check(args, world, rank):
     """--launch-check: the process group over gloo (no GPU), a SUM of ones to count the ranks
     that actually joined, and rank 0's line."""
@@ -159,8 +203,10 @@ def launch_check(args, world, rank):
               file=sys.stderr)
         return 3
     if rank == 0:
-        print(json.dumps({"metric": "launch check", "value": None, "n_gpus": pg_world,
-                          "ranks_joined": joined, "launch_check": True}), flush=True)
+        line = {"metric": "launch check", "value": None, "n_gpus": pg_world, "ranks_joined": joined,
+                "launch_check": True, "config": {"comm": "gloo", "comm_ranks": joined}}
+        line["summary"] = build_summary(line)  # the same last key as a measured line
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
@@ -730,6 +776,7 @@ def main():
         "cpu_baseline": cpu,
         "check": cfg1["check"],
     }
+    line["summary"] = build_summary(line)  # last: the part of the line a truncated tail keeps
     if rank == 0:
         print(json.dumps(line), flush=True)
     del comm

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define M3D_ABI_VERSION 12
+#define M3D_ABI_VERSION 13
 
 /* return codes */
 #define M3D_OK 0
@@ -265,8 +265,9 @@ void m3d_icp_destroy(m3d_icp* s);
  * the queries were T·p of the original source). */
 int m3d_icp_reset(m3d_icp* s, const double* init_host, void* stream);
 /* The loop's fp64 points of the last evaluation (the source after init and every update but the
- * one the evaluation produced; after a reset and before the first evaluation, the source itself),
- * dst [device] ns×3 f64 in the caller's source order.  ABI 12. */
+ * one the evaluation produced), dst [device] ns×3 f64 in the caller's source order.  After a reset
+ * and before the first evaluation: the source with the init applied exactly as RegistrationICP's
+ * pcd.Transform(init) (the source itself when init isIdentity()).  ABI 12; init applied ABI 13. */
 int m3d_icp_copy_points(const m3d_icp* s, double* dst, void* stream);
 /* One full iteration on one device: NN evaluation + estimation terms + solve/update. */
 int m3d_icp_step(m3d_icp* s, void* stream);
@@ -362,7 +363,8 @@ int m3d_ransac_run_sharded(m3d_ctx* ctx, m3d_comm* c, const m3d_corrset* cs,
 /* 1 once the communicator was aborted after a failure (M3D_ERR_COMM from then on), else 0. */
 int m3d_comm_poisoned(const m3d_comm* c);
 
-/* Read the loop state (synchronises the stream). */
+/* Read the loop state (synchronises the stream).  M3D_ERR_HIP when the grid NN's deferral list
+ * overflowed since the last reset (its writes were dropped, the keys are not valid; ABI 13). */
 int m3d_icp_result_get(m3d_icp* s, m3d_icp_result* out, void* stream);
 /* The correspondence set of a per-source index array (RegistrationResult.correspondence_set,
  * icp.py:42 / ransac.py:42-59; ABI 11): pairs_out [host] with room for 2·n int32 receives
@@ -465,6 +467,13 @@ int m3d_debug_xxh3_128(const void* p, size_t len, uint64_t* out2);
 /* Failure injection for the multi-GPU failure tests: what = 1 fails this rank's next local run of
  * m3d_ransac_run_sharded, 2 its next ICP shard-loop iteration (0 clears). */
 int m3d_debug_comm_inject(m3d_comm* c, int what);
+/* Fill every idle block of the block cache on the current device with `byte` (synchronous); a
+ * later object that reuses one starts from those bytes.  Returns the blocks filled (>= 0).  ABI 13. */
+int m3d_debug_block_cache_fill(int byte);
+/* Overwrite the count of a grid loop's deferral list (synchronous on stream): a count past the
+ * list makes the next scan drop its writes and m3d_icp_result_get fail with M3D_ERR_HIP until the
+ * next m3d_icp_reset.  M3D_ERR_INVALID when the loop defers nothing.  ABI 13. */
+int m3d_debug_icp_defer_count(m3d_icp* s, uint32_t count, void* stream);
 
 /* ------------------------------------------------------------------ host text I/O (§8(f) rank 4) */
 

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, f"{s} missing from the ctypes signature table"
-    assert lib.m3d_abi_version() == _lib.ABI_VERSION == 12
+    assert lib.m3d_abi_version() == _lib.ABI_VERSION == 13
 
 
 def test_no_device_here_is_reported_not_crashed():

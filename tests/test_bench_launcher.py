@@ -54,3 +54,30 @@ def test_single_gpu_launch_check_unchanged():
     p = run_bench(["--gpus", "1", "--launch-check"])
     assert p.returncode == 0, p.stderr[-2000:]
     assert json_lines(p.stdout)[0]["n_gpus"] == 1
+
+
+def test_summary_is_the_last_key_and_survives_a_truncated_tail():
+    """the JSON line ends with a compact `summary` of every sub-leg (grid, cold,
+    strong, RANSAC, cfg3, ranks), so a driver that keeps only the last ~1,000 characters of stdout
+    still records them.  The dry line of --launch-check carries it; a full-size line (round 5's
+    recorded bench line, 11 kB) keeps every field and value in its last 1,000 characters."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    p = run_bench(["--gpus", "2", "--launch-check"], M3D_BENCH_SAME_DEVICE="1", M3D_BENCH_BACKEND="gloo")
+    assert p.returncode == 0, p.stderr[-2000:]
+    raw = [x for x in p.stdout.splitlines() if x.startswith("{")][0]
+    line = json.loads(raw)
+    assert list(line)[-1] == "summary"
+    assert tuple(line["summary"]) == bench.SUMMARY_FIELDS
+    assert line["summary"]["n_gpus"] == 2 and line["summary"]["comm_ranks"] == 2
+    full = json.loads((ROOT / "profiles" / "r05_recheck_bench.json").read_text())
+    full.pop("summary", None)
+    full["summary"] = bench.build_summary(full)
+    s = full["summary"]
+    assert len(json.dumps({"summary": s})) < 600
+    assert s["icp_grid"] is not None and s["cfg1_cold_grid_ms"] is not None and s["ransac_strong"] is not None
+    assert s["cfg3_grid"] is not None and s["cfg1_strong"] is not None
+    tail = json.dumps(full)[-1000:]
+    for k, v in s.items():
+        assert f'"{k}": {json.dumps(v)}' in tail, k

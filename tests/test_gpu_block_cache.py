@@ -1,4 +1,4 @@
-"""The device block cache (api.cpp, ABI 12): stream-ordered reuse, trimming, and the
+"""The device block cache (api.cpp, ABI 12-13): stream-ordered reuse, trimming, and the
 cloud-before-loop destruction order."""
 import time
 
@@ -76,3 +76,43 @@ def test_loop_outlives_its_source_cloud():
     assert (got.fitness, got.inlier_rmse) == (want.fitness, want.inlier_rmse)
     del lp  # frees the orphaned Morton copy
     context().trim_block_cache()
+
+
+def test_release_mark_covers_a_solve_only_sequence():
+    """m3d_icp_solve (and m3d_icp_shard_claim) record their stream use, so a loop
+    destroyed right after a solve queued behind long work on stream A goes back to the cache
+    marked AFTER that solve: a new loop on stream B that reuses the block waits for it (round 5's
+    mark was recorded at the previous touching call, before the solve, and B could take the block
+    while the solve was still writing the loop state)."""
+    import torch
+
+    src, tgt, nrm, _ = synth.icp_pair(30_000, seed=8)
+    s, t = Cloud(src), Cloud(tgt, nrm)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=5, nn="grid")
+    a = torch.cuda.Stream()
+    lp = IcpLoop(s, t, 0.12, **kw)
+    sums = torch.zeros(32, dtype=torch.float64, device="cuda")
+    with torch.cuda.stream(a):
+        lp.reset(np.eye(4))
+        lp.step()
+    torch.cuda.synchronize()
+    x = torch.randn(8192, 8192, device="cuda")
+    done_a = torch.cuda.Event()
+    with torch.cuda.stream(a):
+        for _ in range(40):
+            x = x @ x * 1e-4
+        lp.solve(sums)  # the only library call after the long work on A
+        done_a.record(a)
+    del lp  # release marked after A's last touch: the solve
+    b = torch.cuda.Stream()
+    with torch.cuda.stream(b):
+        lp2 = IcpLoop(s, t, 0.12, **kw)  # the cached block: creation waits for its mark
+    assert done_a.query(), "the reused block was handed out before the solve on stream A finished"
+    with torch.cuda.stream(b):
+        lp2.reset(np.eye(4))
+        lp2.steps(6)
+        r = lp2.result()
+    ref = IcpLoop(s, t, 0.12, **kw)
+    ref.reset(np.eye(4))
+    ref.steps(6)
+    np.testing.assert_array_equal(r.transformation, ref.result().transformation)
