@@ -859,6 +859,8 @@ with torch.cuda.stream(st):
     for _ in range(21):  # back to back on the non-blocking stream
         lp.step()
     out["dirty"] = outcome(lp) == want
+    lp.reset(init)  # (a finished loop's scans are no-ops: poke a running one)
+    lp.step()
     rc = lib.m3d_debug_icp_defer_count(lp.h, C.c_uint32(0x7FFFFFF0), stream_handle())
     out["poke_rc"] = rc
     lp.step()
