@@ -16,6 +16,7 @@
 
 #include "linalg.h"
 #include "m3d_internal.h"
+#include "ddmath.h"
 
 namespace m3d {
 hipError_t launch_icp_reset(const m3d_icp* s, const double* T, bool apply_init, hipStream_t st);
@@ -2228,6 +2229,12 @@ int m3d_debug_kabsch3_host(const double* src9, const double* tgt9, double* T16) 
 int m3d_debug_ldlt6_host(const double* A36, const double* b6, double* x6) {
   if (!A36 || !b6 || !x6) return M3D_ERR_INVALID;
   if (!ldlt6_solve_spd(A36, b6, x6)) ldlt6_solve(A36, b6, x6);  // the device solve's rule (icp.hip)
+  return M3D_OK;
+}
+
+int m3d_debug_acos_cr(const double* u, int64_t n, double* out) {
+  if (n < 0 || (n > 0 && (!u || !out))) return M3D_ERR_INVALID;
+  for (int64_t k = 0; k < n; ++k) out[k] = acos_cr(u[k]);  // the device's code, compiled for the host
   return M3D_OK;
 }
 

@@ -149,13 +149,23 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const IcpState* __restrict__ s, int64_t* __restrict__ keys, uint32_t* __restrict__ near2,
     const int32_t* __restrict__ prev, const int64_t* __restrict__ dprev,
     const float4* __restrict__ tgt32, int64_t nt_shard, int64_t nblocks, int64_t q0,
-    int32_t* __restrict__ hlist, uint32_t* __restrict__ hcnt, int cand_cap, uint32_t hcap) {
+    int32_t* __restrict__ hlist, uint32_t* __restrict__ hcnt, int cand_cap, uint32_t hcap, int xchunk) {
   if (s->done) return;
 #if M3D_SCAN_CLOCK
   const unsigned long long clk0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  const int64_t per = (nblocks + 7) / 8;
-  const int64_t blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  // block b runs on XCD b % 8.  xchunk = 0: XCD k takes the k-th eighth of the Morton order (one
+  // region per L2); xchunk = C: XCD k takes chunks k, k + 8, … of C consecutive blocks (the launch
+  // is a multiple of 8·C blocks), so work concentrated in one part of the cloud — a spatial target
+  // shard, whose queries are Morton-contiguous slabs — spreads over all eight XCDs
+  int64_t blk;
+  if (xchunk <= 0) {
+    const int64_t per = (nblocks + 7) / 8;
+    blk = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  } else {
+    const int64_t j = blockIdx.x / 8, k = blockIdx.x % 8;
+    blk = ((j / xchunk) * 8 + k) * xchunk + j % xchunk;
+  }
   if (blk >= nblocks) return;
   const int64_t t = q0 + (blk * kGridBlock + threadIdx.x) / kL;  // queries [q0, ns) in Morton order
   const int sub = threadIdx.x & (kL - 1);
@@ -172,11 +182,16 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     const float4 p = qpts[t];
     float qx, qy, qz;
     xform32(s->Rt32, p, qx, qy, qz);
+    // a query whose largest box (q ± 1.001·√r2_hi: any seed only shrinks it) misses this grid has
+    // no target of the shard within r2_hi: no seed (an own previous target would lie in that box;
+    // another shard's bound is a pseudo key, which every consumer reads as "none"), no scan — on a
+    // spatial target shard (m3d.dist.spatial_shards) most queries leave here, before the dprev load
+    const bool far = g.ncells > 0 && grid_box_miss(g, qx, qy, qz, sqrtf(r2_hi) * 1.001f);
     // seed: the previous correspondence re-evaluated (nnkey.h seed_key), or a bound
-    const int64_t seed = seed_key_j(s, pj, i, p, qx, qy, qz, tgt32, nt_shard, off, dprev);
+    const int64_t seed = far ? kKeyNone : seed_key_j(s, pj, i, p, qx, qy, qz, tgt32, nt_shard, off, dprev);
     if (seed != kKeyNone) k1 = (uint64_t)seed;
     k1d = key_real_d2(k1);
-    if (g.ncells > 0) {
+    if (g.ncells > 0 && !far) {
       float R = sqrtf(search_bound(key_d2(k1), be, r2_hi)) * 1.001f;
       if (M3D_SCAN_PHASE1 && 2.0f * R * g.inv_h > 3.0f) {
         // a box wider than ~4 cells per axis (no seed, or a seed the update moved far — the first
@@ -930,7 +945,12 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
   // flight per wave); 2 rows × 2 points per lane and load batch
   const int L = (ns - q0) > 300000 ? 2 : 4;
   const int64_t nb = ((ns - q0) * L + kGridBlock - 1) / kGridBlock;
-  const unsigned launch = (unsigned)((nb + 7) / 8 * 8);
+  static const int xchunk = [] {
+    const char* e = getenv("M3D_SCAN_XCHUNK");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  const int64_t unit = 8 * (int64_t)std::max(xchunk, 1);
+  const unsigned launch = (unsigned)((nb + unit - 1) / unit * unit);
   // deferral of dense-cell and ambiguous queries to grid_nn_heavy_kernel (api.cpp icp_create)
   const bool defer = hlist != nullptr && hcnt != nullptr && cand_cap > 0 && hcap > 0 && g->dev.ncells > 0 &&
                      src64 != nullptr && tgt64 != nullptr;
@@ -938,7 +958,7 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
 #define M3D_GB(LV, DV)                                                                              \
   grid_nn_batched_kernel<LV, 2, 2, DV><<<launch, kGridBlock, 0, st>>>(qgrid->mpts, ns, g->dev, off, s, keys, \
                                                                      near2, prev, dprev, tgt32, nt_shard, nb, \
-                                                                     q0, hlist, hcnt, cap, (uint32_t)hcap)
+                                                                     q0, hlist, hcnt, cap, (uint32_t)hcap, xchunk)
   if (defer) {
     if (L == 4) M3D_GB(4, true); else M3D_GB(2, true);
   } else {

@@ -114,6 +114,19 @@ __device__ __forceinline__ int grid_coord(float x, float o, float inv_h, int n) 
   return (int)f;
 }
 
+// whether [x − R, x + R] misses every target of an n-cell axis, by grid_coord's unclamped
+// coordinates (same expressions) of its two ends: below 0 (every target has x − o ≥ 0, exactly),
+// or at / past n + 1 (a target's coordinate is < n up to the fp32 rounding of (x − o)·inv_h, which
+// can reach n only for a point within ~1e-7 of the top edge: one cell of margin)
+__device__ __forceinline__ bool grid_miss(float x, float R, float o, float inv_h, int n) {
+  return ((x + R) - o) * inv_h < 0.0f || ((x - R) - o) * inv_h >= (float)(n + 1);
+}
+
+__device__ __forceinline__ bool grid_box_miss(const GridDev& g, float qx, float qy, float qz, float R) {
+  return grid_miss(qx, R, g.o[0], g.inv_h, g.n[0]) || grid_miss(qy, R, g.o[1], g.inv_h, g.n[1]) ||
+         grid_miss(qz, R, g.o[2], g.inv_h, g.n[2]);
+}
+
 // Grid scan of one query by kL cooperating lanes (grid.hip grid_nn_batched_kernel): every lane
 // of the query sees every cell row of the box q ± R and takes the row's points sub, sub + kL, …;
 // the start offsets of kR rows are loaded together, then kR × kB point loads per lane go out at
@@ -133,7 +146,11 @@ __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, 
   const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
   const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
   const int ny = y1 - y0 + 1;
-  const int rows = ny * (z1 - z0 + 1);
+  // a box that misses the grid on some axis (the unclamped cell range lies wholly below cell 0 or
+  // at / past cell n) holds none of its cells: the clamped range would scan an edge column of
+  // targets outside the box.  A spatial target shard (m3d.dist.spatial_shards) sees most queries
+  // leave here.
+  const int rows = grid_box_miss(g, qx, qy, qz, R) ? 0 : ny * (z1 - z0 + 1);
   if (nrows != nullptr) *nrows = rows;
   int cand = 0;
   for (int r0 = 0; r0 < rows; r0 += kR) {

@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "m3d_internal.h"
+#include "ddmath.h"
 
 namespace m3d {
 
@@ -630,7 +631,12 @@ __device__ bool pair_features(const double* p1, const double* n1in, const double
   const double* n1 = n1in;
   const double* n2 = n2in;
   double f2;
-  if (acos(fabs(a1)) > acos(fabs(a2))) {
+  // Open3D's swap test acos(|a1|) > acos(|a2|), decided as correctly rounded acos values would
+  // (ddmath.h acos_gt: the device libm's ulp on a near tie would otherwise pick the other side)
+#ifndef M3D_FPFH_CR_SWAP
+#define M3D_FPFH_CR_SWAP 1  // 0: the device libm's acos on both sides (round 5; A/B only)
+#endif
+  if (M3D_FPFH_CR_SWAP ? acos_gt(fabs(a1), fabs(a2)) : acos(fabs(a1)) > acos(fabs(a2))) {
     n1 = n2in;
     n2 = n1in;
     for (int a = 0; a < 3; ++a) dp[a] = -dp[a];

@@ -101,6 +101,39 @@ def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
     return off, base + (1 if rank < extra else 0)
 
 
+def spatial_shards(points, world: int):
+    """Spatial target shards (cfg3 at N > 1): slabs along the cloud's longest
+    axis, cut at the (k / world)-quantiles of that coordinate.  Returns (perm, bounds): the
+    target reordered as points[perm] holds rank r's slab at [bounds[r], bounds[r + 1]), each slab
+    in increasing original index.
+
+    Why: index shards of an unordered cloud each span the whole surface, so every rank scans every
+    source query against its sparse shard.  A slab's grid covers one region, and a query whose
+    search box misses it leaves at once (nnkey.h grid_miss); the keys, claims and terms are the
+    protocol's own, so the result is the single-device result ON THE REORDERED CLOUD (tie rule:
+    exact fp64 ties go to the lower index of points[perm]).  Cuts fall between distinct coordinate
+    values, so equal points (duplicates) always share a slab and keep their original order; a tie
+    between distinct points in two slabs is the only case where the original cloud's lowest-index
+    rule could pick the other point.  Map a correspondence c of the reordered cloud back with
+    perm[c]."""
+    p = np.asarray(points, np.float64)
+    n = len(p)
+    world = int(world)
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    if n == 0 or world == 1:
+        return np.arange(n, dtype=np.int64), np.array([0] + [n] * world, dtype=np.int64)
+    ext = p.max(axis=0) - p.min(axis=0)
+    x = p[:, int(np.argmax(ext))]
+    xs = np.sort(x)
+    cuts = xs[(np.arange(1, world) * n) // world]  # slab k: cuts[k-1] <= x < cuts[k]
+    slab = np.searchsorted(cuts, x, side="right")
+    perm = np.argsort(slab, kind="stable").astype(np.int64)  # stable: original order inside a slab
+    counts = np.bincount(slab, minlength=world)
+    bounds = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    return perm, bounds
+
+
 def pack_nn_key(d2_f32, idx):
     """numpy: (float32 bits << 32) | idx as int64; KEY_NONE where idx < 0 (the scan's key)."""
     d2 = np.asarray(d2_f32, np.float32)

@@ -91,6 +91,11 @@ def parse():
                          "source (target replicated, SUM of the terms only), or auto: the "
                          "north-star's rule -- shard the target only when it would not fit one "
                          "GPU's HBM budget (M3D_TARGET_SHARD_BYTES, default 64 GiB), else source")
+    ap.add_argument("--target-shards", choices=["spatial", "index"], default="spatial",
+                    help="target shards of the target-sharded runs (cfg3, and cfg1 under --shard "
+                         "target): spatial = slabs of the longest axis (m3d.dist.spatial_shards; "
+                         "a query whose box misses a rank's slab leaves its scan at once), index = "
+                         "ranges of the unordered cloud (every shard spans the whole surface)")
     ap.add_argument("--comm", choices=["lib", "torch"], default="lib",
                     help="N>1 collectives: libm3d's RCCL communicator, or torch.distributed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -406,8 +411,17 @@ def main():
     else:  # single device, or target-sharded: nt targets per rank, sources replicated
         src, tgt_all, nrm_all, T_true = synth.icp_pair(ns, nt * world, seed=0)
         off = rank * nt
-        tgt_c = (Cloud(tgt_all, nrm_all) if not multi else
-                 Cloud(tgt_all[off:off + nt], nrm_all[off:off + nt], center=tgt_all.mean(axis=0)))
+        if not multi:
+            tgt_c = Cloud(tgt_all, nrm_all)
+        else:  # the target as the shards see it: spatially ordered slabs (or index ranges)
+            c_all = tgt_all.mean(axis=0)
+            if args.target_shards == "spatial":
+                perm1, b1 = D.spatial_shards(tgt_all, world)
+                tgt_all, nrm_all = tgt_all[perm1], nrm_all[perm1]
+                off, nt_r = int(b1[rank]), int(b1[rank + 1] - b1[rank])
+            else:
+                nt_r = nt
+            tgt_c = Cloud(tgt_all[off:off + nt_r], nrm_all[off:off + nt_r], center=c_all)
     src_c = Cloud(src)
     K_NN, K_TERMS, K_COMM = _lib.KERNEL_NN, _lib.KERNEL_TERMS, _lib.KERNEL_COMM
 
@@ -533,13 +547,26 @@ def main():
         s3, t3, nr3, T3 = synth.icp_pair(n3, n3, seed=0)
         o3, c3 = D.shard_bounds(n3, world, rank)
         s3c = Cloud(s3)
-        t3c = Cloud(t3, nr3) if not multi else Cloud(t3[o3:o3 + c3], nr3[o3:o3 + c3], center=t3.mean(axis=0))
+        shards3 = "none"
+        if not multi:
+            t3c = Cloud(t3, nr3)
+        else:
+            c3_all = t3.mean(axis=0)
+            t3s, nr3s = t3, nr3
+            if args.target_shards == "spatial":  # slabs: a query whose box misses a slab leaves at once
+                perm3, b3 = D.spatial_shards(t3, world)
+                t3s, nr3s = t3[perm3], nr3[perm3]
+                o3, c3 = int(b3[rank]), int(b3[rank + 1] - b3[rank])
+            shards3 = args.target_shards
+            t3c = Cloud(t3s[o3:o3 + c3], nr3s[o3:o3 + c3], center=c3_all)
+            del t3s, nr3s
         mode3 = "single" if not multi else "target"
         cfg3 = {"metric": "ICP iterations/sec (cfg3: 1M<->1M pair, target sharded over the GPUs, strong scaling)",
                 "unit": "ICP iter/s (whole 1M x 1M problem)", "scaling": "strong",
                 "workload": f"cfg3: {n3}<->{n3} synthetic pair, {it3} point-to-plane iterations per step, "
-                            f"target sharded over {world} GPU(s) ({c3} targets on rank {rank}), sources "
-                            "replicated, MIN fp64 keys + MIN claims + SUM terms per iteration",
+                            f"target sharded over {world} GPU(s) ({shards3} shards, {c3} targets on rank "
+                            f"{rank}), sources replicated, MIN fp64 keys + MIN claims + SUM terms per iteration",
+                "target_shards": shards3,
                 "steps": args.cfg3_steps, "icp_iterations_per_step": it3}
         for nn in ("brute", "grid"):
             lp = IcpLoop(s3c, t3c, r, relative_fitness=-1.0, relative_rmse=-1.0, max_iteration=it3, nn=nn)

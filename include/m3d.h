@@ -467,6 +467,9 @@ int m3d_debug_xxh3_128(const void* p, size_t len, uint64_t* out2);
 /* Failure injection for the multi-GPU failure tests: what = 1 fails this rank's next local run of
  * m3d_ransac_run_sharded, 2 its next ICP shard-loop iteration (0 clears). */
 int m3d_debug_comm_inject(m3d_comm* c, int what);
+/* The FPFH swap test's correctly rounded acos (ddmath.h acos_cr, host-compiled copy of the device
+ * code): out[k] = acos(u[k]) rounded to nearest, for the CPU test against mpmath.  ABI 13. */
+int m3d_debug_acos_cr(const double* u, int64_t n, double* out);
 /* Fill every idle block of the block cache on the current device with `byte` (synchronous); a
  * later object that reuses one starts from those bytes.  Returns the blocks filled (>= 0).  ABI 13. */
 int m3d_debug_block_cache_fill(int byte);

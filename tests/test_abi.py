@@ -178,3 +178,28 @@ def test_host_solve_rule_matches_oracle():
         x, ref = solve(A, b), I.ldlt_solve(A, b)
         assert x[zero] == 0.0 and ref[zero] == 0.0
         np.testing.assert_allclose(x, ref, rtol=1e-10, atol=1e-13)
+
+
+def test_acos_cr_is_correctly_rounded():
+    """ddmath.h acos_cr (the FPFH swap test's acos, host-compiled copy of the device code) equals
+    acos rounded to nearest from 200-bit mpmath on 20,000 arguments — uniform, near 1 (where acos
+    is steep and glibc's own acos misrounds most often) and near 0 — while glibc's math.acos
+    does not everywhere (it is not correctly rounded: the reason the swap test needs this)."""
+    import math
+    import random
+
+    mpmath = pytest.importorskip("mpmath")
+    mpmath.mp.prec = 200
+    lib = _lib.load()
+    rnd = random.Random(11)
+    u = np.array([[r, 1 - r * 1e-6, 1 - rnd.random() ** 8, r * 1e-9, 1 - 2.0 ** -53 * (1 + k % 50)][k % 5]
+                  for k, r in ((k, rnd.random()) for k in range(20000))])
+    out = np.empty_like(u)
+    assert lib.m3d_debug_acos_cr(u.ctypes.data_as(C.c_void_p), len(u), out.ctypes.data_as(C.c_void_p)) == 0
+    ref = np.array([float(mpmath.acos(mpmath.mpf(x))) for x in u])
+    np.testing.assert_array_equal(out, ref)
+    assert sum(math.acos(x) != r for x, r in zip(u, ref)) > 0  # glibc misrounds some of them
+    edge = np.array([0.0, 1.0, 1.0 + 2.0 ** -52, np.nan])
+    out = np.empty_like(edge)
+    lib.m3d_debug_acos_cr(edge.ctypes.data_as(C.c_void_p), 4, out.ctypes.data_as(C.c_void_p))
+    assert out[0] == math.acos(0.0) and out[1] == 0.0 and np.isnan(out[2]) and np.isnan(out[3])

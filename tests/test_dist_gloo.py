@@ -282,3 +282,31 @@ def test_rank_failure_reaches_every_rank(tmp_path, what):
     r1 = (tmp_path / "rank1.txt").read_text()
     assert r0.startswith("M3DCommError"), r0
     assert r1.startswith("RuntimeError: injected"), r1
+
+
+def test_spatial_shards_partition_and_keep_duplicates_together():
+    """m3d.dist.spatial_shards: a permutation whose slabs are contiguous, balanced, ordered along
+    the longest axis, each in increasing original index; equal points never straddle a cut."""
+    from m3d import dist as D
+
+    rng = np.random.default_rng(3)
+    p = rng.normal(size=(10_001, 3)) * np.array([1.0, 5.0, 0.5])  # longest axis: y
+    p[5000:5400] = p[17]  # a block of duplicates
+    for world in (1, 2, 3, 8):
+        perm, b = D.spatial_shards(p, world)
+        assert sorted(perm.tolist()) == list(range(len(p)))
+        assert b[0] == 0 and b[-1] == len(p) and len(b) == world + 1
+        y = p[perm, 1]
+        for k in range(world):
+            seg = perm[b[k]:b[k + 1]]
+            assert (np.diff(seg) > 0).all()  # original order inside a slab
+            if k + 1 < world and b[k + 1] < len(p) and b[k + 1] > b[k]:
+                assert y[b[k]:b[k + 1]].max() < y[b[k + 1]:].min()  # slabs ordered, disjoint in y
+        slab_of = np.empty(len(p), int)
+        for k in range(world):
+            slab_of[perm[b[k]:b[k + 1]]] = k
+        assert len(set(slab_of[5000:5400].tolist()) | {slab_of[17]}) == 1
+        if world == 8:
+            assert np.abs(np.diff(b) - len(p) / 8).max() <= 401  # balanced up to the duplicate block
+    perm, b = D.spatial_shards(np.zeros((0, 3)), 4)
+    assert len(perm) == 0 and list(b) == [0, 0, 0, 0, 0]

@@ -65,6 +65,30 @@ def test_cfg3_geometry_eight_shards_match_unsharded():
     # the first evaluation (identity transform) against the oracle's exact fp64 NN
     ref_j, _ = I.nn_exact(cKDTree(tgt), tgt, src, 0.12)
     np.testing.assert_array_equal(first["claims"], ref_j)
+    # SPATIAL shards (m3d.dist.spatial_shards: 8 slabs of the longest axis, bench.py's cfg3
+    # default): the protocol on the reordered target; its claims mapped back through perm are the
+    # unsharded correspondences of the ORIGINAL cloud at every evaluation, the fitness is the
+    # single-device run's and the transform too (to the SUM's reassociation of the terms)
+    from m3d import dist as D
+
+    perm, sb = D.spatial_shards(tgt, 8)
+    assert sorted(perm.tolist()) == list(range(n)) and sb[0] == 0 and sb[-1] == n
+    assert (np.diff(sb) > n // 8 - n // 50).all()  # balanced within 2 %
+
+    def check_sp(it, lp, kmin, cmin):
+        slot_claims = cmin.cpu().numpy().astype(np.int64)
+        got = np.empty_like(slot_claims)
+        got[lp.source_slots().cpu().numpy()] = slot_claims
+        got = np.where(got == 0x7FFFFFFF, -1, perm[np.minimum(got, n - 1)])
+        np.testing.assert_array_equal(got, ref_corr[it], err_msg=f"spatial shards, evaluation {it}")
+
+    for nn in ("grid", "brute"):
+        loops = run_target_shards(src, tgt[perm], nrm[perm], sb, 3, nn, check_keys=check_sp)
+        r = loops[0].result()
+        np.testing.assert_allclose(r.transformation, ref.transformation, rtol=0, atol=1e-9)
+        assert r.fitness == ref.fitness
+        del loops
+        torch.cuda.empty_cache()
 
 
 # ---------------------------------------------------------------------------- 2 ranks, gloo
