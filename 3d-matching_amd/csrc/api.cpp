@@ -2238,6 +2238,14 @@ int m3d_debug_acos_cr(const double* u, int64_t n, double* out) {
   return M3D_OK;
 }
 
+int m3d_debug_acos_device(m3d_ctx* ctx, const double* u, int64_t n, double* out, int mode, void* stream) {
+  if (!ctx) return M3D_ERR_INVALID;
+  CHECK_ARG(ctx, n >= 0 && (n == 0 || (u && out)) && (mode == 0 || mode == 1), "invalid arguments");
+  hipSetDevice(ctx->device);
+  HIPX(ctx, launch_acos_probe(u, n, out, mode, S(stream)));
+  return M3D_OK;
+}
+
 int m3d_debug_block_cache_fill(int byte) {
   // synchronous: every idle block's release point has passed before, and the fill is complete
   // after, so the next owner sees exactly these bytes

@@ -537,6 +537,7 @@ hipError_t hybrid_search(const m3d_cloud* c, const Grid* g, double radius, int k
                          double hfine = 0.0);
 hipError_t launch_normals(const m3d_cloud* c, const int32_t* nbr, int k, const int32_t* cnt,
                           const double* prev, double* out, hipStream_t st);
+hipError_t launch_acos_probe(const double* u, int64_t n, double* out, int mode, hipStream_t st);
 hipError_t launch_fpfh(const m3d_cloud* c, const double* nrm, const int32_t* nbr, const double* d2,
                        int k, const int32_t* cnt, double* spfh, double* out, hipStream_t st);
 hipError_t feature_nn(const double* fq, int64_t nq, const double* fr, int64_t nr, int32_t* out,

@@ -899,6 +899,18 @@ hipError_t launch_normals(const m3d_cloud* c, const int32_t* nbr, int k, const i
   return hipGetLastError();
 }
 
+// m3d_debug_acos_device: the swap test's acos on the device (mode 0: acos_cr, 1: the libm's acos)
+__global__ void acos_probe_kernel(const double* __restrict__ u, int64_t n, double* __restrict__ out, int mode) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) out[k] = mode == 0 ? acos_cr(u[k]) : acos(u[k]);
+}
+
+hipError_t launch_acos_probe(const double* u, int64_t n, double* out, int mode, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  acos_probe_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(u, n, out, mode);
+  return hipGetLastError();
+}
+
 hipError_t launch_fpfh(const m3d_cloud* c, const double* nrm, const int32_t* nbr, const double* d2,
                        int k, const int32_t* cnt, double* spfh, double* out, hipStream_t st) {
   if (c->n == 0) return hipSuccess;

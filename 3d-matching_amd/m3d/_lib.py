@@ -139,6 +139,7 @@ SIGNATURES = {
     "m3d_comm_poisoned": (C.c_int, [vp]),
     "m3d_debug_comm_inject": (C.c_int, [vp, C.c_int]),
     "m3d_debug_acos_cr": (C.c_int, [vp, C.c_int64, vp]),
+    "m3d_debug_acos_device": (C.c_int, [vp, vp, C.c_int64, vp, C.c_int, vp]),
     "m3d_debug_block_cache_fill": (C.c_int, [C.c_int]),
     "m3d_debug_icp_defer_count": (C.c_int, [vp, C.c_uint32, vp]),
     "m3d_parse_ascii_rows": (C.c_int, [C.c_char_p, C.c_size_t, i64, i32, C.POINTER(dbl),

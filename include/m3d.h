@@ -470,6 +470,9 @@ int m3d_debug_comm_inject(m3d_comm* c, int what);
 /* The FPFH swap test's correctly rounded acos (ddmath.h acos_cr, host-compiled copy of the device
  * code): out[k] = acos(u[k]) rounded to nearest, for the CPU test against mpmath.  ABI 13. */
 int m3d_debug_acos_cr(const double* u, int64_t n, double* out);
+/* The same on the device: out[k] [device] = acos_cr(u[k]) (mode 0) or the device libm's acos
+ * (mode 1) for u [device] n f64.  ABI 13. */
+int m3d_debug_acos_device(m3d_ctx* ctx, const double* u, int64_t n, double* out, int mode, void* stream);
 /* Fill every idle block of the block cache on the current device with `byte` (synchronous); a
  * later object that reuses one starts from those bytes.  Returns the blocks filled (>= 0).  ABI 13. */
 int m3d_debug_block_cache_fill(int byte);

@@ -357,3 +357,40 @@ def test_host_text_io_before_any_device_call(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     assert int(r.stdout.split()[-1]) > 0
+
+
+def test_device_acos_cr_is_correctly_rounded():
+    """The swap test's acos compiled for gfx950 (ddmath.h acos_cr through m3d_debug_acos_device)
+    equals the correctly rounded acos (200-bit mpmath) on 20,000 arguments — uniform, near 1,
+    near 0 — and the host copy bit for bit.  The device libm's own acos is reported beside it:
+    it agrees with glibc's on most arguments but not all, which is why the swap test does not
+    use it."""
+    import ctypes as C
+    import math
+    import random
+
+    import torch
+
+    mpmath = pytest.importorskip("mpmath")
+    mpmath.mp.prec = 200
+    from m3d.core import context, ptr, stream_handle
+
+    rnd = random.Random(11)
+    u = np.array([[r, 1 - r * 1e-6, 1 - rnd.random() ** 8, r * 1e-9, 1 - 2.0 ** -53 * (1 + k % 50)][k % 5]
+                  for k, r in ((k, rnd.random()) for k in range(20000))])
+    ctx = context()
+    ud = torch.from_numpy(u).cuda()
+    outs = []
+    for mode in (0, 1):
+        od = torch.empty_like(ud)
+        ctx.check(ctx.lib.m3d_debug_acos_device(ctx.h, ptr(ud), len(u), ptr(od), mode, stream_handle()),
+                  "acos_device")
+        outs.append(od.cpu().numpy())
+    ref = np.array([float(mpmath.acos(mpmath.mpf(x))) for x in u])
+    np.testing.assert_array_equal(outs[0], ref)
+    host = np.empty_like(u)
+    ctx.lib.m3d_debug_acos_cr(u.ctypes.data_as(C.c_void_p), len(u), host.ctypes.data_as(C.c_void_p))
+    np.testing.assert_array_equal(outs[0], host)
+    glibc = np.array([math.acos(x) for x in u])
+    print(f"device libm acos != glibc: {int((outs[1] != glibc).sum())}, != CR: {int((outs[1] != ref).sum())}; "
+          f"glibc != CR: {int((glibc != ref).sum())} of {len(u)}")
