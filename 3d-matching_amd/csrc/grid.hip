@@ -936,7 +936,8 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           int64_t off, const IcpState* s, int64_t* keys, uint32_t* near2,
                           const int32_t* prev, const int64_t* dprev, const float4* tgt32, int64_t nt_shard,
                           hipStream_t st, int64_t q0, int64_t q1, int32_t* hlist, uint32_t* hcnt,
-                          int32_t cand_cap, const double* src64, const double* tgt64, int32_t hcap) {
+                          int32_t cand_cap, const double* src64, const double* tgt64, int32_t hcap,
+                          int32_t xchunk_loop) {
   if (q1 >= 0) ns = q1;
   if (ns <= q0) return hipSuccess;
   if (qgrid == nullptr || qgrid->mpts == nullptr) return hipErrorInvalidValue;  // Morton query order
@@ -945,10 +946,11 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
   // flight per wave); 2 rows × 2 points per lane and load batch
   const int L = (ns - q0) > 300000 ? 2 : 4;
   const int64_t nb = ((ns - q0) * L + kGridBlock - 1) / kGridBlock;
-  static const int xchunk = [] {
+  static const int xchunk_env = [] {
     const char* e = getenv("M3D_SCAN_XCHUNK");
-    return e ? std::max(0, atoi(e)) : 0;
+    return e ? std::max(0, atoi(e)) : -1;
   }();
+  const int xchunk = xchunk_env >= 0 ? xchunk_env : std::max(0, xchunk_loop);
   const int64_t unit = 8 * (int64_t)std::max(xchunk, 1);
   const unsigned launch = (unsigned)((nb + unit - 1) / unit * unit);
   // deferral of dense-cell and ambiguous queries to grid_nn_heavy_kernel (api.cpp icp_create)

@@ -1080,12 +1080,17 @@ __global__ __launch_bounds__(256) void shard_winner_kernel(
   const int64_t i0 = q0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool valid = i0 < ns;
   const int64_t i = valid ? i0 : 0;
-  double Q[3];
-  q64_of(s->dT, pcd64 + 3 * i, Q);
+  // a query with no candidate on this shard (kKeyNone: e.g. every query whose box missed a spatial
+  // shard's grid) has no winner here and is never ambiguous: its fp64 point and fp32 source are
+  // not read (at 1M sources on one of 8 slabs, ~7/8 of the queries)
+  const uint64_t k1 = valid ? (uint64_t)keys[i] : (uint64_t)kKeyNone;
+  const bool need = k1 != (uint64_t)kKeyNone;
+  double Q[3] = {0.0, 0.0, 0.0};
+  if (need) q64_of(s->dT, pcd64 + 3 * i, Q);
+  const float4 p32 = need ? src32[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   int64_t gj;
   double d;
-  winner_fp64(valid, valid ? (uint64_t)keys[i] : (uint64_t)kKeyNone,
-              valid ? __uint_as_float(near2[i]) : kInf, s, g, tgt64, off, nt_shard, src32[i], Q, gj, d);
+  winner_fp64(valid, k1, need ? __uint_as_float(near2[i]) : kInf, s, g, tgt64, off, nt_shard, p32, Q, gj, d);
   if (!valid) return;
   const int64_t k = gj >= 0 ? __double_as_longlong(d) : kKeyNone;
   lidx[i] = (int32_t)gj;

@@ -346,6 +346,10 @@ struct m3d_icp {
   uint32_t* hcnt = nullptr;  // kDeferWords: count, ticket, fault
   int32_t hcap = 0;          // hlist entries (the scan drops, and flags, a slot at or past it)
   int32_t cand_cap = 0;
+  // grid scan block → XCD mapping (grid.hip): 0 = one contiguous eighth of the Morton order per
+  // XCD; C > 0 = chunks of C blocks dealt round-robin — for a target that covers a slab of the
+  // source's extent (a spatial shard), whose queries' work sits in a few Morton ranges
+  int32_t scan_xchunk = 0;
   bool keys_clean = false;         // host view: every key is kKeyNone (fused tail reset them)
   int32_t* corr = nullptr;         // ns current correspondence (-1 none)
   double* pcd64 = nullptr;         // ns×3: the source as Open3D's RegistrationICP holds it — the
@@ -501,7 +505,7 @@ hipError_t launch_grid_nn(const float4* src32, int64_t ns, const Grid* qgrid, co
                           const int32_t* prev, const int64_t* dprev, const float4* tgt32, int64_t nt_shard,
                           hipStream_t st, int64_t q0 = 0, int64_t q1 = -1, int32_t* hlist = nullptr,
                           uint32_t* hcnt = nullptr, int32_t cand_cap = 0, const double* src64 = nullptr,
-                          const double* tgt64 = nullptr, int32_t hcap = 0);
+                          const double* tgt64 = nullptr, int32_t hcap = 0, int32_t xchunk = 0);
 // the ICP source's Morton-slot copy (out, gout freshly allocated structs): grid.hip morton_source
 hipError_t morton_source(const m3d_cloud* src, double cell, m3d_cloud* out, Grid* gout, TmpArena* ta,
                          hipStream_t st);
