@@ -122,11 +122,15 @@ class OracleShard:
         return self.T, self.fitness, self.rmse, self.iters
 
 
-def _icp_worker(rank, world, port, path, split=False):
+def _icp_worker(rank, world, port, path, split=False, spatial=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     src, tgt, nrm, _ = synth.icp_pair(4000, 6001, seed=21)
     off, cnt = D.shard_bounds(len(tgt), world, rank)
+    if spatial:  # slabs of the longest axis on the reordered target (bench.py's cfg3 default)
+        perm, b = D.spatial_shards(tgt, world)
+        tgt, nrm = tgt[perm], nrm[perm]
+        off, cnt = int(b[rank]), int(b[rank + 1] - b[rank])
     b = OracleShard(src, tgt[off:off + cnt], nrm[off:off + cnt], 0.12, 8)
     drv = D.ShardedIcp(b, off, len(src), "cpu", split=split)
     assert drv.split == bool(split)
@@ -135,12 +139,14 @@ def _icp_worker(rank, world, port, path, split=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,split", [(2, False), (2, 1733), (3, False), (3, 1733)])
-def test_sharded_icp_protocol_matches_single_process(tmp_path, world, split):
+@pytest.mark.parametrize("world,split,spatial", [(2, False, False), (2, 1733, False), (3, False, False),
+                                                 (3, 1733, False), (2, False, True), (3, 1733, True)])
+def test_sharded_icp_protocol_matches_single_process(tmp_path, world, split, spatial):
     """Target shards over gloo equal the single-process oracle, with the exchange in one piece
     and split (the first slot half's MIN in flight — async — while the second half's NN runs,
-    m3d_icp_shard_steps' schedule); world 3 gives uneven shards (6001 targets)."""
-    mp.spawn(_icp_worker, args=(world, free_port(), str(tmp_path), split), nprocs=world, join=True)
+    m3d_icp_shard_steps' schedule); world 3 gives uneven shards (6001 targets); spatial: the slabs
+    of m3d.dist.spatial_shards on the reordered target give the original cloud's transform."""
+    mp.spawn(_icp_worker, args=(world, free_port(), str(tmp_path), split, spatial), nprocs=world, join=True)
     src, tgt, nrm, _ = synth.icp_pair(4000, 6001, seed=21)
     ref = I.registration_icp(src, tgt, 0.12, np.eye(4), tgt_normals=nrm, relative_fitness=-1,
                              relative_rmse=-1, max_iteration=8)
