@@ -86,8 +86,17 @@ __device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const
     ctinf = fmax(ctinf, fabs(ct[i]));
   }
   const double mag = rowl1 * (csinf + pinf) + tabs + ctinf + qinf;
-  const double E = 8.0 * kU * (rowl1 * pinf + tinf + qinf) +
-                   8.0 * kU64 * 1.7320508075688772 * (double)(iters + 2) * mag + 1e-11 * (mag + 1.0);
+  // the fp32 part, term by term (xform32: q = fma(r0, px, fma(r1, py, fma(r2, pz, t′)))):
+  // p rounding u·Σ|r||p| + R rounding u·Σ|r||p| + three fma roundings ≤ 3u(Σ|r||p| + |t′|) +
+  // t′ rounding u|t′| + the target's u|t_c|, Σ|r||p| ≤ ‖r‖₁·|p|∞; ×1.01 for the O(u²) products.
+  // (Round 5 used 8u·(‖r‖₁|p|∞ + |t′| + |t|): 2.6× this at cfg1, and the fp32 → fp64 ambiguity
+  // band, hence the terms pass's fp64 walks, scale with E.)
+#ifndef M3D_TIGHT_E
+#define M3D_TIGHT_E 1
+#endif
+  const double E32 = M3D_TIGHT_E ? 1.01 * kU * (5.0 * rowl1 * pinf + 4.0 * tinf + qinf)
+                                 : 8.0 * kU * (rowl1 * pinf + tinf + qinf);
+  const double E = E32 + 8.0 * kU64 * 1.7320508075688772 * (double)(iters + 2) * mag + 1e-11 * (mag + 1.0);
   // nnkey.h: |√d2f − |Q − t|| ≤ e_q + 3u√d2f with e_q = √3·E; band_of's absolute term 2·e_q
   const double eq = 1.7320508075688772 * E * 1.01;
   const float eqf = __double2float_ru(eq), bef = __double2float_ru(2.0 * eq * 1.01);
