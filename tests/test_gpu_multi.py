@@ -261,3 +261,21 @@ def test_comm_failure_contract_world1():
         lp.shard_steps(c, 0, 1)
     with pytest.raises(M3DCommError):
         cs.run_sharded(c, p)
+
+
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_empty_target_shard_and_empty_target(nn):
+    """A target shard may be empty (m3d.dist.spatial_shards on heavily duplicated data can leave a
+    slab with no point): the emulated 3-shard protocol with an empty middle shard ends at the
+    single-device transform and fitness; an empty target on one device gives Open3D's empty result
+    (identity, fitness 0)."""
+    src, tgt, nrm, _ = synth.icp_pair(20_000, 30_000, seed=7)
+    kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=4, nn=nn)
+    single = icp(Cloud(src), Cloud(tgt, nrm), 0.12, np.eye(4), **kw)
+    loops = run_target_shards(src, tgt, nrm, [0, 15_000, 15_000, 30_000], 4, nn)
+    r = loops[0].result()
+    np.testing.assert_allclose(r.transformation, single.transformation, rtol=0, atol=1e-9)
+    assert r.fitness == single.fitness
+    out = icp(Cloud(src), Cloud(np.zeros((0, 3)), np.zeros((0, 3))), 0.12, np.eye(4), **kw)
+    assert out.fitness == 0.0 and out.inlier_rmse == 0.0
+    np.testing.assert_array_equal(out.transformation, np.eye(4))
