@@ -1001,8 +1001,12 @@ __device__ __forceinline__ void terms_block(const TermsArgs& a, const IcpState* 
 #pragma unroll
   for (int u = 0; u < kP; ++u) {
     const bool own = valid[u] && gj[u] >= a.off && gj[u] < a.off + a.nt_shard;
+    // branch-free: a source whose winner is not on this shard loads target 0 and drops it — but
+    // an EMPTY target shard has no target 0 (no arrays at all): nothing is loaded there
     const int64_t l = own ? gj[u] - a.off : 0;
-    if (a.rec64 != nullptr) {
+    if (a.nt_shard == 0) {
+      for (int k = 0; k < 3; ++k) tq[u][k] = tn[u][k] = 0.0;
+    } else if (a.rec64 != nullptr) {
       const double4 r0 = reinterpret_cast<const double4*>(a.rec64)[2 * l];
       const double4 r1 = reinterpret_cast<const double4*>(a.rec64)[2 * l + 1];
       tq[u][0] = r0.x;
