@@ -279,3 +279,24 @@ def test_empty_target_shard_and_empty_target(nn):
     out = icp(Cloud(src), Cloud(np.zeros((0, 3)), np.zeros((0, 3))), 0.12, np.eye(4), **kw)
     assert out.fitness == 0.0 and out.inlier_rmse == 0.0
     np.testing.assert_array_equal(out.transformation, np.eye(4))
+
+
+@pytest.mark.parametrize("nn", ["brute", "grid"])
+def test_tiny_targets_nn1_and_icp(nn):
+    """Targets of 0, 1 and 2 points: nn1 returns no / the exact fp64 neighbour (icp_oracle.nn_exact),
+    and ICP against a 1-point target (a rank-deficient point-to-plane system: the pivoted LDLT
+    fallback; Open3D's own answer there is arbitrary) runs to a finite transform."""
+    src, tgt, nrm, _ = synth.icp_pair(5_000, 5_000, seed=9)
+    q = Cloud(src)
+    for k in (0, 1, 2):
+        t, n = src[:k] + 0.01, nrm[:k]  # inside the radius of a few sources
+        i, d = nn1(q, Cloud(t, n), np.eye(4), 0.3, nn=nn)
+        if k == 0:
+            assert (i.cpu().numpy() == -1).all()
+            continue
+        ref_j, _ = I.nn_exact(cKDTree(t), t, src, 0.3)
+        np.testing.assert_array_equal(i.cpu().numpy(), ref_j)
+        assert (ref_j >= 0).sum() >= 5
+    out = icp(Cloud(src), Cloud(src[:1] + 0.01, nrm[:1]), 0.3, np.eye(4), nn=nn, relative_fitness=-1,
+              relative_rmse=-1, max_iteration=3)
+    assert np.isfinite(out.transformation).all()
