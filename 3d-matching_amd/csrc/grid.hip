@@ -178,8 +178,10 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_batched_kernel(
     // qpts are the loop's Morton copy (morton_copy_kernel: w = position = slot), so i = t, and the
     // previous correspondence is loaded beside the point instead of after it
     i = t;
-    const int32_t pj = prev != nullptr ? prev[t] : -1;
+    // (the point first: the prev load sits under a scalar branch whose wait would otherwise come
+    // before the point load is issued — one round trip for both instead of two)
     const float4 p = qpts[t];
+    const int32_t pj = prev != nullptr ? prev[t] : -1;
     float qx, qy, qz;
     xform32(s->Rt32, p, qx, qy, qz);
     // a query whose largest box (q ± 1.001·√r2_hi: any seed only shrinks it) misses this grid has

@@ -87,6 +87,14 @@ __device__ __forceinline__ void near_push(uint64_t& k1, float& k1d, float& near2
   k1d = lt ? d2c : k1d;
   near2 = fminf(near2, dd);
 }
+// push target idx at d2f d2 if d2 ≤ r2_hi, branch-free (else a key above every scan key — k1 is at
+// most (r2_hi, 0xFFFFFFFF) — and +inf: no change), so the point's index is read with its
+// coordinates in one 16-B load instead of by a second dependent load under the branch
+__device__ __forceinline__ void push_within(uint64_t& k1, float& k1d, float& near2, float d2, float r2_hi,
+                                            uint32_t idx) {
+  const bool ok = d2 <= r2_hi;
+  near_push(k1, k1d, near2, ok ? make_key(d2, idx) : ~0ull, ok ? d2 : kInf);
+}
 // merge another state (b1, bn2) of the same query into (k1, k1d, near2)
 __device__ __forceinline__ void near_merge(uint64_t& k1, float& k1d, float& near2, uint64_t b1,
                                            float bn2) {
@@ -127,6 +135,37 @@ __device__ __forceinline__ bool grid_box_miss(const GridDev& g, float qx, float 
          grid_miss(qz, R, g.o[2], g.inv_h, g.n[2]);
 }
 
+#ifndef M3D_SCAN_FLATLOAD
+#define M3D_SCAN_FLATLOAD 1
+#endif
+// The start / end offsets of rows r0 .. r0 + kR − 1 of a query's box (rows past `rows`: a = b = 0).
+// Every load is unconditional (a row past the box reads row r0's starts, dropped by the select):
+// loads under a per-lane branch compile to load → s_waitcnt vmcnt(0) → copy, one round trip each;
+// straight-line loads go out together and are waited for once.  The point loads below likewise
+// read slot 0 for a lane past its row's end.
+template <int kR>
+__device__ __forceinline__ void scan_row_starts(const GridDev& g, int r0, int rows, int ny, int x0, int x1,
+                                                int y0, int z0, int32_t* a, int32_t* b) {
+#pragma unroll
+  for (int k = 0; k < kR; ++k) {
+    const int r = r0 + k;
+    if (M3D_SCAN_FLATLOAD) {
+      const int rr = r < rows ? r : r0;  // r0 < rows
+      const int64_t row = ((int64_t)(z0 + rr / ny) * g.n[1] + (y0 + rr % ny)) * g.n[0];
+      const int32_t sa = g.start[row + x0], sb = g.start[row + x1 + 1];
+      a[k] = r < rows ? sa : 0;
+      b[k] = r < rows ? sb : 0;
+    } else {
+      a[k] = b[k] = 0;
+      if (r < rows) {
+        const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
+        a[k] = g.start[row + x0];
+        b[k] = g.start[row + x1 + 1];
+      }
+    }
+  }
+}
+
 // Grid scan of one query by kL cooperating lanes (grid.hip grid_nn_batched_kernel): every lane
 // of the query sees every cell row of the box q ± R and takes the row's points sub, sub + kL, …;
 // the start offsets of kR rows are loaded together, then kR × kB point loads per lane go out at
@@ -156,15 +195,9 @@ __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, 
   for (int r0 = 0; r0 < rows; r0 += kR) {
     int32_t a[kR], b[kR];
     int32_t len = 0;
+    scan_row_starts<kR>(g, r0, rows, ny, x0, x1, y0, z0, a, b);
 #pragma unroll
     for (int k = 0; k < kR; ++k) {
-      const int r = r0 + k;
-      a[k] = b[k] = 0;
-      if (r < rows) {
-        const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
-        a[k] = g.start[row + x0];
-        b[k] = g.start[row + x1 + 1];
-      }
       len = max(len, b[k] - a[k]);
       cand += b[k] - a[k];
     }
@@ -176,7 +209,10 @@ __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, 
 #pragma unroll
         for (int m = 0; m < kB; ++m) {
           const int32_t j = a[k] + base + m * kL;
-          if (j < b[k]) v[k][m] = g.pts[j];
+          if (M3D_SCAN_FLATLOAD)
+            v[k][m] = g.pts[j < b[k] ? j : 0];
+          else if (j < b[k])
+            v[k][m] = g.pts[j];
         }
 #pragma unroll
       for (int k = 0; k < kR; ++k)
@@ -185,8 +221,7 @@ __device__ __forceinline__ void grid_scan(const GridDev& g, float qx, float qy, 
           const int32_t j = a[k] + base + m * kL;
           if (j < b[k]) {
             const float d2 = d2f(qx, qy, qz, v[k][m].x, v[k][m].y, v[k][m].z);
-            if (d2 <= r2_hi)
-              near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(v[k][m].w))), d2);
+            push_within(k1, k1d, n2, d2, r2_hi, (uint32_t)(off + __float_as_int(v[k][m].w)));
           }
         }
     }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Grid-NN ICP timing (AB_LIB=path: another build of libm3d.so) at cfg1 (100k x 100k) and cfg3's per-rank geometry (1M sources x one 125k
 target shard) and 1M x 1M: per-launch averages of the NN and terms kernels (library HIP events).
-Usage: python tools/grid_timing.py [iters]"""
+Usage: [WARM=k] python tools/grid_timing.py [iters] [all|cfg1|1M x 1M|...]"""
 import sys
 from pathlib import Path
 
@@ -18,7 +18,8 @@ if os.environ.get("AB_LIB"):  # time another build of the library (tools/ab/*.so
 from m3d.core import Cloud, IcpLoop, context
 
 it = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-only = sys.argv[2] if len(sys.argv) > 2 else None
+only = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "all" else None
+warm = int(os.environ.get("WARM", "0"))  # WARM=k: kernel events over evaluations k .. iters only
 torch.cuda.set_device(0)
 ctx = context()
 for name, ns, nt_all, shard in (("cfg1 100k x 100k", 100_000, 100_000, 1), ("1M x 125k shard", 1_000_000, 1_000_000, 8),
@@ -32,10 +33,13 @@ for name, ns, nt_all, shard in (("cfg1 100k x 100k", 100_000, 100_000, 1), ("1M 
     lp.reset(np.eye(4))
     lp.steps(it + 1)
     torch.cuda.synchronize()
+    lp.reset(np.eye(4))
+    if warm:  # the first evaluations untimed (stale seeds while the transform still moves)
+        lp.steps(warm)
+        torch.cuda.synchronize()
     ctx.profile(True)
     ctx.profile_read(_lib.KERNEL_NN), ctx.profile_read(_lib.KERNEL_TERMS)
-    lp.reset(np.eye(4))
-    lp.steps(it + 1)
+    lp.steps(it + 1 - warm)
     nn_ms, n = ctx.profile_read(_lib.KERNEL_NN)
     t_ms, tn = ctx.profile_read(_lib.KERNEL_TERMS)
     ctx.profile(False)
