@@ -251,6 +251,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
     uint32_t* __restrict__ hcnt, const double* __restrict__ src64,
     const double* __restrict__ tgt64, int64_t nq, uint32_t hcap) {
   constexpr int kWaves = kGridBlock / kWave;
+  constexpr int kHU = 4;
   __shared__ uint64_t wk[kWaves];
   __shared__ float wn[kWaves];
   __shared__ double wd[kWaves];
@@ -294,11 +295,17 @@ __global__ __launch_bounds__(kGridBlock) void grid_nn_heavy_kernel(
     const int rows = ny * (z1 - z0 + 1);
     for (int r = wave; r < rows; r += kWaves) {
       const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
-      const int32_t b = g.start[row + x1 + 1];
-      for (int32_t j = g.start[row + x0] + lane; j < b; j += kWave) {
-        const float4 v = g.pts[j];
-        const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
-        if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)(off + __float_as_int(v.w))), d2);
+      const int32_t a = g.start[row + x0], b = g.start[row + x1 + 1];
+      // kHU points per lane per round trip (unconditional loads, slot 0 past the row's end)
+      for (int32_t j0 = a + lane; j0 < b; j0 += kHU * kWave) {
+        float4 v[kHU];
+#pragma unroll
+        for (int u = 0; u < kHU; ++u) v[u] = g.pts[j0 + u * kWave < b ? j0 + u * kWave : 0];
+#pragma unroll
+        for (int u = 0; u < kHU; ++u)
+          if (j0 + u * kWave < b)
+            push_within(k1, k1d, n2, d2f(qx, qy, qz, v[u].x, v[u].y, v[u].z), r2_hi,
+                        (uint32_t)(off + __float_as_int(v[u].w)));
       }
     }
     grid_merge_lanes<kWave>(k1, k1d, n2);
@@ -427,23 +434,10 @@ __global__ __launch_bounds__(kGridBlock) void validate_kernel(const float4* __re
     xform32(s->Rt32, p, qx, qy, qz);
     if (g.ncells > 0) {
       const float R = sqrtf(r2_hi) * 1.001f;
-      const int x0 = grid_coord(qx - R, g.o[0], g.inv_h, g.n[0]);
-      const int x1 = grid_coord(qx + R, g.o[0], g.inv_h, g.n[0]);
-      const int y0 = grid_coord(qy - R, g.o[1], g.inv_h, g.n[1]);
-      const int y1 = grid_coord(qy + R, g.o[1], g.inv_h, g.n[1]);
-      const int z0 = grid_coord(qz - R, g.o[2], g.inv_h, g.n[2]);
-      const int z1 = grid_coord(qz + R, g.o[2], g.inv_h, g.n[2]);
-      const int ny = y1 - y0 + 1;
-      const int rows = ny * (z1 - z0 + 1);
-      for (int r = sub; r < rows; r += kL) {
-        const int64_t row = ((int64_t)(z0 + r / ny) * g.n[1] + (y0 + r % ny)) * g.n[0];
-        const int32_t j1 = g.start[row + x1 + 1];
-        for (int32_t j = g.start[row + x0]; j < j1; ++j) {
-          const float4 v = g.pts[j];
-          const float d2 = d2f(qx, qy, qz, v.x, v.y, v.z);
-          if (d2 <= r2_hi) near_push(k1, k1d, n2, make_key(d2, (uint32_t)__float_as_int(v.w)), d2);
-        }
-      }
+      // the grid scan's batched rows and points (nnkey.h grid_scan: kL lanes over each row, the
+      // loads of 2 rows × 2 points per lane in one round trip); the (k1, near2) of the merged
+      // lanes do not depend on which lane pushed which target
+      grid_scan<kL, 2, 2>(g, qx, qy, qz, R, r2_hi, 0, sub, k1, k1d, n2);
     }
   }
 #pragma unroll

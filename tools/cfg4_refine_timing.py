@@ -10,6 +10,12 @@ import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(HERE, "..", "3d-matching_amd")]
+if os.environ.get("AB_LIB"):  # time another build of libm3d.so (tools/ab_build.sh)
+    from pathlib import Path
+
+    from m3d import _lib
+
+    _lib.LIB_PATH = Path(os.environ["AB_LIB"]).resolve()
 
 
 def main():
