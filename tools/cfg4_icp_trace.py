@@ -17,7 +17,8 @@ def main():
     from scipy.spatial import cKDTree
 
     from m3d import plyio, synth
-    from m3d.core import Cloud, IcpLoop
+    from m3d import _lib
+    from m3d.core import Cloud, IcpLoop, context
     from matcher.ransac import global_registration
     from ply import Ply
 
@@ -37,7 +38,9 @@ def main():
     tp, tn = np.asarray(tgt.pcd.points), np.asarray(tgt.pcd.normals)
     r = 0.12
     kt = cKDTree(tp)
-    loop = IcpLoop(Cloud(sp), Cloud(tp, tn), r, nn="grid", persist=False)
+    loop = IcpLoop(Cloud(sp), Cloud(tp, tn), r, nn="grid")
+    ctx = context()
+    ctx.profile(True)
     loop.reset(coarse.transformation)
     Tk = np.array(coarse.transformation, dtype=np.float64)
     print(f"points {len(sp)} / {len(tp)}; coarse fitness {coarse.fitness:.4f}", flush=True)
@@ -49,6 +52,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1)
+        nn_ms, _ = ctx.profile_read(_lib.KERNEL_NN)
+        t_ms, _ = ctx.profile_read(_lib.KERNEL_TERMS)
         x = synth.apply(Tk, sp)
         dd, _ = kt.query(x, k=2, distance_upper_bound=r)
         has = np.isfinite(dd[:, 0])
@@ -56,7 +61,7 @@ def main():
         ok = np.isfinite(dd[:, 1])
         ties = int((dd[ok, 1] - dd[ok, 0] < 1e-5).sum())
         res = loop.result()
-        print(f"step {k:2d}: {ms * 1e3:7.1f} us  with-nn {has.mean():.4f}  ball mean {ball.mean():6.1f} "
+        print(f"step {k:2d}: {ms * 1e3:7.1f} us (nn {nn_ms * 1e3:6.1f}, terms {t_ms * 1e3:6.1f})  with-nn {has.mean():.4f}  ball mean {ball.mean():6.1f} "
               f"max {ball.max():5d} >500 {(ball > 500).sum():4d}  ties {ties:4d}  "
               f"fitness {res.fitness:.5f} rmse {res.inlier_rmse:.5f} it {res.iterations} conv {res.converged}",
               flush=True)

@@ -41,6 +41,51 @@ __global__ __launch_bounds__(256) void gather_kernel(const T* __restrict__ a, ui
   out[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+// The scan's per-query loads (query point, seed, row starts) are the same address on the 4 lanes
+// of a query: every lane loading it (quad-uniform addresses) against one lane per quad loading it
+// and a DPP broadcast to the other three
+template <bool kOneLane>
+__global__ __launch_bounds__(256) void quad_kernel(const float4* __restrict__ a, uint32_t n, uint32_t span,
+                                                   uint32_t* __restrict__ out) {
+  const uint32_t q = (blockIdx.x * 256 + threadIdx.x) >> 2, sub = threadIdx.x & 3;
+  const uint32_t w0 = hash32(blockIdx.x * 4 + (threadIdx.x >> 6)) % (n - span - 16);
+  uint32_t acc = 0;
+  for (int r = 0; r < kRounds; ++r) {
+    const uint32_t h = hash32(q * 977u + r * 131u + (acc & 1u));
+    const uint32_t r0 = w0 + (h % span), r1 = w0 + ((h >> 12) % span);
+    uint32_t x = 0;
+    if (!kOneLane || sub == 0) {
+      const float4 v0 = a[r0], v1 = a[r1];
+      x = bits_of(v0) + bits_of(v1);
+    }
+    if (kOneLane) x = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x00, 0xF, 0xF, false);
+    acc += x;
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+static void run_quad(bool one, uint32_t n, uint32_t span, int blocks) {
+  float4* a; uint32_t* out;
+  hipMalloc(&a, sizeof(float4) * n);
+  hipMalloc(&out, sizeof(uint32_t) * 256 * blocks);
+  hipMemset(a, 0x3c, sizeof(float4) * n);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int it = 0; it < 12; ++it) {
+    hipEventRecord(e0);
+    if (one) quad_kernel<true><<<blocks, 256>>>(a, n, span, out);
+    else quad_kernel<false><<<blocks, 256>>>(a, n, span, out);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    if (it > 1 && ms < best) best = ms;
+  }
+  printf("quad-uniform 16-B loads, %s: n=%u span=%u: %8.2f us\n", one ? "one lane + DPP" : "all 4 lanes", n, span,
+         best * 1e3);
+  hipFree(a); hipFree(out);
+}
+
 template <typename T>
 static void run(const char* name, uint32_t n, uint32_t span, int blocks) {
   T* a; uint32_t* out;
@@ -66,6 +111,10 @@ static void run(const char* name, uint32_t n, uint32_t span, int blocks) {
 }
 
 int main() {
+  for (uint32_t n : {100000u, 1000000u}) {
+    run_quad(false, n, 2048, 1560);
+    run_quad(true, n, 2048, 1560);
+  }
   for (uint32_t n : {100000u, 1000000u}) {
     for (uint32_t span : {2048u, 65536u}) {
       const int blocks = 1560;  // ≈ cfg1's 6,234 waves
