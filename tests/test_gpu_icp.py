@@ -115,6 +115,26 @@ def test_icp_with_far_outliers_grid_identical_to_brute_force():
     assert (a.fitness, a.inlier_rmse) == (b.fitness, b.inlier_rmse) and a.fitness > 0.5
 
 
+@pytest.mark.parametrize("drop", ["half", "slab"])
+def test_partial_overlap_grid_identical_to_brute_force(drop):
+    """Partial overlaps — half of the target cut away (the grid's box then excludes the
+    unpartnered sources: the scan's far exit) or a slab from its middle (unpartnered sources
+    inside the grid, full radius boxes that find nothing): the grid loop keeps the brute-force
+    loop's bits at every iteration count."""
+    src, tgt, nrm, _ = synth.icp_pair(30000, 40000, seed=31)
+    lo, hi = np.quantile(tgt[:, 1], [0.3, 0.7])
+    keep = tgt[:, 0] < np.median(tgt[:, 0]) if drop == "half" else (tgt[:, 1] < lo) | (tgt[:, 1] > hi)
+    s, t = Cloud(src), Cloud(tgt[keep], nrm[keep])
+    for mi in (1, 3, 8, 25):
+        kw = dict(relative_fitness=-1, relative_rmse=-1, max_iteration=mi)
+        a = icp(s, t, 0.12, np.eye(4), nn="brute", **kw)
+        b = icp(s, t, 0.12, np.eye(4), nn="grid", **kw)
+        np.testing.assert_array_equal(b.transformation, a.transformation)
+        assert (b.fitness, b.inlier_rmse, b.iterations) == (a.fitness, a.inlier_rmse, a.iterations)
+        np.testing.assert_array_equal(b.correspondence_set, a.correspondence_set)
+        assert 0.2 < a.fitness < 0.9, a.fitness  # a real partial overlap
+
+
 def test_nn1_exact_ties_pick_lowest_index():
     tgt = np.array([[1.0, 0, 0], [-1.0, 0, 0], [0, 1.0, 0], [1.0, 0, 0]])
     src = np.zeros((3, 3))
