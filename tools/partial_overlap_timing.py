@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Grid ICP on partial overlaps (AB_LIB: another build of libm3d.so): cfg1's 100k x 100k pair with
-half of the target removed (x above its median), and 1M x 1M likewise — the sources without a
-target within r, whose scans the empty-ball certificates skip (grid.hip M3D_SCAN_CERT).  Per-launch
-average of the grid NN over the evaluations (library HIP events), fitness.
+half of the target removed (x above its median), and 1M x 1M likewise — half of the sources have
+no target within r (the round-6 empty-ball certificate experiment, docs/EXPERIMENTS.md §R6).
+Per-launch average of the grid NN over the evaluations (library HIP events), fitness.
 Usage: python tools/partial_overlap_timing.py [iters]"""
 import os
 import sys
@@ -27,7 +27,7 @@ for name, n in (("100k x 50k (half the target)", 100_000), ("1M x 500k (half the
     lp = IcpLoop(Cloud(src), Cloud(tgt[keep], nrm[keep]), 0.12, relative_fitness=-1, relative_rmse=-1,
                  max_iteration=it, nn="grid")
     lp.reset(np.eye(4))
-    lp.steps(it + 1)  # warm (the loop's certificates persist across resets: a fresh loop below)
+    lp.steps(it + 1)  # warm-up; the timed run uses a fresh loop
     torch.cuda.synchronize()
     lp = IcpLoop(Cloud(src), Cloud(tgt[keep], nrm[keep]), 0.12, relative_fitness=-1, relative_rmse=-1,
                  max_iteration=it, nn="grid")
