@@ -40,7 +40,10 @@ constexpr int kNNQ = 4;       // queries per lane (nn_kernel)
 constexpr int kNNTile = 16;   // screen sub-tile (one branch per sub-tile)
 constexpr int kNNLds = 512;   // targets per LDS tile (8 KB, double-buffered)
 constexpr int kNNBlock = 256;
-constexpr int kTermsBlock = 256;
+#ifndef M3D_TERMS_BLOCK
+#define M3D_TERMS_BLOCK 256
+#endif
+constexpr int kTermsBlock = M3D_TERMS_BLOCK;
 constexpr int kTermsPtsDefault = 2;  // sources per terms thread (1 / 4 / 8 were measured slower):
                                      // 2× fewer block partials for the last block to reduce
 static int terms_pts() { return kTermsPtsDefault; }
@@ -58,7 +61,19 @@ struct FrameParams {
 
 // Refresh the fp32 search transform and radius bound for transform T (device side; T and
 // r2 = s->r2 passed in registers by the solve, which has them already).
-__device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const FrameParams& f, int iters) {
+// fp64 → fp32 rounded toward +inf on the vector unit (the library's __double2float_ru bounces the
+// bits through the scalar unit, ≈ 20 dependent instructions each, five of them per refresh):
+// the round-to-nearest value, moved one ulp up when it lies below d (−0 / +0 → the least denormal)
+__device__ __forceinline__ float f32_ru(double d) {
+  const float f = (float)d;
+  const uint32_t u = __float_as_uint(f);
+  const uint32_t up = f == 0.0f ? 1u : ((int32_t)u >= 0 ? u + 1u : u - 1u);
+  return (double)f < d ? __uint_as_float(up) : f;
+}
+
+// r = √r2, taken by the caller (the solve computes it while its factorisation runs)
+__device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, double r, const FrameParams& f,
+                                  int iters) {
   const double* cs = f.cs;
   const double* ct = f.ct;
   const double pinf = f.pinf, qinf = f.qinf;
@@ -99,13 +114,12 @@ __device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const
   const double E = E32 + 8.0 * kU64 * 1.7320508075688772 * (double)(iters + 2) * mag + 1e-11 * (mag + 1.0);
   // nnkey.h: |√d2f − |Q − t|| ≤ e_q + 3u√d2f with e_q = √3·E; band_of's absolute term 2·e_q
   const double eq = 1.7320508075688772 * E * 1.01;
-  const float eqf = __double2float_ru(eq), bef = __double2float_ru(2.0 * eq * 1.01);
+  const float eqf = f32_ru(eq), bef = f32_ru(2.0 * eq * 1.01);
   s->eq = isfinite(eqf) ? eqf : FLT_MAX;
   s->band_e = isfinite(bef) ? bef : FLT_MAX;
-  const double r = sqrt(r2);
   const double e = 2.0 * (3.0 * kU * (r + 1.7320508075688772 * E) * (r + 1.7320508075688772 * E) +
                           2.0 * 1.7320508075688772 * E * r + 3.0 * E * E);
-  float hi = __double2float_ru(r2 + e);
+  float hi = f32_ru(r2 + e);
   if (!isfinite(hi)) hi = FLT_MAX;
   s->r2_hi = hi;
   // Screen bound: |fl(|t|² − 2q·t) − (d² − |q|²)| + rounding of thr ≤ eps,
@@ -113,7 +127,7 @@ __device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const
   const double Q = rowl1 * pinf + tinf;
   const double E1 = 5.0 * kU * (3.0 * qinf * qinf + 6.0 * Q * qinf);
   const double es = 2.0 * (E1 + 6.0 * kU * (double)hi + 12.0 * kU * Q * Q) + 1e-30;
-  const float esf = __double2float_ru(es);
+  const float esf = f32_ru(es);
   s->screen_eps = isfinite(esf) ? esf : FLT_MAX;
   // MFMA screen (nn_mfma_kernel): the same key from fp16 hi/lo operands scaled
   // by S = s16, in S² units.  Per coordinate a = −2Sq, t = St split as x = xh + xl + r with
@@ -131,7 +145,7 @@ __device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const
   const double Eacc = 32.0 * kU * 1.01 * (P + Ws);
   const double E1m = 1.05 * (Esplit + Eacc) / (S * S) + kU * 3.0 * qinf * qinf;
   const double esm = 2.0 * (E1m + 6.0 * kU * (double)hi + 12.0 * kU * Q * Q) + 1e-30;
-  const float esmf = __double2float_ru(esm);
+  const float esmf = f32_ru(esm);
   s->screen_eps_m = isfinite(esmf) ? esmf : FLT_MAX;
   s->mfma_scale = (float)S;
   // operands must stay well inside the fp16 range (max 65504) and the bound finite
@@ -142,7 +156,7 @@ __device__ void refresh_rt32_from(IcpState* s, const double* T, double r2, const
 __device__ void refresh_rt32(IcpState* s, const FrameParams& f) {
   double T[16];
   for (int k = 0; k < 16; ++k) T[k] = s->T[k];
-  refresh_rt32_from(s, T, s->r2, f, s->iters);
+  refresh_rt32_from(s, T, s->r2, sqrt(s->r2), f, s->iters);
 }
 
 __device__ __forceinline__ void set_identity(double* M) {
@@ -884,7 +898,7 @@ struct TermsArgs {
 #if M3D_TAIL_CLOCK  // diagnostic builds only (tools/tail_clock.py): per-wave start / end of the
                     // terms pass, the last block's ticket, reduce and solve steps (100 MHz), and
                     // per wave the number of ambiguous queries it resolved
-__device__ unsigned long long g_tail_clock[3 * 4096 + 8];
+__device__ unsigned long long g_tail_clock[3 * 4096 + 24];  // + 16 finer stamps at 3·4096 + 8
 #endif
 #ifndef M3D_WALK64
 #define M3D_WALK64 1  // build_grid_pts64 (0: resolve_wave gathers fp64 points after an fp32 screen)
@@ -1163,12 +1177,53 @@ struct SolveParams {
 };
 
 // vec6_to_matrix with the three sincos evaluated in lanes 0..2 at once (whole wave calls it)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// sin / cos of |a| ≤ 0.5 by their Taylor series in z = a² (Horner, sine to a¹⁷, cosine to a¹⁸: the
+// first dropped terms are < 2e-20 relative), ≈ 2 ulp; an ICP update's angles are far inside this
+#ifndef M3D_SMALL_SINCOS
+#define M3D_SMALL_SINCOS 1
+#endif
+__device__ __forceinline__ void sincos_small(double a, double* sn, double* cs) {
+  const double z = a * a;
+  double ps = 1.0 / 355687428096000.0;  // 1/17!
+  ps = fma(ps, z, -1.0 / 1307674368000.0);
+  ps = fma(ps, z, 1.0 / 6227020800.0);
+  ps = fma(ps, z, -1.0 / 39916800.0);
+  ps = fma(ps, z, 1.0 / 362880.0);
+  ps = fma(ps, z, -1.0 / 5040.0);
+  ps = fma(ps, z, 1.0 / 120.0);
+  ps = fma(ps, z, -1.0 / 6.0);
+  double pc = 1.0 / 6402373705728000.0;  // 1/18!
+  pc = fma(pc, z, -1.0 / 20922789888000.0);
+  pc = fma(pc, z, 1.0 / 87178291200.0);
+  pc = fma(pc, z, -1.0 / 479001600.0);
+  pc = fma(pc, z, 1.0 / 3628800.0);
+  pc = fma(pc, z, -1.0 / 40320.0);
+  pc = fma(pc, z, 1.0 / 720.0);
+  pc = fma(pc, z, -1.0 / 24.0);
+  pc = fma(pc, z, 0.5);
+  *sn = fma(a * z, ps, a);
+  *cs = fma(-z, pc, 1.0);
+}
+
 __device__ __forceinline__ void vec6_to_matrix_wave(const double x[6], double T[16]) {
   const int lane = threadIdx.x & (kWave - 1);
   double sn, cs;
-  sincos(lane == 0 ? x[0] : (lane == 1 ? x[1] : x[2]), &sn, &cs);
-  vec6_to_matrix_sc(x, __shfl(cs, 0, kWave), __shfl(sn, 0, kWave), __shfl(cs, 1, kWave),
-                    __shfl(sn, 1, kWave), __shfl(cs, 2, kWave), __shfl(sn, 2, kWave), T);
+  const double ang = lane == 0 ? x[0] : (lane == 1 ? x[1] : x[2]);
+  // x is the same in every lane: the branch is uniform
+  if (M3D_SMALL_SINCOS && fmax(fabs(x[0]), fmax(fabs(x[1]), fabs(x[2]))) <= 0.5)
+    sincos_small(ang, &sn, &cs);
+  else
+    sincos(ang, &sn, &cs);
+  // lanes 0..2 hold the results: v_readlane into SGPRs (a ds_bpermute per half costs an LDS trip)
+  vec6_to_matrix_sc(x, readlane_f64(cs, 0), readlane_f64(sn, 0), readlane_f64(cs, 1),
+                    readlane_f64(sn, 1), readlane_f64(cs, 2), readlane_f64(sn, 2), T);
 }
 
 // The state fields the solve reads, loaded by solve_in — in the fused tail before the partial
@@ -1197,7 +1252,8 @@ __device__ __forceinline__ void solve_in(const IcpState* s, SolveIn& in) {
 #if M3D_TAIL_CLOCK
 #define M3D_TCLK(k)                                                                   \
   do {                                                                                \
-    if (threadIdx.x == 0) g_tail_clock[2 * 4096 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0)                                                             \
+      g_tail_clock[(k) < 8 ? 2 * 4096 + (k) : 3 * 4096 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define M3D_TCLK(k) \
@@ -1219,8 +1275,32 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
 #pragma unroll
   for (int k = 0; k < 12; ++k) rt[k] = in.rt[k];
   const double count = sm[28];
+  const double r = sqrt(in.r2);  // for refresh_rt32_from; independent of everything below
+#ifndef M3D_SOLVE_SPEC
+#define M3D_SOLVE_SPEC 1
+#endif
+  // point-to-plane: the unpivoted LDLT of JᵀJ does not depend on the convergence test, so it is
+  // evaluated first, in the same basic block as fitness / rmse (their division and square-root
+  // chains interleave with the factorisation's); its result is used only if the loop goes on
+  double A[36], b[6], x[6];
+  bool spd_ok = false;
+  if (M3D_SOLVE_SPEC && kEst == M3D_EST_POINT_TO_PLANE) {
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int c = a; c < 6; ++c) {
+        A[a * 6 + c] = sm[k];
+        A[c * 6 + a] = sm[k];
+        ++k;
+      }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) b[a] = -sm[21 + a];
+    spd_ok = ldlt6_solve_spd(A, b, x);  // straight-line; x garbage (unused) when it fails
+  }
   const double fit = count > 0.0 ? count / (double)sp.ns : 0.0;
   const double rmse = count > 0.0 ? sqrt(sm[29] / count) : 0.0;
+  M3D_TCLK(10);
   bool stop = false;
   if (evals > 0 && fabs(prev_fit - fit) < sp.rel_fit && fabs(prev_rmse - rmse) < sp.rel_rmse) {
     s->converged = 1;
@@ -1248,24 +1328,27 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   for (int k = 0; k < 12; ++k) s->Rt32_prev[k] = rt[k];
   s->eq_prev = eq;
   s->bound_ok = sp.f.shared;  // bounds compare keys across ranks: only in a shared frame
+  M3D_TCLK(11);
   if (count > 0.0) {
     if (kEst == M3D_EST_POINT_TO_PLANE) {
-      double A[36], b[6], x[6];
-      int k = 0;
-      for (int a = 0; a < 6; ++a)
-        for (int c = a; c < 6; ++c) {
-          A[a * 6 + c] = sm[k];
-          A[c * 6 + a] = sm[k];
-          ++k;
-        }
-      for (int a = 0; a < 6; ++a) b[a] = -sm[21 + a];
+      if (!M3D_SOLVE_SPEC) {
+        int k = 0;
+        for (int a = 0; a < 6; ++a)
+          for (int c = a; c < 6; ++c) {
+            A[a * 6 + c] = sm[k];
+            A[c * 6 + a] = sm[k];
+            ++k;
+          }
+        for (int a = 0; a < 6; ++a) b[a] = -sm[21 + a];
+      }
       M3D_TCLK(3);
 #ifndef M3D_SOLVE_SPD
 #define M3D_SOLVE_SPD 1
 #endif
       // a full-rank JᵀJ unpivoted (no scalar-unit row swaps: 1.6 µs of the tail); a
       // (near-)singular one through Eigen's pivot order, which decides its zero components
-      if (!M3D_SOLVE_SPD || !ldlt6_solve_spd(A, b, x)) ldlt6_solve(A, b, x);
+      if (!M3D_SOLVE_SPEC) spd_ok = M3D_SOLVE_SPD && ldlt6_solve_spd(A, b, x);
+      if (!spd_ok) ldlt6_solve(A, b, x);
       M3D_TCLK(4);
       vec6_to_matrix_wave(x, upd);
       M3D_TCLK(5);
@@ -1293,12 +1376,14 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
   // T ← ΔT·T and the points ← ΔT·points (applied by the next evaluation's query, IcpState::dT)
 #pragma unroll
   for (int k = 0; k < 16; ++k) s->dT[k] = s->last_upd[k] = upd[k];
-  matmul4(upd, T, T);
+  // both are affine (bottom row 0 0 0 1): the 12 products that are not 0 or 1 (the same sums as
+  // matmul4 without its exact-zero terms)
+  matmul4_affine(upd, T, T);
 #pragma unroll
   for (int k = 0; k < 16; ++k) s->T[k] = T[k];
   s->iters = iters + 1;
   M3D_TCLK(6);
-  refresh_rt32_from(s, T, r2, sp.f, iters + 1);
+  refresh_rt32_from(s, T, r2, r, sp.f, iters + 1);
   M3D_TCLK(7);
 }
 
@@ -1380,6 +1465,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
 #pragma unroll
       for (int u = 0; u < kG; ++u) gv[u] += t[r][u];
   }
+  M3D_TCLK(8);  // thread 0's loads landed and added
 #pragma unroll
   for (int u = 0; u < kG; ++u) red[g0 + u * (kTermsBlock / kTermSlots)][slot] = gv[u];
   __syncthreads();
@@ -1389,6 +1475,7 @@ __global__ __launch_bounds__(kTermsBlock) void terms_solve_kernel(
     red[0][threadIdx.x] = t;  // row 0 is consumed by this thread only before the overwrite
     sums[threadIdx.x] = t;
   }
+  M3D_TCLK(9);
   __syncthreads();
   M3D_TCLK(1);
   if (threadIdx.x < kWave) {

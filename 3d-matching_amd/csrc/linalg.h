@@ -337,4 +337,19 @@ M3D_HD void matmul4(const double A[16], const double B[16], double C[16]) {
   for (int k = 0; k < 16; ++k) C[k] = t[k];
 }
 
+// C = A · B for row-major affine 4×4 (bottom rows 0 0 0 1): matmul4's sums in its order, without
+// the terms that multiply by the bottom row's exact 0 / 1 (equal values; the sign of an exact zero
+// entry may differ)
+M3D_HD void matmul4_affine(const double A[16], const double B[16], double C[16]) {
+  double t[12];
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j)
+      t[i * 4 + j] = A[i * 4 + 0] * B[0 * 4 + j] + A[i * 4 + 1] * B[1 * 4 + j] + A[i * 4 + 2] * B[2 * 4 + j];
+    t[i * 4 + 3] = A[i * 4 + 0] * B[3] + A[i * 4 + 1] * B[7] + A[i * 4 + 2] * B[11] + A[i * 4 + 3];
+  }
+  for (int k = 0; k < 12; ++k) C[k] = t[k];
+  C[12] = C[13] = C[14] = 0.0;
+  C[15] = 1.0;
+}
+
 }  // namespace m3d

@@ -25,13 +25,13 @@ lp.reset(np.eye(4))
 lp.steps(20)
 torch.cuda.synchronize()
 NW = 4096
-buf = (C.c_ulonglong * (3 * NW + 8))()
-ctx.lib.m3d_debug_tail_clock(buf, C.c_int(3 * NW + 8))
+buf = (C.c_ulonglong * (3 * NW + 24))()
+ctx.lib.m3d_debug_tail_clock(buf, C.c_int(3 * NW + 24))
 a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
 w = a[: 2 * NW].reshape(-1, 2)
 keep = w[:, 1] > 0
 w = w[keep]
-amb = a[2 * NW + 8:][keep]
+amb = a[2 * NW + 8:3 * NW + 8][keep]
 t0 = w[:, 0].min()
 st, en = (w[:, 0] - t0) * 1e-2, (w[:, 1] - t0) * 1e-2
 du = en - st
@@ -40,6 +40,8 @@ print(f"{nn}: waves {len(w)}; start max {st.max():.2f} us; terms per wave mean {
       f"{np.percentile(du, 90):.2f} max {du.max():.2f}; last wave done {en.max():.2f}; ticket won {tk:.2f}; "
       f"reduced {rd:.2f}; solved {sv:.2f} us | solve: ldlt in {l0:.2f} out {l1:.2f}, vec6 {v6:.2f}, "
       f"T stored {mm:.2f}, refresh {rf:.2f}")
+ld, lr, fr, pv = [(a[3 * NW + k] - t0) * 1e-2 if a[3 * NW + k] > 0 else float("nan") for k in (8, 9, 10, 11)]
+print(f"  reduce: loads landed {ld:.2f}, LDS sum {lr:.2f}; solve: fitness/rmse {fr:.2f}, before solve {pv:.2f} us")
 has = amb > 0
 if has.any():
     print(f"  waves with ambiguous queries: {has.sum()} ({amb.sum()} queries), terms mean {du[has].mean():.2f} "
