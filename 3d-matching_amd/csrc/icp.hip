@@ -40,12 +40,19 @@ constexpr int kNNQ = 4;       // queries per lane (nn_kernel)
 constexpr int kNNTile = 16;   // screen sub-tile (one branch per sub-tile)
 constexpr int kNNLds = 512;   // targets per LDS tile (8 KB, double-buffered)
 constexpr int kNNBlock = 256;
+// terms pass geometry: 512-thread blocks, one source per thread (196 block partials at cfg1, as
+// 256 × 2 gave): two waves per SIMD share the fp64 work and hide each other's round trips — the
+// last terms wave of a cfg1 evaluation ends ≈ 1 µs sooner (docs/EXPERIMENTS.md §R6)
 #ifndef M3D_TERMS_BLOCK
-#define M3D_TERMS_BLOCK 256
+#define M3D_TERMS_BLOCK 512
 #endif
 constexpr int kTermsBlock = M3D_TERMS_BLOCK;
-constexpr int kTermsPtsDefault = 2;  // sources per terms thread (1 / 4 / 8 were measured slower):
-                                     // 2× fewer block partials for the last block to reduce
+#ifndef M3D_TERMS_PTS
+#define M3D_TERMS_PTS 1
+#endif
+constexpr int kTermsPtsDefault = M3D_TERMS_PTS;  // sources per terms thread (with 256-thread blocks
+                                                 // 2 was fastest: 1 doubled the partials, 4 / 8
+                                                 // lengthened each wave's chain)
 static int terms_pts() { return kTermsPtsDefault; }
 constexpr double kU = 5.9604644775390625e-08;
 constexpr double kU64 = 1.1102230246251565e-16;
@@ -1861,11 +1868,10 @@ hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* c
   if (ns == 0) return hipMemsetAsync(s->partials, 0, sizeof(double) * kTermSlots, st);
   const TermsArgs ta = terms_args(s, off, claim, dmin, false);
   const unsigned nb = (unsigned)s->nblocks;
-  static_assert(kTermsPtsDefault == 2, "terms kernels are instantiated for 2 sources per thread");
   if (ta.est == M3D_EST_POINT_TO_PLANE)
-    terms_kernel<2, M3D_EST_POINT_TO_PLANE><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials);
+    terms_kernel<kTermsPtsDefault, M3D_EST_POINT_TO_PLANE><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials);
   else
-    terms_kernel<2, M3D_EST_POINT_TO_POINT><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials);
+    terms_kernel<kTermsPtsDefault, M3D_EST_POINT_TO_POINT><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials);
   return hipGetLastError();
 }
 
@@ -1893,10 +1899,10 @@ static void launch_terms_solve(const TermsArgs& ta, const m3d_icp* s, double* su
   const unsigned nb = (unsigned)s->nblocks;
   const SolveParams sp = solve_params(s);
   if (ta.est == M3D_EST_POINT_TO_PLANE)
-    terms_solve_kernel<2, M3D_EST_POINT_TO_PLANE><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks,
+    terms_solve_kernel<kTermsPtsDefault, M3D_EST_POINT_TO_PLANE><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks,
                                                                              sums, sp, do_solve);
   else
-    terms_solve_kernel<2, M3D_EST_POINT_TO_POINT><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks,
+    terms_solve_kernel<kTermsPtsDefault, M3D_EST_POINT_TO_POINT><<<nb, kTermsBlock, 0, st>>>(ta, s->state, s->partials, s->nblocks,
                                                                              sums, sp, do_solve);
 }
 
