@@ -1287,8 +1287,9 @@ __device__ void solve_state(const double* sums, IcpState* s, const SolveParams& 
 #define M3D_SOLVE_SPEC 1
 #endif
   // point-to-plane: the unpivoted LDLT of JᵀJ does not depend on the convergence test, so it is
-  // evaluated first, in the same basic block as fitness / rmse (their division and square-root
-  // chains interleave with the factorisation's); its result is used only if the loop goes on
+  // written first, in the same basic block as fitness / rmse, for the scheduler to interleave the
+  // chains (measured neutral against M3D_SOLVE_SPEC=0, docs/EXPERIMENTS.md §R6; the same bits);
+  // its result is used only if the loop goes on
   double A[36], b[6], x[6];
   bool spd_ok = false;
   if (M3D_SOLVE_SPEC && kEst == M3D_EST_POINT_TO_PLANE) {
