@@ -13,6 +13,6 @@ for rep in 1 2 3; do
   timeout -k 10 200 python3 tools/grid_timing.py 50 cfg1 > gpurun_out/gt_new_$rep.log 2>&1 || exit $?
   AB_LIB=tools/ab/$v.so timeout -k 10 200 python3 tools/grid_timing.py 50 cfg1 > gpurun_out/gt_${v}_$rep.log 2>&1 || exit $?
 done
-timeout -k 10 200 python3 tools/grid_timing.py 50 "1M x 1M" > gpurun_out/gt_new_1m.log 2>&1 || exit $?
-AB_LIB=tools/ab/$v.so timeout -k 10 200 python3 tools/grid_timing.py 50 "1M x 1M" > gpurun_out/gt_${v}_1m.log 2>&1 || exit $?
+timeout -k 10 200 python3 tools/grid_timing.py 50 "1M x" > gpurun_out/gt_new_1m.log 2>&1 || exit $?
+AB_LIB=tools/ab/$v.so timeout -k 10 200 python3 tools/grid_timing.py 50 "1M x" > gpurun_out/gt_${v}_1m.log 2>&1 || exit $?
 for f in gpurun_out/tclk_new.log gpurun_out/gt_*.log; do [ -f $f ] || continue; echo "== $f"; grep -v amdgpu $f; done
