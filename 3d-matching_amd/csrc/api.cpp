@@ -1610,8 +1610,7 @@ int m3d_icp_step(m3d_icp* s, void* stream) {
     return M3D_OK;
   }
   { KTimer kt(ctx, M3D_KERNEL_TERMS, st); HIPX(ctx, launch_icp_terms_mode(s, 0, nullptr, nullptr, st)); }
-  HIPX(ctx, launch_icp_reduce(s, s->sums, st));
-  HIPX(ctx, launch_icp_solve(s, s->sums, st));
+  HIPX(ctx, launch_icp_reduce_solve(s, st));
   return M3D_OK;
 }
 

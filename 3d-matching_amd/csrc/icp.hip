@@ -1174,47 +1174,6 @@ __global__ __launch_bounds__(kReduceGroups * kTermSlots) void reduce_kernel(
   }
 }
 
-// Past 256 partials (the separate tail of a large source, 1M: 1,954 rows) the same order on 32
-// blocks instead of one: block g adds group g (blocks g, g + 32, …; 32 loads in flight per batch),
-// stores the group sum write-through into partials row g (a row only this block reads), drains it
-// and takes the ticket; the last block adds rows 0..31 in group order with sc1 loads — the same
-// sums, bit for bit, as reduce_kernel.
-__global__ __launch_bounds__(kTermSlots) void reduce_groups_kernel(double* __restrict__ partials,
-                                                                   int64_t nblocks, double* __restrict__ sums,
-                                                                   IcpState* __restrict__ s) {
-  if (s->done) return;
-  const int g = blockIdx.x, slot = threadIdx.x;
-  double v = 0.0;
-  for (int64_t b0 = g; b0 < nblocks; b0 += (int64_t)kReduceGroups * 32) {
-    double t[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int64_t b = b0 + (int64_t)k * kReduceGroups;
-      t[k] = b < nblocks ? partials[b * kTermSlots + slot] : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < 32; ++k)
-      if (b0 + (int64_t)k * kReduceGroups < nblocks) v += t[k];
-  }
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials + (int64_t)g * kTermSlots + slot),
-                     __double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __shared__ int last;
-  __syncthreads();
-  if (slot == 0)
-    last = __hip_atomic_fetch_add(&s->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-           (uint32_t)(kReduceGroups - 1);
-  __syncthreads();
-  if (!last) return;
-  double tot = 0.0;
-  for (int k = 0; k < kReduceGroups; ++k)
-    tot += __longlong_as_double(__hip_atomic_load(
-        reinterpret_cast<unsigned long long*>(partials + (int64_t)k * kTermSlots + slot), __ATOMIC_RELAXED,
-        __HIP_MEMORY_SCOPE_AGENT));
-  sums[slot] = tot;
-  if (slot == 0) s->ticket = 0;
-}
-
 // ------------------------------------------------------------------------------- solve
 struct SolveParams {
   double rel_fit, rel_rmse;
@@ -1443,6 +1402,56 @@ __global__ void solve_kernel(const double* __restrict__ sums, IcpState* __restri
   SolveIn in;
   solve_in(s, in);
   solve_state<kEst>(sums, s, sp, in);
+}
+
+// Past 256 partials (the separate tail of a large source, 1M: 1,954 rows) the same order on 32
+// blocks instead of one: block g adds group g (blocks g, g + 32, …; 32 loads in flight per batch),
+// stores the group sum write-through into partials row g (a row only this block reads), drains it
+// and takes the ticket; the last block adds rows 0..31 in group order with sc1 loads — the same
+// sums, bit for bit, as reduce_kernel — and, for a single-device step (do_solve), runs the solve
+// on them (solve_kernel's work without its launch).
+template <int kEst>
+__global__ __launch_bounds__(kTermSlots) void reduce_groups_kernel(double* __restrict__ partials,
+                                                                   int64_t nblocks, double* __restrict__ sums,
+                                                                   IcpState* __restrict__ s, SolveParams sp,
+                                                                   int do_solve) {
+  if (s->done) return;
+  const int g = blockIdx.x, slot = threadIdx.x;
+  double v = 0.0;
+  for (int64_t b0 = g; b0 < nblocks; b0 += (int64_t)kReduceGroups * 32) {
+    double t[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int64_t b = b0 + (int64_t)k * kReduceGroups;
+      t[k] = b < nblocks ? partials[b * kTermSlots + slot] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (b0 + (int64_t)k * kReduceGroups < nblocks) v += t[k];
+  }
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials + (int64_t)g * kTermSlots + slot),
+                     __double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ int last;
+  __syncthreads();
+  if (slot == 0)
+    last = __hip_atomic_fetch_add(&s->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (uint32_t)(kReduceGroups - 1);
+  __syncthreads();
+  if (!last) return;
+  SolveIn in;
+  if (do_solve) solve_in(s, in);  // its loads overlap the group rows'
+  double tot = 0.0;
+  for (int k = 0; k < kReduceGroups; ++k)
+    tot += __longlong_as_double(__hip_atomic_load(
+        reinterpret_cast<unsigned long long*>(partials + (int64_t)k * kTermSlots + slot), __ATOMIC_RELAXED,
+        __HIP_MEMORY_SCOPE_AGENT));
+  sums[slot] = tot;
+  __shared__ double out[kTermSlots];
+  out[slot] = tot;
+  __syncthreads();
+  if (slot == 0) s->ticket = 0;
+  if (do_solve) solve_state<kEst>(out, s, sp, in);
 }
 
 // Fused single-device iteration tail: terms → block partial → the last block to finish (ticket)
@@ -1919,9 +1928,28 @@ hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* c
 
 hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st) {
   if (s->nblocks > 256)  // group g's first row is block g's: rows 0..31 exist
-    reduce_groups_kernel<<<kReduceGroups, kTermSlots, 0, st>>>(s->partials, s->nblocks, sums, s->state);
+    reduce_groups_kernel<M3D_EST_POINT_TO_PLANE><<<kReduceGroups, kTermSlots, 0, st>>>(
+        s->partials, s->nblocks, sums, s->state, SolveParams{}, 0);
   else
     reduce_kernel<<<1, kReduceGroups * kTermSlots, 0, st>>>(s->partials, s->nblocks, sums, s->state);
+  return hipGetLastError();
+}
+
+static SolveParams solve_params(const m3d_icp* s);
+
+// the single-device separate tail after the terms pass: reduce + solve (one launch past 256
+// partials, reduce_groups_kernel's last block solving; two below)
+hipError_t launch_icp_reduce_solve(const m3d_icp* s, hipStream_t st) {
+  if (s->nblocks <= 256) {
+    hipError_t e = launch_icp_reduce(s, s->sums, st);
+    return e == hipSuccess ? launch_icp_solve(s, s->sums, st) : e;
+  }
+  if (s->params.estimation == M3D_EST_POINT_TO_PLANE)
+    reduce_groups_kernel<M3D_EST_POINT_TO_PLANE><<<kReduceGroups, kTermSlots, 0, st>>>(
+        s->partials, s->nblocks, s->sums, s->state, solve_params(s), 1);
+  else
+    reduce_groups_kernel<M3D_EST_POINT_TO_POINT><<<kReduceGroups, kTermSlots, 0, st>>>(
+        s->partials, s->nblocks, s->sums, s->state, solve_params(s), 1);
   return hipGetLastError();
 }
 

@@ -478,6 +478,7 @@ hipError_t launch_icp_keyinit(const m3d_icp* s, int64_t shard_offset, hipStream_
 hipError_t launch_icp_nn(const m3d_icp* s, int64_t shard_offset, bool self_seed, hipStream_t st,
                          int64_t q0 = 0, int64_t q1 = -1);
 hipError_t launch_icp_reduce(const m3d_icp* s, double* sums, hipStream_t st);
+hipError_t launch_icp_reduce_solve(const m3d_icp* s, hipStream_t st);
 // claim/dmin: target-shard exchange results (m3d_icp_shard_claim), or null
 hipError_t launch_icp_terms_mode(const m3d_icp* s, int64_t off, const int32_t* claim,
                                  const int64_t* dmin, hipStream_t st);
