@@ -10,7 +10,7 @@ import csv
 import sys
 from collections import defaultdict
 
-HOT = ("nn_mfma_kernel", "score_mfma_kernel", "grid_nn_batched_kernel", "terms_solve_kernel",
+HOT = ("nn_mfma_kernel", "score_mfma_kernel", "grid_nn_batched_kernel", "terms_solve_kernel", "reduce_groups_kernel",
        "terms_kernel", "kabsch3_kernel", "kabsch3_one_kernel", "reduce_kernel", "solve_kernel",
        "validate_kernel")
 
